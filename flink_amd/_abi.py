@@ -1,0 +1,114 @@
+"""ctypes view of include/flink_window.h and the loader of the HIP engine library.
+
+The product path is libflink_window.so (hand-written HIP for gfx950, built in-tree by
+flink_amd.build).  There is no CPU fallback: if the library is missing, loading fails loudly.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libflink_window.so")
+
+# return codes
+FW_OK = 0
+FW_ERR_INVALID_ARG = 1
+FW_ERR_NO_TIMESTAMP = 2
+FW_ERR_CAPACITY = 3
+FW_ERR_KEY_GROUP = 4
+FW_ERR_UNSUPPORTED = 5
+FW_ERR_DEVICE = 6
+
+FW_TUMBLING = 0
+FW_SLIDING = 1
+FW_TRIGGER_EVENT_TIME = 0
+FW_TRIGGER_PURGING_EVENT_TIME = 1
+FW_AGG_SUM = 1
+FW_AGG_MIN = 2
+FW_AGG_MAX = 4
+FW_AGG_COUNT = 8
+FW_VALUE_I64 = 0
+FW_VALUE_F64 = 1
+FW_MEM_HOST = 0
+FW_MEM_DEVICE = 1
+
+# every entry point include/flink_window.h declares
+EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sync", "fw_collect",
+                    "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
+                    "fw_get_profile", "fw_version")
+FW_PHASE_INGEST, FW_PHASE_FIXUP, FW_PHASE_LATE, FW_PHASE_FIRE, FW_NPHASES = 0, 1, 2, 3, 4
+
+_i32, _i64, _p = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+_pf64 = ctypes.POINTER(ctypes.c_double)
+
+
+class FwConfig(ctypes.Structure):
+    _fields_ = [("assigner", _i32), ("trigger", _i32), ("size", _i64), ("slide", _i64), ("offset", _i64),
+                ("allowed_lateness", _i64), ("value_type", _i32), ("agg_mask", _i32), ("keep_first_f1", _i32),
+                ("max_parallelism", _i32), ("kg_start", _i32), ("kg_end", _i32), ("device", _i32),
+                ("max_open_slices", _i32), ("key_capacity", _i64), ("max_batch", _i64), ("out_capacity", _i64),
+                ("ingest_mode", _i32), ("reserved", _i32)]
+
+
+class FwOut(ctypes.Structure):
+    _fields_ = [("n", _i64), ("key", _pi64), ("f1", _pi64), ("ts", _pi64), ("sum_i64", _pi64), ("min_i64", _pi64),
+                ("max_i64", _pi64), ("count", _pi64), ("sum_f64", _pf64), ("min_f64", _pf64), ("max_f64", _pf64),
+                ("n_marks", _i64), ("mark_wm", _pi64), ("mark_pos", _pi64)]
+
+
+class FwProfile(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double * 4), ("launches", _i64 * 4), ("records", _i64 * 4)]
+
+
+class FwStats(ctypes.Structure):
+    _fields_ = [("records_in", _i64), ("records_late", _i64), ("panes_fired", _i64), ("late_fires", _i64),
+                ("keys_resident", _i64), ("slices_live", _i64)]
+
+
+def declare(lib, prefix="fw"):
+    """Attach argtypes/restypes for the fw_* (or fwo_* oracle) entry points present in `lib`."""
+    P = ctypes.POINTER
+    sigs = {
+        "create": (_i32, [P(FwConfig), P(_p)]),
+        "push_batch": (_i32, [_p, _p, _p, _p, _p, _p, _i64] + ([_i32] if prefix == "fw" else [])),
+        "advance_watermark": (_i32, [_p, _i64]),
+        "sync": (_i32, [_p]),
+        "collect": (_i32, [_p, P(FwOut)] + ([_i32] if prefix == "fw" else [])),
+        "get_stats": (_i32, [_p, P(FwStats)]),
+        "last_error": (ctypes.c_char_p, [_p]),
+        "destroy": (None, [_p]),
+        "partition_by_operator": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
+        "version": (ctypes.c_char_p, []),
+        "set_profiling": (_i32, [_p, _i32]),
+        "get_profile": (_i32, [_p, P(FwProfile)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, f"{prefix}_{name}", None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = None
+
+
+def open_library(path):
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP engine library not built: {path} (run flink_amd.build.build_all())")
+    return declare(ctypes.CDLL(path), "fw")
+
+
+def load_library():
+    """Load libflink_window.so (no fallback: a missing library is an error)."""
+    global _lib
+    if _lib is None:
+        _lib = open_library(LIB_PATH)
+    return _lib
+
+
+class FwError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[fw error {code}] {msg}")
+        self.code = code

@@ -1,0 +1,1279 @@
+// fw_engine.hip — MI355X (gfx950) keyed event-time window aggregation engine behind the C-ABI of
+// include/flink_window.h.  One engine = one WindowOperator subtask = one GPU.
+//
+// Data layout in HBM:
+//   key directory   dir_keys[D+1]            open addressing, linear probing on fmix64(key); the slot index
+//                                            is the dense key id `kid` (index D holds key Long.MIN_VALUE)
+//   pane slices     per slice slot p < P:    dense columns [p][kid] of the reduce accumulator
+//                                            (sum/min/max/count, first-arrival ordinal, first-arrival f1)
+//                   slice_tag[P]             slice number m held by slot p = floor_mod(m, P), or FREE
+//   output log      fired records + watermark marks, appended on device, drained by fw_collect
+//
+// A pane is (key, window).  Windows are unions of K = size/g consecutive slices of width
+// g = gcd(size, slide) (tumbling: one slice = one window), so a record touches exactly ONE slice
+// whatever the window overlap — the reference keeps one pane per (key, window) instead
+// (HeapReducingState.add, RT/state/heap/HeapReducingState.java:84-122, called once per assigned
+// window from WindowOperator.java:302-333).  Fire combines the K slices of a window; this is exact
+// for integer sum/min/max/count and order-changing (tolerance 1e-9) for double sums.
+//
+// Timers (HeapInternalTimerService, SJ/api/operators/HeapInternalTimerService.java:211-278) are not
+// materialised: a pane exists iff its trigger timer is pending, so the watermark step fires every
+// window whose maxTimestamp lies in (previous watermark, new watermark] and purges every slice whose
+// last window's cleanup time has passed (WindowOperator.onEventTime :336-375, cleanupTime :511-514).
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan_by_key.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/flink_window.h"
+#include "java_semantics.h"
+
+namespace fw {
+
+constexpr int64_t FREE_TAG = INT64_MIN;
+constexpr int64_t EMPTY_KEY = INT64_MIN;
+constexpr int MAX_K = 64;          // max slices per window
+constexpr int BLOCK = 256;
+
+enum Stat { ST_LATE = 0, ST_FIRED = 1, ST_LATE_FIRES = 2, ST_NSTATS = 8 };
+
+// ------------------------------------------------------------------------------------------------
+// device views
+// ------------------------------------------------------------------------------------------------
+struct Cols {  // dense pane columns, each [P][stride]
+  int64_t* sum;        // int64 sum, or double bits
+  int64_t* mn;         // int64 min, or Math.min code of a double
+  int64_t* mx;
+  int64_t* cnt;
+  int64_t* first;      // first-arrival ordinal, INT64_MAX = no pane
+  int64_t* f1v;        // f1 of the first arrival
+  uint8_t* present;    // pane presence when first-arrival is not tracked
+};
+
+struct OutLog {
+  int64_t* key;
+  int64_t* f1;
+  int64_t* ts;
+  int64_t* sum;
+  int64_t* mn;
+  int64_t* mx;
+  int64_t* cnt;
+  unsigned long long* count;  // records appended since the last collect
+  int64_t capacity;
+  int64_t* mark_wm;
+  int64_t* mark_pos;
+  unsigned long long* mark_count;
+  int64_t mark_capacity;
+};
+
+struct Spec {  // window specification + reduce + subtask, passed by value
+  int32_t assigner, trigger;
+  int64_t size, slide, offset, lateness, g;
+  int32_t K;        // slices per window
+  int32_t R;        // slices per slide
+  int32_t mp, kg_start, kg_end;
+  int32_t vt, agg, first;
+  // directory
+  int64_t* dir_keys;
+  int32_t* dir_min_used;
+  uint64_t dir_mask;
+  int64_t D;
+  // slices
+  int32_t P;
+  int64_t stride;   // D + 1
+  int64_t* slice_tag;
+  int32_t* touched;
+  Cols c;
+  OutLog o;
+  int32_t* err;
+  unsigned long long* stats;
+};
+
+__device__ __forceinline__ void set_error(int32_t* err, int32_t code) { atomicCAS(err, 0, code); }
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {  // MurmurHash3 finaliser: directory hash
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() { return __lanemask_lt(); }
+
+// wave-aggregated counter add; returns this lane's slot (only meaningful where pred)
+__device__ __forceinline__ unsigned long long wave_append(unsigned long long* ctr, bool pred) {
+  uint64_t mask = __ballot(pred);
+  if (mask == 0) return 0;
+  int leader = __ffsll((long long)mask) - 1;
+  unsigned long long base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  return base + (unsigned long long)__popcll(mask & lanemask_lt());
+}
+__device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
+  uint64_t mask = __ballot(pred);
+  if (mask != 0 && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)mask) - 1))
+    atomicAdd(ctr, (unsigned long long)__popcll(mask));
+}
+
+// key -> kid (directory slot).  Entries go EMPTY -> key once and never change until engine reset, so
+// a plain (possibly stale) load can only under-report, which the CAS then corrects.
+__device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key) {
+  if (key == EMPTY_KEY) {
+    if (s.dir_min_used[0] == 0) s.dir_min_used[0] = 1;
+    return s.D;
+  }
+  uint64_t h = fmix64((uint64_t)key) & s.dir_mask;
+  for (int64_t probe = 0; probe <= (int64_t)s.dir_mask; ++probe) {
+    int64_t cur = s.dir_keys[h];
+    if (cur == key) return (int64_t)h;
+    if (cur == EMPTY_KEY) {
+      unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[h], (unsigned long long)EMPTY_KEY,
+                                          (unsigned long long)key);
+      if ((int64_t)prev == EMPTY_KEY || (int64_t)prev == key) return (int64_t)h;
+    }
+    h = (h + 1) & s.dir_mask;
+  }
+  return -1;
+}
+
+// slice number m -> slot p, claiming a FREE slot.  Returns -1 when slot p holds another live slice.
+__device__ __forceinline__ int32_t slice_slot(const Spec& s, int64_t m) {
+  int32_t p = (int32_t)floor_mod(m, s.P);
+  int64_t tag = s.slice_tag[p];
+  if (tag == m) return p;
+  if (tag == FREE_TAG) {
+    unsigned long long prev = atomicCAS((unsigned long long*)&s.slice_tag[p], (unsigned long long)FREE_TAG,
+                                        (unsigned long long)m);
+    if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) return p;
+    return -1;
+  }
+  // the cached value may be stale (the slot was freed and re-claimed by a kernel boundary, which
+  // flushes caches) — re-read atomically before giving up
+  unsigned long long now = atomicCAS((unsigned long long*)&s.slice_tag[p], (unsigned long long)FREE_TAG,
+                                     (unsigned long long)m);
+  if ((int64_t)now == FREE_TAG || (int64_t)now == m) return p;
+  return -1;
+}
+
+// Window bookkeeping for one record, following SlidingEventTimeWindows.assignWindows (:64-77) /
+// TumblingEventTimeWindows.assignWindows (:59-68).  Produces the record's slice number m and how many
+// of its windows are late (WindowOperator.isLate :470-472) or already fired (EventTimeTrigger.onElement
+// FIRE branch, EventTimeTrigger.java:38-40).
+struct RecWin {
+  int64_t m;          // slice number
+  int32_t n_windows;  // windows assigned
+  int32_t n_late;     // of which late (dropped)
+  int32_t n_fire;     // of which not late but maxTimestamp <= watermark (per-element fire)
+  bool quirk;         // sliding assignment outside the slice-exact regime
+};
+
+__device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int64_t wm) {
+  RecWin r;
+  r.quirk = false;
+  r.n_late = 0;
+  r.n_fire = 0;
+  if (s.assigner == FW_TUMBLING) {
+    int64_t x = jadd(jsub(ts, s.offset), s.size);
+    r.m = x / s.size - 1;                                        // start = offset + m * size
+    int64_t start = jsub(ts, x % s.size);                        // getWindowStartWithOffset
+    int64_t max_ts = jsub(jadd(start, s.size), 1);               // TimeWindow.maxTimestamp
+    int64_t ct = cleanup_time(max_ts, s.lateness);
+    r.n_windows = 1;
+    if (ct <= wm) r.n_late = 1;
+    else if (max_ts <= wm) r.n_fire = 1;
+    return r;
+  }
+  int64_t x = jadd(jsub(ts, s.offset), s.g);
+  if (x < 0 || jadd(jsub(ts, s.offset), s.slide) < 0) r.quirk = true;   // Java % of a negative numerator
+  r.m = x / s.g - 1;
+  int64_t n_hi = floor_div(r.m, s.R);
+  int64_t n_lo = floor_div(r.m - s.K, s.R) + 1;
+  r.n_windows = (int32_t)(n_hi - n_lo + 1);
+  for (int64_t n = n_lo; n <= n_hi; ++n) {
+    int64_t start = jadd(s.offset, (int64_t)((uint64_t)n * (uint64_t)s.slide));
+    int64_t max_ts = jsub(jadd(start, s.size), 1);
+    int64_t ct = cleanup_time(max_ts, s.lateness);
+    if (ct <= wm) r.n_late++;
+    else if (max_ts <= wm) r.n_fire++;
+  }
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// ingest, direct form: every (record, slice) update is a device-scope atomic on the dense columns.
+// ------------------------------------------------------------------------------------------------
+template <int VT, int AGG, bool FIRST>
+__device__ __forceinline__ void pane_update(const Spec& s, int64_t idx, int64_t vbits, int64_t ord) {
+  if (AGG & FW_AGG_SUM) {
+    if (VT == FW_VALUE_I64) {
+      atomicAdd((unsigned long long*)&s.c.sum[idx], (unsigned long long)vbits);
+    } else {
+      double v; __builtin_memcpy(&v, &vbits, 8);
+      unsafeAtomicAdd((double*)&s.c.sum[idx], v);
+    }
+  }
+  if (AGG & FW_AGG_MIN) {
+    int64_t code = VT == FW_VALUE_I64 ? vbits : f64_min_code(__longlong_as_double(vbits));
+    atomicMin((long long*)&s.c.mn[idx], (long long)code);
+  }
+  if (AGG & FW_AGG_MAX) {
+    int64_t code = VT == FW_VALUE_I64 ? vbits : f64_max_code(__longlong_as_double(vbits));
+    atomicMax((long long*)&s.c.mx[idx], (long long)code);
+  }
+  if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&s.c.cnt[idx], 1ull);
+  if (FIRST) {
+    // first arrival = min ordinal; values only decrease within a kernel, so a stale load that is
+    // already below our ordinal proves we are not first
+    int64_t cur = s.c.first[idx];
+    if (ord < cur) atomicMin((long long*)&s.c.first[idx], (long long)ord);
+  } else {
+    if (s.c.present[idx] == 0) s.c.present[idx] = 1;
+  }
+}
+
+struct BatchIn {
+  const int64_t* key;
+  const int32_t* key_hash;
+  const int64_t* ts;
+  const int64_t* val;   // int64 or double bits
+  int64_t n;
+  int64_t ord_base;     // arrival ordinal of record 0
+  int64_t wm;           // current watermark
+  // per-element fire list (allowed lateness > 0)
+  unsigned long long* late_key;   // (pane id << idx_bits) | idx
+  unsigned long long* late_count;
+  int64_t late_capacity;
+  int32_t idx_bits;
+};
+
+template <int VT, int AGG, bool FIRST>
+__global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < b.n; i0 += stride) {
+    int64_t i = i0 + threadIdx.x;
+    bool valid = i < b.n;
+    int64_t key = 0, ts = 0, v = 0;
+    int32_t h = 0;
+    if (valid) {
+      key = b.key[i];
+      ts = b.ts[i];
+      v = b.val[i];
+      h = b.key_hash ? b.key_hash[i] : long_hash_code(key);
+    }
+    bool ok = valid;
+    if (ok && ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
+    if (ok) {
+      int32_t kg = key_group_for_hash(h, s.mp);   // AbstractKeyedStateBackend.setCurrentKey :167-170
+      if (kg < s.kg_start || kg > s.kg_end) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
+    }
+    RecWin w;
+    w.m = 0; w.n_late = 0; w.n_fire = 0; w.n_windows = 0; w.quirk = false;
+    if (ok) {
+      w = record_windows(s, ts, b.wm);
+      if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
+    }
+    // late statistics: (record, window) pairs dropped (wave-uniform reduction)
+    {
+      unsigned long long late = ok ? (unsigned long long)w.n_late : 0ull;
+      if (__any(late != 0)) {
+        for (int off = 32; off > 0; off >>= 1) late += __shfl_xor(late, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late);
+      }
+    }
+    bool live = ok && (w.n_windows - w.n_late) > 0;
+    bool late_fire = live && w.n_fire > 0;          // tumbling only (sliding + lateness rejected at create)
+    // slice slot: wave-uniform fast path (in-order streams keep a wave inside one slice)
+    const uint64_t lm = __ballot(live);
+    const int leader = lm ? __ffsll((long long)lm) - 1 : 0;
+    const int64_t m0 = __shfl(w.m, leader);
+    const bool uniform = __all(!live || w.m == m0);
+    int32_t p = -1;
+    if (uniform) {
+      int32_t p0 = -1;
+      if ((int)(threadIdx.x & 63) == leader && lm != 0) p0 = slice_slot(s, m0);
+      p0 = __shfl(p0, leader);
+      p = live ? p0 : -1;
+    } else if (live) {
+      p = slice_slot(s, w.m);
+    }
+    if (live && p < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
+    int64_t kid = -1;
+    if (live) {
+      kid = dir_find_or_insert(s, key);
+      if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
+    }
+    if (b.late_key) {  // kernel argument: uniform
+      const bool want = live && late_fire;
+      unsigned long long pos = wave_append(b.late_count, want);
+      if (want) {
+        if ((int64_t)pos < b.late_capacity) {
+          unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
+          b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
+        } else {
+          set_error(s.err, FW_ERR_CAPACITY);
+        }
+        live = false;
+      }
+    }
+    if (live) {
+      int64_t idx = (int64_t)p * s.stride + kid;
+      pane_update<VT, AGG, FIRST>(s, idx, v, b.ord_base + i);
+      if (s.touched[p] == 0) s.touched[p] = 1;
+    }
+  }
+}
+
+// after ingest: record f1 of panes whose first arrival lies in this batch
+__global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f1col, int64_t ord_base, int64_t n) {
+  for (int32_t p = 0; p < s.P; ++p) {
+    if (s.touched[p] == 0) continue;
+    const int64_t base = (int64_t)p * s.stride;
+    for (int64_t kid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; kid < s.stride;
+         kid += (int64_t)gridDim.x * blockDim.x) {
+      int64_t ord = s.c.first[base + kid];
+      if (ord >= ord_base && ord < ord_base + n) s.c.f1v[base + kid] = f1col[ord - ord_base];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-element fires (allowed lateness > 0, tumbling): ordered per-pane scan over this batch's records
+// whose window already fired.  WindowOperator.java:317-325 + EventTimeTrigger.java:38-40.
+// ------------------------------------------------------------------------------------------------
+struct LateAcc {
+  int64_t sum;    // int64 or double bits
+  int64_t mn, mx, cnt;
+  int32_t vt;
+  __host__ __device__ LateAcc() : sum(0), mn(INT64_MAX), mx(INT64_MIN), cnt(0), vt(0) {}
+};
+struct LateCombine {
+  __device__ LateAcc operator()(const LateAcc& a, const LateAcc& b) const {
+    LateAcc r;
+    r.vt = a.vt;
+    if (a.vt == FW_VALUE_I64) {
+      r.sum = jadd(a.sum, b.sum);
+    } else {
+      r.sum = __double_as_longlong(__longlong_as_double(a.sum) + __longlong_as_double(b.sum));
+    }
+    r.mn = a.mn < b.mn ? a.mn : b.mn;
+    r.mx = a.mx > b.mx ? a.mx : b.mx;
+    r.cnt = jadd(a.cnt, b.cnt);
+    return r;
+  }
+};
+
+__global__ void k_late_prepare(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
+                               const int64_t* val, unsigned long long* seg, LateAcc* acc) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nl) return;
+  unsigned long long k = sorted_key[j];
+  int64_t i = (int64_t)(k & ((1ull << idx_bits) - 1));
+  seg[j] = k >> idx_bits;
+  int64_t v = val[i];
+  LateAcc a;
+  a.vt = s.vt;
+  a.sum = v;
+  a.mn = s.vt == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v));
+  a.mx = s.vt == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v));
+  a.cnt = 1;
+  acc[j] = a;
+}
+
+__device__ __forceinline__ bool pane_present(const Spec& s, int64_t idx) {
+  return s.first ? s.c.first[idx] != INT64_MAX : s.c.present[idx] != 0;
+}
+
+__device__ __forceinline__ LateAcc pane_load(const Spec& s, int64_t idx) {
+  LateAcc a;
+  a.vt = s.vt;
+  a.sum = s.c.sum ? s.c.sum[idx] : 0;
+  a.mn = s.c.mn ? s.c.mn[idx] : INT64_MAX;
+  a.mx = s.c.mx ? s.c.mx[idx] : INT64_MIN;
+  a.cnt = s.c.cnt ? s.c.cnt[idx] : 0;
+  return a;
+}
+
+__device__ __forceinline__ void emit_record(const Spec& s, unsigned long long pos, int64_t key, int64_t f1, int64_t ts,
+                                            const LateAcc& a) {
+  if ((int64_t)pos >= s.o.capacity) { set_error(s.err, FW_ERR_CAPACITY); return; }
+  s.o.key[pos] = key;
+  if (s.o.f1) s.o.f1[pos] = f1;
+  s.o.ts[pos] = ts;
+  if (s.o.sum) s.o.sum[pos] = a.sum;
+  if (s.o.mn) s.o.mn[pos] = s.vt == FW_VALUE_I64 ? a.mn : __double_as_longlong(f64_from_code(a.mn));
+  if (s.o.mx) s.o.mx[pos] = s.vt == FW_VALUE_I64 ? a.mx : __double_as_longlong(f64_from_code(a.mx));
+  if (s.o.cnt) s.o.cnt[pos] = a.cnt;
+}
+
+__device__ __forceinline__ int64_t kid_key(const Spec& s, int64_t kid) { return kid == s.D ? EMPTY_KEY : s.dir_keys[kid]; }
+
+__device__ __forceinline__ int64_t slot_max_ts(const Spec& s, int32_t p) {
+  int64_t m = s.slice_tag[p];
+  int64_t start = jadd(s.offset, (int64_t)((uint64_t)m * (uint64_t)s.size));  // tumbling: slice = window
+  return jsub(jadd(start, s.size), 1);
+}
+
+// emit one result per late record: state(base) (+) prefix
+__global__ void k_late_emit(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
+                            const unsigned long long* seg, const LateAcc* acc, const LateAcc* scanned,
+                            const int64_t* f1col, int64_t ord_base) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = j < nl;
+  unsigned long long pos = wave_append(s.o.count, act);
+  if (!act) return;
+  unsigned long long pane = seg[j];
+  int64_t idx = (int64_t)pane;
+  int32_t p = (int32_t)(pane / (unsigned long long)s.stride);
+  int64_t kid = (int64_t)(pane % (unsigned long long)s.stride);
+  bool head = j == 0 || seg[j - 1] != pane;
+  bool base_present = pane_present(s, idx);
+  LateCombine op;
+  LateAcc out;
+  if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && !head) out = acc[j];   // state was purged by the previous fire
+  else if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) out = base_present ? op(pane_load(s, idx), acc[j]) : acc[j];
+  else out = base_present ? op(pane_load(s, idx), scanned[j]) : scanned[j];
+  int64_t f1 = 0;
+  if (s.first) {
+    // first arrival: the pane's if it existed, else the segment head (purging: the record itself
+    // unless it is the head of a segment over an existing pane)
+    int64_t i_self = (int64_t)(sorted_key[j] & ((1ull << idx_bits) - 1));
+    if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) {
+      f1 = (head && base_present) ? s.c.f1v[idx] : f1col[i_self];
+    } else if (base_present) {
+      f1 = s.c.f1v[idx];
+    } else {
+      int64_t jh = j;
+      while (jh > 0 && seg[jh - 1] == pane) --jh;
+      f1 = f1col[(int64_t)(sorted_key[jh] & ((1ull << idx_bits) - 1))];
+    }
+  }
+  emit_record(s, pos, kid_key(s, kid), f1, slot_max_ts(s, p), out);
+}
+
+// write the pane state after the batch's per-element fires (segment tails)
+__global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
+                              const unsigned long long* seg, const LateAcc* scanned, const int64_t* f1col,
+                              int64_t ord_base) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nl) return;
+  unsigned long long pane = seg[j];
+  bool tail = j == nl - 1 || seg[j + 1] != pane;
+  if (!tail) return;
+  int64_t idx = (int64_t)pane;
+  int32_t p = (int32_t)(pane / (unsigned long long)s.stride);
+  if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) {
+    // FIRE_AND_PURGE after the last element: pane cleared (AbstractHeapState.clear)
+    if (s.c.sum) s.c.sum[idx] = 0;
+    if (s.c.mn) s.c.mn[idx] = INT64_MAX;
+    if (s.c.mx) s.c.mx[idx] = INT64_MIN;
+    if (s.c.cnt) s.c.cnt[idx] = 0;
+    if (s.first) s.c.first[idx] = INT64_MAX; else s.c.present[idx] = 0;
+    return;
+  }
+  bool base_present = pane_present(s, idx);
+  LateCombine op;
+  LateAcc st = base_present ? op(pane_load(s, idx), scanned[j]) : scanned[j];
+  if (s.c.sum) s.c.sum[idx] = st.sum;
+  if (s.c.mn) s.c.mn[idx] = st.mn;
+  if (s.c.mx) s.c.mx[idx] = st.mx;
+  if (s.c.cnt) s.c.cnt[idx] = st.cnt;
+  if (!base_present) {
+    int64_t jh = j;
+    while (jh > 0 && seg[jh - 1] == pane) --jh;
+    int64_t ih = (int64_t)(sorted_key[jh] & ((1ull << idx_bits) - 1));
+    if (s.first) { s.c.first[idx] = ord_base + ih; s.c.f1v[idx] = f1col[ih]; }
+    else s.c.present[idx] = 1;
+  }
+  (void)p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// watermark: plan fires/purges from the live slices, fire, purge, mark
+// ------------------------------------------------------------------------------------------------
+struct FireTask {
+  int64_t max_ts;
+  int32_t slots[MAX_K];   // slot of each slice of the window, -1 if not live
+};
+
+struct WmPlan {
+  int32_t n_tasks;
+  int32_t n_purge;
+  int32_t purge_slots[1024];
+};
+
+__device__ __forceinline__ int64_t window_start_n(const Spec& s, int64_t n) {
+  return jadd(s.offset, (int64_t)((uint64_t)n * (uint64_t)(s.assigner == FW_TUMBLING ? s.size : s.slide)));
+}
+
+// one block: live slices -> windows with maxTimestamp in (wm_old, wm_new] (owned by their first live
+// slice) and slices whose last window's cleanup time <= wm_new
+__global__ void k_wm_plan(Spec s, int64_t wm_old, int64_t wm_new, FireTask* tasks, int32_t max_tasks, WmPlan* plan) {
+  __shared__ int32_t n_tasks, n_purge;
+  if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; }
+  __syncthreads();
+  for (int32_t p = threadIdx.x; p < s.P; p += blockDim.x) {
+    int64_t m = s.slice_tag[p];
+    if (m == FREE_TAG) continue;
+    int64_t n_hi = floor_div(m, s.R);
+    int64_t n_lo = floor_div(m - s.K, s.R) + 1;
+    bool purge_now = false;
+    for (int64_t n = n_lo; n <= n_hi; ++n) {
+      int64_t start = window_start_n(s, n);
+      int64_t max_ts = jsub(jadd(start, s.size), 1);
+      bool fires = max_ts > wm_old && max_ts <= wm_new;
+      if (fires && s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) purge_now = true;  // tumbling only
+      if (!fires) continue;
+      // owner = first live slice of window n
+      int64_t m0 = n * s.R;
+      bool owner = true;
+      for (int64_t mm = m0; mm < m; ++mm) {
+        if (s.slice_tag[floor_mod(mm, s.P)] == mm) { owner = false; break; }
+      }
+      if (!owner) continue;
+      int32_t t = atomicAdd(&n_tasks, 1);
+      if (t >= max_tasks) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+      tasks[t].max_ts = max_ts;
+      for (int k = 0; k < s.K; ++k) {
+        int64_t mm = m0 + k;
+        int32_t pp = (int32_t)floor_mod(mm, s.P);
+        tasks[t].slots[k] = s.slice_tag[pp] == mm ? pp : -1;
+      }
+    }
+    int64_t last_start = window_start_n(s, n_hi);
+    int64_t ct = cleanup_time(jsub(jadd(last_start, s.size), 1), s.lateness);
+    if (ct <= wm_new) purge_now = true;
+    if (purge_now) {
+      int32_t q = atomicAdd(&n_purge, 1);
+      if (q < 1024) plan->purge_slots[q] = p;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    plan->n_tasks = n_tasks < max_tasks ? n_tasks : max_tasks;
+    plan->n_purge = n_purge < 1024 ? n_purge : 1024;
+  }
+}
+
+template <int VT, int AGG, bool FIRST>
+__global__ __launch_bounds__(BLOCK) void k_fire(Spec s, const FireTask* tasks, const WmPlan* plan) {
+  const int32_t nt = plan->n_tasks;
+  const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+  LateCombine op;
+  for (int32_t t = 0; t < nt; ++t) {
+    const FireTask& task = tasks[t];
+    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < s.stride; k0 += gstride) {
+      int64_t kid = k0 + threadIdx.x;
+      bool any = false;
+      LateAcc a;
+      a.vt = VT;
+      int64_t best_ord = INT64_MAX, f1 = 0;
+      if (kid < s.stride) {
+        for (int k = 0; k < s.K; ++k) {
+          int32_t p = task.slots[k];
+          if (p < 0) continue;
+          int64_t idx = (int64_t)p * s.stride + kid;
+          bool pres;
+          if (FIRST) {
+            int64_t o = s.c.first[idx];
+            pres = o != INT64_MAX;
+            if (pres && o < best_ord) { best_ord = o; f1 = s.c.f1v[idx]; }
+          } else {
+            pres = s.c.present[idx] != 0;
+          }
+          if (!pres) continue;
+          LateAcc b = pane_load(s, idx);
+          a = any ? op(a, b) : b;
+          any = true;
+        }
+      }
+      unsigned long long pos = wave_append(s.o.count, any);
+      wave_count(&s.stats[ST_FIRED], any);
+      if (any) emit_record(s, pos, kid_key(s, kid), f1, task.max_ts, a);
+    }
+  }
+}
+
+// reset purged slices to the empty state and free their slots
+__global__ __launch_bounds__(BLOCK) void k_purge(Spec s, const WmPlan* plan) {
+  const int32_t np = plan->n_purge;
+  for (int32_t q = 0; q < np; ++q) {
+    int32_t p = plan->purge_slots[q];
+    const int64_t base = (int64_t)p * s.stride;
+    for (int64_t kid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; kid < s.stride;
+         kid += (int64_t)gridDim.x * blockDim.x) {
+      int64_t idx = base + kid;
+      if (s.c.sum) s.c.sum[idx] = 0;
+      if (s.c.mn) s.c.mn[idx] = INT64_MAX;
+      if (s.c.mx) s.c.mx[idx] = INT64_MIN;
+      if (s.c.cnt) s.c.cnt[idx] = 0;
+      if (s.first) s.c.first[idx] = INT64_MAX; else s.c.present[idx] = 0;
+    }
+  }
+}
+
+__global__ void k_free_and_mark(Spec s, const WmPlan* plan, int64_t wm) {
+  // runs after k_purge (stream order): free slots, then record the watermark's position in the log
+  for (int32_t q = threadIdx.x; q < plan->n_purge; q += blockDim.x) s.slice_tag[plan->purge_slots[q]] = FREE_TAG;
+  if (threadIdx.x == 0) {
+    unsigned long long mc = *s.o.mark_count;
+    if ((int64_t)mc < s.o.mark_capacity) {
+      unsigned long long cnt = *s.o.count;
+      s.o.mark_wm[mc] = wm;
+      s.o.mark_pos[mc] = (int64_t)(cnt < (unsigned long long)s.o.capacity ? cnt : (unsigned long long)s.o.capacity);
+      *s.o.mark_count = mc + 1;
+    } else {
+      set_error(s.err, FW_ERR_CAPACITY);
+    }
+  }
+}
+
+__global__ void k_mark_only(Spec s, int64_t wm) {
+  unsigned long long mc = *s.o.mark_count;
+  if ((int64_t)mc < s.o.mark_capacity) {
+    unsigned long long cnt = *s.o.count;
+    s.o.mark_wm[mc] = wm;
+    s.o.mark_pos[mc] = (int64_t)(cnt < (unsigned long long)s.o.capacity ? cnt : (unsigned long long)s.o.capacity);
+    *s.o.mark_count = mc + 1;
+  } else {
+    set_error(s.err, FW_ERR_CAPACITY);
+  }
+}
+
+// fill helpers
+__global__ void k_fill_i64(int64_t* p, int64_t v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// keyBy routing (multi-GPU exchange): stable counting sort of records by operator index
+// KeyGroupStreamPartitioner.selectChannels (SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65)
+// ------------------------------------------------------------------------------------------------
+constexpr int PART_MAX = 64;
+constexpr int PART_CHUNK = 4096;   // records per block (contiguous)
+
+__device__ __forceinline__ int32_t route(const int64_t* key, const int32_t* kh, int64_t i, int32_t mp, int32_t par) {
+  int32_t h = kh ? kh[i] : long_hash_code(key[i]);
+  return operator_index_for_key_group(mp, par, key_group_for_hash(h, mp));
+}
+
+__global__ __launch_bounds__(BLOCK) void k_part_count(const int64_t* key, const int32_t* kh, int64_t n, int32_t mp,
+                                                      int32_t par, int64_t* block_counts) {
+  __shared__ int64_t cnt[PART_MAX];
+  for (int d = threadIdx.x; d < par; d += blockDim.x) cnt[d] = 0;
+  __syncthreads();
+  int64_t lo = (int64_t)blockIdx.x * PART_CHUNK, hi = lo + PART_CHUNK < n ? lo + PART_CHUNK : n;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd((unsigned long long*)&cnt[route(key, kh, i, mp, par)], 1ull);
+  __syncthreads();
+  for (int d = threadIdx.x; d < par; d += blockDim.x) block_counts[(int64_t)blockIdx.x * par + d] = cnt[d];
+}
+
+// single block: exclusive scan over (dest, block) -> per-block write offsets; totals
+__global__ void k_part_scan(int64_t* block_counts, int64_t nblocks, int32_t par, int64_t* counts, int64_t* offsets) {
+  if (threadIdx.x != 0) return;
+  int64_t run = 0;
+  for (int32_t d = 0; d < par; ++d) {
+    offsets[d] = run;
+    int64_t tot = 0;
+    for (int64_t b = 0; b < nblocks; ++b) {
+      int64_t c = block_counts[b * par + d];
+      block_counts[b * par + d] = run;
+      run += c;
+      tot += c;
+    }
+    counts[d] = tot;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, const int32_t* kh, const int64_t* f1,
+                                                        const int64_t* ts, const int64_t* val, int64_t n, int32_t mp,
+                                                        int32_t par, const int64_t* block_offsets, int64_t* okey,
+                                                        int32_t* okh, int64_t* of1, int64_t* ots, int64_t* oval) {
+  __shared__ int64_t base[PART_MAX];
+  __shared__ int32_t wave_cnt[BLOCK / 64][PART_MAX];
+  for (int d = threadIdx.x; d < par; d += blockDim.x) base[d] = block_offsets[(int64_t)blockIdx.x * par + d];
+  __syncthreads();
+  int64_t lo = (int64_t)blockIdx.x * PART_CHUNK, hi = lo + PART_CHUNK < n ? lo + PART_CHUNK : n;
+  const int wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+  for (int64_t c0 = lo; c0 < hi; c0 += blockDim.x) {
+    int64_t i = c0 + threadIdx.x;
+    bool act = i < hi;
+    int32_t dst = act ? route(key, kh, i, mp, par) : -1;
+    int32_t rank = 0;
+    for (int d = 0; d < par; ++d) {
+      uint64_t m = __ballot(dst == d);
+      if (dst == d) rank = __popcll(m & lanemask_lt());
+      if (lane == 0) wave_cnt[wave][d] = __popcll(m);
+    }
+    __syncthreads();
+    if (act) {
+      int64_t pos = base[dst] + rank;
+      for (int w = 0; w < wave; ++w) pos += wave_cnt[w][dst];
+      okey[pos] = key[i];
+      if (okh) okh[pos] = kh ? kh[i] : long_hash_code(key[i]);
+      if (of1) of1[pos] = f1 ? f1[i] : ts[i];
+      ots[pos] = ts[i];
+      oval[pos] = val[i];
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < par; d += blockDim.x) {
+      int32_t tot = 0;
+      for (int w = 0; w < BLOCK / 64; ++w) tot += wave_cnt[w][d];
+      base[d] += tot;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace fw
+
+// ==================================================================================================
+// host side
+// ==================================================================================================
+using namespace fw;
+
+namespace {
+
+int64_t gcd64(int64_t a, int64_t b) { while (b) { int64_t t = a % b; a = b; b = t; } return a; }
+int64_t next_pow2(int64_t x) { int64_t p = 1; while (p < x) p <<= 1; return p; }
+int bits_for(uint64_t x) { int b = 0; while (b < 64 && (x >> b) != 0) ++b; return b; }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct fw_engine {
+  fw_config cfg{};
+  std::string err;
+  int32_t sticky = FW_OK;
+  hipStream_t stream = nullptr;
+  Spec s{};
+  int64_t cur_wm = INT64_MIN;
+  int64_t ordinal = 0;
+  int64_t records_in = 0;
+  int grid = 0;
+  std::vector<void*> allocs;
+  // staging for host-memory pushes
+  int64_t *st_key = nullptr, *st_ts = nullptr, *st_val = nullptr, *st_f1 = nullptr;
+  int32_t* st_hash = nullptr;
+  // late path
+  unsigned long long *late_key = nullptr, *late_key_sorted = nullptr, *late_count = nullptr, *seg = nullptr;
+  unsigned long long *late_idx_in = nullptr, *late_idx_out = nullptr;
+  LateAcc *late_acc = nullptr, *late_scan = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  int32_t idx_bits = 0;
+  int64_t late_fires_host = 0;
+  // device-time accounting (fw_set_profiling)
+  bool profiling = false;
+  struct Timed { int phase; hipEvent_t a, b; int64_t records; };
+  std::vector<Timed> timed;
+  std::vector<hipEvent_t> event_pool;
+  double prof_ms[FW_NPHASES] = {0, 0, 0, 0};
+  int64_t prof_launches[FW_NPHASES] = {0, 0, 0, 0};
+  int64_t prof_records[FW_NPHASES] = {0, 0, 0, 0};
+  hipEvent_t take_event() {
+    hipEvent_t ev = nullptr;
+    if (!event_pool.empty()) { ev = event_pool.back(); event_pool.pop_back(); }
+    else (void)hipEventCreate(&ev);
+    return ev;
+  }
+  int open_phase = -1;
+  hipEvent_t open_ev = nullptr;
+  void phase_begin(int ph) {
+    if (!profiling) return;
+    open_phase = ph;
+    open_ev = take_event();
+    (void)hipEventRecord(open_ev, stream);
+  }
+  void phase_end(int64_t records) {
+    if (!profiling || open_phase < 0) return;
+    hipEvent_t b = take_event();
+    (void)hipEventRecord(b, stream);
+    timed.push_back({open_phase, open_ev, b, records});
+    open_phase = -1;
+  }
+  // watermark plan
+  FireTask* tasks = nullptr;
+  int32_t max_tasks = 0;
+  WmPlan* plan = nullptr;
+  // partition scratch
+  int64_t* part_block_counts = nullptr;
+  int64_t part_blocks_cap = 0;
+  // host output copies
+  std::vector<int64_t> h_key, h_f1, h_ts, h_sum, h_mn, h_mx, h_cnt, h_mark_wm, h_mark_pos;
+  std::vector<double> h_sum_d, h_mn_d, h_mx_d;
+  int dev = 0;
+
+  template <class T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(T) > 0 ? n * sizeof(T) : 1) != hipSuccess) return nullptr;
+    allocs.push_back(p);
+    return (T*)p;
+  }
+  ~fw_engine() {
+    if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
+    for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+    for (auto ev : event_pool) (void)hipEventDestroy(ev);
+    for (void* p : allocs) (void)hipFree(p);
+  }
+};
+
+static thread_local std::string g_create_error;
+
+static int fail(fw_engine* e, int code, const std::string& msg) {
+  if (e) { e->err = msg; if (e->sticky == FW_OK) e->sticky = code; }
+  return code;
+}
+#define HIPCHK(e, x) do { hipError_t _r = (x); if (_r != hipSuccess) \
+  return fail(e, FW_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_r)); } while (0)
+
+static int launch_fill(fw_engine* e, int64_t* p, int64_t v, int64_t n) {
+  if (!p || n <= 0) return FW_OK;
+  int blocks = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, 4096);
+  hipLaunchKernelGGL(k_fill_i64, dim3(blocks), dim3(BLOCK), 0, e->stream, p, v, n);
+  return FW_OK;
+}
+
+template <int VT, int AGG, bool FIRST>
+static void launch_ingest_t(fw_engine* e, const BatchIn& b) {
+  int blocks = (int)std::min<int64_t>((b.n + BLOCK - 1) / BLOCK, e->grid);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((k_ingest_direct<VT, AGG, FIRST>), dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b);
+}
+template <int VT, int AGG, bool FIRST>
+static void launch_fire_t(fw_engine* e) {
+  int blocks = (int)std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid);
+  hipLaunchKernelGGL((k_fire<VT, AGG, FIRST>), dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->tasks, e->plan);
+}
+
+// dispatch over (value type, aggregate mask, first-arrival) — the instantiated reduce shapes
+#define FW_DISPATCH(FN, e, ...)                                                                  \
+  do {                                                                                           \
+    const Spec& _s = (e)->s;                                                                     \
+    const bool _f = _s.first != 0;                                                               \
+    if (_s.vt == FW_VALUE_I64) {                                                                 \
+      switch (_s.agg) {                                                                          \
+        case 1: if (_f) FN<0, 1, true>(e, ##__VA_ARGS__); else FN<0, 1, false>(e, ##__VA_ARGS__); break;   \
+        case 15: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
+        default: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
+      }                                                                                          \
+    } else {                                                                                     \
+      switch (_s.agg) {                                                                          \
+        case 1: if (_f) FN<1, 1, true>(e, ##__VA_ARGS__); else FN<1, 1, false>(e, ##__VA_ARGS__); break;   \
+        default: if (_f) FN<1, 15, true>(e, ##__VA_ARGS__); else FN<1, 15, false>(e, ##__VA_ARGS__); break; \
+      }                                                                                          \
+    }                                                                                            \
+  } while (0)
+
+extern "C" {
+
+const char* fw_version(void) { return "flink_amd fw 0.1 (gfx950)"; }
+
+int fw_create(const fw_config* cfg_in, fw_engine** out) {
+  if (!cfg_in || !out) return FW_ERR_INVALID_ARG;
+  *out = nullptr;
+  fw_config c = *cfg_in;
+  auto* e = new fw_engine();
+  e->cfg = c;
+  auto bad = [&](const char* m) { g_create_error = m; delete e; return FW_ERR_INVALID_ARG; };
+  auto unsupported = [&](const char* m) { g_create_error = m; delete e; return FW_ERR_UNSUPPORTED; };
+  if (c.size <= 0) return bad("window size must be > 0");
+  if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING) return bad("unknown assigner");
+  if (c.assigner == FW_SLIDING && c.slide <= 0) return bad("slide must be > 0");
+  if (c.allowed_lateness < 0) return bad("allowed lateness must be >= 0");
+  if (c.max_parallelism <= 0 || c.max_parallelism > (1 << 15) || c.kg_start < 0 || c.kg_end < c.kg_start ||
+      c.kg_end >= c.max_parallelism)
+    return bad("bad key-group range");
+  if (c.value_type != FW_VALUE_I64 && c.value_type != FW_VALUE_F64) return bad("bad value type");
+  if ((c.agg_mask & ~15) != 0 || c.agg_mask == 0) return bad("bad aggregate mask");
+  if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
+  if (c.assigner == FW_SLIDING && (c.allowed_lateness > 0 || c.trigger != FW_TRIGGER_EVENT_TIME))
+    return unsupported("sliding windows with allowed lateness or PurgingTrigger are not implemented on the slice path");
+  HIPCHK(e, hipSetDevice(c.device));
+  e->dev = c.device;
+  HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  hipDeviceProp_t prop;
+  HIPCHK(e, hipGetDeviceProperties(&prop, c.device));
+  e->grid = prop.multiProcessorCount * 8;
+
+  Spec& s = e->s;
+  s.assigner = c.assigner;
+  s.trigger = c.trigger;
+  s.size = c.size;
+  s.slide = c.assigner == FW_TUMBLING ? c.size : c.slide;
+  s.offset = c.offset;
+  s.lateness = c.allowed_lateness;
+  s.g = c.assigner == FW_TUMBLING ? c.size : gcd64(c.size, s.slide);
+  s.K = (int32_t)(c.size / s.g);
+  s.R = (int32_t)(s.slide / s.g);
+  if (s.K > MAX_K) return unsupported("more than 64 slices per window (size / gcd(size, slide))");
+  s.mp = c.max_parallelism;
+  s.kg_start = c.kg_start;
+  s.kg_end = c.kg_end;
+  s.vt = c.value_type;
+  s.agg = c.agg_mask == FW_AGG_SUM ? FW_AGG_SUM : 15;   // instantiated reduce shapes
+  s.first = c.keep_first_f1 ? 1 : 0;
+
+  s.D = next_pow2(std::max<int64_t>(2 * c.key_capacity, 64));
+  s.dir_mask = (uint64_t)s.D - 1;
+  s.stride = s.D + 1;
+  int32_t P = c.max_open_slices;
+  if (P <= 0) {
+    int64_t late_slices = (c.allowed_lateness + s.g - 1) / s.g;
+    P = (int32_t)std::min<int64_t>(2 * s.K + late_slices + 8, 1024);
+  }
+  if (P > 1024) P = 1024;
+  s.P = P;
+
+  s.dir_keys = e->alloc<int64_t>((size_t)s.D);
+  s.dir_min_used = e->alloc<int32_t>(1);
+  s.slice_tag = e->alloc<int64_t>((size_t)P);
+  s.touched = e->alloc<int32_t>((size_t)P);
+  const size_t cells = (size_t)P * (size_t)s.stride;
+  s.c.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>(cells) : nullptr;
+  s.c.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(cells) : nullptr;
+  s.c.mx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>(cells) : nullptr;
+  s.c.cnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>(cells) : nullptr;
+  if (s.first) {
+    s.c.first = e->alloc<int64_t>(cells);
+    s.c.f1v = e->alloc<int64_t>(cells);
+    s.c.present = nullptr;
+  } else {
+    s.c.first = nullptr;
+    s.c.f1v = nullptr;
+    s.c.present = e->alloc<uint8_t>(cells);
+  }
+  OutLog& o = s.o;
+  o.capacity = c.out_capacity;
+  o.key = e->alloc<int64_t>((size_t)o.capacity);
+  o.f1 = s.first ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.ts = e->alloc<int64_t>((size_t)o.capacity);
+  o.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.mx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.cnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.count = e->alloc<unsigned long long>(1);
+  o.mark_capacity = 1 << 16;
+  o.mark_wm = e->alloc<int64_t>((size_t)o.mark_capacity);
+  o.mark_pos = e->alloc<int64_t>((size_t)o.mark_capacity);
+  o.mark_count = e->alloc<unsigned long long>(1);
+  s.err = e->alloc<int32_t>(1);
+  s.stats = e->alloc<unsigned long long>(ST_NSTATS);
+
+  e->st_key = e->alloc<int64_t>((size_t)c.max_batch);
+  e->st_ts = e->alloc<int64_t>((size_t)c.max_batch);
+  e->st_val = e->alloc<int64_t>((size_t)c.max_batch);
+  e->st_f1 = e->alloc<int64_t>((size_t)c.max_batch);
+  e->st_hash = e->alloc<int32_t>((size_t)c.max_batch);
+
+  e->max_tasks = std::max(64, 4 * P);
+  e->tasks = e->alloc<FireTask>((size_t)e->max_tasks);
+  e->plan = e->alloc<WmPlan>(1);
+
+  for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
+
+  // late path (allowed lateness > 0)
+  if (c.allowed_lateness > 0) {
+    e->idx_bits = bits_for((uint64_t)c.max_batch);
+    int pane_bits = bits_for((uint64_t)P * (uint64_t)s.stride);
+    if (e->idx_bits + pane_bits > 64) { delete e; return FW_ERR_UNSUPPORTED; }
+    size_t nb = (size_t)c.max_batch;
+    e->late_key = e->alloc<unsigned long long>(nb);
+    e->late_key_sorted = e->alloc<unsigned long long>(nb);
+    e->late_count = e->alloc<unsigned long long>(1);
+    e->seg = e->alloc<unsigned long long>(nb);
+    e->late_acc = e->alloc<LateAcc>(nb);
+    e->late_scan = e->alloc<LateAcc>(nb);
+    size_t t1 = 0, t2 = 0;
+    (void)rocprim::radix_sort_keys(nullptr, t1, e->late_key, e->late_key_sorted, (size_t)c.max_batch, 0, 64, e->stream);
+    (void)rocprim::deterministic_inclusive_scan_by_key(nullptr, t2, e->seg, e->late_acc, e->late_scan, (size_t)c.max_batch,
+                                                 LateCombine(), rocprim::equal_to<unsigned long long>(), e->stream);
+    e->temp_bytes = std::max(t1, t2);
+    e->temp = e->alloc<char>(e->temp_bytes);
+    for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
+  } else {
+    e->late_count = e->alloc<unsigned long long>(1);
+  }
+
+  // initial state
+  launch_fill(e, s.dir_keys, EMPTY_KEY, s.D);
+  launch_fill(e, s.slice_tag, FREE_TAG, P);
+  launch_fill(e, s.c.sum, 0, (int64_t)cells);
+  launch_fill(e, s.c.mn, INT64_MAX, (int64_t)cells);
+  launch_fill(e, s.c.mx, INT64_MIN, (int64_t)cells);
+  launch_fill(e, s.c.cnt, 0, (int64_t)cells);
+  launch_fill(e, s.c.first, INT64_MAX, (int64_t)cells);
+  if (s.c.present) HIPCHK(e, hipMemsetAsync(s.c.present, 0, cells, e->stream));
+  HIPCHK(e, hipMemsetAsync(s.dir_min_used, 0, 4, e->stream));
+  HIPCHK(e, hipMemsetAsync(s.touched, 0, 4 * (size_t)P, e->stream));
+  HIPCHK(e, hipMemsetAsync(o.count, 0, 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(o.mark_count, 0, 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(s.err, 0, 4, e->stream));
+  HIPCHK(e, hipMemsetAsync(s.stats, 0, 8 * ST_NSTATS, e->stream));
+  HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, hipGetLastError());
+  *out = e;
+  return FW_OK;
+}
+
+static int check_device_error(fw_engine* e) {
+  int32_t derr = 0;
+  HIPCHK(e, hipMemcpyAsync(&derr, e->s.err, 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (derr != 0 && e->sticky == FW_OK) {
+    const char* msg = "device error";
+    switch (derr) {
+      case FW_ERR_NO_TIMESTAMP:
+        msg = "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time characteristic set to "
+              "'ProcessingTime', or did you forget to call 'DataStream.assignTimestampsAndWatermarks(...)'?";
+        break;
+      case FW_ERR_KEY_GROUP: msg = "Unexpected key group index. This indicates a bug."; break;
+      case FW_ERR_CAPACITY: msg = "capacity exceeded (key directory, slice pool, per-element fire list or output log)"; break;
+      case FW_ERR_UNSUPPORTED: msg = "sliding-window timestamp below offset - slide: not supported by the slice path"; break;
+    }
+    return fail(e, derr, msg);
+  }
+  return e->sticky;
+}
+
+int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1, const int64_t* ts,
+                  const void* value, int64_t n, int32_t mem) {
+  if (!e) return FW_ERR_INVALID_ARG;
+  if (e->sticky) return e->sticky;
+  if (n < 0 || (n > 0 && (!key || !ts || !value))) return fail(e, FW_ERR_INVALID_ARG, "null column");
+  if (n > e->cfg.max_batch) return fail(e, FW_ERR_CAPACITY, "batch larger than max_batch");
+  if (n == 0) return FW_OK;
+  HIPCHK(e, hipSetDevice(e->dev));
+  const int64_t *dk = key, *dts = ts, *dv = (const int64_t*)value, *df1 = f1;
+  const int32_t* dh = key_hash;
+  if (mem == FW_MEM_HOST) {
+    HIPCHK(e, hipMemcpyAsync(e->st_key, key, 8 * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->st_ts, ts, 8 * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->st_val, value, 8 * n, hipMemcpyHostToDevice, e->stream));
+    dk = e->st_key; dts = e->st_ts; dv = e->st_val;
+    if (key_hash) { HIPCHK(e, hipMemcpyAsync(e->st_hash, key_hash, 4 * n, hipMemcpyHostToDevice, e->stream)); dh = e->st_hash; }
+    if (f1) { HIPCHK(e, hipMemcpyAsync(e->st_f1, f1, 8 * n, hipMemcpyHostToDevice, e->stream)); df1 = e->st_f1; }
+  }
+  if (!df1) df1 = dts;
+  BatchIn b;
+  b.key = dk; b.key_hash = dh; b.ts = dts; b.val = dv; b.n = n;
+  b.ord_base = e->ordinal;
+  b.wm = e->cur_wm;
+  b.late_key = e->late_key;
+  b.late_count = e->late_count;
+  b.late_capacity = e->late_key ? e->cfg.max_batch : 0;
+  b.idx_bits = e->idx_bits;
+  e->phase_begin(FW_PHASE_INGEST);
+  FW_DISPATCH(launch_ingest_t, e, b);
+  e->phase_end(n);
+  HIPCHK(e, hipGetLastError());
+  if (e->s.first) {
+    e->phase_begin(FW_PHASE_FIXUP);
+    hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
+                       e->stream, e->s, df1, e->ordinal, n);
+    e->phase_end(e->s.stride);
+  }
+  HIPCHK(e, hipMemsetAsync(e->s.touched, 0, 4 * (size_t)e->s.P, e->stream));
+  if (e->cfg.allowed_lateness > 0) {
+    // per-element fires: need the count on the host to size the sort
+    unsigned long long nl = 0;
+    HIPCHK(e, hipMemcpyAsync(&nl, e->late_count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (nl > (unsigned long long)e->cfg.max_batch) nl = e->cfg.max_batch;
+    if (nl > 0) {
+      e->phase_begin(FW_PHASE_LATE);
+      size_t tb = e->temp_bytes;
+      HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, e->late_key, e->late_key_sorted, (size_t)nl, 0, 64, e->stream));
+      int blocks = (int)((nl + BLOCK - 1) / BLOCK);
+      hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
+                         e->idx_bits, dv, e->seg, e->late_acc);
+      tb = e->temp_bytes;
+      HIPCHK(e, rocprim::deterministic_inclusive_scan_by_key(e->temp, tb, e->seg, e->late_acc, e->late_scan, (size_t)nl,
+                                                             LateCombine(), rocprim::equal_to<unsigned long long>(), e->stream));
+      hipLaunchKernelGGL(k_late_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
+                         e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, e->ordinal);
+      hipLaunchKernelGGL(k_late_commit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
+                         e->idx_bits, e->seg, e->late_scan, df1, e->ordinal);
+      e->phase_end((int64_t)nl);
+      e->late_fires_host += (int64_t)nl;
+      HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
+    }
+  }
+  HIPCHK(e, hipGetLastError());
+  e->ordinal += n;
+  e->records_in += n;
+  return FW_OK;
+}
+
+int fw_advance_watermark(fw_engine* e, int64_t wm) {
+  if (!e) return FW_ERR_INVALID_ARG;
+  if (e->sticky) return e->sticky;
+  HIPCHK(e, hipSetDevice(e->dev));
+  if (wm <= e->cur_wm) {
+    hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
+    HIPCHK(e, hipGetLastError());
+    return FW_OK;
+  }
+  e->phase_begin(FW_PHASE_FIRE);
+  hipLaunchKernelGGL(k_wm_plan, dim3(1), dim3(256), 0, e->stream, e->s, e->cur_wm, wm, e->tasks, e->max_tasks, e->plan);
+  FW_DISPATCH(launch_fire_t, e);
+  int blocks = (int)std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid);
+  hipLaunchKernelGGL(k_purge, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->plan);
+  hipLaunchKernelGGL(k_free_and_mark, dim3(1), dim3(256), 0, e->stream, e->s, e->plan, wm);
+  e->phase_end(e->s.stride);
+  HIPCHK(e, hipGetLastError());
+  e->cur_wm = wm;
+  return FW_OK;
+}
+
+int fw_sync(fw_engine* e) {
+  if (!e) return FW_ERR_INVALID_ARG;
+  HIPCHK(e, hipSetDevice(e->dev));
+  return check_device_error(e);
+}
+
+int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
+  if (!e || !o) return FW_ERR_INVALID_ARG;
+  HIPCHK(e, hipSetDevice(e->dev));
+  int rc = check_device_error(e);
+  if (rc) return rc;
+  unsigned long long cnt = 0, mc = 0;
+  HIPCHK(e, hipMemcpyAsync(&cnt, e->s.o.count, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(&mc, e->s.o.mark_count, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if ((int64_t)cnt > e->s.o.capacity) return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded");
+  const int64_t n = (int64_t)cnt;
+  std::memset(o, 0, sizeof(*o));
+  o->n = n;
+  o->n_marks = (int64_t)mc;
+  const OutLog& L = e->s.o;
+  const bool f64 = e->s.vt == FW_VALUE_F64;
+  if (mem == FW_MEM_DEVICE) {
+    o->key = L.key; o->f1 = L.f1; o->ts = L.ts;
+    if (f64) { o->sum_f64 = (const double*)L.sum; o->min_f64 = (const double*)L.mn; o->max_f64 = (const double*)L.mx; }
+    else { o->sum_i64 = L.sum; o->min_i64 = L.mn; o->max_i64 = L.mx; }
+    o->count = L.cnt;
+    o->mark_wm = L.mark_wm; o->mark_pos = L.mark_pos;
+  } else {
+    auto cp = [&](std::vector<int64_t>& h, const int64_t* d, int64_t cnt_) -> const int64_t* {
+      if (!d) return nullptr;
+      h.resize((size_t)std::max<int64_t>(cnt_, 1));
+      if (cnt_ > 0) (void)hipMemcpyAsync(h.data(), d, 8 * cnt_, hipMemcpyDeviceToHost, e->stream);
+      return h.data();
+    };
+    o->key = cp(e->h_key, L.key, n);
+    o->f1 = cp(e->h_f1, L.f1, n);
+    o->ts = cp(e->h_ts, L.ts, n);
+    const int64_t* su = cp(e->h_sum, L.sum, n);
+    const int64_t* mn = cp(e->h_mn, L.mn, n);
+    const int64_t* mx = cp(e->h_mx, L.mx, n);
+    o->count = cp(e->h_cnt, L.cnt, n);
+    if (f64) { o->sum_f64 = (const double*)su; o->min_f64 = (const double*)mn; o->max_f64 = (const double*)mx; }
+    else { o->sum_i64 = su; o->min_i64 = mn; o->max_i64 = mx; }
+    o->mark_wm = cp(e->h_mark_wm, L.mark_wm, (int64_t)mc);
+    o->mark_pos = cp(e->h_mark_pos, L.mark_pos, (int64_t)mc);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  // only the fields the reduce function asked for
+  const int32_t um = e->cfg.agg_mask;
+  if (!(um & FW_AGG_SUM)) { o->sum_i64 = nullptr; o->sum_f64 = nullptr; }
+  if (!(um & FW_AGG_MIN)) { o->min_i64 = nullptr; o->min_f64 = nullptr; }
+  if (!(um & FW_AGG_MAX)) { o->max_i64 = nullptr; o->max_f64 = nullptr; }
+  if (!(um & FW_AGG_COUNT)) o->count = nullptr;
+  // the log restarts; device pointers handed out above stay valid until the next enqueue
+  HIPCHK(e, hipMemsetAsync(L.count, 0, 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(L.mark_count, 0, 8, e->stream));
+  if (mem == FW_MEM_HOST) HIPCHK(e, hipStreamSynchronize(e->stream));
+  return FW_OK;
+}
+
+int fw_get_stats(fw_engine* e, fw_stats* st) {
+  if (!e || !st) return FW_ERR_INVALID_ARG;
+  HIPCHK(e, hipSetDevice(e->dev));
+  unsigned long long d[ST_NSTATS];
+  HIPCHK(e, hipMemcpyAsync(d, e->s.stats, sizeof(d), hipMemcpyDeviceToHost, e->stream));
+  std::vector<int64_t> tags((size_t)e->s.P);
+  HIPCHK(e, hipMemcpyAsync(tags.data(), e->s.slice_tag, 8 * (size_t)e->s.P, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  std::memset(st, 0, sizeof(*st));
+  st->records_in = e->records_in;
+  st->records_late = (int64_t)d[ST_LATE];
+  st->panes_fired = (int64_t)d[ST_FIRED] + e->late_fires_host;
+  st->late_fires = e->late_fires_host;
+  int64_t live = 0;
+  for (int64_t t : tags) live += t != FREE_TAG;
+  st->slices_live = live;
+  st->keys_resident = -1;
+  return FW_OK;
+}
+
+int fw_set_profiling(fw_engine* e, int32_t enable) {
+  if (!e) return FW_ERR_INVALID_ARG;
+  e->profiling = enable != 0;
+  return FW_OK;
+}
+
+int fw_get_profile(fw_engine* e, fw_profile* out) {
+  if (!e || !out) return FW_ERR_INVALID_ARG;
+  HIPCHK(e, hipSetDevice(e->dev));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (auto& t : e->timed) {
+    float ms = 0.f;
+    HIPCHK(e, hipEventElapsedTime(&ms, t.a, t.b));
+    e->prof_ms[t.phase] += ms;
+    e->prof_launches[t.phase] += 1;
+    e->prof_records[t.phase] += t.records;
+    e->event_pool.push_back(t.a);
+    e->event_pool.push_back(t.b);
+  }
+  e->timed.clear();
+  for (int i = 0; i < FW_NPHASES; ++i) {
+    out->ms[i] = e->prof_ms[i];
+    out->launches[i] = e->prof_launches[i];
+    out->records[i] = e->prof_records[i];
+    e->prof_ms[i] = 0; e->prof_launches[i] = 0; e->prof_records[i] = 0;
+  }
+  return FW_OK;
+}
+
+const char* fw_last_error(const fw_engine* e) { return e ? e->err.c_str() : g_create_error.c_str(); }
+
+void fw_destroy(fw_engine* e) { delete e; }
+
+int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,
+                             const int64_t* ts, const void* value, int64_t n, int32_t max_parallelism,
+                             int32_t parallelism, int64_t* out_key, int32_t* out_key_hash, int64_t* out_f1,
+                             int64_t* out_ts, void* out_value, int64_t* counts, int64_t* offsets) {
+  if (!e) return FW_ERR_INVALID_ARG;
+  if (parallelism <= 0 || parallelism > PART_MAX || max_parallelism < parallelism) return fail(e, FW_ERR_INVALID_ARG, "bad parallelism");
+  HIPCHK(e, hipSetDevice(e->dev));
+  int64_t nblocks = std::max<int64_t>((n + PART_CHUNK - 1) / PART_CHUNK, 1);
+  if (nblocks * parallelism > e->part_blocks_cap) {
+    e->part_block_counts = e->alloc<int64_t>((size_t)(nblocks * parallelism));
+    if (!e->part_block_counts) return fail(e, FW_ERR_DEVICE, "alloc");
+    e->part_blocks_cap = nblocks * parallelism;
+  }
+  hipLaunchKernelGGL(k_part_count, dim3((unsigned)nblocks), dim3(BLOCK), 0, e->stream, key, key_hash, n, max_parallelism,
+                     parallelism, e->part_block_counts);
+  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, e->stream, e->part_block_counts, nblocks, parallelism, counts, offsets);
+  hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblocks), dim3(BLOCK), 0, e->stream, key, key_hash, f1, ts,
+                     (const int64_t*)value, n, max_parallelism, parallelism, e->part_block_counts, out_key, out_key_hash,
+                     out_f1, out_ts, (int64_t*)out_value);
+  HIPCHK(e, hipGetLastError());
+  return FW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+"""keyBy exchange across the GPUs of one node: one process per GPU = one operator subtask.
+
+Mirrors the reference's hash edge between source and window operator:
+  routing   KeyGroupStreamPartitioner.selectChannels        SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65
+            -> KeyGroupRangeAssignment.assignKeyToParallelOperator (kg * p / mp)  KeyGroupRangeAssignment.java:40-42,105-107
+  transport RecordWriter.emit over local/remote channels    flink-runtime/.../io/network/api/writer/RecordWriter.java:82-85
+  watermark RecordWriterOutput.emitWatermark -> broadcastEmit (RecordWriterOutput.java:80-84, RecordWriter.java:92-95),
+            receiver takes the min over channels             SJ/runtime/io/StreamInputProcessor.java:147-161
+MI355X form: the HIP partition kernel (fw_partition_by_operator) counting-sorts a batch by destination
+in HBM; one all-to-all of per-destination counts, one all-to-all of the packed (key, ts, value)
+records over xGMI (RCCL: torch.distributed backend "nccl"), one MIN all-reduce of the watermark.
+The same class runs on CPU tensors with the gloo backend for the multi-process tests; there the
+routing is the numpy restatement in flink_amd.keygroups (the GPU path always uses the HIP kernel).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .keygroups import operator_index_np
+
+
+class KeyByExchange:
+    def __init__(self, engine, world, rank, max_parallelism, batch, device):
+        self.eng = engine
+        self.world, self.rank, self.mp = world, rank, max_parallelism
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        if self.cuda:
+            z = lambda dt=torch.int64: torch.empty(batch, dtype=dt, device=self.device)
+            self.s_key, self.s_ts, self.s_val, self.s_f1 = z(), z(), z(), z()
+            self.s_hash = z(torch.int32)
+            self.counts = torch.zeros(world, dtype=torch.int64, device=self.device)
+            self.offsets = torch.zeros(world, dtype=torch.int64, device=self.device)
+
+    def _route_cuda(self, k, t, v):
+        n = k.numel()
+        P = lambda x: ctypes.c_void_p(x.data_ptr())
+        rc = self.eng.lib.fw_partition_by_operator(self.eng.h, P(k), None, None, P(t), P(v), n, self.mp, self.world,
+                                                   P(self.s_key), None, None, P(self.s_ts), P(self.s_val),
+                                                   P(self.counts), P(self.offsets))
+        if rc != 0:
+            raise RuntimeError(f"fw_partition_by_operator failed: {rc}")
+        self.eng.sync()                       # partition runs on the engine's stream
+        return self.s_key[:n], self.s_ts[:n], self.s_val[:n], self.counts
+
+    def _route_host(self, k, t, v):
+        dest = operator_index_np(k.numpy(), self.mp, self.world)
+        order = np.argsort(dest, kind="stable")
+        counts = torch.from_numpy(np.bincount(dest, minlength=self.world).astype(np.int64))
+        idx = torch.from_numpy(order)
+        return k[idx], t[idx], v[idx], counts
+
+    def exchange(self, k, t, v):
+        """Route a source batch to the key-group owners; returns this rank's received (key, ts, value)."""
+        sk, st, sv, counts = self._route_cuda(k, t, v) if self.cuda else self._route_host(k, t, v)
+        recv_counts = torch.empty_like(counts)
+        dist.all_to_all_single(recv_counts, counts)
+        send_splits = counts.tolist()
+        recv_splits = recv_counts.tolist()
+        packed = torch.stack([sk, st, sv.view(torch.int64)], dim=1)
+        out = torch.empty((sum(recv_splits), 3), dtype=torch.int64, device=packed.device)
+        dist.all_to_all_single(out, packed, recv_splits, send_splits)
+        return out[:, 0].contiguous(), out[:, 1].contiguous(), out[:, 2].contiguous().view(v.dtype)
+
+    def align_watermark(self, wm_local):
+        """Min over all input channels (StreamInputProcessor.java:147-161)."""
+        x = torch.tensor([wm_local], dtype=torch.int64, device=self.device)
+        dist.all_reduce(x, op=dist.ReduceOp.MIN)
+        return int(x.item())
+
+    def step(self, k, t, v, wm_local):
+        rk, rt, rv = self.exchange(k, t, v)
+        if rk.numel():
+            self.eng.push(rk, rt, rv)
+        self.eng.advance_watermark(self.align_watermark(wm_local))

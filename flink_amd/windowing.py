@@ -1,0 +1,352 @@
+"""Host mirror of the reference's event-time window operator surface, driving the HIP engine.
+
+Names and behaviour follow the reference (paths relative to the reference root,
+SJ = flink-streaming-java/src/main/java/org/apache/flink/streaming/):
+  TumblingEventTimeWindows.of(size[, offset])   SJ/api/windowing/assigners/TumblingEventTimeWindows.java:92-116
+  SlidingEventTimeWindows.of(size, slide[, off]) SJ/api/windowing/assigners/SlidingEventTimeWindows.java:107-133
+  EventTimeTrigger.create()                      SJ/api/windowing/triggers/EventTimeTrigger.java
+  PurgingTrigger.of(trigger)                     SJ/api/windowing/triggers/PurgingTrigger.java
+  WindowOperator.processElement/processWatermark SJ/runtime/operators/windowing/WindowOperator.java:222-375
+  StreamRecord / Watermark                       SJ/runtime/streamrecord/StreamRecord.java, SJ/api/watermark/Watermark.java
+
+The Java operator hands the engine one batch per watermark epoch (all records between two
+watermarks see the same current watermark, StreamInputProcessor.java:147-177), so batching
+records until the next watermark is exactly equivalent to per-record processing.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from .keygroups import DEFAULT_MAX_PARALLELISM
+
+LONG_MIN = -(1 << 63)
+LONG_MAX = (1 << 63) - 1
+
+
+def _java_rem(a, b):
+    """Java `%` on longs (truncating toward zero)."""
+    r = abs(a) % abs(b)
+    return -r if a < 0 else r
+
+
+def java_string_hash(s):
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+# ------------------------------------------------------------------ assigners / triggers
+class TumblingEventTimeWindows:
+    def __init__(self, size, offset):
+        self.size, self.offset, self.slide = size, offset, size
+
+    @staticmethod
+    def of(size, offset=None):
+        if offset is None:
+            return TumblingEventTimeWindows(size, 0)
+        return TumblingEventTimeWindows(size, _java_rem(offset, size))
+
+    kind = _abi.FW_TUMBLING
+
+
+class SlidingEventTimeWindows:
+    def __init__(self, size, slide, offset):
+        self.size, self.slide, self.offset = size, slide, offset
+
+    @staticmethod
+    def of(size, slide, offset=None):
+        if offset is None:
+            return SlidingEventTimeWindows(size, slide, 0)
+        return SlidingEventTimeWindows(size, slide, _java_rem(offset, slide))
+
+    kind = _abi.FW_SLIDING
+
+
+class EventTimeTrigger:
+    code = _abi.FW_TRIGGER_EVENT_TIME
+
+    @staticmethod
+    def create():
+        return EventTimeTrigger()
+
+
+class PurgingTrigger:
+    code = _abi.FW_TRIGGER_PURGING_EVENT_TIME
+
+    def __init__(self, nested):
+        if not isinstance(nested, EventTimeTrigger):
+            raise NotImplementedError("only PurgingTrigger.of(EventTimeTrigger.create()) is on the GPU path")
+        self.nested = nested
+
+    @staticmethod
+    def of(nested):
+        return PurgingTrigger(nested)
+
+
+class ReduceFunction:
+    """The reduce functions the engine implements, as (record -> accumulator) field sets.
+
+    A record is (key, f1, value).  reduce(value1 = stored, value2 = new) returns value1 with
+    sum = v1 + v2, min = Math.min, max = Math.max, count = c1 + c2; f1 stays value1's (first arrival).
+    `SumReducer()` is WindowOperatorTest.SumReducer (WindowOperatorTest.java:2245-2252).
+    """
+    FIELDS = {"sum": _abi.FW_AGG_SUM, "min": _abi.FW_AGG_MIN, "max": _abi.FW_AGG_MAX, "count": _abi.FW_AGG_COUNT}
+
+    def __init__(self, fields=("sum",), value_type="i64", keep_first_f1=False):
+        self.fields = tuple(fields)
+        self.mask = 0
+        for f in self.fields:
+            self.mask |= self.FIELDS[f]
+        self.value_type = value_type
+        self.keep_first_f1 = keep_first_f1
+
+    @property
+    def vt(self):
+        return _abi.FW_VALUE_I64 if self.value_type == "i64" else _abi.FW_VALUE_F64
+
+
+def SumReducer(value_type="i64"):
+    return ReduceFunction(("sum",), value_type)
+
+
+# ------------------------------------------------------------------ stream elements
+class StreamRecord:
+    __slots__ = ("value", "timestamp")
+
+    def __init__(self, value, timestamp):
+        self.value, self.timestamp = value, timestamp
+
+    def __repr__(self):
+        return f"StreamRecord({self.value!r}, {self.timestamp})"
+
+    def __eq__(self, o):
+        return isinstance(o, StreamRecord) and self.value == o.value and self.timestamp == o.timestamp
+
+    def __hash__(self):
+        return hash((self.value, self.timestamp))
+
+
+class Watermark:
+    __slots__ = ("timestamp",)
+
+    def __init__(self, timestamp):
+        self.timestamp = timestamp
+
+    def __repr__(self):
+        return f"Watermark({self.timestamp})"
+
+    def __eq__(self, o):
+        return isinstance(o, Watermark) and o.timestamp == self.timestamp
+
+    def __hash__(self):
+        return hash(("wm", self.timestamp))
+
+
+# ------------------------------------------------------------------ engine wrapper
+def _ptr(a):
+    """Pointer of a numpy array or a torch tensor (device pointer for GPU tensors)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(ctypes.c_void_p)
+    return ctypes.c_void_p(a.data_ptr())
+
+
+def _is_device(a):
+    return a is not None and not isinstance(a, np.ndarray) and getattr(a, "is_cuda", False)
+
+
+class WindowEngine:
+    """One fw_engine (one operator subtask on one GPU) behind the C-ABI."""
+
+    def __init__(self, config, lib=None, prefix="fw"):
+        self.lib = lib if lib is not None else _abi.load_library()
+        self.prefix = prefix
+        self.cfg = config
+        h = ctypes.c_void_p()
+        rc = self._fn("create")(ctypes.byref(config), ctypes.byref(h))
+        if rc != 0:
+            raise _abi.FwError(rc, self._fn("last_error")(None).decode() or "fw_create failed")
+        self.h = h
+
+    def _fn(self, name):
+        return getattr(self.lib, f"{self.prefix}_{name}")
+
+    def _check(self, rc):
+        if rc != 0:
+            raise _abi.FwError(rc, self._fn("last_error")(self.h).decode())
+
+    def push(self, key, ts, value, key_hash=None, f1=None):
+        n = len(key)
+        if self.prefix == "fw":
+            mem = _abi.FW_MEM_DEVICE if _is_device(key) else _abi.FW_MEM_HOST
+            self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n, mem))
+        else:
+            self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n))
+
+    def advance_watermark(self, wm):
+        self._check(self._fn("advance_watermark")(self.h, wm))
+
+    def sync(self):
+        if self.prefix == "fw":
+            self._check(self._fn("sync")(self.h))
+
+    def collect(self):
+        """Results since the last collect: dict of numpy columns + (mark_wm, mark_pos)."""
+        o = _abi.FwOut()
+        if self.prefix == "fw":
+            self._check(self._fn("collect")(self.h, ctypes.byref(o), _abi.FW_MEM_HOST))
+        else:
+            self._check(self._fn("collect")(self.h, ctypes.byref(o)))
+        n = o.n
+        res = {"n": n}
+        for name in ("key", "f1", "ts", "sum_i64", "min_i64", "max_i64", "count", "sum_f64", "min_f64", "max_f64"):
+            p = getattr(o, name)
+            if n == 0:
+                res[name] = np.zeros(0, np.float64 if name.endswith("f64") else np.int64)
+            else:
+                res[name] = np.ctypeslib.as_array(p, shape=(n,)).copy() if p else None
+        nm = o.n_marks
+        res["mark_wm"] = np.ctypeslib.as_array(o.mark_wm, shape=(nm,)).copy() if nm > 0 else np.zeros(0, np.int64)
+        res["mark_pos"] = np.ctypeslib.as_array(o.mark_pos, shape=(nm,)).copy() if nm > 0 else np.zeros(0, np.int64)
+        if self.prefix != "fw":
+            self._fn("clear_output")(self.h)
+        return res
+
+    def stats(self):
+        st = _abi.FwStats()
+        self._check(self._fn("get_stats")(self.h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in _abi.FwStats._fields_}
+
+    def close(self):
+        if self.h:
+            self._fn("destroy")(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_config(assigner, reduce_function, trigger=None, allowed_lateness=0, max_parallelism=DEFAULT_MAX_PARALLELISM,
+                key_group_range=None, device=0, key_capacity=1 << 16, max_batch=1 << 20, out_capacity=1 << 20,
+                max_open_slices=0, ingest_mode=0):
+    trigger = trigger if trigger is not None else EventTimeTrigger.create()
+    kg = key_group_range if key_group_range is not None else (0, max_parallelism - 1)
+    c = _abi.FwConfig()
+    c.assigner = assigner.kind
+    c.trigger = trigger.code
+    c.size = assigner.size
+    c.slide = assigner.slide
+    c.offset = assigner.offset
+    c.allowed_lateness = allowed_lateness
+    c.value_type = reduce_function.vt
+    c.agg_mask = reduce_function.mask
+    c.keep_first_f1 = 1 if reduce_function.keep_first_f1 else 0
+    c.max_parallelism = max_parallelism
+    c.kg_start, c.kg_end = kg
+    c.device = device
+    c.max_open_slices = max_open_slices
+    c.key_capacity = key_capacity
+    c.max_batch = max_batch
+    c.out_capacity = out_capacity
+    c.ingest_mode = ingest_mode
+    return c
+
+
+class WindowOperator:
+    """Event-time WindowOperator (non-merging, reduce) on the GPU.
+
+    processElement(StreamRecord((key, value) | (key, f1, value), ts)) buffers the record;
+    processWatermark(Watermark) hands the buffered epoch to the engine, advances the watermark and
+    appends the fired results followed by the watermark to the output (AbstractStreamOperator
+    .processWatermark :803-808: timers fire, then the watermark is forwarded).
+    `engine_factory(config)` lets the tests run the oracle behind the same surface.
+    """
+
+    def __init__(self, assigner, reduce_function, trigger=None, allowed_lateness=0, engine_factory=None, **kw):
+        self.assigner = assigner
+        self.reduce = reduce_function
+        self.config = make_config(assigner, reduce_function, trigger, allowed_lateness, **kw)
+        self.engine = (engine_factory or WindowEngine)(self.config)
+        self._keys, self._hash, self._f1, self._ts, self._val = [], [], [], [], []
+        self._key_ids, self._key_names = {}, {}
+        self.output = []
+
+    # keys: int (Long) keys pass through; other keys (e.g. String) are interned and carry hashCode()
+    def _key(self, k):
+        if isinstance(k, (int, np.integer)) and not isinstance(k, bool):
+            return int(k), None
+        kid = self._key_ids.get(k)
+        if kid is None:
+            kid = len(self._key_ids) + 1
+            self._key_ids[k] = kid
+            self._key_names[kid] = k
+        return kid, java_string_hash(k) if isinstance(k, str) else hash(k) & 0x7FFFFFFF
+
+    def processElement(self, record):
+        v = record.value
+        key, h = self._key(v[0])
+        if len(v) == 3:
+            f1, val = v[1], v[2]
+        else:
+            f1, val = record.timestamp, v[1]
+        self._keys.append(key)
+        self._hash.append(h)
+        self._f1.append(f1)
+        self._ts.append(record.timestamp)
+        self._val.append(val)
+
+    def _flush(self):
+        if not self._keys:
+            return
+        keys = np.array(self._keys, dtype=np.int64)
+        hashes = None
+        if any(h is not None for h in self._hash):
+            from .keygroups import long_hash_code
+            hashes = np.array([h if h is not None else long_hash_code(k) for k, h in zip(self._keys, self._hash)],
+                              dtype=np.int32)
+        ts = np.array(self._ts, dtype=np.int64)
+        f1 = np.array(self._f1, dtype=np.int64)
+        val = np.array(self._val, dtype=np.int64 if self.reduce.value_type == "i64" else np.float64)
+        self._keys, self._hash, self._f1, self._ts, self._val = [], [], [], [], []
+        self.engine.push(keys, ts, val, key_hash=hashes, f1=f1)
+
+    def processWatermark(self, mark):
+        self._flush()
+        self.engine.advance_watermark(mark.timestamp)
+        self._drain()
+
+    def _record(self, res, i):
+        k = int(res["key"][i])
+        key = self._key_names.get(k, k) if self._key_names else k
+        vals = []
+        if self.reduce.keep_first_f1:
+            vals.append(int(res["f1"][i]))
+        for f in self.reduce.fields:
+            col = res[{"sum": "sum", "min": "min", "max": "max", "count": "count"}[f] +
+                      ("" if f == "count" else ("_i64" if self.reduce.value_type == "i64" else "_f64"))]
+            vals.append(col[i].item())
+        return StreamRecord(tuple([key] + vals), int(res["ts"][i]))
+
+    def _drain(self):
+        res = self.engine.collect()
+        pos = 0
+        for wm, mp in zip(res["mark_wm"], res["mark_pos"]):
+            while pos < mp:
+                self.output.append(self._record(res, pos))
+                pos += 1
+            self.output.append(Watermark(int(wm)))
+        while pos < res["n"]:
+            self.output.append(self._record(res, pos))
+            pos += 1
+
+    def getOutput(self):
+        return self.output
+
+    def close(self):
+        self.engine.close()

@@ -1,0 +1,186 @@
+/*
+ * flink_window.h — C-ABI of the MI355X keyed event-time window aggregation engine.
+ *
+ * This is the drop-in boundary for Flink's event-time `KeyedStream.window(...).reduce(...)`
+ * path, i.e. the non-merging event-time branch of
+ *   flink-streaming-java/.../runtime/operators/windowing/WindowOperator.java
+ * running on the heap keyed-state backend and the heap timer service.
+ *
+ * One engine = one operator subtask (one GPU).  A thin JNI shim in a `GpuWindowOperator`
+ *  calls these functions; in this repository the Python host mirror
+ * (flink_amd/windowing.py) and the tests call them through ctypes.
+ *
+ * Reference interface each entry point replaces (file:line, paths relative to the reference
+ * root, SJ = flink-streaming-java/src/main/java/org/apache/flink/streaming/):
+ *
+ *   fw_create            <- WindowOperator constructor + open()        SJ/runtime/operators/windowing/WindowOperator.java:150-220
+ *                           WindowedStream.reduce -> apply(...)         SJ/api/datastream/WindowedStream.java:185-203,368-425
+ *   fw_push_batch        <- WindowOperator.processElement, per record   SJ/runtime/operators/windowing/WindowOperator.java:222-226,302-333
+ *                           called by StreamInputProcessor.processInput SJ/runtime/io/StreamInputProcessor.java:169-177
+ *                           key groups: KeyGroupRangeAssignment         flink-runtime/.../runtime/state/KeyGroupRangeAssignment.java:51-64
+ *   fw_advance_watermark <- AbstractStreamOperator.processWatermark     SJ/api/operators/AbstractStreamOperator.java:803-808
+ *                           HeapInternalTimerService.advanceWatermark   SJ/api/operators/HeapInternalTimerService.java:264-278
+ *                           WindowOperator.onEventTime                  SJ/runtime/operators/windowing/WindowOperator.java:336-375
+ *   fw_collect           <- Output.collect / Output.emitWatermark       SJ/api/operators/Output.java:42-44
+ *                           (TimestampedCollector, ts = window.maxTimestamp(): WindowOperator.java:435-438)
+ *   fw_get_stats         <- numRecordsIn / numRecordsOut counters       SJ/runtime/io/StreamInputProcessor.java:131-132,173
+ *   fw_destroy           <- WindowOperator.close()/dispose()            SJ/api/operators/StreamOperator.java:78,87
+ *
+ * Conventions
+ *  - Every function returns FW_OK (0) or an FW_ERR_* code; no exception crosses the ABI.
+ *    fw_last_error() returns a message for the last failure.
+ *  - Calls on one engine must be serialised by the caller (mirrors the task checkpoint lock,
+ *    SJ/runtime/tasks/StreamTask.java:131).  Engines on different devices are independent.
+ *  - fw_push_batch and fw_advance_watermark only ENQUEUE device work; errors found on the device
+ *    (Long.MIN_VALUE timestamps, key group outside this subtask's range, capacity) are reported by
+ *    the next synchronising call (fw_collect, fw_sync).
+ *  - Watermarks: a watermark not larger than the current one changes nothing but still appears as a
+ *    mark in the output, as the operator forwards every processWatermark call.
+ */
+#ifndef FLINK_WINDOW_H
+#define FLINK_WINDOW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---- */
+#define FW_OK                 0
+#define FW_ERR_INVALID_ARG    1  /* bad config / argument                                               */
+#define FW_ERR_NO_TIMESTAMP   2  /* record with Long.MIN_VALUE timestamp: TumblingEventTimeWindows.java:60-67 */
+#define FW_ERR_CAPACITY       3  /* key directory, slice pool, batch or output log capacity exceeded        */
+#define FW_ERR_KEY_GROUP      4  /* key group of a record outside [kg_start, kg_end] of this subtask         */
+#define FW_ERR_UNSUPPORTED    5  /* configuration this backend does not implement                            */
+#define FW_ERR_DEVICE         6  /* HIP runtime failure                                                      */
+
+/* ---- window assigner (SJ/api/windowing/assigners) ---- */
+#define FW_TUMBLING 0            /* TumblingEventTimeWindows.of(size[, offset])  (offset already % size)     */
+#define FW_SLIDING  1            /* SlidingEventTimeWindows.of(size, slide[, offset]) (offset already % slide) */
+
+/* ---- trigger (SJ/api/windowing/triggers) ---- */
+#define FW_TRIGGER_EVENT_TIME          0   /* EventTimeTrigger.create()                    */
+#define FW_TRIGGER_PURGING_EVENT_TIME  1   /* PurgingTrigger.of(EventTimeTrigger.create()) */
+
+/* ---- reduce function: which fields the ReduceFunction aggregates ----
+ * The input record is (key, f1, ts, value).  The accumulator is the reduce of the records in
+ * arrival order with reduce(value1 = stored, value2 = incoming) (HeapReducingState.java:116):
+ *   sum   = value1.sum + value2.sum                (Java long wraps / Java double +)
+ *   min   = Math.min(value1.min, value2.min)       (NaN wins, -0.0 < +0.0)
+ *   max   = Math.max(value1.max, value2.max)
+ *   count = value1.count + value2.count            (each record starts at 1)
+ *   f1    = value1.f1                              (first arrival into the pane: SumAggregator.java:64-72)
+ */
+#define FW_AGG_SUM    1
+#define FW_AGG_MIN    2
+#define FW_AGG_MAX    4
+#define FW_AGG_COUNT  8
+
+#define FW_VALUE_I64  0
+#define FW_VALUE_F64  1
+
+/* memory kinds for buffers crossing the ABI */
+#define FW_MEM_HOST    0
+#define FW_MEM_DEVICE  1
+
+typedef struct fw_engine fw_engine;
+
+typedef struct {
+  int32_t assigner;          /* FW_TUMBLING | FW_SLIDING                                        */
+  int32_t trigger;           /* FW_TRIGGER_*                                                    */
+  int64_t size;              /* window size (ms)                                                */
+  int64_t slide;             /* slide (ms); ignored for tumbling                                */
+  int64_t offset;            /* window offset (ms), as held by the assigner                     */
+  int64_t allowed_lateness;  /* WindowedStream.allowedLateness (ms), >= 0                       */
+  int32_t value_type;        /* FW_VALUE_I64 | FW_VALUE_F64                                     */
+  int32_t agg_mask;          /* OR of FW_AGG_*                                                  */
+  int32_t keep_first_f1;     /* 1: output f1 of the first arrival into the pane                 */
+  int32_t max_parallelism;   /* number of key groups (KeyGroupRangeAssignment, default 128)     */
+  int32_t kg_start;          /* first key group owned by this subtask (inclusive)               */
+  int32_t kg_end;            /* last key group owned by this subtask (inclusive)                */
+  int32_t device;            /* HIP device ordinal                                              */
+  int32_t max_open_slices;   /* pane slices resident at once; 0 = derive from the window spec  */
+  int64_t key_capacity;      /* distinct keys over the engine lifetime                          */
+  int64_t max_batch;         /* max records per fw_push_batch                                   */
+  int64_t out_capacity;      /* max fired records between two fw_collect calls                  */
+  int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate     */
+  int32_t reserved;
+} fw_config;
+
+/* Output between two collects: records and watermark marks.  Records [mark_pos[i-1], mark_pos[i])
+ * are the results emitted before watermark mark_wm[i] was forwarded (records before the first mark
+ * have pos 0..mark_pos[0]).  Records after the last mark were emitted by per-element fires that
+ * no watermark has followed yet.  Columns that the config does not produce are NULL.
+ * Pointers are engine-owned and valid until the next call on the engine. */
+typedef struct {
+  int64_t n;
+  const int64_t* key;
+  const int64_t* f1;
+  const int64_t* ts;         /* window.maxTimestamp() */
+  const int64_t* sum_i64;
+  const int64_t* min_i64;
+  const int64_t* max_i64;
+  const int64_t* count;
+  const double*  sum_f64;
+  const double*  min_f64;
+  const double*  max_f64;
+  int64_t n_marks;
+  const int64_t* mark_wm;
+  const int64_t* mark_pos;
+} fw_out;
+
+typedef struct {
+  int64_t records_in;        /* numRecordsIn                                  */
+  int64_t records_late;      /* (record, window) pairs dropped by isLate      */
+  int64_t panes_fired;       /* timer fires that emitted a result             */
+  int64_t late_fires;        /* per-element fires (allowed lateness > 0)      */
+  int64_t keys_resident;     /* distinct keys in the key directory            */
+  int64_t slices_live;       /* pane slices resident                          */
+} fw_stats;
+
+int         fw_create(const fw_config* cfg, fw_engine** out);
+/* key: record keys (int64).  key_hash: optional Java key.hashCode() per record (NULL = Long.hashCode(key)).
+ * f1: optional pass-through field (NULL = ts).  ts: event timestamps.  value: int64 or double per value_type. */
+int         fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,
+                          const int64_t* ts, const void* value, int64_t n, int32_t mem);
+int         fw_advance_watermark(fw_engine* e, int64_t wm);
+int         fw_sync(fw_engine* e);
+int         fw_collect(fw_engine* e, fw_out* out, int32_t mem);
+int         fw_get_stats(fw_engine* e, fw_stats* st);
+const char* fw_last_error(const fw_engine* e);
+void        fw_destroy(fw_engine* e);
+
+/* Key-group routing for the multi-GPU keyBy exchange
+ * (KeyGroupStreamPartitioner.selectChannels, SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65;
+ *  KeyGroupRangeAssignment.assignKeyToParallelOperator, KeyGroupRangeAssignment.java:40-42,105-107).
+ * Counting-sorts n records by destination operator index into out_* (device pointers) and writes
+ * per-destination counts and offsets (int64[parallelism]).  Stable within a destination. */
+int         fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* key_hash,
+                                     const int64_t* f1, const int64_t* ts, const void* value, int64_t n,
+                                     int32_t max_parallelism, int32_t parallelism,
+                                     int64_t* out_key, int32_t* out_key_hash, int64_t* out_f1,
+                                     int64_t* out_ts, void* out_value, int64_t* counts, int64_t* offsets);
+
+/* Device-time accounting (HIP events on the engine's stream around each kernel phase), for the
+ * roofline figures of bench.py.  Off by default; enabling it adds event records, not syncs. */
+#define FW_PHASE_INGEST  0   /* per-record ingest (key group, slice, directory, pane update)  */
+#define FW_PHASE_FIXUP   1   /* first-arrival f1 gather for new panes                         */
+#define FW_PHASE_LATE    2   /* per-element fires (allowed lateness > 0)                      */
+#define FW_PHASE_FIRE    3   /* watermark: plan + fire + purge + mark                         */
+#define FW_NPHASES       4
+typedef struct {
+  double  ms[FW_NPHASES];        /* accumulated device milliseconds per phase */
+  int64_t launches[FW_NPHASES];  /* timed launches per phase                  */
+  int64_t records[FW_NPHASES];   /* records (ingest) or panes scanned (fire)  */
+} fw_profile;
+int         fw_set_profiling(fw_engine* e, int32_t enable);
+int         fw_get_profile(fw_engine* e, fw_profile* out);   /* synchronises; resets the counters */
+
+/* library version string */
+const char* fw_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

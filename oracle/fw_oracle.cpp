@@ -1,0 +1,492 @@
+// fw_oracle.cpp — CPU restatement of the reference's event-time WindowOperator path.
+//
+// TEST INFRASTRUCTURE ONLY.  This file is the parity oracle: only tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg may load it, and only as the checker or the timed CPU column.
+// The product path (flink_amd/, libflink_window.so) never links or calls it.
+//
+// It restates, literally and single-threaded, the Java code of the reference (kalmanchapman/flink
+// 1.2-SNAPSHOT, paths relative to /root/reference; SJ = flink-streaming-java/src/main/java/org/
+// apache/flink/streaming/, RT = flink-runtime/src/main/java/org/apache/flink/runtime/):
+//   murmurHash                  flink-core/.../util/MathUtils.java:134-158
+//   Long.hashCode / Tuple1      JDK Long.hashCode; flink-core/.../api/java/tuple/Tuple1.java:137-139
+//   key groups                  RT/state/KeyGroupRangeAssignment.java:40-107
+//   TimeWindow                  SJ/api/windowing/windows/TimeWindow.java:41-62,239-241
+//   Tumbling assigner           SJ/api/windowing/assigners/TumblingEventTimeWindows.java:59-68
+//   Sliding assigner            SJ/api/windowing/assigners/SlidingEventTimeWindows.java:64-77
+//   processElement              SJ/runtime/operators/windowing/WindowOperator.java:222-226,302-333
+//   onEventTime                 WindowOperator.java:336-375; fire :435-438; cleanup :420-428
+//   isLate/cleanupTime          WindowOperator.java:470-472,479-486,511-514,527-530
+//   EventTimeTrigger            SJ/api/windowing/triggers/EventTimeTrigger.java:37-62
+//   PurgingTrigger              SJ/api/windowing/triggers/PurgingTrigger.java:47-53
+//   HeapReducingState.add       RT/state/heap/HeapReducingState.java:84-122
+//   AbstractHeapState.clear     RT/state/heap/AbstractHeapState.java:90-119
+//   StateTable                  RT/state/heap/StateTable.java:27-77
+//   timer service               SJ/api/operators/HeapInternalTimerService.java:211-236,264-278
+//   InternalTimer               SJ/api/operators/InternalTimer.java:59-86
+//   processWatermark            SJ/api/operators/AbstractStreamOperator.java:803-808
+//   reduce functions            SJ/api/functions/aggregation/SumAggregator.java:64-72, SumFunction.java:60-77,
+//                               JDK Math.min/Math.max (double), Long arithmetic (wrapping)
+//
+// Java semantics kept: wrapping int32/int64 arithmetic (done in unsigned), logical >>>, truncating %,
+// Long.MIN_VALUE-timestamp error, cleanup-time overflow clamp, arrival-order left fold.
+//
+// C API (fwo_*) mirrors include/flink_window.h so tests can drive oracle and engine identically.
+#include "../include/flink_window.h"
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// ---------------- Java integer helpers ----------------
+inline int32_t jint_mul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+inline int32_t jint_add(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+inline int32_t rotl32(int32_t v, int r) { uint32_t u = (uint32_t)v; return (int32_t)((u << r) | (u >> (32 - r))); }
+inline int32_t ushr32(int32_t v, int r) { return (int32_t)((uint32_t)v >> r); }
+inline int64_t jlong_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+inline int64_t jlong_sub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+
+// MathUtils.murmurHash(int) — MathUtils.java:134-158
+int32_t murmurHash(int32_t code) {
+  code = jint_mul(code, (int32_t)0xcc9e2d51);
+  code = rotl32(code, 15);
+  code = jint_mul(code, (int32_t)0x1b873593);
+  code = rotl32(code, 13);
+  code = jint_add(jint_mul(code, 5), (int32_t)0xe6546b64);
+  code ^= 4;
+  code ^= ushr32(code, 16);
+  code = jint_mul(code, (int32_t)0x85ebca6b);
+  code ^= ushr32(code, 13);
+  code = jint_mul(code, (int32_t)0xc2b2ae35);
+  code ^= ushr32(code, 16);
+  if (code >= 0) return code;
+  else if (code != INT32_MIN) return -code;
+  else return 0;
+}
+// JDK Long.hashCode(long) = (int)(value ^ (value >>> 32))
+int32_t longHashCode(int64_t v) { return (int32_t)(uint32_t)((uint64_t)v ^ ((uint64_t)v >> 32)); }
+// KeyGroupRangeAssignment.computeKeyGroupForKeyHash — :62-64
+int32_t computeKeyGroupForKeyHash(int32_t keyHash, int32_t maxParallelism) {
+  return murmurHash(keyHash) % maxParallelism;
+}
+// KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup — :105-107
+int32_t computeOperatorIndexForKeyGroup(int32_t maxParallelism, int32_t parallelism, int32_t keyGroupId) {
+  return keyGroupId * parallelism / maxParallelism;
+}
+
+// ---------------- windows ----------------
+struct TimeWindow {  // TimeWindow.java:41-62
+  int64_t start, end;
+  int64_t maxTimestamp() const { return jlong_sub(end, 1); }
+  bool operator==(const TimeWindow& o) const { return start == o.start && end == o.end; }
+  bool operator<(const TimeWindow& o) const { return start != o.start ? start < o.start : end < o.end; }
+};
+struct TimeWindowHash {
+  size_t operator()(const TimeWindow& w) const { return std::hash<int64_t>()(w.start) * 31 + std::hash<int64_t>()(w.end); }
+};
+// TimeWindow.getWindowStartWithOffset — :239-241
+int64_t getWindowStartWithOffset(int64_t timestamp, int64_t offset, int64_t windowSize) {
+  int64_t num = jlong_add(jlong_sub(timestamp, offset), windowSize);
+  return jlong_sub(timestamp, num % windowSize);
+}
+
+// ---------------- accumulator = the reduced record ----------------
+struct Acc {
+  int64_t key;
+  int64_t f1;
+  int64_t sum_i, min_i, max_i, count;
+  double sum_d, min_d, max_d;
+};
+
+// JDK Math.min(double,double) / Math.max(double,double)
+double javaMin(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && std::signbit(b)) return b;
+  return (a <= b) ? a : b;
+}
+double javaMax(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && std::signbit(a)) return b;
+  return (a >= b) ? a : b;
+}
+
+struct Config {
+  fw_config c;
+  int64_t size() const { return c.size; }
+};
+
+// ReduceFunction.reduce(value1 = stored, value2 = incoming); non-aggregated fields from value1
+// (SumAggregator.java:64-72 copies value1; user lambdas of the form Tuple.of(a.f0, a.f1, ...) likewise).
+Acc reduceFn(const fw_config& c, const Acc& v1, const Acc& v2) {
+  Acc r = v1;
+  if (c.value_type == FW_VALUE_I64) {
+    r.sum_i = jlong_add(v1.sum_i, v2.sum_i);                 // SumFunction.LongSum :60-66
+    r.min_i = v1.min_i <= v2.min_i ? v1.min_i : v2.min_i;     // Math.min(long,long)
+    r.max_i = v1.max_i >= v2.max_i ? v1.max_i : v2.max_i;     // Math.max(long,long)
+  } else {
+    r.sum_d = v1.sum_d + v2.sum_d;                            // SumFunction.DoubleSum :68-77
+    r.min_d = javaMin(v1.min_d, v2.min_d);
+    r.max_d = javaMax(v1.max_d, v2.max_d);
+  }
+  r.count = jlong_add(v1.count, v2.count);
+  return r;
+}
+
+// ---------------- timers ----------------
+struct InternalTimer {  // InternalTimer.java:59-86 — equality on (timestamp, key, namespace)
+  int64_t timestamp;
+  int64_t key;
+  TimeWindow ns;
+  bool operator<(const InternalTimer& o) const {
+    if (timestamp != o.timestamp) return timestamp < o.timestamp;  // queue order: timestamp (ties arbitrary)
+    if (key != o.key) return key < o.key;
+    return ns < o.ns;
+  }
+};
+
+enum TriggerResult { CONTINUE = 0, FIRE_AND_PURGE = 1, FIRE = 2, PURGE = 3 };
+inline bool isFire(TriggerResult r) { return r == FIRE || r == FIRE_AND_PURGE; }
+inline bool isPurge(TriggerResult r) { return r == PURGE || r == FIRE_AND_PURGE; }
+
+struct OutRec {
+  Acc acc;
+  int64_t ts;
+};
+
+struct Operator {
+  fw_config cfg;
+  std::string err;
+  int64_t currentWatermark = INT64_MIN;   // HeapInternalTimerService.currentWatermark initial value
+  // StateTable: per key group -> namespace -> key -> value   (StateTable.java:36)
+  std::vector<std::unordered_map<TimeWindow, std::unordered_map<int64_t, Acc>, TimeWindowHash>> state;
+  // event-time timers: set gives both the HashSet dedupe and the PriorityQueue order
+  std::set<InternalTimer> timers;
+  // current key context
+  int64_t curKey = 0;
+  int32_t curKeyGroup = 0;
+  // outputs
+  std::vector<OutRec> out;
+  std::vector<int64_t> mark_wm, mark_pos;
+  fw_stats stats{};
+  // materialised output columns for fwo_collect
+  std::vector<int64_t> c_key, c_f1, c_ts, c_sum_i, c_min_i, c_max_i, c_count;
+  std::vector<double> c_sum_d, c_min_d, c_max_d;
+
+  explicit Operator(const fw_config& c) : cfg(c) {
+    state.resize((size_t)(cfg.kg_end - cfg.kg_start + 1));
+  }
+
+  // ---- WindowAssigner.assignWindows ----
+  int assignWindows(int64_t timestamp, std::vector<TimeWindow>& ws) {
+    ws.clear();
+    if (!(timestamp > INT64_MIN)) {
+      err = "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Is the time characteristic set to "
+            "'ProcessingTime', or did you forget to call 'DataStream.assignTimestampsAndWatermarks(...)'?";
+      return FW_ERR_NO_TIMESTAMP;
+    }
+    if (cfg.assigner == FW_TUMBLING) {  // TumblingEventTimeWindows.java:59-68
+      int64_t start = getWindowStartWithOffset(timestamp, cfg.offset, cfg.size);
+      ws.push_back({start, jlong_add(start, cfg.size)});
+    } else {  // SlidingEventTimeWindows.java:64-77
+      int64_t lastStart = getWindowStartWithOffset(timestamp, cfg.offset, cfg.slide);
+      int64_t bound = jlong_sub(timestamp, cfg.size);
+      int64_t guard = cfg.size / cfg.slide + 2;
+      for (int64_t start = lastStart; start > bound; start = jlong_sub(start, cfg.slide)) {
+        ws.push_back({start, jlong_add(start, cfg.size)});
+        if ((int64_t)ws.size() > guard) { err = "sliding window enumeration wrapped around"; return FW_ERR_INVALID_ARG; }
+      }
+    }
+    return FW_OK;
+  }
+
+  // ---- WindowOperator helpers ----
+  int64_t cleanupTime(const TimeWindow& w) const {  // :511-514
+    int64_t ct = jlong_add(w.maxTimestamp(), cfg.allowed_lateness);
+    return ct >= w.maxTimestamp() ? ct : INT64_MAX;
+  }
+  bool isLate(const TimeWindow& w) const { return cleanupTime(w) <= currentWatermark; }  // :470-472
+  bool isCleanupTime(const TimeWindow& w, int64_t time) const { return cleanupTime(w) == time; }  // :527-530
+
+  // ---- keyed state: HeapReducingState ----
+  std::unordered_map<TimeWindow, std::unordered_map<int64_t, Acc>, TimeWindowHash>* nsMap() {
+    if (curKeyGroup < cfg.kg_start || curKeyGroup > cfg.kg_end) return nullptr;  // StateTable.get :55-57
+    return &state[(size_t)(curKeyGroup - cfg.kg_start)];
+  }
+  int stateAdd(const TimeWindow& ns, const Acc& value) {  // HeapReducingState.add :84-122
+    auto* m = nsMap();
+    if (!m) { err = "Unexpected key group index. This indicates a bug."; return FW_ERR_KEY_GROUP; }  // StateTable.set :59-63
+    auto& keyed = (*m)[ns];
+    auto it = keyed.find(curKey);
+    if (it == keyed.end()) keyed.emplace(curKey, value);
+    else it->second = reduceFn(cfg, it->second, value);
+    return FW_OK;
+  }
+  const Acc* stateGet(const TimeWindow& ns) {  // HeapReducingState.get :72-82
+    auto* m = nsMap();
+    if (!m) return nullptr;
+    auto nit = m->find(ns);
+    if (nit == m->end()) return nullptr;
+    auto kit = nit->second.find(curKey);
+    return kit == nit->second.end() ? nullptr : &kit->second;
+  }
+  void stateClear(const TimeWindow& ns) {  // AbstractHeapState.clear :90-119
+    auto* m = nsMap();
+    if (!m) return;
+    auto nit = m->find(ns);
+    if (nit == m->end()) return;
+    if (nit->second.erase(curKey) == 0) return;
+    if (!nit->second.empty()) return;
+    m->erase(nit);
+  }
+
+  // ---- timer service ----
+  void registerEventTimeTimer(const TimeWindow& ns, int64_t time) { timers.insert({time, curKey, ns}); }  // :211-218
+  void deleteEventTimeTimer(const TimeWindow& ns, int64_t time) { timers.erase({time, curKey, ns}); }    // :229-236
+
+  // ---- trigger ----
+  TriggerResult triggerOnElement(const TimeWindow& w) {  // EventTimeTrigger.java:37-45
+    TriggerResult r;
+    if (w.maxTimestamp() <= currentWatermark) {
+      r = FIRE;
+    } else {
+      registerEventTimeTimer(w, w.maxTimestamp());
+      r = CONTINUE;
+    }
+    if (cfg.trigger == FW_TRIGGER_PURGING_EVENT_TIME) return isFire(r) ? FIRE_AND_PURGE : r;  // PurgingTrigger :47-50
+    return r;
+  }
+  TriggerResult triggerOnEventTime(const TimeWindow& w, int64_t time) {  // EventTimeTrigger.java:48-52
+    TriggerResult r = (time == w.maxTimestamp()) ? FIRE : CONTINUE;
+    if (cfg.trigger == FW_TRIGGER_PURGING_EVENT_TIME) return isFire(r) ? FIRE_AND_PURGE : r;  // PurgingTrigger :52-55
+    return r;
+  }
+  void triggerClear(const TimeWindow& w) { deleteEventTimeTimer(w, w.maxTimestamp()); }  // EventTimeTrigger.java:59-62
+
+  // ---- WindowOperator.fire / cleanup / registerCleanupTimer ----
+  void fire(const TimeWindow& w, const Acc& contents) {  // :435-438, InternalSingleValueWindowFunction + PassThrough
+    out.push_back({contents, w.maxTimestamp()});
+    stats.panes_fired++;
+  }
+  void cleanup(const TimeWindow& w) {  // :420-428
+    stateClear(w);
+    triggerClear(w);
+  }
+  void registerCleanupTimer(const TimeWindow& w) { registerEventTimeTimer(w, cleanupTime(w)); }  // :479-486
+
+  // ---- OneInputStreamOperator.processElement ----
+  int processElement(int64_t key, int32_t keyHash, int64_t f1, int64_t ts, int64_t vi, double vd) {
+    std::vector<TimeWindow> elementWindows;
+    int rc = assignWindows(ts, elementWindows);
+    if (rc) return rc;
+    // setKeyContextElement1 -> AbstractKeyedStateBackend.setCurrentKey :167-170
+    curKey = key;
+    curKeyGroup = computeKeyGroupForKeyHash(keyHash, cfg.max_parallelism);
+    stats.records_in++;
+    Acc value{};
+    value.key = key;
+    value.f1 = f1;
+    value.sum_i = value.min_i = value.max_i = vi;
+    value.sum_d = value.min_d = value.max_d = vd;
+    value.count = 1;
+    for (const TimeWindow& window : elementWindows) {  // :302-333
+      if (isLate(window)) { stats.records_late++; continue; }
+      rc = stateAdd(window, value);
+      if (rc) return rc;
+      TriggerResult triggerResult = triggerOnElement(window);
+      if (isFire(triggerResult)) {
+        const Acc* contents = stateGet(window);
+        if (contents == nullptr) continue;
+        Acc copy = *contents;
+        fire(window, copy);
+        stats.late_fires++;
+      }
+      if (isPurge(triggerResult)) cleanup(window);
+      else registerCleanupTimer(window);
+    }
+    return FW_OK;
+  }
+
+  // ---- WindowOperator.onEventTime :336-375 ----
+  void onEventTime(const InternalTimer& timer) {
+    curKey = timer.key;
+    const TimeWindow& window = timer.ns;
+    const Acc* c = stateGet(window);
+    if (c == nullptr) return;
+    Acc contents = *c;
+    TriggerResult triggerResult = triggerOnEventTime(window, timer.timestamp);
+    if (isFire(triggerResult)) fire(window, contents);
+    if (isPurge(triggerResult) || isCleanupTime(window, timer.timestamp)) cleanup(window);
+  }
+
+  // ---- AbstractStreamOperator.processWatermark :803-808 -> advanceWatermark :264-278 ----
+  void processWatermark(int64_t time) {
+    currentWatermark = time;
+    while (!timers.empty() && timers.begin()->timestamp <= time) {
+      InternalTimer timer = *timers.begin();
+      timers.erase(timers.begin());
+      curKeyGroup = computeKeyGroupForKeyHash(keyHashOf(timer.key), cfg.max_parallelism);
+      onEventTime(timer);
+    }
+    mark_wm.push_back(time);
+    mark_pos.push_back((int64_t)out.size());
+  }
+
+  // key -> key.hashCode(), remembered from processElement for keys that came with an explicit hash
+  std::unordered_map<int64_t, int32_t> explicitHash;
+  int32_t keyHashOf(int64_t key) const {
+    auto it = explicitHash.find(key);
+    return it == explicitHash.end() ? longHashCode(key) : it->second;
+  }
+};
+
+}  // namespace
+
+struct fw_engine {
+  Operator op;
+  explicit fw_engine(const fw_config& c) : op(c) {}
+};
+
+extern "C" {
+
+int fwo_create(const fw_config* cfg, fw_engine** out) {
+  if (!cfg || !out) return FW_ERR_INVALID_ARG;
+  if (cfg->size <= 0 || (cfg->assigner == FW_SLIDING && cfg->slide <= 0) || cfg->allowed_lateness < 0 ||
+      cfg->max_parallelism <= 0 || cfg->kg_start < 0 || cfg->kg_end < cfg->kg_start || cfg->kg_end >= cfg->max_parallelism)
+    return FW_ERR_INVALID_ARG;
+  *out = new fw_engine(*cfg);
+  return FW_OK;
+}
+
+// processElement for each record, in order (one StreamInputProcessor pass)
+int fwo_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1, const int64_t* ts,
+                   const void* value, int64_t n) {
+  Operator& op = e->op;
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t h = key_hash ? key_hash[i] : longHashCode(key[i]);
+    if (key_hash) op.explicitHash[key[i]] = h;
+    int64_t vi = 0;
+    double vd = 0.0;
+    if (op.cfg.value_type == FW_VALUE_I64) vi = ((const int64_t*)value)[i];
+    else vd = ((const double*)value)[i];
+    int rc = op.processElement(key[i], h, f1 ? f1[i] : ts[i], ts[i], vi, vd);
+    if (rc) return rc;
+  }
+  return FW_OK;
+}
+
+int fwo_advance_watermark(fw_engine* e, int64_t wm) {
+  e->op.processWatermark(wm);
+  return FW_OK;
+}
+
+int fwo_collect(fw_engine* e, fw_out* o) {
+  Operator& op = e->op;
+  size_t n = op.out.size();
+  op.c_key.resize(n); op.c_f1.resize(n); op.c_ts.resize(n);
+  op.c_sum_i.resize(n); op.c_min_i.resize(n); op.c_max_i.resize(n); op.c_count.resize(n);
+  op.c_sum_d.resize(n); op.c_min_d.resize(n); op.c_max_d.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    const Acc& a = op.out[i].acc;
+    op.c_key[i] = a.key; op.c_f1[i] = a.f1; op.c_ts[i] = op.out[i].ts;
+    op.c_sum_i[i] = a.sum_i; op.c_min_i[i] = a.min_i; op.c_max_i[i] = a.max_i; op.c_count[i] = a.count;
+    op.c_sum_d[i] = a.sum_d; op.c_min_d[i] = a.min_d; op.c_max_d[i] = a.max_d;
+  }
+  std::memset(o, 0, sizeof(*o));
+  o->n = (int64_t)n;
+  o->key = op.c_key.data();
+  o->f1 = op.c_f1.data();
+  o->ts = op.c_ts.data();
+  o->sum_i64 = op.c_sum_i.data(); o->min_i64 = op.c_min_i.data(); o->max_i64 = op.c_max_i.data();
+  o->count = op.c_count.data();
+  o->sum_f64 = op.c_sum_d.data(); o->min_f64 = op.c_min_d.data(); o->max_f64 = op.c_max_d.data();
+  o->n_marks = (int64_t)op.mark_wm.size();
+  o->mark_wm = op.mark_wm.data();
+  o->mark_pos = op.mark_pos.data();
+  return FW_OK;
+}
+
+// drop collected output (keeps operator state)
+int fwo_clear_output(fw_engine* e) {
+  e->op.out.clear();
+  e->op.mark_wm.clear();
+  e->op.mark_pos.clear();
+  return FW_OK;
+}
+
+int fwo_get_stats(fw_engine* e, fw_stats* st) {
+  *st = e->op.stats;
+  size_t keys = 0;
+  for (auto& m : e->op.state) for (auto& kv : m) keys += kv.second.size();
+  st->keys_resident = (int64_t)keys;
+  return FW_OK;
+}
+
+const char* fwo_last_error(const fw_engine* e) { return e ? e->op.err.c_str() : "null engine"; }
+void fwo_destroy(fw_engine* e) { delete e; }
+
+// pure functions exported for golden-vector tests
+int32_t fwo_murmur_hash(int32_t code) { return murmurHash(code); }
+int32_t fwo_long_hash_code(int64_t v) { return longHashCode(v); }
+int32_t fwo_key_group(int32_t key_hash, int32_t max_parallelism) { return computeKeyGroupForKeyHash(key_hash, max_parallelism); }
+int32_t fwo_operator_index(int32_t max_parallelism, int32_t parallelism, int32_t kg) {
+  return computeOperatorIndexForKeyGroup(max_parallelism, parallelism, kg);
+}
+// KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex :78-89
+void fwo_key_group_range(int32_t max_parallelism, int32_t parallelism, int32_t op_index, int32_t* start, int32_t* end) {
+  *start = op_index == 0 ? 0 : ((op_index * max_parallelism - 1) / parallelism) + 1;
+  *end = ((op_index + 1) * max_parallelism - 1) / parallelism;
+}
+int64_t fwo_window_start(int64_t ts, int64_t offset, int64_t size) { return getWindowStartWithOffset(ts, offset, size); }
+
+// ---- parallel CPU job: p operator subtasks (one thread each) behind a KeyGroupStreamPartitioner.
+// Each subtask owns computeKeyGroupRangeForOperatorIndex(mp, p, i) and sees the records routed to it
+// (assignKeyToParallelOperator) in input order, plus every watermark (RecordWriter.broadcastEmit).
+// Watermarks: after every `wm_every` records, wm = max ts seen so far - wm_lag; a final wm at the end.
+// Returns total fired records; the per-subtask sum of f2 (or f64 sum) for a checksum.
+int64_t fwo_run_parallel(const fw_config* cfg, int32_t parallelism, const int64_t* key, const int64_t* ts,
+                         const void* value, int64_t n, int64_t wm_every, int64_t wm_lag, int64_t final_wm,
+                         int64_t* checksum_out) {
+  std::vector<int64_t> fired(parallelism, 0), csum(parallelism, 0);
+  auto worker = [&](int32_t idx) {
+    fw_config c = *cfg;
+    fwo_key_group_range(cfg->max_parallelism, parallelism, idx, &c.kg_start, &c.kg_end);
+    Operator op(c);
+    int64_t maxTs = INT64_MIN;
+    for (int64_t i = 0; i < n; ++i) {
+      if (ts[i] > maxTs) maxTs = ts[i];
+      int32_t h = longHashCode(key[i]);
+      int32_t kg = computeKeyGroupForKeyHash(h, c.max_parallelism);
+      if (computeOperatorIndexForKeyGroup(c.max_parallelism, parallelism, kg) == idx) {
+        int64_t vi = 0; double vd = 0.0;
+        if (c.value_type == FW_VALUE_I64) vi = ((const int64_t*)value)[i]; else vd = ((const double*)value)[i];
+        op.processElement(key[i], h, ts[i], ts[i], vi, vd);
+      }
+      if (wm_every > 0 && (i + 1) % wm_every == 0) {
+        op.processWatermark(jlong_sub(maxTs, wm_lag));
+        for (auto& r : op.out) csum[idx] = jlong_add(csum[idx], c.value_type == FW_VALUE_I64 ? r.acc.sum_i : (int64_t)r.acc.count);
+        fired[idx] += (int64_t)op.out.size();
+        op.out.clear();
+      }
+    }
+    op.processWatermark(final_wm);
+    for (auto& r : op.out) csum[idx] = jlong_add(csum[idx], c.value_type == FW_VALUE_I64 ? r.acc.sum_i : (int64_t)r.acc.count);
+    fired[idx] += (int64_t)op.out.size();
+  };
+  std::vector<std::thread> th;
+  for (int32_t i = 0; i < parallelism; ++i) th.emplace_back(worker, i);
+  for (auto& t : th) t.join();
+  int64_t total = 0, cs = 0;
+  for (int32_t i = 0; i < parallelism; ++i) { total += fired[i]; cs = jlong_add(cs, csum[i]); }
+  if (checksum_out) *checksum_out = cs;
+  return total;
+}
+
+}  // extern "C"

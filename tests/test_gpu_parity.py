@@ -1,0 +1,223 @@
+"""HIP engine parity: the reference's golden fixtures and oracle comparisons on seeded streams.
+
+Bar: bit-exact for int64 sum/min/max/count and first-arrival f1; double sums within relative 1e-9 of
+the oracle (measured against sum|v|: values are positive here), double min/max/count exact.
+"""
+import numpy as np
+import pytest
+
+from harness import (WINDOW_FIXTURES, drive, epochs_of, expected_epochs, fixture_config, gen_stream, load_golden,
+                     replay)
+
+pytestmark = pytest.mark.gpu
+
+LONG_MAX = (1 << 63) - 1
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from flink_amd import _abi
+    from flink_amd.windowing import WindowEngine
+    _abi.load_library()
+    return WindowEngine
+
+
+@pytest.fixture(scope="module")
+def oracle_engine():
+    from oracle.oracle import OracleEngine
+    return OracleEngine
+
+
+@pytest.mark.parametrize("name", WINDOW_FIXTURES)
+def test_golden_fixture(hip, name):
+    fx = load_golden(name)
+    got = replay(fx, hip)
+    assert got == expected_epochs(fx), fx["source"]
+
+
+def _cfg(assigner, fields=("sum",), vt="i64", first=False, lateness=0, trigger=None, **kw):
+    from flink_amd.windowing import ReduceFunction, make_config
+    args = dict(key_capacity=1 << 14, max_batch=1 << 16, out_capacity=1 << 20)
+    args.update(kw)
+    return make_config(assigner, ReduceFunction(fields, vt, first), trigger, lateness, **args)
+
+
+def _compare(a, b, fields, rel=0.0):
+    assert len(a) == len(b)
+    for (wa, ra), (wb, rb) in zip(a, b):
+        assert wa == wb
+        assert len(ra) == len(rb), f"wm {wa}: {len(ra)} vs {len(rb)} records"
+        if rel == 0.0:
+            assert ra == rb, f"wm {wa}"
+        else:
+            for x, y in zip(ra, rb):
+                for u, v in zip(x, y):
+                    if isinstance(u, float):
+                        assert abs(u - v) <= rel * max(1.0, abs(v)), (wa, x, y)
+                    else:
+                        assert u == v, (wa, x, y)
+
+
+def _run_both(hip, oracle_engine, cfg, keys, ts, vals, batch, lag, fields, first=False, rel=0.0, f1=None):
+    eg = hip(cfg)
+    eo = oracle_engine(cfg)
+    rg = drive(eg, keys, ts, vals, batch, lag, LONG_MAX, f1=f1)
+    ro = drive(eo, keys, ts, vals, batch, lag, LONG_MAX, f1=f1)
+    sg, so = eg.stats(), eo.stats()
+    eg.close()
+    eo.close()
+    _compare(epochs_of(rg, fields, first), epochs_of(ro, fields, first), fields, rel)
+    return sg, so
+
+
+def test_tumbling_long_sum_first_arrival(hip, oracle_engine):
+    """C1 shape at small scale: keyed tumbling 1 s long-sum, f1 of the first arrival (Tuple3 job)."""
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys, ts, vals = gen_stream(200_000, 4096, rate=1 << 16)
+    cfg = _cfg(TumblingEventTimeWindows.of(1000), first=True)
+    sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 1 << 14, 1, ["sum_i64"], first=True)
+    assert sg["panes_fired"] == so["panes_fired"]
+
+
+def test_tumbling_all_fields_int(hip, oracle_engine):
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys, ts, vals = gen_stream(100_000, 1000, rate=1 << 15, ooo=300)
+    cfg = _cfg(TumblingEventTimeWindows.of(1000, 250), ("sum", "min", "max", "count"))
+    _run_both(hip, oracle_engine, cfg, keys, ts, vals, 10_000, 1, ["sum_i64", "min_i64", "max_i64", "count"])
+
+
+def test_sliding_double_multi_field(hip, oracle_engine):
+    """C3 shape: sliding 10 s / 1 s, double sum/min/max/count (sum to 1e-9 relative)."""
+    from flink_amd.windowing import SlidingEventTimeWindows
+    keys, ts, vals = gen_stream(150_000, 2000, rate=1 << 13, value_type="f64")
+    cfg = _cfg(SlidingEventTimeWindows.of(10_000, 1000), ("sum", "min", "max", "count"), "f64", True)
+    _run_both(hip, oracle_engine, cfg, keys, ts, vals, 8192, 1, ["sum_f64", "min_f64", "max_f64", "count"],
+              first=True, rel=1e-9)
+
+
+def test_sliding_uneven_slide(hip, oracle_engine):
+    """size not a multiple of slide: slices of gcd(size, slide)."""
+    from flink_amd.windowing import SlidingEventTimeWindows
+    keys, ts, vals = gen_stream(60_000, 300, rate=1 << 12, ooo=700)
+    cfg = _cfg(SlidingEventTimeWindows.of(2500, 1000, 300), ("sum", "count"))
+    _run_both(hip, oracle_engine, cfg, keys, ts, vals, 3000, 500, ["sum_i64", "count"])
+
+
+def test_zipf_out_of_order_lateness(hip, oracle_engine):
+    """C4 shape: Zipf(1.2) keys, out-of-order ts, bounded WM lag, allowed lateness -> per-element fires."""
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys, ts, vals = gen_stream(200_000, 1 << 12, rate=1 << 16, zipf=1.2, ooo=200)
+    cfg = _cfg(TumblingEventTimeWindows.of(1000), ("sum", "count"), first=True, lateness=100)
+    sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 1 << 14, 150, ["sum_i64", "count"], first=True)
+    assert so["late_fires"] > 0 and sg["late_fires"] == so["late_fires"]
+    assert sg["records_late"] == so["records_late"] and so["records_late"] > 0
+
+
+def test_purging_trigger_lateness(hip, oracle_engine):
+    from flink_amd.windowing import EventTimeTrigger, PurgingTrigger, TumblingEventTimeWindows
+    keys, ts, vals = gen_stream(80_000, 500, rate=1 << 14, ooo=400)
+    cfg = _cfg(TumblingEventTimeWindows.of(500), ("sum", "max"), first=True, lateness=300,
+               trigger=PurgingTrigger.of(EventTimeTrigger.create()))
+    _run_both(hip, oracle_engine, cfg, keys, ts, vals, 4000, 350, ["sum_i64", "max_i64"], first=True)
+
+
+def test_java_double_min_max_semantics(hip, oracle_engine):
+    """Math.min/Math.max: NaN wins, -0.0 < +0.0 (never fmin/fmax)."""
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys = np.array([1, 1, 2, 2, 3, 3, 4], np.int64)
+    ts = np.array([10, 20, 10, 20, 10, 20, 30], np.int64)
+    vals = np.array([0.0, -0.0, 1.5, float("nan"), -0.0, 0.0, float("-inf")], np.float64)
+    cfg = _cfg(TumblingEventTimeWindows.of(100), ("min", "max", "count"), "f64")
+    eg, eo = hip(cfg), oracle_engine(cfg)
+    for e in (eg, eo):
+        e.push(keys, ts, vals)
+        e.advance_watermark(1000)
+    rg, ro = eg.collect(), eo.collect()
+    def rows(r):
+        return sorted((int(r["key"][i]), np.float64(r["min_f64"][i]).tobytes() if not np.isnan(r["min_f64"][i]) else b"nan",
+                       np.float64(r["max_f64"][i]).tobytes() if not np.isnan(r["max_f64"][i]) else b"nan",
+                       int(r["count"][i])) for i in range(r["n"]))
+    assert rows(rg) == rows(ro)
+    eg.close(); eo.close()
+
+
+def test_extreme_keys_and_timestamps(hip, oracle_engine):
+    """Long.MIN_VALUE / MAX_VALUE keys, negative timestamps, the cleanup-time clamp."""
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys = np.array([-(1 << 63), LONG_MAX, 0, -1, 1 << 32, -(1 << 63), 7], np.int64)
+    ts = np.array([-5000, -5000, -1, 0, 999, -4999, LONG_MAX - 10], np.int64)
+    vals = np.array([1, 2, 3, 4, 5, 6, 7], np.int64)
+    cfg = _cfg(TumblingEventTimeWindows.of(1000, -300), ("sum", "count"), lateness=5000)
+    eg, eo = hip(cfg), oracle_engine(cfg)
+    rg = drive(eg, keys, ts, vals, 7, 0, LONG_MAX)
+    ro = drive(eo, keys, ts, vals, 7, 0, LONG_MAX)
+    _compare(epochs_of(rg, ["sum_i64", "count"]), epochs_of(ro, ["sum_i64", "count"]), None)
+    eg.close(); eo.close()
+
+
+def test_missing_timestamp_fails(hip):
+    from flink_amd import _abi
+    from flink_amd.windowing import TumblingEventTimeWindows
+    e = hip(_cfg(TumblingEventTimeWindows.of(1000)))
+    e.push(np.array([1, 2], np.int64), np.array([5, -(1 << 63)], np.int64), np.array([1, 1], np.int64))
+    with pytest.raises(_abi.FwError, match="Long.MIN_VALUE timestamp"):
+        e.sync()
+    e.close()
+
+
+def test_foreign_key_group_fails(hip):
+    from flink_amd import _abi
+    from flink_amd.windowing import TumblingEventTimeWindows
+    e = hip(_cfg(TumblingEventTimeWindows.of(1000), max_parallelism=128, key_group_range=(0, 0)))
+    e.push(np.array([42], np.int64), np.array([5], np.int64), np.array([1], np.int64))
+    with pytest.raises(_abi.FwError, match="Unexpected key group index"):
+        e.sync()
+    e.close()
+
+
+def test_device_resident_input(hip, oracle_engine):
+    """Columns already in HBM (torch tensors): no host copy on the push path."""
+    import torch
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys, ts, vals = gen_stream(50_000, 777, rate=1 << 14)
+    cfg = _cfg(TumblingEventTimeWindows.of(1000), first=True)
+    eg = hip(cfg)
+    dk, dt, dv = (torch.from_numpy(a).cuda() for a in (keys, ts, vals))
+    out = []
+    for s in range(0, len(keys), 10_000):
+        eg.push(dk[s:s + 10_000], dt[s:s + 10_000], dv[s:s + 10_000])
+        eg.advance_watermark(int(ts[:s + 10_000].max()) - 1)
+        out.append(eg.collect())
+    eg.advance_watermark(LONG_MAX)
+    out.append(eg.collect())
+    eo = oracle_engine(cfg)
+    ro = drive(eo, keys, ts, vals, 10_000, 1, LONG_MAX)
+    _compare(epochs_of(out, ["sum_i64"], True), epochs_of(ro, ["sum_i64"], True), None)
+    eg.close(); eo.close()
+
+
+def test_partition_by_operator_matches_key_group_routing(hip):
+    """fw_partition_by_operator = KeyGroupStreamPartitioner routing, stable per destination."""
+    import ctypes
+    import torch
+    from flink_amd.keygroups import operator_index_np
+    from flink_amd.windowing import TumblingEventTimeWindows
+    e = hip(_cfg(TumblingEventTimeWindows.of(1000)))
+    keys, ts, vals = gen_stream(100_003, 1 << 20, rate=1 << 14)
+    d = {n: torch.from_numpy(a).cuda() for n, a in (("k", keys), ("t", ts), ("v", vals))}
+    ok, of1, ot, ov = (torch.empty_like(d["k"]) for _ in range(4))
+    okh = torch.empty(len(keys), dtype=torch.int32, device="cuda")
+    counts = torch.zeros(8, dtype=torch.int64, device="cuda")
+    offs = torch.zeros(8, dtype=torch.int64, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    rc = e.lib.fw_partition_by_operator(e.h, P(d["k"]), None, None, P(d["t"]), P(d["v"]), len(keys), 128, 8,
+                                        P(ok), P(okh), P(of1), P(ot), P(ov), P(counts), P(offs))
+    assert rc == 0
+    e.sync()
+    dest = operator_index_np(keys, 128, 8)
+    order = np.argsort(dest, kind="stable")
+    assert np.array_equal(ok.cpu().numpy(), keys[order])
+    assert np.array_equal(ov.cpu().numpy(), vals[order])
+    assert np.array_equal(ot.cpu().numpy(), ts[order])
+    assert np.array_equal(counts.cpu().numpy(), np.bincount(dest, minlength=8))
+    e.close()
