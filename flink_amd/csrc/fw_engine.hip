@@ -83,6 +83,8 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int32_t* dir_min_used;
   uint64_t dir_mask;
   int64_t D;
+  int32_t kb_bits;  // log2(slots per directory bucket); probing stays inside the home bucket
+  int32_t nb;       // directory buckets = D >> kb_bits
   // slices
   int32_t P;
   int64_t stride;   // D + 1
@@ -124,14 +126,20 @@ __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
 }
 
 // key -> kid (directory slot).  Entries go EMPTY -> key once and never change until engine reset, so
-// a plain (possibly stale) load can only under-report, which the CAS then corrects.
+// a plain (possibly stale) load can only under-report, which the CAS then corrects.  Probing stays
+// inside the key's home bucket of 2^kb_bits slots, so every kid of a key lies in the bucket its hash
+// names: the partitioned ingest (k_route / k_aggregate) owns whole buckets exclusively.
 __device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key) {
   if (key == EMPTY_KEY) {
     if (s.dir_min_used[0] == 0) s.dir_min_used[0] = 1;
     return s.D;
   }
-  uint64_t h = fmix64((uint64_t)key) & s.dir_mask;
-  for (int64_t probe = 0; probe <= (int64_t)s.dir_mask; ++probe) {
+  const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
+  const uint64_t kbm = (1ull << s.kb_bits) - 1;
+  const uint64_t base = home & ~kbm;
+  uint64_t off = home & kbm;
+  for (uint64_t probe = 0; probe <= kbm; ++probe) {
+    const uint64_t h = base + off;
     int64_t cur = s.dir_keys[h];
     if (cur == key) return (int64_t)h;
     if (cur == EMPTY_KEY) {
@@ -139,7 +147,7 @@ __device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key
                                           (unsigned long long)key);
       if ((int64_t)prev == EMPTY_KEY || (int64_t)prev == key) return (int64_t)h;
     }
-    h = (h + 1) & s.dir_mask;
+    off = (off + 1) & kbm;
   }
   return -1;
 }
@@ -340,6 +348,297 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
          kid += (int64_t)gridDim.x * blockDim.x) {
       int64_t ord = s.c.first[base + kid];
       if (ord >= ord_base && ord < ord_base + n) s.c.f1v[base + kid] = f1col[ord - ord_base];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// ingest, partitioned form: k_route counting-sorts each tile of RT_TILE records by
+// (batch slice q, directory bucket) through LDS and writes the tile back coalesced; k_aggregate
+// gives every (q, bucket) to one workgroup, which owns those panes exclusively: it probes the
+// bucket's directory slice cached in LDS, reduces all the bucket's records with LDS atomics, and
+// folds the result into the dense columns with plain read-modify-writes (one per pane per batch).
+// ------------------------------------------------------------------------------------------------
+constexpr int RT_TILE = 8192;
+constexpr int RT_THREADS = 1024;
+constexpr int RT_Q = 2;                 // slices per batch handled by the partitioned form
+constexpr int AG_THREADS = 512;
+constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
+
+struct RouteBuf {
+  int64_t* key;          // [ntiles][RT_TILE]
+  int64_t* val;
+  uint16_t* idx;         // record index within its tile (first arrival)
+  int32_t* seg_start;    // [NBQ][ntiles] start of (q,bucket) segment within the tile
+  int32_t* seg_len;
+  int32_t* batch_slot;   // [RT_Q] pane-slice slot of batch slice q, -1 if unused
+  int32_t ntiles;
+};
+
+__device__ __forceinline__ int32_t batch_slice_q(const RouteBuf& r, int32_t p) {
+  for (int q = 0; q < RT_Q; ++q) {
+    int32_t v = r.batch_slot[q];
+    if (v == p) return q;
+    if (v == -1) {
+      int32_t prev = atomicCAS(&r.batch_slot[q], -1, p);
+      if (prev == -1 || prev == p) return q;
+    }
+  }
+  return -1;
+}
+
+// block-wide exclusive scan of n <= blockDim.x ints in place; returns the total
+__device__ int32_t block_exclusive_scan(int32_t* a, int n, int32_t* wave_tot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
+  int32_t v = tid < n ? a[tid] : 0;
+  int32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    int32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wave_tot[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    int32_t w = lane < nw ? wave_tot[lane] : 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      int32_t y = __shfl_up(w, o);
+      if (lane >= o) w += y;
+    }
+    if (lane < nw) wave_tot[lane] = w;   // inclusive wave prefix
+  }
+  __syncthreads();
+  int32_t excl = x - v + (wave > 0 ? wave_tot[wave - 1] : 0);
+  int32_t total = wave_tot[nw - 1];
+  __syncthreads();
+  if (tid < n) a[tid] = excl;
+  __syncthreads();
+  return total;
+}
+
+template <int VT, int AGG, bool FIRST>
+__global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBuf r) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int64_t* st_key = (int64_t*)smem;
+  int64_t* st_val = st_key + RT_TILE;
+  uint16_t* st_idx = (uint16_t*)(st_val + RT_TILE);
+  int32_t* cnt = (int32_t*)(st_idx + RT_TILE);      // [NBQ + 1]
+  int32_t* wtot = cnt + (RT_Q * 256 + 1);            // [16]
+  const int nbq = RT_Q * s.nb;
+  const int64_t t = blockIdx.x;
+  const int64_t base = t * RT_TILE;
+  for (int x = threadIdx.x; x <= nbq; x += blockDim.x) cnt[x] = 0;
+  __syncthreads();
+  constexpr int PER = RT_TILE / RT_THREADS;
+  int32_t bid[PER], rank[PER];
+  int64_t kk[PER], vv[PER];
+  const uint64_t kbm = (1ull << s.kb_bits) - 1;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int64_t i = base + (int64_t)k * RT_THREADS + threadIdx.x;
+    const bool valid = i < b.n;
+    int64_t key = 0, ts = 0, v = 0;
+    int32_t h = 0;
+    if (valid) {
+      key = b.key[i];
+      ts = b.ts[i];
+      v = b.val[i];
+      h = b.key_hash ? b.key_hash[i] : long_hash_code(key);
+    }
+    bool ok = valid;
+    if (ok && ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
+    if (ok) {
+      int32_t kg = key_group_for_hash(h, s.mp);
+      if (kg < s.kg_start || kg > s.kg_end) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
+    }
+    RecWin w;
+    w.m = 0; w.n_late = 0; w.n_fire = 0; w.n_windows = 0; w.quirk = false;
+    if (ok) {
+      w = record_windows(s, ts, b.wm);
+      if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
+    }
+    {
+      unsigned long long late = ok ? (unsigned long long)w.n_late : 0ull;
+      if (__any(late != 0)) {
+        for (int off = 32; off > 0; off >>= 1) late += __shfl_xor(late, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late);
+      }
+    }
+    bool live = ok && (w.n_windows - w.n_late) > 0;
+    const bool late_fire = live && w.n_fire > 0;
+    // slice slot + batch slice index: one lane per wave when the wave sits in one slice
+    const uint64_t lm = __ballot(live);
+    const int leader = lm ? __ffsll((long long)lm) - 1 : 0;
+    const int64_t m0 = __shfl(w.m, leader);
+    const bool uniform = __all(!live || w.m == m0);
+    int32_t p = -1, q = -1;
+    if (uniform) {
+      int32_t p0 = -1, q0 = -1;
+      if ((int)(threadIdx.x & 63) == leader && lm != 0) {
+        p0 = slice_slot(s, m0);
+        if (p0 >= 0) q0 = batch_slice_q(r, p0);
+      }
+      p0 = __shfl(p0, leader);
+      q0 = __shfl(q0, leader);
+      p = live ? p0 : -1;
+      q = live ? q0 : -1;
+    } else if (live) {
+      p = slice_slot(s, w.m);
+      if (p >= 0) q = batch_slice_q(r, p);
+    }
+    if (live && p < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
+    bid[k] = -1;
+    rank[k] = 0;
+    kk[k] = key;
+    vv[k] = v;
+    const bool routed = live && !late_fire && q >= 0 && key != EMPTY_KEY;
+    const bool direct = live && !routed;   // per-element fire, overflow slice, or the Long.MIN_VALUE key
+    int64_t kid = -1;
+    if (direct) {
+      kid = dir_find_or_insert(s, key);
+      if (kid < 0) set_error(s.err, FW_ERR_CAPACITY);
+    }
+    if (b.late_key) {
+      const bool want = direct && kid >= 0 && late_fire;
+      unsigned long long pos = wave_append(b.late_count, want);
+      if (want) {
+        if ((int64_t)pos < b.late_capacity) {
+          unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
+          b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
+        } else {
+          set_error(s.err, FW_ERR_CAPACITY);
+        }
+      }
+    }
+    if (direct && !late_fire && kid >= 0) {
+      pane_update<VT, AGG, FIRST>(s, (int64_t)p * s.stride + kid, v, b.ord_base + i);
+      if (s.touched[p] == 0) s.touched[p] = 1;
+    }
+    if (routed) {
+      const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
+      bid[k] = q * s.nb + (int32_t)(home >> s.kb_bits);
+      rank[k] = atomicAdd(&cnt[bid[k]], 1);
+    }
+    (void)kbm;
+  }
+  __syncthreads();
+  // segment table of this tile (counts before the scan)
+  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_len[(int64_t)x * r.ntiles + t] = cnt[x];
+  const int32_t total = block_exclusive_scan(cnt, nbq, wtot);
+  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_start[(int64_t)x * r.ntiles + t] = cnt[x];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (bid[k] >= 0) {
+      const int32_t pos = cnt[bid[k]] + rank[k];
+      st_key[pos] = kk[k];
+      st_val[pos] = vv[k];
+      st_idx[pos] = (uint16_t)(k * RT_THREADS + threadIdx.x);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < total; j += blockDim.x) {
+    r.key[base + j] = st_key[j];
+    r.val[base + j] = st_val[j];
+    if (FIRST) r.idx[base + j] = st_idx[j];
+  }
+}
+
+template <int VT, int AGG, bool FIRST>
+__global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, const int64_t* f1col, int64_t ord_base) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int bid = blockIdx.x;
+  const int q = bid / s.nb, bkt = bid % s.nb;
+  const int32_t p = r.batch_slot[q];
+  if (p < 0) return;
+  const int KB = 1 << s.kb_bits;
+  const uint64_t kbm = (uint64_t)KB - 1;
+  int64_t* ldir = (int64_t*)smem;                       // [KB]
+  int64_t* lsum = ldir + KB;                            // [KB]
+  int64_t* lmin = lsum + KB;                            // [KB] (AGG 15)
+  int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KB : 0);
+  int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KB : 0);
+  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KB : 0));  // [KB]
+  int32_t* segoff = (int32_t*)(lfirst + KB);            // [ntiles + 1]
+  int32_t* wtot = segoff + r.ntiles + 1;                // [16]
+  const int64_t dbase = (int64_t)bkt * KB;
+  for (int x = threadIdx.x; x < KB; x += blockDim.x) {
+    ldir[x] = s.dir_keys[dbase + x];
+    lsum[x] = 0;
+    if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
+    if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
+    if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
+    lfirst[x] = NO_FIRST;
+  }
+  // segment prefix over tiles, in chunks of blockDim
+  int32_t run = 0;
+  for (int t0 = 0; t0 < r.ntiles; t0 += blockDim.x) {
+    const int n = min((int)blockDim.x, r.ntiles - t0);
+    __syncthreads();
+    if ((int)threadIdx.x < n) segoff[t0 + threadIdx.x] = r.seg_len[(int64_t)bid * r.ntiles + t0 + threadIdx.x];
+    __syncthreads();
+    int32_t tot = block_exclusive_scan(segoff + t0, n, wtot);
+    if ((int)threadIdx.x < n) segoff[t0 + threadIdx.x] += run;
+    run += tot;
+  }
+  if (threadIdx.x == 0) segoff[r.ntiles] = run;
+  __syncthreads();
+  const int32_t total = run;
+  for (int32_t g = threadIdx.x; g < total; g += blockDim.x) {
+    // tile of record g: last t with segoff[t] <= g
+    int lo = 0, hi = r.ntiles;
+    while (hi - lo > 1) {
+      int mid = (lo + hi) >> 1;
+      if (segoff[mid] <= g) lo = mid; else hi = mid;
+    }
+    const int t = lo;
+    const int64_t ri = (int64_t)t * RT_TILE + r.seg_start[(int64_t)bid * r.ntiles + t] + (g - segoff[t]);
+    const int64_t key = r.key[ri];
+    const int64_t v = r.val[ri];
+    const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
+    uint64_t kl = home & kbm;
+    bool found = false;
+    for (uint64_t probe = 0; probe <= kbm; ++probe) {
+      int64_t cur = ldir[kl];
+      if (cur == key) { found = true; break; }
+      if (cur == EMPTY_KEY) {
+        unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)kl],
+                                            (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+        int64_t now = (int64_t)prev == EMPTY_KEY ? key : (int64_t)prev;
+        ldir[kl] = now;   // only globally confirmed keys enter the cache
+        if (now == key) { found = true; break; }
+      }
+      kl = (kl + 1) & kbm;
+    }
+    if (!found) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+    if (AGG & FW_AGG_SUM) {
+      if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
+      else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
+    }
+    if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
+    if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
+    if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
+    const uint32_t oi = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
+    atomicMin(&lfirst[kl], oi);
+  }
+  __syncthreads();
+  // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
+  for (int x = threadIdx.x; x < KB; x += blockDim.x) {
+    const uint32_t lf = lfirst[x];
+    if (lf == NO_FIRST) continue;
+    const int64_t idx = (int64_t)p * s.stride + dbase + x;
+    if (AGG & FW_AGG_SUM) {
+      if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[x]);
+      else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(lsum[x]));
+    }
+    if (AGG & FW_AGG_MIN) { int64_t o = s.c.mn[idx]; if (lmin[x] < o) s.c.mn[idx] = lmin[x]; }
+    if (AGG & FW_AGG_MAX) { int64_t o = s.c.mx[idx]; if (lmax[x] > o) s.c.mx[idx] = lmax[x]; }
+    if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[x]);
+    if (FIRST) {
+      if (s.c.first[idx] == INT64_MAX) {   // pane created in this batch: its first arrival is ours
+        s.c.first[idx] = ord_base + (int64_t)lf;
+        s.c.f1v[idx] = f1col[lf];
+      }
+    } else {
+      s.c.present[idx] = 1;
     }
   }
 }
@@ -807,6 +1106,11 @@ struct fw_engine {
   FireTask* tasks = nullptr;
   int32_t max_tasks = 0;
   WmPlan* plan = nullptr;
+  // partitioned ingest (ingest_mode 2)
+  bool routed = false;
+  RouteBuf rb{};
+  int32_t max_tiles = 0;
+  size_t route_lds = 0, agg_lds = 0;
   // partition scratch
   int64_t* part_block_counts = nullptr;
   int64_t part_blocks_cap = 0;
@@ -852,6 +1156,25 @@ static void launch_ingest_t(fw_engine* e, const BatchIn& b) {
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL((k_ingest_direct<VT, AGG, FIRST>), dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b);
 }
+template <int VT, int AGG, bool FIRST>
+static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_route<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)e->route_lds);
+    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)e->agg_lds);
+    attr_set = true;
+  }
+  RouteBuf r = e->rb;
+  r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
+  const size_t agg_lds = e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 4;
+  (void)hipMemsetAsync(r.batch_slot, 0xFF, sizeof(int32_t) * RT_Q, e->stream);
+  hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, e->stream, e->s, b, r);
+  hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST>), dim3(RT_Q * e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, r,
+                     f1col, b.ord_base);
+}
+
 template <int VT, int AGG, bool FIRST>
 static void launch_fire_t(fw_engine* e) {
   int blocks = (int)std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid);
@@ -928,6 +1251,12 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
 
   s.D = next_pow2(std::max<int64_t>(2 * c.key_capacity, 64));
   s.dir_mask = (uint64_t)s.D - 1;
+  {
+    int dbits = bits_for((uint64_t)s.D) - 1;                  // D = 2^dbits
+    int kb = std::max(std::min(dbits, 9), dbits - 8);          // <= 256 buckets of >= 512 slots
+    s.kb_bits = kb;
+    s.nb = (int32_t)(s.D >> kb);
+  }
   s.stride = s.D + 1;
   int32_t P = c.max_open_slices;
   if (P <= 0) {
@@ -978,6 +1307,28 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   e->st_f1 = e->alloc<int64_t>((size_t)c.max_batch);
   e->st_hash = e->alloc<int32_t>((size_t)c.max_batch);
 
+  // ingest form: partitioned (LDS pre-aggregation) when a directory bucket fits in LDS and
+  // batches are large; direct atomics otherwise
+  {
+    const int KB = 1 << s.kb_bits;
+    const bool fits = KB <= 1024 && c.max_batch >= 4096 && c.max_batch <= (1ll << 26);
+    if (c.ingest_mode == 2 && !fits) return unsupported("partitioned ingest needs <= 1024 directory slots per bucket");
+    e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && c.max_batch >= (1 << 16));
+    if (e->routed) {
+      e->max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
+      const size_t cap = (size_t)e->max_tiles * RT_TILE;
+      e->rb.key = e->alloc<int64_t>(cap);
+      e->rb.val = e->alloc<int64_t>(cap);
+      e->rb.idx = e->alloc<uint16_t>(cap);
+      e->rb.seg_start = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
+      e->rb.seg_len = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
+      e->rb.batch_slot = e->alloc<int32_t>(RT_Q);
+      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
+      const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
+      e->agg_lds = (size_t)KB * (8 * ncols + 4) + 4 * (size_t)(e->max_tiles + 1 + 16);
+      if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
+    }
+  }
   e->max_tasks = std::max(64, 4 * P);
   e->tasks = e->alloc<FireTask>((size_t)e->max_tasks);
   e->plan = e->alloc<WmPlan>(1);
@@ -1077,7 +1428,8 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.late_capacity = e->late_key ? e->cfg.max_batch : 0;
   b.idx_bits = e->idx_bits;
   e->phase_begin(FW_PHASE_INGEST);
-  FW_DISPATCH(launch_ingest_t, e, b);
+  if (e->routed) FW_DISPATCH(launch_routed_t, e, b, df1);
+  else FW_DISPATCH(launch_ingest_t, e, b);
   e->phase_end(n);
   HIPCHK(e, hipGetLastError());
   if (e->s.first) {

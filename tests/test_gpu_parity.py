@@ -28,18 +28,26 @@ def oracle_engine():
     return OracleEngine
 
 
+MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned")]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("name", WINDOW_FIXTURES)
-def test_golden_fixture(hip, name):
+def test_golden_fixture(hip, name, mode):
     fx = load_golden(name)
-    got = replay(fx, hip)
+    got = replay(fx, hip, ingest_mode=mode)
     assert got == expected_epochs(fx), fx["source"]
 
 
-def _cfg(assigner, fields=("sum",), vt="i64", first=False, lateness=0, trigger=None, **kw):
+def _cfg(assigner, fields=("sum",), vt="i64", first=False, lateness=0, trigger=None, mode=0, **kw):
     from flink_amd.windowing import ReduceFunction, make_config
-    args = dict(key_capacity=1 << 14, max_batch=1 << 16, out_capacity=1 << 20)
+    args = dict(key_capacity=1 << 14, max_batch=1 << 16, out_capacity=1 << 20, ingest_mode=mode)
     args.update(kw)
     return make_config(assigner, ReduceFunction(fields, vt, first), trigger, lateness, **args)
+
+
+def _cfgm(mode, *a, **kw):
+    return _cfg(*a, mode=mode, **kw)
 
 
 def _compare(a, b, fields, rel=0.0):
@@ -70,53 +78,59 @@ def _run_both(hip, oracle_engine, cfg, keys, ts, vals, batch, lag, fields, first
     return sg, so
 
 
-def test_tumbling_long_sum_first_arrival(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_tumbling_long_sum_first_arrival(hip, oracle_engine, mode):
     """C1 shape at small scale: keyed tumbling 1 s long-sum, f1 of the first arrival (Tuple3 job)."""
     from flink_amd.windowing import TumblingEventTimeWindows
     keys, ts, vals = gen_stream(200_000, 4096, rate=1 << 16)
-    cfg = _cfg(TumblingEventTimeWindows.of(1000), first=True)
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(1000), first=True)
     sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 1 << 14, 1, ["sum_i64"], first=True)
     assert sg["panes_fired"] == so["panes_fired"]
 
 
-def test_tumbling_all_fields_int(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_tumbling_all_fields_int(hip, oracle_engine, mode):
     from flink_amd.windowing import TumblingEventTimeWindows
     keys, ts, vals = gen_stream(100_000, 1000, rate=1 << 15, ooo=300)
-    cfg = _cfg(TumblingEventTimeWindows.of(1000, 250), ("sum", "min", "max", "count"))
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(1000, 250), ("sum", "min", "max", "count"))
     _run_both(hip, oracle_engine, cfg, keys, ts, vals, 10_000, 1, ["sum_i64", "min_i64", "max_i64", "count"])
 
 
-def test_sliding_double_multi_field(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_sliding_double_multi_field(hip, oracle_engine, mode):
     """C3 shape: sliding 10 s / 1 s, double sum/min/max/count (sum to 1e-9 relative)."""
     from flink_amd.windowing import SlidingEventTimeWindows
     keys, ts, vals = gen_stream(150_000, 2000, rate=1 << 13, value_type="f64")
-    cfg = _cfg(SlidingEventTimeWindows.of(10_000, 1000), ("sum", "min", "max", "count"), "f64", True)
+    cfg = _cfgm(mode, SlidingEventTimeWindows.of(10_000, 1000), ("sum", "min", "max", "count"), "f64", True)
     _run_both(hip, oracle_engine, cfg, keys, ts, vals, 8192, 1, ["sum_f64", "min_f64", "max_f64", "count"],
               first=True, rel=1e-9)
 
 
-def test_sliding_uneven_slide(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_sliding_uneven_slide(hip, oracle_engine, mode):
     """size not a multiple of slide: slices of gcd(size, slide)."""
     from flink_amd.windowing import SlidingEventTimeWindows
     keys, ts, vals = gen_stream(60_000, 300, rate=1 << 12, ooo=700)
-    cfg = _cfg(SlidingEventTimeWindows.of(2500, 1000, 300), ("sum", "count"))
+    cfg = _cfgm(mode, SlidingEventTimeWindows.of(2500, 1000, 300), ("sum", "count"))
     _run_both(hip, oracle_engine, cfg, keys, ts, vals, 3000, 500, ["sum_i64", "count"])
 
 
-def test_zipf_out_of_order_lateness(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_zipf_out_of_order_lateness(hip, oracle_engine, mode):
     """C4 shape: Zipf(1.2) keys, out-of-order ts, bounded WM lag, allowed lateness -> per-element fires."""
     from flink_amd.windowing import TumblingEventTimeWindows
     keys, ts, vals = gen_stream(200_000, 1 << 12, rate=1 << 16, zipf=1.2, ooo=200)
-    cfg = _cfg(TumblingEventTimeWindows.of(1000), ("sum", "count"), first=True, lateness=100)
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(1000), ("sum", "count"), first=True, lateness=100)
     sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 1 << 14, 150, ["sum_i64", "count"], first=True)
     assert so["late_fires"] > 0 and sg["late_fires"] == so["late_fires"]
     assert sg["records_late"] == so["records_late"] and so["records_late"] > 0
 
 
-def test_purging_trigger_lateness(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_purging_trigger_lateness(hip, oracle_engine, mode):
     from flink_amd.windowing import EventTimeTrigger, PurgingTrigger, TumblingEventTimeWindows
     keys, ts, vals = gen_stream(80_000, 500, rate=1 << 14, ooo=400)
-    cfg = _cfg(TumblingEventTimeWindows.of(500), ("sum", "max"), first=True, lateness=300,
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(500), ("sum", "max"), first=True, lateness=300,
                trigger=PurgingTrigger.of(EventTimeTrigger.create()))
     _run_both(hip, oracle_engine, cfg, keys, ts, vals, 4000, 350, ["sum_i64", "max_i64"], first=True)
 
@@ -141,13 +155,14 @@ def test_java_double_min_max_semantics(hip, oracle_engine):
     eg.close(); eo.close()
 
 
-def test_extreme_keys_and_timestamps(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_extreme_keys_and_timestamps(hip, oracle_engine, mode):
     """Long.MIN_VALUE / MAX_VALUE keys, negative timestamps, the cleanup-time clamp."""
     from flink_amd.windowing import TumblingEventTimeWindows
     keys = np.array([-(1 << 63), LONG_MAX, 0, -1, 1 << 32, -(1 << 63), 7], np.int64)
     ts = np.array([-5000, -5000, -1, 0, 999, -4999, LONG_MAX - 10], np.int64)
     vals = np.array([1, 2, 3, 4, 5, 6, 7], np.int64)
-    cfg = _cfg(TumblingEventTimeWindows.of(1000, -300), ("sum", "count"), lateness=5000)
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(1000, -300), ("sum", "count"), lateness=5000)
     eg, eo = hip(cfg), oracle_engine(cfg)
     rg = drive(eg, keys, ts, vals, 7, 0, LONG_MAX)
     ro = drive(eo, keys, ts, vals, 7, 0, LONG_MAX)
@@ -175,12 +190,13 @@ def test_foreign_key_group_fails(hip):
     e.close()
 
 
-def test_device_resident_input(hip, oracle_engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_device_resident_input(hip, oracle_engine, mode):
     """Columns already in HBM (torch tensors): no host copy on the push path."""
     import torch
     from flink_amd.windowing import TumblingEventTimeWindows
     keys, ts, vals = gen_stream(50_000, 777, rate=1 << 14)
-    cfg = _cfg(TumblingEventTimeWindows.of(1000), first=True)
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(1000), first=True)
     eg = hip(cfg)
     dk, dt, dv = (torch.from_numpy(a).cuda() for a in (keys, ts, vals))
     out = []
