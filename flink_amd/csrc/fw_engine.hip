@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan_by_key.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -670,12 +671,13 @@ struct LateCombine {
 };
 
 __global__ void k_late_prepare(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
-                               const int64_t* val, unsigned long long* seg, LateAcc* acc) {
+                               const int64_t* val, unsigned long long* seg, LateAcc* acc, int64_t* headpos) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nl) return;
   unsigned long long k = sorted_key[j];
   int64_t i = (int64_t)(k & ((1ull << idx_bits) - 1));
   seg[j] = k >> idx_bits;
+  headpos[j] = (j == 0 || (sorted_key[j - 1] >> idx_bits) != (k >> idx_bits)) ? j : 0;
   int64_t v = val[i];
   LateAcc a;
   a.vt = s.vt;
@@ -723,7 +725,7 @@ __device__ __forceinline__ int64_t slot_max_ts(const Spec& s, int32_t p) {
 // emit one result per late record: state(base) (+) prefix
 __global__ void k_late_emit(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
                             const unsigned long long* seg, const LateAcc* acc, const LateAcc* scanned,
-                            const int64_t* f1col, int64_t ord_base) {
+                            const int64_t* f1col, int64_t ord_base, const int64_t* headpos) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool act = j < nl;
   unsigned long long pos = wave_append(s.o.count, act);
@@ -749,9 +751,7 @@ __global__ void k_late_emit(Spec s, const unsigned long long* sorted_key, int64_
     } else if (base_present) {
       f1 = s.c.f1v[idx];
     } else {
-      int64_t jh = j;
-      while (jh > 0 && seg[jh - 1] == pane) --jh;
-      f1 = f1col[(int64_t)(sorted_key[jh] & ((1ull << idx_bits) - 1))];
+      f1 = f1col[(int64_t)(sorted_key[headpos[j]] & ((1ull << idx_bits) - 1))];
     }
   }
   emit_record(s, pos, kid_key(s, kid), f1, slot_max_ts(s, p), out);
@@ -760,7 +760,7 @@ __global__ void k_late_emit(Spec s, const unsigned long long* sorted_key, int64_
 // write the pane state after the batch's per-element fires (segment tails)
 __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
                               const unsigned long long* seg, const LateAcc* scanned, const int64_t* f1col,
-                              int64_t ord_base) {
+                              int64_t ord_base, const int64_t* headpos) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nl) return;
   unsigned long long pane = seg[j];
@@ -785,9 +785,7 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
   if (s.c.mx) s.c.mx[idx] = st.mx;
   if (s.c.cnt) s.c.cnt[idx] = st.cnt;
   if (!base_present) {
-    int64_t jh = j;
-    while (jh > 0 && seg[jh - 1] == pane) --jh;
-    int64_t ih = (int64_t)(sorted_key[jh] & ((1ull << idx_bits) - 1));
+    int64_t ih = (int64_t)(sorted_key[headpos[j]] & ((1ull << idx_bits) - 1));
     if (s.first) { s.c.first[idx] = ord_base + ih; s.c.f1v[idx] = f1col[ih]; }
     else s.c.present[idx] = 1;
   }
@@ -1069,6 +1067,7 @@ struct fw_engine {
   unsigned long long *late_key = nullptr, *late_key_sorted = nullptr, *late_count = nullptr, *seg = nullptr;
   unsigned long long *late_idx_in = nullptr, *late_idx_out = nullptr;
   LateAcc *late_acc = nullptr, *late_scan = nullptr;
+  int64_t *headpos = nullptr, *headpos_scan = nullptr;
   void* temp = nullptr;
   size_t temp_bytes = 0;
   int32_t idx_bits = 0;
@@ -1347,11 +1346,15 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->seg = e->alloc<unsigned long long>(nb);
     e->late_acc = e->alloc<LateAcc>(nb);
     e->late_scan = e->alloc<LateAcc>(nb);
-    size_t t1 = 0, t2 = 0;
+    e->headpos = e->alloc<int64_t>(nb);
+    e->headpos_scan = e->alloc<int64_t>(nb);
+    size_t t1 = 0, t2 = 0, t3 = 0;
     (void)rocprim::radix_sort_keys(nullptr, t1, e->late_key, e->late_key_sorted, (size_t)c.max_batch, 0, 64, e->stream);
     (void)rocprim::deterministic_inclusive_scan_by_key(nullptr, t2, e->seg, e->late_acc, e->late_scan, (size_t)c.max_batch,
                                                  LateCombine(), rocprim::equal_to<unsigned long long>(), e->stream);
-    e->temp_bytes = std::max(t1, t2);
+    (void)rocprim::inclusive_scan(nullptr, t3, e->headpos, e->headpos_scan, (size_t)c.max_batch,
+                                  rocprim::maximum<int64_t>(), e->stream);
+    e->temp_bytes = std::max(std::max(t1, t2), t3);
     e->temp = e->alloc<char>(e->temp_bytes);
     for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
   } else {
@@ -1451,14 +1454,17 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
       HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, e->late_key, e->late_key_sorted, (size_t)nl, 0, 64, e->stream));
       int blocks = (int)((nl + BLOCK - 1) / BLOCK);
       hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
-                         e->idx_bits, dv, e->seg, e->late_acc);
+                         e->idx_bits, dv, e->seg, e->late_acc, e->headpos);
+      tb = e->temp_bytes;
+      HIPCHK(e, rocprim::inclusive_scan(e->temp, tb, e->headpos, e->headpos_scan, (size_t)nl,
+                                        rocprim::maximum<int64_t>(), e->stream));
       tb = e->temp_bytes;
       HIPCHK(e, rocprim::deterministic_inclusive_scan_by_key(e->temp, tb, e->seg, e->late_acc, e->late_scan, (size_t)nl,
                                                              LateCombine(), rocprim::equal_to<unsigned long long>(), e->stream));
       hipLaunchKernelGGL(k_late_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
-                         e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, e->ordinal);
+                         e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, e->ordinal, e->headpos_scan);
       hipLaunchKernelGGL(k_late_commit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
-                         e->idx_bits, e->seg, e->late_scan, df1, e->ordinal);
+                         e->idx_bits, e->seg, e->late_scan, df1, e->ordinal, e->headpos_scan);
       e->phase_end((int64_t)nl);
       e->late_fires_host += (int64_t)nl;
       HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
