@@ -175,6 +175,7 @@ def main():
             fired, pushed = int(x[0].item()) & mask, int(x[1].item()) & mask
         check = "ok" if fired == pushed else "MISMATCH"
 
+    form = eng.stats()["ingest_form"]
     events = args.steps * batch * world
     value = events / dt
     ing_ms = prof.ms[_abi.FW_PHASE_INGEST]
@@ -198,7 +199,7 @@ def main():
                                f"{rate} events/s event time, watermark every {batch} events per source",
                    "batch_per_gpu": batch, "keys": n_keys, "max_parallelism": mp, "parallelism": f"kg{world}",
                    "reduce": "Tuple3(a.f0, a.f1, a.f2 + b.f2), f1 = first arrival"},
-        "roofline": {"bound": "hbm", "kernel": "k_ingest_direct", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_ingest_direct" if form == 1 else "k_route+k_aggregate", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "bytes_per_event": 24, "ingest_ms_per_launch": ing_ms / max(ing_n, 1),
                      "fire_ms_total": prof.ms[_abi.FW_PHASE_FIRE], "fixup_ms_total": prof.ms[_abi.FW_PHASE_FIXUP],

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
 constexpr int RT_TILE = 8192;
 constexpr int RT_THREADS = 1024;
 constexpr int RT_Q = 2;                 // slices per batch handled by the partitioned form
-constexpr int AG_THREADS = 512;
+constexpr int AG_THREADS = 1024;
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
@@ -558,8 +558,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KB : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KB : 0);
   uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KB : 0));  // [KB]
-  int32_t* segoff = (int32_t*)(lfirst + KB);            // [ntiles + 1]
-  int32_t* wtot = segoff + r.ntiles + 1;                // [16]
+  int32_t* segoff = (int32_t*)(lfirst + KB);            // [2 * ntiles]
   const int64_t dbase = (int64_t)bkt * KB;
   for (int x = threadIdx.x; x < KB; x += blockDim.x) {
     ldir[x] = s.dir_keys[dbase + x];
@@ -569,31 +568,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
     lfirst[x] = NO_FIRST;
   }
-  // segment prefix over tiles, in chunks of blockDim
-  int32_t run = 0;
-  for (int t0 = 0; t0 < r.ntiles; t0 += blockDim.x) {
-    const int n = min((int)blockDim.x, r.ntiles - t0);
-    __syncthreads();
-    if ((int)threadIdx.x < n) segoff[t0 + threadIdx.x] = r.seg_len[(int64_t)bid * r.ntiles + t0 + threadIdx.x];
-    __syncthreads();
-    int32_t tot = block_exclusive_scan(segoff + t0, n, wtot);
-    if ((int)threadIdx.x < n) segoff[t0 + threadIdx.x] += run;
-    run += tot;
+  // this (q, bucket)'s segment of every tile: (start, len) pairs in LDS
+  int32_t* segs = segoff;                               // [2 * ntiles]
+  for (int t = threadIdx.x; t < r.ntiles; t += blockDim.x) {
+    segs[2 * t] = r.seg_start[(int64_t)bid * r.ntiles + t];
+    segs[2 * t + 1] = r.seg_len[(int64_t)bid * r.ntiles + t];
   }
-  if (threadIdx.x == 0) segoff[r.ntiles] = run;
   __syncthreads();
-  const int32_t total = run;
-  for (int32_t g = threadIdx.x; g < total; g += blockDim.x) {
-    // tile of record g: last t with segoff[t] <= g
-    int lo = 0, hi = r.ntiles;
-    while (hi - lo > 1) {
-      int mid = (lo + hi) >> 1;
-      if (segoff[mid] <= g) lo = mid; else hi = mid;
-    }
-    const int t = lo;
-    const int64_t ri = (int64_t)t * RT_TILE + r.seg_start[(int64_t)bid * r.ntiles + t] + (g - segoff[t]);
-    const int64_t key = r.key[ri];
-    const int64_t v = r.val[ri];
+  auto process = [&](int64_t key, int64_t v, uint32_t oi) {
     const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
     uint64_t kl = home & kbm;
     bool found = false;
@@ -609,7 +591,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
       }
       kl = (kl + 1) & kbm;
     }
-    if (!found) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+    if (!found) { set_error(s.err, FW_ERR_CAPACITY); return; }
     if (AGG & FW_AGG_SUM) {
       if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
       else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
@@ -617,8 +599,44 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
-    const uint32_t oi = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
     atomicMin(&lfirst[kl], oi);
+  };
+  // each wave takes AG_UNROLL segments per round, one record per lane, all loads issued before any
+  // LDS work so that AG_UNROLL HBM round trips overlap; records past a segment's first 64 follow
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  constexpr int U = 8;
+  for (int t0 = wave * U; t0 < r.ntiles; t0 += nw * U) {
+    int64_t kk[U], vv[U];
+    uint32_t oo[U];
+    bool has[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u;
+      has[u] = false;
+      if (t < r.ntiles) {
+        const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
+        if (lane < ln) {
+          const int64_t ri = (int64_t)t * RT_TILE + st + lane;
+          kk[u] = r.key[ri];
+          vv[u] = r.val[ri];
+          oo[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
+          has[u] = true;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (has[u]) process(kk[u], vv[u], oo[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // long segments (hot keys)
+      const int t = t0 + u;
+      if (t >= r.ntiles) continue;
+      const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
+      for (int j = 64 + lane; j < ln; j += 64) {
+        const int64_t ri = (int64_t)t * RT_TILE + st + j;
+        process(r.key[ri], r.val[ri], (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u));
+      }
+    }
   }
   __syncthreads();
   // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
@@ -1167,7 +1185,7 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   }
   RouteBuf r = e->rb;
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
-  const size_t agg_lds = e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 4;
+  const size_t agg_lds = e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8;
   (void)hipMemsetAsync(r.batch_slot, 0xFF, sizeof(int32_t) * RT_Q, e->stream);
   hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, e->stream, e->s, b, r);
   hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST>), dim3(RT_Q * e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, r,
@@ -1324,7 +1342,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       e->rb.batch_slot = e->alloc<int32_t>(RT_Q);
       e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
       const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-      e->agg_lds = (size_t)KB * (8 * ncols + 4) + 4 * (size_t)(e->max_tiles + 1 + 16);
+      e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles;
       if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
     }
   }
@@ -1575,6 +1593,7 @@ int fw_get_stats(fw_engine* e, fw_stats* st) {
   for (int64_t t : tags) live += t != FREE_TAG;
   st->slices_live = live;
   st->keys_resident = -1;
+  st->ingest_form = e->routed ? 2 : 1;
   return FW_OK;
 }
 

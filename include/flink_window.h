@@ -137,6 +137,7 @@ typedef struct {
   int64_t late_fires;        /* per-element fires (allowed lateness > 0)      */
   int64_t keys_resident;     /* distinct keys in the key directory            */
   int64_t slices_live;       /* pane slices resident                          */
+  int64_t ingest_form;       /* 1 = direct atomics, 2 = partitioned + LDS     */
 } fw_stats;
 
 int         fw_create(const fw_config* cfg, fw_engine** out);

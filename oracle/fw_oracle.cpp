@@ -426,6 +426,7 @@ int fwo_get_stats(fw_engine* e, fw_stats* st) {
   size_t keys = 0;
   for (auto& m : e->op.state) for (auto& kv : m) keys += kv.second.size();
   st->keys_resident = (int64_t)keys;
+  st->ingest_form = 0;
   return FW_OK;
 }
 
