@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--ingest-mode", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 23, help="events in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="events in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
     return ap.parse_args()
 

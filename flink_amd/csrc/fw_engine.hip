@@ -26,6 +26,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -266,6 +267,8 @@ struct BatchIn {
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t c_m = INT64_MIN;   // per-wave cache of the last slice -> slot lookup
+  int32_t c_p = -1;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < b.n; i0 += stride) {
     int64_t i = i0 + threadIdx.x;
     bool valid = i < b.n;
@@ -306,10 +309,13 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
     const bool uniform = __all(!live || w.m == m0);
     int32_t p = -1;
     if (uniform) {
-      int32_t p0 = -1;
-      if ((int)(threadIdx.x & 63) == leader && lm != 0) p0 = slice_slot(s, m0);
-      p0 = __shfl(p0, leader);
-      p = live ? p0 : -1;
+      if (lm != 0 && m0 != c_m) {   // wave-uniform: resolve once per slice change
+        int32_t p0 = -1;
+        if ((int)(threadIdx.x & 63) == leader) p0 = slice_slot(s, m0);
+        c_p = __shfl(p0, leader);
+        c_m = c_p >= 0 ? m0 : INT64_MIN;
+      }
+      p = live ? c_p : -1;
     } else if (live) {
       p = slice_slot(s, w.m);
     }
@@ -374,6 +380,7 @@ struct RouteBuf {
   int32_t* seg_len;
   int32_t* batch_slot;   // [RT_Q] pane-slice slot of batch slice q, -1 if unused
   int32_t ntiles;
+  int32_t dbg;           // ablation knob (FW_DEBUG_AGG): 0 normal, 1 loads only, 2 no LDS atomics
 };
 
 __device__ __forceinline__ int32_t batch_slice_q(const RouteBuf& r, int32_t p) {
@@ -431,20 +438,31 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
   __syncthreads();
   constexpr int PER = RT_TILE / RT_THREADS;
   int32_t bid[PER], rank[PER];
-  int64_t kk[PER], vv[PER];
-  const uint64_t kbm = (1ull << s.kb_bits) - 1;
+  int64_t kk[PER], vv[PER], tt[PER];
+  int32_t hh[PER];
+  // phase A: every load of the tile in flight before any dependent work
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int64_t i = base + (int64_t)k * RT_THREADS + threadIdx.x;
+    kk[k] = 0; tt[k] = 0; vv[k] = 0; hh[k] = 0;
+    if (i < b.n) {
+      kk[k] = b.key[i];
+      tt[k] = b.ts[i];
+      vv[k] = b.val[i];
+      if (b.key_hash) hh[k] = b.key_hash[i];
+    }
+  }
+  // phase B: per record; the (slice -> slot, batch slice) lookup is cached per wave, as a wave of an
+  // in-order stream stays in one slice for the whole tile
+  int64_t c_m = INT64_MIN;
+  int32_t c_p = -1, c_q = -1;
+  unsigned long long late_pairs = 0;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int64_t i = base + (int64_t)k * RT_THREADS + threadIdx.x;
     const bool valid = i < b.n;
-    int64_t key = 0, ts = 0, v = 0;
-    int32_t h = 0;
-    if (valid) {
-      key = b.key[i];
-      ts = b.ts[i];
-      v = b.val[i];
-      h = b.key_hash ? b.key_hash[i] : long_hash_code(key);
-    }
+    const int64_t key = kk[k], ts = tt[k], v = vv[k];
+    const int32_t h = b.key_hash ? hh[k] : long_hash_code(key);
     bool ok = valid;
     if (ok && ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
     if (ok) {
@@ -457,31 +475,28 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
       w = record_windows(s, ts, b.wm);
       if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
     }
-    {
-      unsigned long long late = ok ? (unsigned long long)w.n_late : 0ull;
-      if (__any(late != 0)) {
-        for (int off = 32; off > 0; off >>= 1) late += __shfl_xor(late, off);
-        if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late);
-      }
-    }
+    if (ok) late_pairs += (unsigned long long)w.n_late;
     bool live = ok && (w.n_windows - w.n_late) > 0;
     const bool late_fire = live && w.n_fire > 0;
-    // slice slot + batch slice index: one lane per wave when the wave sits in one slice
     const uint64_t lm = __ballot(live);
     const int leader = lm ? __ffsll((long long)lm) - 1 : 0;
     const int64_t m0 = __shfl(w.m, leader);
     const bool uniform = __all(!live || w.m == m0);
     int32_t p = -1, q = -1;
     if (uniform) {
-      int32_t p0 = -1, q0 = -1;
-      if ((int)(threadIdx.x & 63) == leader && lm != 0) {
-        p0 = slice_slot(s, m0);
-        if (p0 >= 0) q0 = batch_slice_q(r, p0);
+      if (lm != 0 && m0 != c_m) {   // wave-uniform branch
+        int32_t p0 = -1, q0 = -1;
+        if ((int)(threadIdx.x & 63) == leader) {
+          p0 = slice_slot(s, m0);
+          if (p0 >= 0) q0 = batch_slice_q(r, p0);
+        }
+        c_p = __shfl(p0, leader);
+        c_q = __shfl(q0, leader);
+        c_m = c_p >= 0 ? m0 : INT64_MIN;
+        if (c_p < 0) { p = -1; q = -1; }
       }
-      p0 = __shfl(p0, leader);
-      q0 = __shfl(q0, leader);
-      p = live ? p0 : -1;
-      q = live ? q0 : -1;
+      p = live ? c_p : -1;
+      q = live ? c_q : -1;
     } else if (live) {
       p = slice_slot(s, w.m);
       if (p >= 0) q = batch_slice_q(r, p);
@@ -489,8 +504,6 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     if (live && p < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
     bid[k] = -1;
     rank[k] = 0;
-    kk[k] = key;
-    vv[k] = v;
     const bool routed = live && !late_fire && q >= 0 && key != EMPTY_KEY;
     const bool direct = live && !routed;   // per-element fire, overflow slice, or the Long.MIN_VALUE key
     int64_t kid = -1;
@@ -519,7 +532,10 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
       bid[k] = q * s.nb + (int32_t)(home >> s.kb_bits);
       rank[k] = atomicAdd(&cnt[bid[k]], 1);
     }
-    (void)kbm;
+  }
+  if (__any(late_pairs != 0)) {
+    for (int off = 32; off > 0; off >>= 1) late_pairs += __shfl_xor(late_pairs, off);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late_pairs);
   }
   __syncthreads();
   // segment table of this tile (counts before the scan)
@@ -592,6 +608,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
       kl = (kl + 1) & kbm;
     }
     if (!found) { set_error(s.err, FW_ERR_CAPACITY); return; }
+    if (r.dbg == 2) { asm volatile("" :: "v"(kl), "v"(v), "v"(oi)); return; }
     if (AGG & FW_AGG_SUM) {
       if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
       else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
@@ -623,6 +640,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
           has[u] = true;
         }
       }
+    }
+    if (r.dbg == 1) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (has[u]) asm volatile("" :: "v"(kk[u]), "v"(vv[u]), "v"(oo[u]));
+      continue;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -1340,6 +1363,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       e->rb.seg_start = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
       e->rb.seg_len = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
       e->rb.batch_slot = e->alloc<int32_t>(RT_Q);
+      const char* dbg = getenv("FW_DEBUG_AGG");
+      e->rb.dbg = dbg ? atoi(dbg) : 0;
       e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
       const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
       e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles;
