@@ -595,10 +595,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
     uint64_t kl = home & kbm;
     bool found = false;
+    uint32_t nprobe = 0, ncas = 0;
     for (uint64_t probe = 0; probe <= kbm; ++probe) {
       int64_t cur = ldir[kl];
+      ++nprobe;
       if (cur == key) { found = true; break; }
       if (cur == EMPTY_KEY) {
+        if (r.dbg == 3) break;
+        ++ncas;
         unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)kl],
                                             (unsigned long long)EMPTY_KEY, (unsigned long long)key);
         int64_t now = (int64_t)prev == EMPTY_KEY ? key : (int64_t)prev;
@@ -606,6 +610,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
         if (now == key) { found = true; break; }
       }
       kl = (kl + 1) & kbm;
+    }
+    if (r.dbg >= 3) {
+      atomicAdd(&s.stats[5], (unsigned long long)nprobe);
+      atomicAdd(&s.stats[6], (unsigned long long)ncas);
+      atomicAdd(&s.stats[7], 1ull);
+      if (!found) return;
     }
     if (!found) { set_error(s.err, FW_ERR_CAPACITY); return; }
     if (r.dbg == 2) { asm volatile("" :: "v"(kl), "v"(v), "v"(oi)); return; }
@@ -1619,6 +1629,13 @@ int fw_get_stats(fw_engine* e, fw_stats* st) {
   st->slices_live = live;
   st->keys_resident = -1;
   st->ingest_form = e->routed ? 2 : 1;
+  return FW_OK;
+}
+
+int fw_debug_counters(fw_engine* e, int64_t* out8) {
+  if (!e || !out8) return FW_ERR_INVALID_ARG;
+  HIPCHK(e, hipMemcpyAsync(out8, e->s.stats, 8 * ST_NSTATS, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
   return FW_OK;
 }
 

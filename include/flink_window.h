@@ -178,6 +178,9 @@ typedef struct {
 int         fw_set_profiling(fw_engine* e, int32_t enable);
 int         fw_get_profile(fw_engine* e, fw_profile* out);   /* synchronises; resets the counters */
 
+/* diagnostics: raw device counters (8 x int64) */
+int         fw_debug_counters(fw_engine* e, int64_t* out8);
+
 /* library version string */
 const char* fw_version(void);
 
