@@ -443,14 +443,11 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
   // phase A: every load of the tile in flight before any dependent work
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int64_t i = base + (int64_t)k * RT_THREADS + threadIdx.x;
-    kk[k] = 0; tt[k] = 0; vv[k] = 0; hh[k] = 0;
-    if (i < b.n) {
-      kk[k] = b.key[i];
-      tt[k] = b.ts[i];
-      vv[k] = b.val[i];
-      if (b.key_hash) hh[k] = b.key_hash[i];
-    }
+    const int64_t i = min(base + (int64_t)k * RT_THREADS + threadIdx.x, b.n - 1);   // unconditional loads
+    kk[k] = b.key[i];
+    tt[k] = b.ts[i];
+    vv[k] = b.val[i];
+    hh[k] = b.key_hash ? b.key_hash[i] : 0;
   }
   // phase B: per record; the (slice -> slot, batch slice) lookup is cached per wave, as a wave of an
   // in-order stream stays in one slice for the whole tile
@@ -636,20 +633,17 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     int64_t kk[U], vv[U];
     uint32_t oo[U];
     bool has[U];
+    // unconditional loads (inactive lanes read record 0): the compiler cannot sink them into the
+    // per-record branches, so all U segments are in flight together
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = t0 + u;
-      has[u] = false;
-      if (t < r.ntiles) {
-        const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
-        if (lane < ln) {
-          const int64_t ri = (int64_t)t * RT_TILE + st + lane;
-          kk[u] = r.key[ri];
-          vv[u] = r.val[ri];
-          oo[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
-          has[u] = true;
-        }
-      }
+      const int t = min(t0 + u, r.ntiles - 1);
+      const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
+      has[u] = (t0 + u < r.ntiles) && lane < ln;
+      const int64_t ri = has[u] ? (int64_t)t * RT_TILE + st + lane : 0;
+      kk[u] = r.key[ri];
+      vv[u] = r.val[ri];
+      oo[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
     }
     if (r.dbg == 1) {
 #pragma unroll
@@ -1104,7 +1098,8 @@ struct fw_engine {
   fw_config cfg{};
   std::string err;
   int32_t sticky = FW_OK;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;       // stream all engine work is ordered on
+  hipStream_t own_stream = nullptr;   // the engine's own stream, if it created one
   Spec s{};
   int64_t cur_wm = INT64_MIN;
   int64_t ordinal = 0;
@@ -1177,7 +1172,8 @@ struct fw_engine {
     return (T*)p;
   }
   ~fw_engine() {
-    if (stream) { (void)hipStreamSynchronize(stream); (void)hipStreamDestroy(stream); }
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (own_stream) (void)hipStreamDestroy(own_stream);
     for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
@@ -1276,7 +1272,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     return unsupported("sliding windows with allowed lateness or PurgingTrigger are not implemented on the slice path");
   HIPCHK(e, hipSetDevice(c.device));
   e->dev = c.device;
-  HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  HIPCHK(e, hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+  e->stream = e->own_stream;
   hipDeviceProp_t prop;
   HIPCHK(e, hipGetDeviceProperties(&prop, c.device));
   e->grid = prop.multiProcessorCount * 8;
@@ -1636,6 +1633,15 @@ int fw_debug_counters(fw_engine* e, int64_t* out8) {
   if (!e || !out8) return FW_ERR_INVALID_ARG;
   HIPCHK(e, hipMemcpyAsync(out8, e->s.stats, 8 * ST_NSTATS, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  return FW_OK;
+}
+
+int fw_set_stream(fw_engine* e, void* stream) {
+  if (!e) return FW_ERR_INVALID_ARG;
+  HIPCHK(e, hipSetDevice(e->dev));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (e->own_stream) { HIPCHK(e, hipStreamDestroy(e->own_stream)); e->own_stream = nullptr; }
+  e->stream = (hipStream_t)stream;
   return FW_OK;
 }
 

@@ -178,10 +178,22 @@ class WindowEngine:
         if rc != 0:
             raise _abi.FwError(rc, self._fn("last_error")(self.h).decode())
 
+    def use_stream(self, stream_handle):
+        """Order engine work on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
+        if self.prefix == "fw":
+            self._check(self._fn("set_stream")(self.h, ctypes.c_void_p(stream_handle)))
+            self._stream = stream_handle
+
     def push(self, key, ts, value, key_hash=None, f1=None):
         n = len(key)
         if self.prefix == "fw":
             mem = _abi.FW_MEM_DEVICE if _is_device(key) else _abi.FW_MEM_HOST
+            if mem == _abi.FW_MEM_DEVICE:
+                # device columns are produced on torch's current stream: run the engine on it
+                import torch
+                cur = torch.cuda.current_stream(key.device).cuda_stream
+                if getattr(self, "_stream", None) != cur:
+                    self.use_stream(cur)
             self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n, mem))
         else:
             self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n))

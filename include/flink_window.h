@@ -178,6 +178,10 @@ typedef struct {
 int         fw_set_profiling(fw_engine* e, int32_t enable);
 int         fw_get_profile(fw_engine* e, fw_profile* out);   /* synchronises; resets the counters */
 
+/* Order all engine work on the caller's HIP stream (hipStream_t), e.g. the stream that produced
+ * device-resident input columns, instead of the engine's own stream.  Synchronises first. */
+int         fw_set_stream(fw_engine* e, void* stream);
+
 /* diagnostics: raw device counters (8 x int64) */
 int         fw_debug_counters(fw_engine* e, int64_t* out8);
 
