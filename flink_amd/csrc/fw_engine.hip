@@ -76,6 +76,7 @@ struct OutLog {
 struct Spec {  // window specification + reduce + subtask, passed by value
   int32_t assigner, trigger;
   int64_t size, slide, offset, lateness, g;
+  double inv_size, inv_g;   // reciprocals for jdivmod
   int32_t K;        // slices per window
   int32_t R;        // slices per slide
   int32_t mp, kg_start, kg_end;
@@ -192,8 +193,10 @@ __device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int6
   r.n_fire = 0;
   if (s.assigner == FW_TUMBLING) {
     int64_t x = jadd(jsub(ts, s.offset), s.size);
-    r.m = x / s.size - 1;                                        // start = offset + m * size
-    int64_t start = jsub(ts, x % s.size);                        // getWindowStartWithOffset
+    int64_t q, rem;
+    jdivmod(x, s.size, s.inv_size, q, rem);
+    r.m = q - 1;                                                 // start = offset + m * size
+    int64_t start = jsub(ts, rem);                               // getWindowStartWithOffset
     int64_t max_ts = jsub(jadd(start, s.size), 1);               // TimeWindow.maxTimestamp
     int64_t ct = cleanup_time(max_ts, s.lateness);
     r.n_windows = 1;
@@ -203,7 +206,11 @@ __device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int6
   }
   int64_t x = jadd(jsub(ts, s.offset), s.g);
   if (x < 0 || jadd(jsub(ts, s.offset), s.slide) < 0) r.quirk = true;   // Java % of a negative numerator
-  r.m = x / s.g - 1;
+  {
+    int64_t q, rem;
+    jdivmod(x, s.g, s.inv_g, q, rem);
+    r.m = q - 1;
+  }
   int64_t n_hi = floor_div(r.m, s.R);
   int64_t n_lo = floor_div(r.m - s.K, s.R) + 1;
   r.n_windows = (int32_t)(n_hi - n_lo + 1);
@@ -360,27 +367,28 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
 }
 
 // ------------------------------------------------------------------------------------------------
-// ingest, partitioned form: k_route counting-sorts each tile of RT_TILE records by
-// (batch slice q, directory bucket) through LDS and writes the tile back coalesced; k_aggregate
-// gives every (q, bucket) to one workgroup, which owns those panes exclusively: it probes the
-// bucket's directory slice cached in LDS, reduces all the bucket's records with LDS atomics, and
-// folds the result into the dense columns with plain read-modify-writes (one per pane per batch).
+// ingest, partitioned form.  k_route resolves each record's dense key id (directory
+// probe, L2-resident), counting-sorts a tile of RT_TILE records by (batch slice q, directory bucket)
+// through LDS and writes the tile back coalesced as 12 B records (kid-in-bucket | tile index, value).
+// k_aggregate gives every (q, bucket) to one workgroup: it owns those panes exclusively, reduces the
+// bucket's records with LDS atomics and folds the result into the dense columns with plain
+// read-modify-writes (one per pane per batch) — no device-scope atomics per record.
 // ------------------------------------------------------------------------------------------------
-constexpr int RT_TILE = 8192;
-constexpr int RT_THREADS = 1024;
+constexpr int RT_TILE = 4096;
+constexpr int RT_THREADS = 512;
 constexpr int RT_Q = 2;                 // slices per batch handled by the partitioned form
 constexpr int AG_THREADS = 1024;
+constexpr int RT_MAX_KB_BITS = 10;      // kid-in-bucket must fit the record's meta word
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
-  int64_t* key;          // [ntiles][RT_TILE]
-  int64_t* val;
-  uint16_t* idx;         // record index within its tile (first arrival)
+  uint32_t* meta;        // [ntiles][RT_TILE]  kid-in-bucket (low 16 bits) | index in tile (high 16)
+  int64_t* val;          // [ntiles][RT_TILE]
   int32_t* seg_start;    // [NBQ][ntiles] start of (q,bucket) segment within the tile
   int32_t* seg_len;
   int32_t* batch_slot;   // [RT_Q] pane-slice slot of batch slice q, -1 if unused
   int32_t ntiles;
-  int32_t dbg;           // ablation knob (FW_DEBUG_AGG): 0 normal, 1 loads only, 2 no LDS atomics
+  int32_t dbg;
 };
 
 __device__ __forceinline__ int32_t batch_slice_q(const RouteBuf& r, int32_t p) {
@@ -423,33 +431,48 @@ __device__ int32_t block_exclusive_scan(int32_t* a, int n, int32_t* wave_tot) {
   return total;
 }
 
+// directory lookup with the home slot already loaded (lets a thread issue all its first probes
+// together); falls back to the probing loop on a miss
+__device__ __forceinline__ int64_t dir_resolve(const Spec& s, int64_t key, uint64_t home, int64_t first) {
+  if (first == key) return (int64_t)home;
+  if (key == EMPTY_KEY) return dir_find_or_insert(s, key);
+  return dir_find_or_insert(s, key);
+}
+
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBuf r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int64_t* st_key = (int64_t*)smem;
-  int64_t* st_val = st_key + RT_TILE;
-  uint16_t* st_idx = (uint16_t*)(st_val + RT_TILE);
-  int32_t* cnt = (int32_t*)(st_idx + RT_TILE);      // [NBQ + 1]
-  int32_t* wtot = cnt + (RT_Q * 256 + 1);            // [16]
+  int64_t* st_val = (int64_t*)smem;                   // [RT_TILE]
+  uint32_t* st_meta = (uint32_t*)(st_val + RT_TILE);  // [RT_TILE]
+  int32_t* cnt = (int32_t*)(st_meta + RT_TILE);       // [RT_Q * 256 + 1]
+  int32_t* wtot = cnt + (RT_Q * 256 + 1);             // [16]
   const int nbq = RT_Q * s.nb;
   const int64_t t = blockIdx.x;
   const int64_t base = t * RT_TILE;
   for (int x = threadIdx.x; x <= nbq; x += blockDim.x) cnt[x] = 0;
-  __syncthreads();
   constexpr int PER = RT_TILE / RT_THREADS;
   int32_t bid[PER], rank[PER];
-  int64_t kk[PER], vv[PER], tt[PER];
+  int64_t kk[PER], vv[PER], tt[PER], d0[PER];
+  uint64_t hm[PER];
   int32_t hh[PER];
-  // phase A: every load of the tile in flight before any dependent work
+  // phase A: every input load of the tile in flight before any dependent work (clamped indices:
+  // unconditional loads cannot be sunk into per-record branches)
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int64_t i = min(base + (int64_t)k * RT_THREADS + threadIdx.x, b.n - 1);   // unconditional loads
+    const int64_t i = min(base + (int64_t)k * RT_THREADS + threadIdx.x, b.n - 1);
     kk[k] = b.key[i];
     tt[k] = b.ts[i];
     vv[k] = b.val[i];
     hh[k] = b.key_hash ? b.key_hash[i] : 0;
   }
-  // phase B: per record; the (slice -> slot, batch slice) lookup is cached per wave, as a wave of an
+  // phase B: home slots, then every first directory probe in flight together (L2-resident table)
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    hm[k] = fmix64((uint64_t)kk[k]) & s.dir_mask;
+    d0[k] = s.dir_keys[hm[k]];
+  }
+  __syncthreads();   // cnt zeroed
+  // phase C: per record; the (slice -> slot, batch slice) lookup is cached per wave, as a wave of an
   // in-order stream stays in one slice for the whole tile
   int64_t c_m = INT64_MIN;
   int32_t c_p = -1, c_q = -1;
@@ -490,7 +513,6 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
         c_p = __shfl(p0, leader);
         c_q = __shfl(q0, leader);
         c_m = c_p >= 0 ? m0 : INT64_MIN;
-        if (c_p < 0) { p = -1; q = -1; }
       }
       p = live ? c_p : -1;
       q = live ? c_q : -1;
@@ -501,15 +523,15 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     if (live && p < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
     bid[k] = -1;
     rank[k] = 0;
-    const bool routed = live && !late_fire && q >= 0 && key != EMPTY_KEY;
-    const bool direct = live && !routed;   // per-element fire, overflow slice, or the Long.MIN_VALUE key
     int64_t kid = -1;
-    if (direct) {
-      kid = dir_find_or_insert(s, key);
-      if (kid < 0) set_error(s.err, FW_ERR_CAPACITY);
+    if (live) {
+      kid = dir_resolve(s, key, hm[k], d0[k]);
+      if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
     }
+    const bool routed = live && !late_fire && q >= 0 && kid != s.D;
+    const bool direct = live && !routed;   // per-element fire, overflow slice, or the Long.MIN_VALUE key
     if (b.late_key) {
-      const bool want = direct && kid >= 0 && late_fire;
+      const bool want = direct && late_fire;
       unsigned long long pos = wave_append(b.late_count, want);
       if (want) {
         if ((int64_t)pos < b.late_capacity) {
@@ -520,14 +542,14 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
         }
       }
     }
-    if (direct && !late_fire && kid >= 0) {
+    if (direct && !late_fire) {
       pane_update<VT, AGG, FIRST>(s, (int64_t)p * s.stride + kid, v, b.ord_base + i);
       if (s.touched[p] == 0) s.touched[p] = 1;
     }
     if (routed) {
-      const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
-      bid[k] = q * s.nb + (int32_t)(home >> s.kb_bits);
+      bid[k] = q * s.nb + (int32_t)(kid >> s.kb_bits);
       rank[k] = atomicAdd(&cnt[bid[k]], 1);
+      hm[k] = (uint64_t)kid;   // reuse: kid for the scatter
     }
   }
   if (__any(late_pairs != 0)) {
@@ -539,20 +561,19 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
   for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_len[(int64_t)x * r.ntiles + t] = cnt[x];
   const int32_t total = block_exclusive_scan(cnt, nbq, wtot);
   for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_start[(int64_t)x * r.ntiles + t] = cnt[x];
+  const uint32_t kbm = (1u << s.kb_bits) - 1;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (bid[k] >= 0) {
       const int32_t pos = cnt[bid[k]] + rank[k];
-      st_key[pos] = kk[k];
       st_val[pos] = vv[k];
-      st_idx[pos] = (uint16_t)(k * RT_THREADS + threadIdx.x);
+      st_meta[pos] = ((uint32_t)hm[k] & kbm) | ((uint32_t)(k * RT_THREADS + threadIdx.x) << 16);
     }
   }
   __syncthreads();
   for (int j = threadIdx.x; j < total; j += blockDim.x) {
-    r.key[base + j] = st_key[j];
     r.val[base + j] = st_val[j];
-    if (FIRST) r.idx[base + j] = st_idx[j];
+    r.meta[base + j] = st_meta[j];
   }
 }
 
@@ -564,58 +585,28 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
   const int32_t p = r.batch_slot[q];
   if (p < 0) return;
   const int KB = 1 << s.kb_bits;
-  const uint64_t kbm = (uint64_t)KB - 1;
-  int64_t* ldir = (int64_t*)smem;                       // [KB]
-  int64_t* lsum = ldir + KB;                            // [KB]
+  const uint32_t kbm = (uint32_t)KB - 1;
+  int64_t* lsum = (int64_t*)smem;                       // [KB]
   int64_t* lmin = lsum + KB;                            // [KB] (AGG 15)
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KB : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KB : 0);
   uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KB : 0));  // [KB]
-  int32_t* segoff = (int32_t*)(lfirst + KB);            // [2 * ntiles]
+  int32_t* segs = (int32_t*)(lfirst + KB);              // [2 * ntiles]: (start, len)
   const int64_t dbase = (int64_t)bkt * KB;
   for (int x = threadIdx.x; x < KB; x += blockDim.x) {
-    ldir[x] = s.dir_keys[dbase + x];
     lsum[x] = 0;
     if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
     if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
     if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
     lfirst[x] = NO_FIRST;
   }
-  // this (q, bucket)'s segment of every tile: (start, len) pairs in LDS
-  int32_t* segs = segoff;                               // [2 * ntiles]
   for (int t = threadIdx.x; t < r.ntiles; t += blockDim.x) {
     segs[2 * t] = r.seg_start[(int64_t)bid * r.ntiles + t];
     segs[2 * t + 1] = r.seg_len[(int64_t)bid * r.ntiles + t];
   }
   __syncthreads();
-  auto process = [&](int64_t key, int64_t v, uint32_t oi) {
-    const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
-    uint64_t kl = home & kbm;
-    bool found = false;
-    uint32_t nprobe = 0, ncas = 0;
-    for (uint64_t probe = 0; probe <= kbm; ++probe) {
-      int64_t cur = ldir[kl];
-      ++nprobe;
-      if (cur == key) { found = true; break; }
-      if (cur == EMPTY_KEY) {
-        if (r.dbg == 3) break;
-        ++ncas;
-        unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)kl],
-                                            (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-        int64_t now = (int64_t)prev == EMPTY_KEY ? key : (int64_t)prev;
-        ldir[kl] = now;   // only globally confirmed keys enter the cache
-        if (now == key) { found = true; break; }
-      }
-      kl = (kl + 1) & kbm;
-    }
-    if (r.dbg >= 3) {
-      atomicAdd(&s.stats[5], (unsigned long long)nprobe);
-      atomicAdd(&s.stats[6], (unsigned long long)ncas);
-      atomicAdd(&s.stats[7], 1ull);
-      if (!found) return;
-    }
-    if (!found) { set_error(s.err, FW_ERR_CAPACITY); return; }
-    if (r.dbg == 2) { asm volatile("" :: "v"(kl), "v"(v), "v"(oi)); return; }
+  auto process = [&](uint32_t meta, int64_t v, int t) {
+    const uint32_t kl = meta & kbm;
     if (AGG & FW_AGG_SUM) {
       if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
       else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
@@ -623,37 +614,28 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
-    atomicMin(&lfirst[kl], oi);
+    atomicMin(&lfirst[kl], (uint32_t)(t * RT_TILE) + (meta >> 16));   // batch index of the record
   };
-  // each wave takes AG_UNROLL segments per round, one record per lane, all loads issued before any
-  // LDS work so that AG_UNROLL HBM round trips overlap; records past a segment's first 64 follow
+  // each wave takes U segments per round, one record per lane; unconditional loads (inactive lanes
+  // read record 0) keep all U segments in flight together; records past a segment's first 64 follow
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   constexpr int U = 8;
   for (int t0 = wave * U; t0 < r.ntiles; t0 += nw * U) {
-    int64_t kk[U], vv[U];
-    uint32_t oo[U];
+    int64_t vv[U];
+    uint32_t mm[U];
     bool has[U];
-    // unconditional loads (inactive lanes read record 0): the compiler cannot sink them into the
-    // per-record branches, so all U segments are in flight together
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = min(t0 + u, r.ntiles - 1);
       const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
       has[u] = (t0 + u < r.ntiles) && lane < ln;
       const int64_t ri = has[u] ? (int64_t)t * RT_TILE + st + lane : 0;
-      kk[u] = r.key[ri];
       vv[u] = r.val[ri];
-      oo[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
-    }
-    if (r.dbg == 1) {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (has[u]) asm volatile("" :: "v"(kk[u]), "v"(vv[u]), "v"(oo[u]));
-      continue;
+      mm[u] = r.meta[ri];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (has[u]) process(kk[u], vv[u], oo[u]);
+      if (has[u]) process(mm[u], vv[u], t0 + u);
 #pragma unroll
     for (int u = 0; u < U; ++u) {   // long segments (hot keys)
       const int t = t0 + u;
@@ -661,7 +643,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
       const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
       for (int j = 64 + lane; j < ln; j += 64) {
         const int64_t ri = (int64_t)t * RT_TILE + st + j;
-        process(r.key[ri], r.val[ri], (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u));
+        process(r.meta[ri], r.val[ri], t);
       }
     }
   }
@@ -1287,6 +1269,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.lateness = c.allowed_lateness;
   s.g = c.assigner == FW_TUMBLING ? c.size : gcd64(c.size, s.slide);
   s.K = (int32_t)(c.size / s.g);
+  s.inv_size = 1.0 / (double)s.size;
+  s.inv_g = 1.0 / (double)s.g;
   s.R = (int32_t)(s.slide / s.g);
   if (s.K > MAX_K) return unsupported("more than 64 slices per window (size / gcd(size, slide))");
   s.mp = c.max_parallelism;
@@ -1358,22 +1342,21 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   // batches are large; direct atomics otherwise
   {
     const int KB = 1 << s.kb_bits;
-    const bool fits = KB <= 1024 && c.max_batch >= 4096 && c.max_batch <= (1ll << 26);
+    const bool fits = s.kb_bits <= RT_MAX_KB_BITS && c.max_batch >= 4096 && c.max_batch <= (1ll << 26);
     if (c.ingest_mode == 2 && !fits) return unsupported("partitioned ingest needs <= 1024 directory slots per bucket");
     e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && c.max_batch >= (1 << 16));
     if (e->routed) {
       e->max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
       const size_t cap = (size_t)e->max_tiles * RT_TILE;
-      e->rb.key = e->alloc<int64_t>(cap);
+      e->rb.meta = e->alloc<uint32_t>(cap);
       e->rb.val = e->alloc<int64_t>(cap);
-      e->rb.idx = e->alloc<uint16_t>(cap);
       e->rb.seg_start = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
       e->rb.seg_len = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
       e->rb.batch_slot = e->alloc<int32_t>(RT_Q);
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
-      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
-      const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
+      e->route_lds = (size_t)RT_TILE * (8 + 4) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
+      const int ncols = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
       e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles;
       if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
     }

@@ -61,6 +61,28 @@ FW_HD int64_t cleanup_time(int64_t max_ts, int64_t allowed_lateness) {
   return ct >= max_ts ? ct : INT64_MAX;
 }
 
+// Java truncating division and remainder of x by a positive divisor d (x = q*d + r, r has x's sign).
+// Exact; fast path through a double reciprocal when |x| < 2^52 (the 64-bit integer divide is a long
+// instruction sequence on the GPU), fixed up by at most a couple of correction steps.
+FW_HD void jdivmod(int64_t x, int64_t d, double inv_d, int64_t& q, int64_t& r) {
+  const int64_t lim = (int64_t)1 << 52;
+  if (x > -lim && x < lim && d < lim) {
+    int64_t qq = (int64_t)((double)x * inv_d);
+    int64_t rr = x - qq * d;
+    if (x >= 0) {
+      while (rr < 0) { --qq; rr += d; }
+      while (rr >= d) { ++qq; rr -= d; }
+    } else {
+      while (rr > 0) { ++qq; rr -= d; }
+      while (rr <= -d) { --qq; rr += d; }
+    }
+    q = qq; r = rr;
+    return;
+  }
+  q = x / d;
+  r = x % d;
+}
+
 // floor division / modulo on int64 (slice numbering; not Java semantics, internal indexing)
 FW_HD int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b, r = a % b;
