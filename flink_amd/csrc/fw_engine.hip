@@ -433,9 +433,13 @@ __device__ int32_t block_exclusive_scan(int32_t* a, int n, int32_t* wave_tot) {
 
 // directory lookup with the home slot already loaded (lets a thread issue all its first probes
 // together); falls back to the probing loop on a miss
-__device__ __forceinline__ int64_t dir_resolve(const Spec& s, int64_t key, uint64_t home, int64_t first) {
-  if (first == key) return (int64_t)home;
-  if (key == EMPTY_KEY) return dir_find_or_insert(s, key);
+__device__ __forceinline__ int64_t dir_resolve(const Spec& s, int64_t key, uint64_t home, int64_t d0, int64_t d1) {
+  // linear probing: the key sits in the first slot of its probe sequence that holds it, and no EMPTY
+  // slot comes before it; two slots are checked from registers (load factor <= 1/4 keeps nearly every
+  // key within them), the loop handles the rest and inserts
+  const uint64_t kbm = (1ull << s.kb_bits) - 1;
+  if (d0 == key) return (int64_t)home;
+  if (d0 != EMPTY_KEY && d1 == key) return (int64_t)((home & ~kbm) | ((home + 1) & kbm));
   return dir_find_or_insert(s, key);
 }
 
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
   for (int x = threadIdx.x; x <= nbq; x += blockDim.x) cnt[x] = 0;
   constexpr int PER = RT_TILE / RT_THREADS;
   int32_t bid[PER], rank[PER];
-  int64_t kk[PER], vv[PER], tt[PER], d0[PER];
+  int64_t kk[PER], vv[PER], tt[PER], d0[PER], d1[PER];
   uint64_t hm[PER];
   int32_t hh[PER];
   // phase A: every input load of the tile in flight before any dependent work (clamped indices:
@@ -469,7 +473,9 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     hm[k] = fmix64((uint64_t)kk[k]) & s.dir_mask;
+    const uint64_t kbm = (1ull << s.kb_bits) - 1;
     d0[k] = s.dir_keys[hm[k]];
+    d1[k] = s.dir_keys[(hm[k] & ~kbm) | ((hm[k] + 1) & kbm)];
   }
   __syncthreads();   // cnt zeroed
   // phase C: per record; the (slice -> slot, batch slice) lookup is cached per wave, as a wave of an
@@ -525,7 +531,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     rank[k] = 0;
     int64_t kid = -1;
     if (live) {
-      kid = dir_resolve(s, key, hm[k], d0[k]);
+      kid = dir_resolve(s, key, hm[k], d0[k], d1[k]);
       if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
     }
     const bool routed = live && !late_fire && q >= 0 && kid != s.D;
@@ -1280,7 +1286,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.agg = c.agg_mask == FW_AGG_SUM ? FW_AGG_SUM : 15;   // instantiated reduce shapes
   s.first = c.keep_first_f1 ? 1 : 0;
 
-  s.D = next_pow2(std::max<int64_t>(2 * c.key_capacity, 64));
+  // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys): short linear-probe sequences
+  s.D = next_pow2(std::max<int64_t>((c.key_capacity <= (1 << 20) ? 4 : 2) * c.key_capacity, 64));
   s.dir_mask = (uint64_t)s.D - 1;
   {
     int dbits = bits_for((uint64_t)s.D) - 1;                  // D = 2^dbits
