@@ -87,6 +87,24 @@ def cpu_baseline(cfg, n_keys, rate, n):
                       f"watermark every 2^22 events, final MAX_WATERMARK; {fired} windows fired"}
 
 
+def pmc_traffic():
+    """HBM bytes per ingest launch from the committed rocprofv3 PMC summary of THIS library build
+    (profiles/*_pmc.json, written by tools/summarize_profiles.py from separate FETCH_SIZE / WRITE_SIZE
+    passes), or None when no summary matches the library's md5."""
+    import glob
+    import hashlib
+    lib = os.path.join(ROOT, "flink_amd", "lib", "libflink_window.so")
+    md5 = hashlib.md5(open(lib, "rb").read()).hexdigest()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime, reverse=True):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+        if d.get("library_md5") == md5 and d.get("ingest_traffic_bytes_per_launch"):
+            return d["ingest_traffic_bytes_per_launch"], os.path.basename(f)
+    return None, None
+
+
 def main():
     args = parse()
     world, rank, local = dist_init(args)
@@ -182,6 +200,7 @@ def main():
     ing_n = prof.launches[_abi.FW_PHASE_INGEST]
     ing_rec = prof.records[_abi.FW_PHASE_INGEST]
     achieved = (24.0 * ing_rec / ing_n) / (ing_ms / ing_n / 1e3) / 1e9 if ing_n else 0.0
+    traffic, traffic_src = pmc_traffic()
     line = {
         "metric": "events/sec (whole node) keyed 1s tumbling sum; % of HBM roofline",
         "value": value,
@@ -203,7 +222,9 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "bytes_per_event": 24, "ingest_ms_per_launch": ing_ms / max(ing_n, 1),
                      "fire_ms_total": prof.ms[_abi.FW_PHASE_FIRE], "fixup_ms_total": prof.ms[_abi.FW_PHASE_FIXUP],
-                     "traffic": None},
+                     "traffic": traffic, "traffic_unit": "bytes per ingest launch (FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": 24.0 * ing_rec / ing_n if ing_n else None},
         "check": check,
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
