@@ -375,7 +375,7 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
 // read-modify-writes (one per pane per batch) — no device-scope atomics per record.
 // ------------------------------------------------------------------------------------------------
 constexpr int RT_TILE = 4096;
-constexpr int RT_THREADS = 512;
+constexpr int RT_THREADS = 1024;
 constexpr int RT_Q = 2;                 // slices per batch handled by the partitioned form
 constexpr int AG_THREADS = 1024;
 constexpr int RT_MAX_KB_BITS = 10;      // kid-in-bucket must fit the record's meta word
@@ -564,9 +564,9 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
   }
   __syncthreads();
   // segment table of this tile (counts before the scan)
-  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_len[(int64_t)x * r.ntiles + t] = cnt[x];
+  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_len[t * nbq + x] = cnt[x];      // tile-major: coalesced
   const int32_t total = block_exclusive_scan(cnt, nbq, wtot);
-  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_start[(int64_t)x * r.ntiles + t] = cnt[x];
+  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_start[t * nbq + x] = cnt[x];
   const uint32_t kbm = (1u << s.kb_bits) - 1;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -606,9 +606,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
     lfirst[x] = NO_FIRST;
   }
+  const int nbq = RT_Q * s.nb;
   for (int t = threadIdx.x; t < r.ntiles; t += blockDim.x) {
-    segs[2 * t] = r.seg_start[(int64_t)bid * r.ntiles + t];
-    segs[2 * t + 1] = r.seg_len[(int64_t)bid * r.ntiles + t];
+    segs[2 * t] = r.seg_start[(int64_t)t * nbq + bid];
+    segs[2 * t + 1] = r.seg_len[(int64_t)t * nbq + bid];
   }
   __syncthreads();
   auto process = [&](uint32_t meta, int64_t v, int t) {
