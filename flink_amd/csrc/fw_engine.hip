@@ -498,7 +498,8 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     RecWin w;
     w.m = 0; w.n_late = 0; w.n_fire = 0; w.n_windows = 0; w.quirk = false;
     if (ok) {
-      w = record_windows(s, ts, b.wm);
+      if (r.dbg & 2) { w.m = 1700000000; w.n_windows = 1; }
+      else w = record_windows(s, ts, b.wm);
       if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
     }
     if (ok) late_pairs += (unsigned long long)w.n_late;
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     rank[k] = 0;
     int64_t kid = -1;
     if (live) {
-      kid = dir_resolve(s, key, hm[k], d0[k], d1[k]);
+      kid = (r.dbg & 1) ? (int64_t)hm[k] : dir_resolve(s, key, hm[k], d0[k], d1[k]);
       if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
     }
     const bool routed = live && !late_fire && q >= 0 && kid != s.D;
@@ -554,7 +555,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     }
     if (routed) {
       bid[k] = q * s.nb + (int32_t)(kid >> s.kb_bits);
-      rank[k] = atomicAdd(&cnt[bid[k]], 1);
+      rank[k] = (r.dbg & 8) ? 0 : atomicAdd(&cnt[bid[k]], 1);
       hm[k] = (uint64_t)kid;   // reuse: kid for the scatter
     }
   }
@@ -577,6 +578,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     }
   }
   __syncthreads();
+  if (r.dbg & 4) return;
   for (int j = threadIdx.x; j < total; j += blockDim.x) {
     r.val[base + j] = st_val[j];
     r.meta[base + j] = st_meta[j];
