@@ -382,8 +382,9 @@ constexpr int RT_MAX_KB_BITS = 10;      // kid-in-bucket must fit the record's m
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
-  uint32_t* meta;        // [ntiles][RT_TILE]  kid-in-bucket (low 16 bits) | index in tile (high 16)
+  int64_t* key;          // [ntiles][RT_TILE]
   int64_t* val;          // [ntiles][RT_TILE]
+  uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
   int32_t* seg_start;    // [NBQ][ntiles] start of (q,bucket) segment within the tile
   int32_t* seg_len;
   int32_t* batch_slot;   // [RT_Q] pane-slice slot of batch slice q, -1 if unused
@@ -446,9 +447,10 @@ __device__ __forceinline__ int64_t dir_resolve(const Spec& s, int64_t key, uint6
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBuf r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int64_t* st_val = (int64_t*)smem;                   // [RT_TILE]
-  uint32_t* st_meta = (uint32_t*)(st_val + RT_TILE);  // [RT_TILE]
-  int32_t* cnt = (int32_t*)(st_meta + RT_TILE);       // [RT_Q * 256 + 1]
+  int64_t* st_key = (int64_t*)smem;                   // [RT_TILE]
+  int64_t* st_val = st_key + RT_TILE;                 // [RT_TILE]
+  uint16_t* st_idx = (uint16_t*)(st_val + RT_TILE);   // [RT_TILE]
+  int32_t* cnt = (int32_t*)(st_idx + RT_TILE);        // [RT_Q * 256 + 1]
   int32_t* wtot = cnt + (RT_Q * 256 + 1);             // [16]
   const int nbq = RT_Q * s.nb;
   const int64_t t = blockIdx.x;
@@ -456,8 +458,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
   for (int x = threadIdx.x; x <= nbq; x += blockDim.x) cnt[x] = 0;
   constexpr int PER = RT_TILE / RT_THREADS;
   int32_t bid[PER], rank[PER];
-  int64_t kk[PER], vv[PER], tt[PER], d0[PER], d1[PER];
-  uint64_t hm[PER];
+  int64_t kk[PER], vv[PER], tt[PER];
   int32_t hh[PER];
   // phase A: every input load of the tile in flight before any dependent work (clamped indices:
   // unconditional loads cannot be sunk into per-record branches)
@@ -468,14 +469,6 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     tt[k] = b.ts[i];
     vv[k] = b.val[i];
     hh[k] = b.key_hash ? b.key_hash[i] : 0;
-  }
-  // phase B: home slots, then every first directory probe in flight together (L2-resident table)
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    hm[k] = fmix64((uint64_t)kk[k]) & s.dir_mask;
-    const uint64_t kbm = (1ull << s.kb_bits) - 1;
-    d0[k] = s.dir_keys[hm[k]];
-    d1[k] = s.dir_keys[(hm[k] & ~kbm) | ((hm[k] + 1) & kbm)];
   }
   __syncthreads();   // cnt zeroed
   // phase C: per record; the (slice -> slot, batch slice) lookup is cached per wave, as a wave of an
@@ -530,15 +523,17 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
     if (live && p < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
     bid[k] = -1;
     rank[k] = 0;
+    // routed records keep their key (resolved to a kid in k_aggregate's LDS directory slice); the rest
+    // (per-element fires, an overflow slice, the Long.MIN_VALUE key) resolve here and update directly
+    const bool routed = live && !late_fire && q >= 0 && key != EMPTY_KEY;
+    const bool direct = live && !routed;
     int64_t kid = -1;
-    if (live) {
-      kid = (r.dbg & 1) ? (int64_t)hm[k] : dir_resolve(s, key, hm[k], d0[k], d1[k]);
-      if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
+    if (direct) {
+      kid = dir_find_or_insert(s, key);
+      if (kid < 0) set_error(s.err, FW_ERR_CAPACITY);
     }
-    const bool routed = live && !late_fire && q >= 0 && kid != s.D;
-    const bool direct = live && !routed;   // per-element fire, overflow slice, or the Long.MIN_VALUE key
     if (b.late_key) {
-      const bool want = direct && late_fire;
+      const bool want = direct && kid >= 0 && late_fire;
       unsigned long long pos = wave_append(b.late_count, want);
       if (want) {
         if ((int64_t)pos < b.late_capacity) {
@@ -549,14 +544,14 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
         }
       }
     }
-    if (direct && !late_fire) {
+    if (direct && !late_fire && kid >= 0) {
       pane_update<VT, AGG, FIRST>(s, (int64_t)p * s.stride + kid, v, b.ord_base + i);
       if (s.touched[p] == 0) s.touched[p] = 1;
     }
     if (routed) {
-      bid[k] = q * s.nb + (int32_t)(kid >> s.kb_bits);
+      const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
+      bid[k] = q * s.nb + (int32_t)(home >> s.kb_bits);
       rank[k] = (r.dbg & 8) ? 0 : atomicAdd(&cnt[bid[k]], 1);
-      hm[k] = (uint64_t)kid;   // reuse: kid for the scatter
     }
   }
   if (__any(late_pairs != 0)) {
@@ -568,20 +563,21 @@ __global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBu
   for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_len[t * nbq + x] = cnt[x];      // tile-major: coalesced
   const int32_t total = block_exclusive_scan(cnt, nbq, wtot);
   for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_start[t * nbq + x] = cnt[x];
-  const uint32_t kbm = (1u << s.kb_bits) - 1;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (bid[k] >= 0) {
       const int32_t pos = cnt[bid[k]] + rank[k];
+      st_key[pos] = kk[k];
       st_val[pos] = vv[k];
-      st_meta[pos] = ((uint32_t)hm[k] & kbm) | ((uint32_t)(k * RT_THREADS + threadIdx.x) << 16);
+      st_idx[pos] = (uint16_t)(k * RT_THREADS + threadIdx.x);
     }
   }
   __syncthreads();
   if (r.dbg & 4) return;
   for (int j = threadIdx.x; j < total; j += blockDim.x) {
+    r.key[base + j] = st_key[j];
     r.val[base + j] = st_val[j];
-    r.meta[base + j] = st_meta[j];
+    if (FIRST) r.idx[base + j] = st_idx[j];
   }
 }
 
@@ -594,7 +590,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
   if (p < 0) return;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
-  int64_t* lsum = (int64_t*)smem;                       // [KB]
+  int64_t* ldir = (int64_t*)smem;                       // [KB] this bucket's directory slice
+  int64_t* lsum = ldir + KB;                            // [KB]
   int64_t* lmin = lsum + KB;                            // [KB] (AGG 15)
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KB : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KB : 0);
@@ -602,6 +599,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
   int32_t* segs = (int32_t*)(lfirst + KB);              // [2 * ntiles]: (start, len)
   const int64_t dbase = (int64_t)bkt * KB;
   for (int x = threadIdx.x; x < KB; x += blockDim.x) {
+    ldir[x] = s.dir_keys[dbase + x];
     lsum[x] = 0;
     if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
     if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
@@ -614,8 +612,36 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     segs[2 * t + 1] = r.seg_len[(int64_t)t * nbq + bid];
   }
   __syncthreads();
-  auto process = [&](uint32_t meta, int64_t v, int t) {
-    const uint32_t kl = meta & kbm;
+  // key -> slot in this bucket: the first four probe slots compared without branching (directory
+  // load factor <= 1/4 keeps almost every key there); the loop below takes the rest and inserts
+  // new keys (a global CAS confirms every slot before it enters the LDS copy)
+  auto find = [&](int64_t key, uint32_t& kl, bool& slow) {
+    const uint32_t h = (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm;
+    const int64_t a0 = ldir[h], a1 = ldir[(h + 1) & kbm], a2 = ldir[(h + 2) & kbm], a3 = ldir[(h + 3) & kbm];
+    slow = false;
+    if (a0 == key) kl = h;
+    else if (a0 != EMPTY_KEY && a1 == key) kl = (h + 1) & kbm;
+    else if (a0 != EMPTY_KEY && a1 != EMPTY_KEY && a2 == key) kl = (h + 2) & kbm;
+    else if (a0 != EMPTY_KEY && a1 != EMPTY_KEY && a2 != EMPTY_KEY && a3 == key) kl = (h + 3) & kbm;
+    else { slow = true; kl = h; }
+  };
+  auto find_slow = [&](int64_t key, uint32_t& kl) -> bool {
+    uint32_t x = (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm;
+    for (uint32_t probe = 0; probe <= kbm; ++probe) {
+      int64_t cur = ldir[x];
+      if (cur == key) { kl = x; return true; }
+      if (cur == EMPTY_KEY) {
+        unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)x],
+                                            (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+        int64_t now = (int64_t)prev == EMPTY_KEY ? key : (int64_t)prev;
+        ldir[x] = now;   // only globally confirmed keys enter the cache
+        if (now == key) { kl = x; return true; }
+      }
+      x = (x + 1) & kbm;
+    }
+    return false;
+  };
+  auto update = [&](uint32_t kl, int64_t v, uint32_t oi) {
     if (AGG & FW_AGG_SUM) {
       if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
       else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
@@ -623,15 +649,26 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
-    atomicMin(&lfirst[kl], (uint32_t)(t * RT_TILE) + (meta >> 16));   // batch index of the record
+    atomicMin(&lfirst[kl], oi);   // batch index of the record: first arrival
+  };
+  auto process = [&](bool act, int64_t key, int64_t v, uint32_t oi) {
+    uint32_t kl = 0;
+    bool slow = false;
+    if (act) find(key, kl, slow);
+    if (__any(act && slow)) {
+      if (act && slow) {
+        if (!find_slow(key, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
+      }
+    }
+    if (act) update(kl, v, oi);
   };
   // each wave takes U segments per round, one record per lane; unconditional loads (inactive lanes
   // read record 0) keep all U segments in flight together; records past a segment's first 64 follow
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   constexpr int U = 8;
   for (int t0 = wave * U; t0 < r.ntiles; t0 += nw * U) {
-    int64_t vv[U];
-    uint32_t mm[U];
+    int64_t kk[U], vv[U];
+    uint32_t oo[U];
     bool has[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -639,20 +676,23 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
       const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
       has[u] = (t0 + u < r.ntiles) && lane < ln;
       const int64_t ri = has[u] ? (int64_t)t * RT_TILE + st + lane : 0;
+      kk[u] = r.key[ri];
       vv[u] = r.val[ri];
-      mm[u] = r.meta[ri];
+      oo[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (has[u]) process(mm[u], vv[u], t0 + u);
+    for (int u = 0; u < U; ++u) process(has[u], kk[u], vv[u], oo[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {   // long segments (hot keys)
-      const int t = t0 + u;
-      if (t >= r.ntiles) continue;
-      const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
-      for (int j = 64 + lane; j < ln; j += 64) {
-        const int64_t ri = (int64_t)t * RT_TILE + st + j;
-        process(r.meta[ri], r.val[ri], t);
+      const int t = min(t0 + u, r.ntiles - 1);
+      const int32_t ln = (t0 + u < r.ntiles) ? segs[2 * t + 1] : 0;
+      if (ln <= 64) continue;       // wave-uniform
+      const int32_t st = segs[2 * t];
+      for (int j0 = 64; j0 < ln; j0 += 64) {
+        const int j = j0 + lane;
+        const bool act = j < ln;
+        const int64_t ri = act ? (int64_t)t * RT_TILE + st + j : 0;
+        process(act, r.key[ri], r.val[ri], (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u));
       }
     }
   }
@@ -1358,15 +1398,16 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (e->routed) {
       e->max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
       const size_t cap = (size_t)e->max_tiles * RT_TILE;
-      e->rb.meta = e->alloc<uint32_t>(cap);
+      e->rb.key = e->alloc<int64_t>(cap);
       e->rb.val = e->alloc<int64_t>(cap);
+      e->rb.idx = e->alloc<uint16_t>(cap);
       e->rb.seg_start = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
       e->rb.seg_len = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
       e->rb.batch_slot = e->alloc<int32_t>(RT_Q);
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
-      e->route_lds = (size_t)RT_TILE * (8 + 4) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
-      const int ncols = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
+      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
+      const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
       e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles;
       if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
     }
