@@ -375,7 +375,7 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
 // read-modify-writes (one per pane per batch) — no device-scope atomics per record.
 // ------------------------------------------------------------------------------------------------
 constexpr int RT_TILE = 4096;
-constexpr int RT_THREADS = 1024;
+constexpr int RT_THREADS = 512;
 constexpr int RT_Q = 2;                 // slices per batch handled by the partitioned form
 constexpr int AG_THREADS = 1024;
 constexpr int RT_MAX_KB_BITS = 10;      // kid-in-bucket must fit the record's meta word
@@ -445,7 +445,7 @@ __device__ __forceinline__ int64_t dir_resolve(const Spec& s, int64_t key, uint6
 }
 
 template <int VT, int AGG, bool FIRST>
-__global__ __launch_bounds__(RT_THREADS) void k_route(Spec s, BatchIn b, RouteBuf r) {
+__global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, RouteBuf r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int64_t* st_key = (int64_t*)smem;                   // [RT_TILE]
   int64_t* st_val = st_key + RT_TILE;                 // [RT_TILE]
