@@ -80,6 +80,7 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int32_t K;        // slices per window
   int32_t R;        // slices per slide
   int32_t mp, kg_start, kg_end;
+  int32_t mp_mask;  // mp - 1 when mp is a power of two, else 0
   int32_t vt, agg, first;
   // directory
   int64_t* dir_keys;
@@ -156,23 +157,25 @@ __device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key
 }
 
 // slice number m -> slot p, claiming a FREE slot.  Returns -1 when slot p holds another live slice.
-__device__ __forceinline__ int32_t slice_slot(const Spec& s, int64_t m) {
-  int32_t p = (int32_t)floor_mod(m, s.P);
-  int64_t tag = s.slice_tag[p];
+// Out of line: one call per wave and slice change on the hot path.
+__device__ __noinline__ int32_t slice_slot_at(int64_t* slice_tag, int32_t P, int64_t m) {
+  int32_t p = (int32_t)floor_mod(m, P);
+  int64_t tag = slice_tag[p];
   if (tag == m) return p;
   if (tag == FREE_TAG) {
-    unsigned long long prev = atomicCAS((unsigned long long*)&s.slice_tag[p], (unsigned long long)FREE_TAG,
+    unsigned long long prev = atomicCAS((unsigned long long*)&slice_tag[p], (unsigned long long)FREE_TAG,
                                         (unsigned long long)m);
     if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) return p;
     return -1;
   }
   // the cached value may be stale (the slot was freed and re-claimed by a kernel boundary, which
   // flushes caches) — re-read atomically before giving up
-  unsigned long long now = atomicCAS((unsigned long long*)&s.slice_tag[p], (unsigned long long)FREE_TAG,
+  unsigned long long now = atomicCAS((unsigned long long*)&slice_tag[p], (unsigned long long)FREE_TAG,
                                      (unsigned long long)m);
   if ((int64_t)now == FREE_TAG || (int64_t)now == m) return p;
   return -1;
 }
+__device__ __forceinline__ int32_t slice_slot(const Spec& s, int64_t m) { return slice_slot_at(s.slice_tag, s.P, m); }
 
 // Window bookkeeping for one record, following SlidingEventTimeWindows.assignWindows (:64-77) /
 // TumblingEventTimeWindows.assignWindows (:59-68).  Produces the record's slice number m and how many
@@ -186,24 +189,14 @@ struct RecWin {
   bool quirk;         // sliding assignment outside the slice-exact regime
 };
 
-__device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int64_t wm) {
+struct SlideSpec { int64_t offset, size, slide, g, lateness; double inv_g; int32_t K, R; };
+
+// sliding assignment, out of line (the tumbling case is inlined on the hot path)
+__device__ __noinline__ RecWin record_windows_sliding(SlideSpec s, int64_t ts, int64_t wm) {
   RecWin r;
   r.quirk = false;
   r.n_late = 0;
   r.n_fire = 0;
-  if (s.assigner == FW_TUMBLING) {
-    int64_t x = jadd(jsub(ts, s.offset), s.size);
-    int64_t q, rem;
-    jdivmod(x, s.size, s.inv_size, q, rem);
-    r.m = q - 1;                                                 // start = offset + m * size
-    int64_t start = jsub(ts, rem);                               // getWindowStartWithOffset
-    int64_t max_ts = jsub(jadd(start, s.size), 1);               // TimeWindow.maxTimestamp
-    int64_t ct = cleanup_time(max_ts, s.lateness);
-    r.n_windows = 1;
-    if (ct <= wm) r.n_late = 1;
-    else if (max_ts <= wm) r.n_fire = 1;
-    return r;
-  }
   int64_t x = jadd(jsub(ts, s.offset), s.g);
   if (x < 0 || jadd(jsub(ts, s.offset), s.slide) < 0) r.quirk = true;   // Java % of a negative numerator
   {
@@ -222,6 +215,32 @@ __device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int6
     else if (max_ts <= wm) r.n_fire++;
   }
   return r;
+}
+
+__device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int64_t wm) {
+  if (s.assigner != FW_TUMBLING)
+    return record_windows_sliding(SlideSpec{s.offset, s.size, s.slide, s.g, s.lateness, s.inv_g, s.K, s.R}, ts, wm);
+  RecWin r;
+  r.quirk = false;
+  r.n_late = 0;
+  r.n_fire = 0;
+  int64_t x = jadd(jsub(ts, s.offset), s.size);
+  int64_t q, rem;
+  jdivmod(x, s.size, s.inv_size, q, rem);
+  r.m = q - 1;                                                 // start = offset + m * size
+  int64_t start = jsub(ts, rem);                               // getWindowStartWithOffset
+  int64_t max_ts = jsub(jadd(start, s.size), 1);               // TimeWindow.maxTimestamp
+  int64_t ct = cleanup_time(max_ts, s.lateness);
+  r.n_windows = 1;
+  if (ct <= wm) r.n_late = 1;
+  else if (max_ts <= wm) r.n_fire = 1;
+  return r;
+}
+
+// key group of a record (KeyGroupRangeAssignment.assignToKeyGroup :51-64); murmurHash is >= 0, so for
+// the usual power-of-two maxParallelism the remainder is a mask
+__device__ __forceinline__ int32_t record_key_group(const Spec& s, int32_t key_hash) {
+  return s.mp_mask ? (murmur_hash(key_hash) & s.mp_mask) : key_group_for_hash(key_hash, s.mp);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -290,7 +309,7 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
     bool ok = valid;
     if (ok && ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
     if (ok) {
-      int32_t kg = key_group_for_hash(h, s.mp);   // AbstractKeyedStateBackend.setCurrentKey :167-170
+      int32_t kg = record_key_group(s, h);   // AbstractKeyedStateBackend.setCurrentKey :167-170
       if (kg < s.kg_start || kg > s.kg_end) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
     }
     RecWin w;
@@ -367,27 +386,38 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
 }
 
 // ------------------------------------------------------------------------------------------------
-// ingest, partitioned form.  k_route resolves each record's dense key id (directory
-// probe, L2-resident), counting-sorts a tile of RT_TILE records by (batch slice q, directory bucket)
-// through LDS and writes the tile back coalesced as 12 B records (kid-in-bucket | tile index, value).
-// k_aggregate gives every (q, bucket) to one workgroup: it owns those panes exclusively, reduces the
-// bucket's records with LDS atomics and folds the result into the dense columns with plain
-// read-modify-writes (one per pane per batch) — no device-scope atomics per record.
+// ingest, partitioned form.  Two kernels per batch:
+//  k_route      one workgroup per tile of RT_TILE records: streams the tile's columns in with 16-B
+//               loads, does the per-record operator work (key group check, window/slice, lateness),
+//               counting-sorts the routable records through LDS by bin = (batch slice q, directory
+//               bucket) and writes the tile back bin-sorted (key, value, index-in-tile) with a per-tile
+//               table of segment starts.  Records that cannot be routed (per-element fires, a third
+//               slice in one batch, the Long.MIN_VALUE key) take the direct path after the scatter.
+//  k_aggregate  one workgroup per directory bucket: owns every pane of that bucket for this batch,
+//               gathers the bucket's segment from every tile (16-lane groups, 4 segments per wave
+//               instruction), resolves keys in an LDS copy of the bucket's directory slice, reduces with
+//               LDS atomics and folds each touched pane into the dense columns once.
+// No device-scope atomic per record: the routed form is bounded by HBM traffic, not the memory-side
+// atomic rate (tools/microbench/ingest_mb.hip: ~24 G random 8-B atomics/s chip-wide).
 // ------------------------------------------------------------------------------------------------
 constexpr int RT_TILE = 4096;
 constexpr int RT_THREADS = 512;
 constexpr int RT_Q = 2;                 // slices per batch handled by the partitioned form
 constexpr int AG_THREADS = 1024;
-constexpr int RT_MAX_KB_BITS = 10;      // kid-in-bucket must fit the record's meta word
+constexpr int RT_MAX_KB_BITS = 10;      // directory slots per bucket held in LDS by k_aggregate
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
-  int64_t* key;          // [ntiles][RT_TILE]
+  int64_t* key;          // [ntiles][RT_TILE] routed records, each tile sorted by bin
   int64_t* val;          // [ntiles][RT_TILE]
   uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
-  int32_t* seg_start;    // [NBQ][ntiles] start of (q,bucket) segment within the tile
-  int32_t* seg_len;
-  int32_t* batch_slot;   // [RT_Q] pane-slice slot of batch slice q, -1 if unused
+  uint16_t* seg;         // [ntiles][nbq + 1] start of each bin's segment in the tile; [nbq] = routed count
+  int32_t* batch_slot;   // [RT_Q] pane-slice slot of batch slice q, -1 if unused (this batch's parity half)
+  int32_t* next_slot;    // [RT_Q] the other parity half: reset by k_aggregate for the next batch
+  unsigned long long* dlist;    // direct-path records: (batch index << 32) | (slot << 1) | per-element fire
+  unsigned long long* dcount;   // this batch's direct-list length
+  unsigned long long* next_dcount;
+  int64_t dcap;
   int32_t ntiles;
   int32_t dbg;
 };
@@ -404,99 +434,104 @@ __device__ __forceinline__ int32_t batch_slice_q(const RouteBuf& r, int32_t p) {
   return -1;
 }
 
-// block-wide exclusive scan of n <= blockDim.x ints in place; returns the total
-__device__ int32_t block_exclusive_scan(int32_t* a, int n, int32_t* wave_tot) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
-  int32_t v = tid < n ? a[tid] : 0;
-  int32_t x = v;
+// exclusive scan of a[0..n) in place (n <= 8 * blockDim.x), contiguous chunks per thread
+template <int NT>
+__device__ __forceinline__ void block_scan_excl(int32_t* a, int n, int32_t* wtot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per = (n + NT - 1) / NT;
+  int32_t loc[8];
+  int32_t sum = 0;
+  for (int i = 0; i < per; ++i) {
+    const int x = threadIdx.x * per + i;
+    loc[i] = x < n ? a[x] : 0;
+    sum += loc[i];
+  }
+  int32_t incl = sum;
   for (int o = 1; o < 64; o <<= 1) {
-    int32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
+    const int32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
   }
-  if (lane == 63) wave_tot[wave] = x;
+  if (lane == 63) wtot[wave] = incl;
   __syncthreads();
-  if (wave == 0) {
-    int32_t w = lane < nw ? wave_tot[lane] : 0;
-    for (int o = 1; o < 64; o <<= 1) {
-      int32_t y = __shfl_up(w, o);
-      if (lane >= o) w += y;
-    }
-    if (lane < nw) wave_tot[lane] = w;   // inclusive wave prefix
+  int32_t run = incl - sum;
+  for (int w = 0; w < wave; ++w) run += wtot[w];
+  for (int i = 0; i < per; ++i) {
+    const int x = threadIdx.x * per + i;
+    if (x < n) a[x] = run;
+    run += loc[i];
   }
   __syncthreads();
-  int32_t excl = x - v + (wave > 0 ? wave_tot[wave - 1] : 0);
-  int32_t total = wave_tot[nw - 1];
-  __syncthreads();
-  if (tid < n) a[tid] = excl;
-  __syncthreads();
-  return total;
-}
-
-// directory lookup with the home slot already loaded (lets a thread issue all its first probes
-// together); falls back to the probing loop on a miss
-__device__ __forceinline__ int64_t dir_resolve(const Spec& s, int64_t key, uint64_t home, int64_t d0, int64_t d1) {
-  // linear probing: the key sits in the first slot of its probe sequence that holds it, and no EMPTY
-  // slot comes before it; two slots are checked from registers (load factor <= 1/4 keeps nearly every
-  // key within them), the loop handles the rest and inserts
-  const uint64_t kbm = (1ull << s.kb_bits) - 1;
-  if (d0 == key) return (int64_t)home;
-  if (d0 != EMPTY_KEY && d1 == key) return (int64_t)((home & ~kbm) | ((home + 1) & kbm));
-  return dir_find_or_insert(s, key);
 }
 
 template <int VT, int AGG, bool FIRST>
-__global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, RouteBuf r) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int64_t* st_key = (int64_t*)smem;                   // [RT_TILE]
-  int64_t* st_val = st_key + RT_TILE;                 // [RT_TILE]
-  uint16_t* st_idx = (uint16_t*)(st_val + RT_TILE);   // [RT_TILE]
-  int32_t* cnt = (int32_t*)(st_idx + RT_TILE);        // [RT_Q * 256 + 1]
-  int32_t* wtot = cnt + (RT_Q * 256 + 1);             // [16]
+__device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, const RouteBuf& r, unsigned char* smem,
+                                           const bool tail) {
+  constexpr int NT = RT_THREADS;
+  constexpr int PER = RT_TILE / NT;     // records per thread
+  constexpr int V = PER / 2;            // 16-B vectors per column per thread
   const int nbq = RT_Q * s.nb;
-  const int64_t t = blockIdx.x;
-  const int64_t base = t * RT_TILE;
-  for (int x = threadIdx.x; x <= nbq; x += blockDim.x) cnt[x] = 0;
-  constexpr int PER = RT_TILE / RT_THREADS;
-  int32_t bid[PER], rank[PER];
-  int64_t kk[PER], vv[PER], tt[PER];
-  int32_t hh[PER];
-  // phase A: every input load of the tile in flight before any dependent work (clamped indices:
-  // unconditional loads cannot be sunk into per-record branches)
+  int64_t* st_key = (int64_t*)smem;
+  int64_t* st_val = st_key + RT_TILE;
+  uint16_t* st_idx = (uint16_t*)(st_val + RT_TILE);
+  int32_t* cnt = (int32_t*)(st_idx + RT_TILE);   // [nbq + 1]
+  int32_t* wtot = cnt + (RT_Q * 256 + 8);        // [NT / 64]
+  const int64_t base = (int64_t)blockIdx.x * RT_TILE;
+  for (int x = threadIdx.x; x <= nbq; x += NT) cnt[x] = 0;
+  // phase A: every load of the tile in flight before any dependent work; record (j, e) of this thread
+  // is tile index 2 * (j * NT + tid) + e
+  int64_t kk[PER], tt[PER], vv[PER];
+  int32_t* lhash = (int32_t*)st_val;    // Java key hashes (optional column) parked in st_val until the scatter
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int64_t i = min(base + (int64_t)k * RT_THREADS + threadIdx.x, b.n - 1);
-    kk[k] = b.key[i];
-    tt[k] = b.ts[i];
-    vv[k] = b.val[i];
-    hh[k] = b.key_hash ? b.key_hash[i] : 0;
+  for (int j = 0; j < V; ++j) {
+    const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
+    if (!tail) {
+      const longlong2 a = *(const longlong2*)(b.key + i);
+      const longlong2 c = *(const longlong2*)(b.ts + i);
+      const longlong2 d = *(const longlong2*)(b.val + i);
+      kk[2 * j] = a.x; kk[2 * j + 1] = a.y;
+      tt[2 * j] = c.x; tt[2 * j + 1] = c.y;
+      vv[2 * j] = d.x; vv[2 * j + 1] = d.y;
+      if (b.key_hash) *(int2*)(lhash + (i - base)) = *(const int2*)(b.key_hash + i);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int64_t ie = min(i + e, b.n - 1);
+        kk[2 * j + e] = b.key[ie];
+        tt[2 * j + e] = b.ts[ie];
+        vv[2 * j + e] = b.val[ie];
+        if (b.key_hash) lhash[i + e - base] = b.key_hash[ie];
+      }
+    }
   }
-  __syncthreads();   // cnt zeroed
-  // phase C: per record; the (slice -> slot, batch slice) lookup is cached per wave, as a wave of an
-  // in-order stream stays in one slice for the whole tile
+  __syncthreads();   // cnt zeroed, key hashes parked
+  // phase B: per record operator work; the (slice -> slot, batch slice) lookup is cached per wave, as a
+  // wave of an in-order stream stays in one slice
   int64_t c_m = INT64_MIN;
   int32_t c_p = -1, c_q = -1;
   unsigned long long late_pairs = 0;
+  int32_t bin[PER];                   // >= 0 routed bin, -1 not routed
+  int32_t rank[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int64_t i = base + (int64_t)k * RT_THREADS + threadIdx.x;
-    const bool valid = i < b.n;
-    const int64_t key = kk[k], ts = tt[k], v = vv[k];
-    const int32_t h = b.key_hash ? hh[k] : long_hash_code(key);
+    const int64_t i = base + 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
+    const bool valid = !tail || i < b.n;
+    const int64_t key = kk[k], ts = tt[k];
     bool ok = valid;
     if (ok && ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
     if (ok) {
-      int32_t kg = key_group_for_hash(h, s.mp);
+      const int32_t h = b.key_hash ? lhash[i - base] : long_hash_code(key);
+      const int32_t kg = record_key_group(s, h);   // AbstractKeyedStateBackend.setCurrentKey :167-170
       if (kg < s.kg_start || kg > s.kg_end) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
     }
     RecWin w;
     w.m = 0; w.n_late = 0; w.n_fire = 0; w.n_windows = 0; w.quirk = false;
     if (ok) {
-      if (r.dbg & 2) { w.m = 1700000000; w.n_windows = 1; }
+      if (r.dbg & 4) { w.m = (int64_t)((double)ts * s.inv_size); w.n_windows = 1; }
       else w = record_windows(s, ts, b.wm);
       if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
     }
     if (ok) late_pairs += (unsigned long long)w.n_late;
-    bool live = ok && (w.n_windows - w.n_late) > 0;
+    const bool live = ok && (w.n_windows - w.n_late) > 0;
     const bool late_fire = live && w.n_fire > 0;
     const uint64_t lm = __ballot(live);
     const int leader = lm ? __ffsll((long long)lm) - 1 : 0;
@@ -520,38 +555,21 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, Rout
       p = slice_slot(s, w.m);
       if (p >= 0) q = batch_slice_q(r, p);
     }
-    if (live && p < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
-    bid[k] = -1;
+    bin[k] = -1;
     rank[k] = 0;
-    // routed records keep their key (resolved to a kid in k_aggregate's LDS directory slice); the rest
-    // (per-element fires, an overflow slice, the Long.MIN_VALUE key) resolve here and update directly
-    const bool routed = live && !late_fire && q >= 0 && key != EMPTY_KEY;
-    const bool direct = live && !routed;
-    int64_t kid = -1;
-    if (direct) {
-      kid = dir_find_or_insert(s, key);
-      if (kid < 0) set_error(s.err, FW_ERR_CAPACITY);
-    }
-    if (b.late_key) {
-      const bool want = direct && kid >= 0 && late_fire;
-      unsigned long long pos = wave_append(b.late_count, want);
-      if (want) {
-        if ((int64_t)pos < b.late_capacity) {
-          unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
-          b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
-        } else {
-          set_error(s.err, FW_ERR_CAPACITY);
-        }
-      }
-    }
-    if (direct && !late_fire && kid >= 0) {
-      pane_update<VT, AGG, FIRST>(s, (int64_t)p * s.stride + kid, v, b.ord_base + i);
-      if (s.touched[p] == 0) s.touched[p] = 1;
-    }
+    const bool routed = live && p >= 0 && !late_fire && q >= 0 && key != EMPTY_KEY;
+    if (live && p < 0) set_error(s.err, FW_ERR_CAPACITY);
     if (routed) {
-      const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
-      bid[k] = q * s.nb + (int32_t)(home >> s.kb_bits);
-      rank[k] = (r.dbg & 8) ? 0 : atomicAdd(&cnt[bid[k]], 1);
+      bin[k] = q * s.nb + (int32_t)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits);
+      rank[k] = atomicAdd(&cnt[bin[k]], 1);
+    }
+    // direct path (rare: per-element fires, a slice beyond the batch's RT_Q, the Long.MIN_VALUE key):
+    // listed for k_aggregate, whose workgroup owning the key's bucket applies it
+    const bool direct = live && p >= 0 && !routed;
+    const unsigned long long dpos = wave_append(r.dcount, direct);
+    if (direct) {
+      if ((int64_t)dpos < r.dcap) r.dlist[dpos] = ((unsigned long long)i << 32) | ((unsigned long long)p << 1) | (late_fire ? 1ull : 0ull);
+      else set_error(s.err, FW_ERR_CAPACITY);
     }
   }
   if (__any(late_pairs != 0)) {
@@ -559,35 +577,44 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, Rout
     if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late_pairs);
   }
   __syncthreads();
-  // segment table of this tile (counts before the scan)
-  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_len[t * nbq + x] = cnt[x];      // tile-major: coalesced
-  const int32_t total = block_exclusive_scan(cnt, nbq, wtot);
-  for (int x = threadIdx.x; x < nbq; x += blockDim.x) r.seg_start[t * nbq + x] = cnt[x];
+  block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
+  uint16_t* seg = r.seg + (int64_t)blockIdx.x * (nbq + 1);
+  for (int x = threadIdx.x; x <= nbq; x += NT) seg[x] = (uint16_t)cnt[x];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    if (bid[k] >= 0) {
-      const int32_t pos = cnt[bid[k]] + rank[k];
+    if (bin[k] >= 0) {
+      const int32_t pos = cnt[bin[k]] + rank[k];
       st_key[pos] = kk[k];
       st_val[pos] = vv[k];
-      st_idx[pos] = (uint16_t)(k * RT_THREADS + threadIdx.x);
+      st_idx[pos] = (uint16_t)(2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1));
     }
   }
   __syncthreads();
-  if (r.dbg & 4) return;
-  for (int j = threadIdx.x; j < total; j += blockDim.x) {
-    r.key[base + j] = st_key[j];
-    r.val[base + j] = st_val[j];
-    if (FIRST) r.idx[base + j] = st_idx[j];
+  const int32_t total = cnt[nbq];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
+    if (pos < total) {
+      *(longlong2*)(r.key + base + pos) = *(const longlong2*)(st_key + pos);
+      *(longlong2*)(r.val + base + pos) = *(const longlong2*)(st_val + pos);
+      if (FIRST) *(uint32_t*)(r.idx + base + pos) = *(const uint32_t*)(st_idx + pos);
+    }
   }
 }
 
 template <int VT, int AGG, bool FIRST>
-__global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, const int64_t* f1col, int64_t ord_base) {
+__global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, RouteBuf r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int bid = blockIdx.x;
-  const int q = bid / s.nb, bkt = bid % s.nb;
-  const int32_t p = r.batch_slot[q];
-  if (p < 0) return;
+  // every tile but the last is whole, so its 16-B loads need no bounds (uniform branch)
+  route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(blockIdx.x + 1) * RT_TILE > b.n);
+}
+
+template <int VT, int AGG, bool FIRST>
+__global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, RouteBuf r, const int64_t* f1col) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NT = AG_THREADS;
+  const int bkt = blockIdx.x;
+  const int nbq = RT_Q * s.nb;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
   int64_t* ldir = (int64_t*)smem;                       // [KB] this bucket's directory slice
@@ -595,45 +622,25 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
   int64_t* lmin = lsum + KB;                            // [KB] (AGG 15)
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KB : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KB : 0);
-  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KB : 0));  // [KB]
-  int32_t* segs = (int32_t*)(lfirst + KB);              // [2 * ntiles]: (start, len)
+  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KB : 0));  // [KB] batch index of the first arrival
+  int32_t* sst = (int32_t*)(lfirst + KB);               // [ntiles] segment start within the tile
+  int32_t* sln = sst + r.ntiles;                        // [ntiles] segment length
   const int64_t dbase = (int64_t)bkt * KB;
-  for (int x = threadIdx.x; x < KB; x += blockDim.x) {
-    ldir[x] = s.dir_keys[dbase + x];
-    lsum[x] = 0;
-    if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
-    if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
-    if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
-    lfirst[x] = NO_FIRST;
-  }
-  const int nbq = RT_Q * s.nb;
-  for (int t = threadIdx.x; t < r.ntiles; t += blockDim.x) {
-    segs[2 * t] = r.seg_start[(int64_t)t * nbq + bid];
-    segs[2 * t + 1] = r.seg_len[(int64_t)t * nbq + bid];
-  }
+  for (int x = threadIdx.x; x < KB; x += NT) ldir[x] = s.dir_keys[dbase + x];
   __syncthreads();
-  // key -> slot in this bucket: the first four probe slots compared without branching (directory
-  // load factor <= 1/4 keeps almost every key there); the loop below takes the rest and inserts
-  // new keys (a global CAS confirms every slot before it enters the LDS copy)
-  auto find = [&](int64_t key, uint32_t& kl, bool& slow) {
-    const uint32_t h = (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm;
-    const int64_t a0 = ldir[h], a1 = ldir[(h + 1) & kbm], a2 = ldir[(h + 2) & kbm], a3 = ldir[(h + 3) & kbm];
-    slow = false;
-    if (a0 == key) kl = h;
-    else if (a0 != EMPTY_KEY && a1 == key) kl = (h + 1) & kbm;
-    else if (a0 != EMPTY_KEY && a1 != EMPTY_KEY && a2 == key) kl = (h + 2) & kbm;
-    else if (a0 != EMPTY_KEY && a1 != EMPTY_KEY && a2 != EMPTY_KEY && a3 == key) kl = (h + 3) & kbm;
-    else { slow = true; kl = h; }
-  };
-  auto find_slow = [&](int64_t key, uint32_t& kl) -> bool {
-    uint32_t x = (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = lane >> 4, sub = lane & 15;
+
+  // key -> slot in this bucket: the home slot compared from a register; the loop takes the rest and
+  // inserts new keys (a global CAS confirms every slot before it enters the LDS copy)
+  auto find_slow = [&](int64_t key, uint32_t x, uint32_t& kl) -> bool {
     for (uint32_t probe = 0; probe <= kbm; ++probe) {
-      int64_t cur = ldir[x];
+      const int64_t cur = ldir[x];
       if (cur == key) { kl = x; return true; }
       if (cur == EMPTY_KEY) {
-        unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)x],
-                                            (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-        int64_t now = (int64_t)prev == EMPTY_KEY ? key : (int64_t)prev;
+        const unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)x],
+                                                  (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+        const int64_t now = (int64_t)prev == EMPTY_KEY ? key : (int64_t)prev;
         ldir[x] = now;   // only globally confirmed keys enter the cache
         if (now == key) { kl = x; return true; }
       }
@@ -641,7 +648,16 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     }
     return false;
   };
-  auto update = [&](uint32_t kl, int64_t v, uint32_t oi) {
+  auto process = [&](bool act, int64_t key, int64_t v, uint32_t oi) {
+    if (r.dbg & 1) { if (act && key == 0x1234567890ll && v == 3) lsum[0] = (int64_t)oi; return; }
+    uint32_t kl = (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm;
+    const int64_t d0 = ldir[kl];
+    if (__any(act && d0 != key)) {
+      if (act && d0 != key) {
+        if (!find_slow(key, kl, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
+      }
+    }
+    if (!act) return;
     if (AGG & FW_AGG_SUM) {
       if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
       else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
@@ -649,74 +665,151 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, RouteBuf r, co
     if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
     if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
-    atomicMin(&lfirst[kl], oi);   // batch index of the record: first arrival
+    atomicMin(&lfirst[kl], oi);
   };
-  auto process = [&](bool act, int64_t key, int64_t v, uint32_t oi) {
-    uint32_t kl = 0;
-    bool slow = false;
-    if (act) find(key, kl, slow);
-    if (__any(act && slow)) {
-      if (act && slow) {
-        if (!find_slow(key, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
-      }
-    }
-    if (act) update(kl, v, oi);
-  };
-  // each wave takes U segments per round, one record per lane; unconditional loads (inactive lanes
-  // read record 0) keep all U segments in flight together; records past a segment's first 64 follow
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  constexpr int U = 8;
-  for (int t0 = wave * U; t0 < r.ntiles; t0 += nw * U) {
-    int64_t kk[U], vv[U];
-    uint32_t oo[U];
-    bool has[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int t = min(t0 + u, r.ntiles - 1);
-      const int32_t st = segs[2 * t], ln = segs[2 * t + 1];
-      has[u] = (t0 + u < r.ntiles) && lane < ln;
-      const int64_t ri = has[u] ? (int64_t)t * RT_TILE + st + lane : 0;
-      kk[u] = r.key[ri];
-      vv[u] = r.val[ri];
-      oo[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) process(has[u], kk[u], vv[u], oo[u]);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {   // long segments (hot keys)
-      const int t = min(t0 + u, r.ntiles - 1);
-      const int32_t ln = (t0 + u < r.ntiles) ? segs[2 * t + 1] : 0;
-      if (ln <= 64) continue;       // wave-uniform
-      const int32_t st = segs[2 * t];
-      for (int j0 = 64; j0 < ln; j0 += 64) {
-        const int j = j0 + lane;
-        const bool act = j < ln;
-        const int64_t ri = act ? (int64_t)t * RT_TILE + st + j : 0;
-        process(act, r.key[ri], r.val[ri], (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[ri] : 0u));
-      }
-    }
+
+  const int64_t ord_base = b.ord_base;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {   // the other parity half serves the next batch
+    for (int q = 0; q < RT_Q; ++q) r.next_slot[q] = -1;
+    *r.next_dcount = 0;
   }
-  __syncthreads();
-  // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
-  for (int x = threadIdx.x; x < KB; x += blockDim.x) {
-    const uint32_t lf = lfirst[x];
-    if (lf == NO_FIRST) continue;
-    const int64_t idx = (int64_t)p * s.stride + dbase + x;
-    if (AGG & FW_AGG_SUM) {
-      if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[x]);
-      else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(lsum[x]));
-    }
-    if (AGG & FW_AGG_MIN) { int64_t o = s.c.mn[idx]; if (lmin[x] < o) s.c.mn[idx] = lmin[x]; }
-    if (AGG & FW_AGG_MAX) { int64_t o = s.c.mx[idx]; if (lmax[x] > o) s.c.mx[idx] = lmax[x]; }
-    if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[x]);
-    if (FIRST) {
-      if (s.c.first[idx] == INT64_MAX) {   // pane created in this batch: its first arrival is ours
-        s.c.first[idx] = ord_base + (int64_t)lf;
-        s.c.f1v[idx] = f1col[lf];
+  // direct-path records of this bucket (listed by k_route): per-element fires join the late list, the
+  // rest update their pane with device-scope atomics; no other workgroup touches this bucket's panes,
+  // and none of them is a pane the LDS fold below writes (other slice, or the Long.MIN_VALUE key column)
+  const int64_t nd = min((int64_t)*r.dcount, r.dcap);
+  if (nd > 0) {
+    for (int64_t x0 = 0; x0 < nd; x0 += NT) {
+      const int64_t x = x0 + threadIdx.x;
+      const unsigned long long ent = x < nd ? r.dlist[x] : 0ull;
+      const int64_t i = (int64_t)(ent >> 32);
+      const int32_t p = (int32_t)((ent >> 1) & 0x7FFFFFFFull);
+      const bool fire = (ent & 1ull) != 0;
+      const int64_t key = x < nd ? b.key[i] : 0;
+      bool mine = x < nd && (key == EMPTY_KEY ? bkt == 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) == bkt);
+      int64_t kid = -1;
+      if (mine) {
+        uint32_t kl = 0;
+        if (key == EMPTY_KEY) { kid = dir_find_or_insert(s, key); }
+        else if (find_slow(key, (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm, kl)) kid = dbase + kl;
+        if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); mine = false; }
       }
-    } else {
-      s.c.present[idx] = 1;
+      const bool want = mine && fire && b.late_key != nullptr;
+      const unsigned long long pos = wave_append(b.late_count, want);
+      if (want) {
+        if ((int64_t)pos < b.late_capacity) {
+          const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
+          b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
+        } else {
+          set_error(s.err, FW_ERR_CAPACITY);
+        }
+      }
+      if (mine && !fire) pane_update<VT, AGG, FIRST>(s, (int64_t)p * s.stride + kid, b.val[i], ord_base + i);
     }
+    __syncthreads();
+    if (FIRST) {   // f1 of panes whose first arrival is a direct record of this batch
+      for (int64_t x = threadIdx.x; x < nd; x += NT) {
+        const unsigned long long ent = r.dlist[x];
+        if (ent & 1ull) continue;
+        const int64_t i = (int64_t)(ent >> 32);
+        const int32_t p = (int32_t)((ent >> 1) & 0x7FFFFFFFull);
+        const int64_t key = b.key[i];
+        if (key == EMPTY_KEY ? bkt != 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) != bkt) continue;
+        uint32_t kl = 0;
+        int64_t kid = -1;
+        if (key == EMPTY_KEY) kid = s.D;
+        else if (find_slow(key, (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm, kl)) kid = dbase + kl;
+        if (kid < 0) continue;
+        const int64_t idx = (int64_t)p * s.stride + kid;
+        if (__hip_atomic_load(&s.c.first[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ord_base + i)
+          s.c.f1v[idx] = f1col[i];
+      }
+    }
+    __syncthreads();
+  }
+
+  for (int q = 0; q < RT_Q; ++q) {
+    const int32_t p = r.batch_slot[q];
+    if (p < 0) continue;                                // uniform: no record of the batch in slice q
+    const int bin = q * s.nb + bkt;
+    for (int x = threadIdx.x; x < KB; x += NT) {
+      lsum[x] = 0;
+      if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
+      if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
+      if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
+      lfirst[x] = NO_FIRST;
+    }
+    for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+      const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
+      const int32_t a0 = seg[bin], a1 = seg[bin + 1];
+      sst[t] = a0;
+      sln[t] = a1 - a0;
+    }
+    __syncthreads();
+    // each 16-lane group reads one tile's segment, 2 records per lane per round; UR rounds of 4 segments
+    // per wave-step, every load issued before any dependent work
+    constexpr int UR = 4;
+    for (int tb = wave * 4 * UR; tb < r.ntiles; tb += (NT / 64) * 4 * UR) {
+      int64_t ka[UR], kb2[UR], va[UR], vb[UR];
+      uint32_t ia[UR], ib[UR];
+      bool aa[UR], ab[UR];
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        const int tt = tb + u * 4 + grp;
+        const int t = min(tt, r.ntiles - 1);
+        const int32_t st = sst[t], ln = tt < r.ntiles ? sln[t] : 0;
+        aa[u] = sub < ln;
+        ab[u] = sub + 16 < ln;
+        const int64_t pa = (int64_t)t * RT_TILE + (aa[u] ? st + sub : 0);        // inactive lanes read the tile's first slot
+        const int64_t pb = (int64_t)t * RT_TILE + (ab[u] ? st + sub + 16 : 0);
+        ka[u] = r.key[pa]; kb2[u] = r.key[pb];
+        va[u] = r.val[pa]; vb[u] = r.val[pb];
+        ia[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pa] : 0u);
+        ib[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pb] : 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        process(aa[u], ka[u], va[u], ia[u]);
+        process(ab[u], kb2[u], vb[u], ib[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {   // segments longer than 32 records (hot keys, skew)
+        const int tt = tb + u * 4 + grp;
+        const int32_t ln = tt < r.ntiles ? sln[tt] : 0;
+        if (__any(ln > 32)) {
+          const int t = min(tt, r.ntiles - 1);
+          for (int j0 = 32; __any(j0 < ln); j0 += 16) {
+            const bool act = j0 + sub < ln;
+            const int64_t pp = (int64_t)t * RT_TILE + (act ? sst[t] + j0 + sub : 0);
+            process(act, r.key[pp], r.val[pp], (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pp] : 0u));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
+    // (direct-path updates of k_route finished before this kernel started)
+    for (int x = threadIdx.x; x < KB; x += NT) {
+      const uint32_t lf = lfirst[x];
+      if (lf == NO_FIRST || (r.dbg & 2)) continue;
+      const int64_t idx = (int64_t)p * s.stride + dbase + x;
+      if (AGG & FW_AGG_SUM) {
+        if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[x]);
+        else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(lsum[x]));
+      }
+      if (AGG & FW_AGG_MIN) { const int64_t o = s.c.mn[idx]; if (lmin[x] < o) s.c.mn[idx] = lmin[x]; }
+      if (AGG & FW_AGG_MAX) { const int64_t o = s.c.mx[idx]; if (lmax[x] > o) s.c.mx[idx] = lmax[x]; }
+      if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[x]);
+      if (FIRST) {
+        const int64_t cand = ord_base + (int64_t)lf;
+        if (cand < s.c.first[idx]) {   // first arrival: earlier than any previous batch or direct update
+          s.c.first[idx] = cand;
+          s.c.f1v[idx] = f1col[lf];
+        }
+      } else {
+        s.c.present[idx] = 1;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1185,6 +1278,9 @@ struct fw_engine {
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
   RouteBuf rb{};
+  int32_t* slots = nullptr;                 // batch slice -> pane slot, two parity halves
+  unsigned long long* dcounts = nullptr;    // direct-list lengths, two parity halves
+  int64_t batches = 0;
   int32_t max_tiles = 0;
   size_t route_lds = 0, agg_lds = 0;
   // partition scratch
@@ -1246,10 +1342,15 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   RouteBuf r = e->rb;
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
   const size_t agg_lds = e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8;
-  (void)hipMemsetAsync(r.batch_slot, 0xFF, sizeof(int32_t) * RT_Q, e->stream);
+  const int par = (int)(e->batches & 1);
+  r.batch_slot = e->slots + par * RT_Q;
+  r.next_slot = e->slots + (1 - par) * RT_Q;
+  r.dcount = e->dcounts + par;
+  r.next_dcount = e->dcounts + (1 - par);
   hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, e->stream, e->s, b, r);
-  hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST>), dim3(RT_Q * e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, r,
-                     f1col, b.ord_base);
+  hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b, r,
+                     f1col);
+  e->batches++;
 }
 
 template <int VT, int AGG, bool FIRST>
@@ -1323,6 +1424,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.R = (int32_t)(s.slide / s.g);
   if (s.K > MAX_K) return unsupported("more than 64 slices per window (size / gcd(size, slide))");
   s.mp = c.max_parallelism;
+  s.mp_mask = (c.max_parallelism & (c.max_parallelism - 1)) == 0 ? c.max_parallelism - 1 : 0;
   s.kg_start = c.kg_start;
   s.kg_end = c.kg_end;
   s.vt = c.value_type;
@@ -1401,12 +1503,14 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       e->rb.key = e->alloc<int64_t>(cap);
       e->rb.val = e->alloc<int64_t>(cap);
       e->rb.idx = e->alloc<uint16_t>(cap);
-      e->rb.seg_start = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
-      e->rb.seg_len = e->alloc<int32_t>((size_t)RT_Q * s.nb * e->max_tiles);
-      e->rb.batch_slot = e->alloc<int32_t>(RT_Q);
+      e->rb.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * e->max_tiles);
+      e->slots = e->alloc<int32_t>(2 * RT_Q);
+      e->dcounts = e->alloc<unsigned long long>(2);
+      e->rb.dcap = c.max_batch;
+      e->rb.dlist = e->alloc<unsigned long long>((size_t)c.max_batch);
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
-      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 1) + 4 * 16;
+      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 8) + 4 * (RT_THREADS / 64);
       const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
       e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles;
       if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
@@ -1461,6 +1565,10 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(s.err, 0, 4, e->stream));
   HIPCHK(e, hipMemsetAsync(s.stats, 0, 8 * ST_NSTATS, e->stream));
   HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
+  if (e->routed) {
+    HIPCHK(e, hipMemsetAsync(e->slots, 0xFF, sizeof(int32_t) * 2 * RT_Q, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 16, e->stream));
+  }
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
   *out = e;
@@ -1505,6 +1613,14 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     if (key_hash) { HIPCHK(e, hipMemcpyAsync(e->st_hash, key_hash, 4 * n, hipMemcpyHostToDevice, e->stream)); dh = e->st_hash; }
     if (f1) { HIPCHK(e, hipMemcpyAsync(e->st_f1, f1, 8 * n, hipMemcpyHostToDevice, e->stream)); df1 = e->st_f1; }
   }
+  if (e->routed && mem == FW_MEM_DEVICE) {
+    // k_route streams the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
+    auto mis = [](const void* ptr, uintptr_t a) { return ((uintptr_t)ptr & (a - 1)) != 0; };
+    if (mis(dk, 16)) { HIPCHK(e, hipMemcpyAsync(e->st_key, dk, 8 * n, hipMemcpyDeviceToDevice, e->stream)); dk = e->st_key; }
+    if (mis(dts, 16)) { HIPCHK(e, hipMemcpyAsync(e->st_ts, dts, 8 * n, hipMemcpyDeviceToDevice, e->stream)); dts = e->st_ts; }
+    if (mis(dv, 16)) { HIPCHK(e, hipMemcpyAsync(e->st_val, dv, 8 * n, hipMemcpyDeviceToDevice, e->stream)); dv = e->st_val; }
+    if (dh && mis(dh, 8)) { HIPCHK(e, hipMemcpyAsync(e->st_hash, dh, 4 * n, hipMemcpyDeviceToDevice, e->stream)); dh = e->st_hash; }
+  }
   if (!df1) df1 = dts;
   BatchIn b;
   b.key = dk; b.key_hash = dh; b.ts = dts; b.val = dv; b.n = n;
@@ -1519,13 +1635,13 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   else FW_DISPATCH(launch_ingest_t, e, b);
   e->phase_end(n);
   HIPCHK(e, hipGetLastError());
-  if (e->s.first) {
+  if (e->s.first && !e->routed) {   // the partitioned form sets f1 in k_aggregate
     e->phase_begin(FW_PHASE_FIXUP);
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
                        e->stream, e->s, df1, e->ordinal, n);
     e->phase_end(e->s.stride);
   }
-  HIPCHK(e, hipMemsetAsync(e->s.touched, 0, 4 * (size_t)e->s.P, e->stream));
+  if (!e->routed) HIPCHK(e, hipMemsetAsync(e->s.touched, 0, 4 * (size_t)e->s.P, e->stream));
   if (e->cfg.allowed_lateness > 0) {
     // per-element fires: need the count on the host to size the sort
     unsigned long long nl = 0;

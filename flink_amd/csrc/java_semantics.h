@@ -63,7 +63,10 @@ FW_HD int64_t cleanup_time(int64_t max_ts, int64_t allowed_lateness) {
 
 // Java truncating division and remainder of x by a positive divisor d (x = q*d + r, r has x's sign).
 // Exact; fast path through a double reciprocal when |x| < 2^52 (the 64-bit integer divide is a long
-// instruction sequence on the GPU), fixed up by at most a couple of correction steps.
+// instruction sequence on the GPU, kept out of line), fixed up by at most a couple of correction steps.
+struct QR { int64_t q, r; };
+__host__ __device__ __attribute__((noinline)) inline QR jdivmod_wide(int64_t x, int64_t d) { return QR{x / d, x % d}; }
+
 FW_HD void jdivmod(int64_t x, int64_t d, double inv_d, int64_t& q, int64_t& r) {
   const int64_t lim = (int64_t)1 << 52;
   if (x > -lim && x < lim && d < lim) {
@@ -79,8 +82,9 @@ FW_HD void jdivmod(int64_t x, int64_t d, double inv_d, int64_t& q, int64_t& r) {
     q = qq; r = rr;
     return;
   }
-  q = x / d;
-  r = x % d;
+  const QR w = jdivmod_wide(x, d);
+  q = w.q;
+  r = w.r;
 }
 
 // floor division / modulo on int64 (slice numbering; not Java semantics, internal indexing)
