@@ -111,6 +111,18 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {  // MurmurHash3 finalis
   return k;
 }
 
+// inverse of fmix64 (fmix64 is a bijection on 64-bit words): k ^= k >> 33 is an involution, and the
+// multipliers are odd, so their inverses mod 2^64 exist
+__device__ __forceinline__ uint64_t fmix64_inv(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0x9cb4b2f8129337dbull;
+  h ^= h >> 33;
+  h *= 0x4f74430c22a54005ull;
+  h ^= h >> 33;
+  return h;
+}
+constexpr uint64_t EMPTY_H = 0x8f780810af31a493ull;   // fmix64(Long.MIN_VALUE): the hash of an empty slot
+
 __device__ __forceinline__ uint64_t lanemask_lt() { return __lanemask_lt(); }
 
 // wave-aggregated counter add; returns this lane's slot (only meaningful where pred)
@@ -402,33 +414,52 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
 // ------------------------------------------------------------------------------------------------
 constexpr int RT_TILE = 4096;
 constexpr int RT_THREADS = 512;
-constexpr int RT_Q = 2;                 // slices per batch handled by the partitioned form
+constexpr int RT_Q = 2;                 // slices per tile routed through LDS (more go to the direct path)
+constexpr int RT_HS = 8;                // tile-local slice set (claims and per-tile routing)
+constexpr int RT_GS = 64;               // distinct routed slices per batch (k_aggregate rounds)
 constexpr int AG_THREADS = 1024;
 constexpr int RT_MAX_KB_BITS = 10;      // directory slots per bucket held in LDS by k_aggregate
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
-  int64_t* key;          // [ntiles][RT_TILE] routed records, each tile sorted by bin
-  int64_t* val;          // [ntiles][RT_TILE]
+  longlong2* kv;         // [ntiles][RT_TILE] routed records (fmix64(key), value), each tile sorted by bin
   uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
   uint16_t* seg;         // [ntiles][nbq + 1] start of each bin's segment in the tile; [nbq] = routed count
-  int32_t* batch_slot;   // [RT_Q] pane-slice slot of batch slice q, -1 if unused (this batch's parity half)
-  int32_t* next_slot;    // [RT_Q] the other parity half: reset by k_aggregate for the next batch
+  int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
   unsigned long long* dlist;    // direct-path records: (batch index << 32) | (slot << 1) | per-element fire
   unsigned long long* dcount;   // this batch's direct-list length
   unsigned long long* next_dcount;
   int64_t dcap;
+  long long* stamps;     // diagnostics (FW_DEBUG_AGG & 16): per-workgroup phase timestamps, 8 per workgroup
   int32_t ntiles;
   int32_t dbg;
 };
 
-__device__ __forceinline__ int32_t batch_slice_q(const RouteBuf& r, int32_t p) {
-  for (int q = 0; q < RT_Q; ++q) {
-    int32_t v = r.batch_slot[q];
-    if (v == p) return q;
-    if (v == -1) {
-      int32_t prev = atomicCAS(&r.batch_slot[q], -1, p);
-      if (prev == -1 || prev == p) return q;
+#define FW_STAMP(r, base, k) do { if ((r).stamps && threadIdx.x == 0) (r).stamps[(base) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+
+// Pane-slice slots are a pure function of the slice number (p = floor_mod(m, P)), so claiming one is an
+// idempotent plain store: every claimer of slot p in a batch stores the same m, unless two slices that
+// collide mod P are live at once — the pool is then exhausted (FW_ERR_CAPACITY), which k_aggregate
+// detects from the tile headers after the kernel boundary.  No device-scope atomic on the hot path.
+__device__ __noinline__ void claim_slice_slot(int64_t* slice_tag, int32_t P, int64_t m, int32_t* err) {
+  const int32_t p = (int32_t)floor_mod(m, P);
+  const int64_t tag = slice_tag[p];
+  if (tag == m) return;
+  if (tag == FREE_TAG) slice_tag[p] = m;
+  else set_error(err, FW_ERR_CAPACITY);
+}
+
+// tile-local slice set in LDS: index of slice m, inserting it (and claiming its pane slot) if new;
+// -1 when the set is full
+__device__ __forceinline__ int32_t tile_slice(const Spec& s, int64_t* lset, int64_t m) {
+  for (int q = 0; q < RT_HS; ++q) {
+    const int64_t cur = lset[q];
+    if (cur == m) return q;
+    if (cur == FREE_TAG) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&lset[q], (unsigned long long)FREE_TAG,
+                                                (unsigned long long)m);
+      if ((int64_t)prev == FREE_TAG) { claim_slice_slot(s.slice_tag, s.P, m, s.err); return q; }
+      if ((int64_t)prev == m) return q;
     }
   }
   return -1;
@@ -470,17 +501,19 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   constexpr int PER = RT_TILE / NT;     // records per thread
   constexpr int V = PER / 2;            // 16-B vectors per column per thread
   const int nbq = RT_Q * s.nb;
-  int64_t* st_key = (int64_t*)smem;
-  int64_t* st_val = st_key + RT_TILE;
-  uint16_t* st_idx = (uint16_t*)(st_val + RT_TILE);
+  longlong2* st_kv = (longlong2*)smem;
+  uint16_t* st_idx = (uint16_t*)(st_kv + RT_TILE);
   int32_t* cnt = (int32_t*)(st_idx + RT_TILE);   // [nbq + 1]
   int32_t* wtot = cnt + (RT_Q * 256 + 8);        // [NT / 64]
+  int64_t* lset = (int64_t*)(wtot + 16);         // [RT_HS] the tile's slices
   const int64_t base = (int64_t)blockIdx.x * RT_TILE;
+  FW_STAMP(r, 0, 0);
   for (int x = threadIdx.x; x <= nbq; x += NT) cnt[x] = 0;
+  if (threadIdx.x < RT_HS) lset[threadIdx.x] = FREE_TAG;
   // phase A: every load of the tile in flight before any dependent work; record (j, e) of this thread
   // is tile index 2 * (j * NT + tid) + e
   int64_t kk[PER], tt[PER], vv[PER];
-  int32_t* lhash = (int32_t*)st_val;    // Java key hashes (optional column) parked in st_val until the scatter
+  int32_t* lhash = (int32_t*)st_kv;     // Java key hashes (optional column) parked in st_kv until the scatter
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
@@ -504,10 +537,11 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     }
   }
   __syncthreads();   // cnt zeroed, key hashes parked
+  FW_STAMP(r, 0, 1);
   // phase B: per record operator work; the (slice -> slot, batch slice) lookup is cached per wave, as a
   // wave of an in-order stream stays in one slice
   int64_t c_m = INT64_MIN;
-  int32_t c_p = -1, c_q = -1;
+  int32_t c_q = -1;
   unsigned long long late_pairs = 0;
   int32_t bin[PER];                   // >= 0 routed bin, -1 not routed
   int32_t rank[PER];
@@ -537,38 +571,33 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     const int leader = lm ? __ffsll((long long)lm) - 1 : 0;
     const int64_t m0 = __shfl(w.m, leader);
     const bool uniform = __all(!live || w.m == m0);
-    int32_t p = -1, q = -1;
+    int32_t q = -1;
     if (uniform) {
       if (lm != 0 && m0 != c_m) {   // wave-uniform branch
-        int32_t p0 = -1, q0 = -1;
-        if ((int)(threadIdx.x & 63) == leader) {
-          p0 = slice_slot(s, m0);
-          if (p0 >= 0) q0 = batch_slice_q(r, p0);
-        }
-        c_p = __shfl(p0, leader);
+        int32_t q0 = -1;
+        if ((int)(threadIdx.x & 63) == leader) q0 = tile_slice(s, lset, m0);
         c_q = __shfl(q0, leader);
-        c_m = c_p >= 0 ? m0 : INT64_MIN;
+        c_m = m0;
       }
-      p = live ? c_p : -1;
       q = live ? c_q : -1;
     } else if (live) {
-      p = slice_slot(s, w.m);
-      if (p >= 0) q = batch_slice_q(r, p);
+      q = tile_slice(s, lset, w.m);
     }
     bin[k] = -1;
     rank[k] = 0;
-    const bool routed = live && p >= 0 && !late_fire && q >= 0 && key != EMPTY_KEY;
-    if (live && p < 0) set_error(s.err, FW_ERR_CAPACITY);
+    const bool routed = live && !late_fire && q >= 0 && q < RT_Q && key != EMPTY_KEY;
     if (routed) {
-      bin[k] = q * s.nb + (int32_t)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits);
+      const uint64_t hk = fmix64((uint64_t)key);
+      bin[k] = q * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
       rank[k] = atomicAdd(&cnt[bin[k]], 1);
+      kk[k] = (int64_t)hk;   // routed records carry the directory hash (a bijection of the key)
     }
     // direct path (rare: per-element fires, a slice beyond the batch's RT_Q, the Long.MIN_VALUE key):
     // listed for k_aggregate, whose workgroup owning the key's bucket applies it
-    const bool direct = live && p >= 0 && !routed;
+    const bool direct = live && !routed;
     const unsigned long long dpos = wave_append(r.dcount, direct);
     if (direct) {
-      if ((int64_t)dpos < r.dcap) r.dlist[dpos] = ((unsigned long long)i << 32) | ((unsigned long long)p << 1) | (late_fire ? 1ull : 0ull);
+      if ((int64_t)dpos < r.dcap) r.dlist[dpos] = ((unsigned long long)i << 1) | (late_fire ? 1ull : 0ull);
       else set_error(s.err, FW_ERR_CAPACITY);
     }
   }
@@ -577,6 +606,8 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late_pairs);
   }
   __syncthreads();
+  FW_STAMP(r, 0, 2);
+  if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];
   block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
   uint16_t* seg = r.seg + (int64_t)blockIdx.x * (nbq + 1);
   for (int x = threadIdx.x; x <= nbq; x += NT) seg[x] = (uint16_t)cnt[x];
@@ -584,22 +615,26 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   for (int k = 0; k < PER; ++k) {
     if (bin[k] >= 0) {
       const int32_t pos = cnt[bin[k]] + rank[k];
-      st_key[pos] = kk[k];
-      st_val[pos] = vv[k];
+      st_kv[pos] = make_longlong2(kk[k], vv[k]);
       st_idx[pos] = (uint16_t)(2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1));
     }
   }
   __syncthreads();
+  FW_STAMP(r, 0, 3);
   const int32_t total = cnt[nbq];
+#pragma unroll 2
+  for (int k = 0; k < PER; ++k) {
+    const int32_t pos = k * NT + (int)threadIdx.x;
+    if (pos < total) r.kv[base + pos] = st_kv[pos];
+  }
+  if (FIRST) {
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
-    const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
-    if (pos < total) {
-      *(longlong2*)(r.key + base + pos) = *(const longlong2*)(st_key + pos);
-      *(longlong2*)(r.val + base + pos) = *(const longlong2*)(st_val + pos);
-      if (FIRST) *(uint32_t*)(r.idx + base + pos) = *(const uint32_t*)(st_idx + pos);
+    for (int j = 0; j < V; ++j) {
+      const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
+      if (pos < total) *(uint32_t*)(r.idx + base + pos) = *(const uint32_t*)(st_idx + pos);
     }
   }
+  FW_STAMP(r, 0, 4);
 }
 
 template <int VT, int AGG, bool FIRST>
@@ -617,8 +652,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   const int nbq = RT_Q * s.nb;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
-  int64_t* ldir = (int64_t*)smem;                       // [KB] this bucket's directory slice
-  int64_t* lsum = ldir + KB;                            // [KB]
+  uint64_t* lh = (uint64_t*)smem;                       // [KB] fmix64 of this bucket's directory slice (EMPTY_H = free)
+  int64_t* lsum = (int64_t*)(lh + KB);                  // [KB]
   int64_t* lmin = lsum + KB;                            // [KB] (AGG 15)
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KB : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KB : 0);
@@ -626,38 +661,47 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   int32_t* sst = (int32_t*)(lfirst + KB);               // [ntiles] segment start within the tile
   int32_t* sln = sst + r.ntiles;                        // [ntiles] segment length
   const int64_t dbase = (int64_t)bkt * KB;
-  for (int x = threadIdx.x; x < KB; x += NT) ldir[x] = s.dir_keys[dbase + x];
+  const int64_t SB = (int64_t)8 << 16;
+  FW_STAMP(r, SB, 0);
+  for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
   __syncthreads();
+  FW_STAMP(r, SB, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int grp = lane >> 4, sub = lane & 15;
 
-  // key -> slot in this bucket: the home slot compared from a register; the loop takes the rest and
-  // inserts new keys (a global CAS confirms every slot before it enters the LDS copy)
-  auto find_slow = [&](int64_t key, uint32_t x, uint32_t& kl) -> bool {
+  // directory hash -> slot in this bucket.  Linear probing keeps a key within the run that starts at
+  // its home slot, so the first four slots are compared without branching (the directory's load factor
+  // <= 1/4 keeps nearly every key there); the loop takes the rest and inserts new keys (a global CAS on
+  // the key, fmix64_inv(h), confirms every slot before it enters the LDS copy)
+  auto find_slow = [&](uint64_t h, uint32_t& kl) -> bool {
+    uint32_t x = (uint32_t)h & kbm;
     for (uint32_t probe = 0; probe <= kbm; ++probe) {
-      const int64_t cur = ldir[x];
-      if (cur == key) { kl = x; return true; }
-      if (cur == EMPTY_KEY) {
+      const uint64_t cur = lh[x];
+      if (cur == h) { kl = x; return true; }
+      if (cur == EMPTY_H) {
+        const int64_t key = (int64_t)fmix64_inv(h);
         const unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)x],
                                                   (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-        const int64_t now = (int64_t)prev == EMPTY_KEY ? key : (int64_t)prev;
-        ldir[x] = now;   // only globally confirmed keys enter the cache
-        if (now == key) { kl = x; return true; }
+        const uint64_t now = (int64_t)prev == EMPTY_KEY ? h : fmix64(prev);
+        lh[x] = now;   // only globally confirmed keys enter the cache
+        if (now == h) { kl = x; return true; }
       }
       x = (x + 1) & kbm;
     }
     return false;
   };
-  auto process = [&](bool act, int64_t key, int64_t v, uint32_t oi) {
-    if (r.dbg & 1) { if (act && key == 0x1234567890ll && v == 3) lsum[0] = (int64_t)oi; return; }
-    uint32_t kl = (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm;
-    const int64_t d0 = ldir[kl];
-    if (__any(act && d0 != key)) {
-      if (act && d0 != key) {
-        if (!find_slow(key, kl, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
+  auto process = [&](bool act, uint64_t h, int64_t v, uint32_t oi) {
+    if (r.dbg & 1) { if (act && h == 0x1234567890ull && v == 3) lsum[0] = (int64_t)oi; return; }
+    const uint32_t h0 = (uint32_t)h & kbm;
+    const uint64_t a0 = lh[h0], a1 = lh[(h0 + 1) & kbm], a2 = lh[(h0 + 2) & kbm], a3 = lh[(h0 + 3) & kbm];
+    uint32_t kl = a0 == h ? h0 : a1 == h ? ((h0 + 1) & kbm) : a2 == h ? ((h0 + 2) & kbm) : ((h0 + 3) & kbm);
+    const bool hit = a0 == h || a1 == h || a2 == h || a3 == h;
+    if (!(r.dbg & 64) && __any(act && !hit)) {
+      if (act && !hit) {
+        if (!find_slow(h, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
       }
     }
-    if (!act) return;
+    if (!act || (r.dbg & 32)) return;
     if (AGG & FW_AGG_SUM) {
       if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
       else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
@@ -669,10 +713,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   };
 
   const int64_t ord_base = b.ord_base;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {   // the other parity half serves the next batch
-    for (int q = 0; q < RT_Q; ++q) r.next_slot[q] = -1;
-    *r.next_dcount = 0;
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *r.next_dcount = 0;   // the other parity half serves the next batch
   // direct-path records of this bucket (listed by k_route): per-element fires join the late list, the
   // rest update their pane with device-scope atomics; no other workgroup touches this bucket's panes,
   // and none of them is a pane the LDS fold below writes (other slice, or the Long.MIN_VALUE key column)
@@ -681,16 +722,20 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     for (int64_t x0 = 0; x0 < nd; x0 += NT) {
       const int64_t x = x0 + threadIdx.x;
       const unsigned long long ent = x < nd ? r.dlist[x] : 0ull;
-      const int64_t i = (int64_t)(ent >> 32);
-      const int32_t p = (int32_t)((ent >> 1) & 0x7FFFFFFFull);
+      const int64_t i = (int64_t)(ent >> 1);
       const bool fire = (ent & 1ull) != 0;
       const int64_t key = x < nd ? b.key[i] : 0;
       bool mine = x < nd && (key == EMPTY_KEY ? bkt == 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) == bkt);
       int64_t kid = -1;
+      int32_t p = -1;
+      if (mine) {
+        p = slice_slot(s, record_windows(s, b.ts[i], b.wm).m);   // claimed by k_route unless its tile set overflowed
+        if (p < 0) { set_error(s.err, FW_ERR_CAPACITY); mine = false; }
+      }
       if (mine) {
         uint32_t kl = 0;
         if (key == EMPTY_KEY) { kid = dir_find_or_insert(s, key); }
-        else if (find_slow(key, (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm, kl)) kid = dbase + kl;
+        else if (find_slow(fmix64((uint64_t)key), kl)) kid = dbase + kl;
         if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); mine = false; }
       }
       const bool want = mine && fire && b.late_key != nullptr;
@@ -710,15 +755,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       for (int64_t x = threadIdx.x; x < nd; x += NT) {
         const unsigned long long ent = r.dlist[x];
         if (ent & 1ull) continue;
-        const int64_t i = (int64_t)(ent >> 32);
-        const int32_t p = (int32_t)((ent >> 1) & 0x7FFFFFFFull);
+        const int64_t i = (int64_t)(ent >> 1);
         const int64_t key = b.key[i];
         if (key == EMPTY_KEY ? bkt != 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) != bkt) continue;
         uint32_t kl = 0;
         int64_t kid = -1;
         if (key == EMPTY_KEY) kid = s.D;
-        else if (find_slow(key, (uint32_t)(fmix64((uint64_t)key) & s.dir_mask) & kbm, kl)) kid = dbase + kl;
+        else if (find_slow(fmix64((uint64_t)key), kl)) kid = dbase + kl;
         if (kid < 0) continue;
+        const int32_t p = (int32_t)floor_mod(record_windows(s, b.ts[i], b.wm).m, s.P);
         const int64_t idx = (int64_t)p * s.stride + kid;
         if (__hip_atomic_load(&s.c.first[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ord_base + i)
           s.c.f1v[idx] = f1col[i];
@@ -727,10 +772,33 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     __syncthreads();
   }
 
-  for (int q = 0; q < RT_Q; ++q) {
-    const int32_t p = r.batch_slot[q];
-    if (p < 0) continue;                                // uniform: no record of the batch in slice q
-    const int bin = q * s.nb + bkt;
+  // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same set)
+  int64_t* gsl = (int64_t*)(sln + r.ntiles);            // [RT_GS]
+  if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
+  __syncthreads();
+  for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+    for (int qq = 0; qq < RT_Q; ++qq) {
+      const int64_t m = r.hdr[(int64_t)t * RT_Q + qq];
+      if (m == FREE_TAG) break;
+      int g = 0;
+      for (; g < RT_GS; ++g) {
+        const int64_t cur = gsl[g];
+        if (cur == m) break;
+        if (cur == FREE_TAG) {
+          const unsigned long long prev = atomicCAS((unsigned long long*)&gsl[g], (unsigned long long)FREE_TAG, (unsigned long long)m);
+          if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) break;
+        }
+      }
+      if (g == RT_GS) set_error(s.err, FW_ERR_CAPACITY);   // more distinct slices in one batch than RT_GS
+    }
+  }
+  __syncthreads();
+  for (int g = 0; g < RT_GS; ++g) {
+    const int64_t m = gsl[g];
+    if (m == FREE_TAG) break;                            // uniform
+    const int32_t p = (int32_t)floor_mod(m, s.P);
+    if (bkt == 0 && threadIdx.x == 0 && s.slice_tag[p] != m) set_error(s.err, FW_ERR_CAPACITY);   // colliding claims
+    const int q = g;
     for (int x = threadIdx.x; x < KB; x += NT) {
       lsum[x] = 0;
       if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
@@ -739,17 +807,25 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       lfirst[x] = NO_FIRST;
     }
     for (int t = threadIdx.x; t < r.ntiles; t += NT) {
-      const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
-      const int32_t a0 = seg[bin], a1 = seg[bin + 1];
+      const int64_t h0 = r.hdr[(int64_t)t * RT_Q], h1 = r.hdr[(int64_t)t * RT_Q + 1];
+      const int ql = h0 == m ? 0 : (h1 == m ? 1 : -1);
+      int32_t a0 = 0, a1 = 0;
+      if (ql >= 0) {
+        const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
+        const int bin = ql * s.nb + bkt;
+        a0 = seg[bin];
+        a1 = seg[bin + 1];
+      }
       sst[t] = a0;
       sln[t] = a1 - a0;
     }
     __syncthreads();
+    FW_STAMP(r, SB, 2 + 3 * min(q, 1));
     // each 16-lane group reads one tile's segment, 2 records per lane per round; UR rounds of 4 segments
     // per wave-step, every load issued before any dependent work
-    constexpr int UR = 4;
+    constexpr int UR = 6;
     for (int tb = wave * 4 * UR; tb < r.ntiles; tb += (NT / 64) * 4 * UR) {
-      int64_t ka[UR], kb2[UR], va[UR], vb[UR];
+      longlong2 ra[UR], rb2[UR];
       uint32_t ia[UR], ib[UR];
       bool aa[UR], ab[UR];
 #pragma unroll
@@ -761,15 +837,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         ab[u] = sub + 16 < ln;
         const int64_t pa = (int64_t)t * RT_TILE + (aa[u] ? st + sub : 0);        // inactive lanes read the tile's first slot
         const int64_t pb = (int64_t)t * RT_TILE + (ab[u] ? st + sub + 16 : 0);
-        ka[u] = r.key[pa]; kb2[u] = r.key[pb];
-        va[u] = r.val[pa]; vb[u] = r.val[pb];
+        ra[u] = r.kv[pa];
+        rb2[u] = r.kv[pb];
         ia[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pa] : 0u);
         ib[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pb] : 0u);
       }
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
-        process(aa[u], ka[u], va[u], ia[u]);
-        process(ab[u], kb2[u], vb[u], ib[u]);
+        process(aa[u], (uint64_t)ra[u].x, ra[u].y, ia[u]);
+        process(ab[u], (uint64_t)rb2[u].x, rb2[u].y, ib[u]);
       }
 #pragma unroll
       for (int u = 0; u < UR; ++u) {   // segments longer than 32 records (hot keys, skew)
@@ -780,12 +856,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
           for (int j0 = 32; __any(j0 < ln); j0 += 16) {
             const bool act = j0 + sub < ln;
             const int64_t pp = (int64_t)t * RT_TILE + (act ? sst[t] + j0 + sub : 0);
-            process(act, r.key[pp], r.val[pp], (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pp] : 0u));
+            const longlong2 rr = r.kv[pp];
+            process(act, (uint64_t)rr.x, rr.y, (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pp] : 0u));
           }
         }
       }
     }
     __syncthreads();
+    FW_STAMP(r, SB, 3 + 3 * min(q, 1));
     // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
     // (direct-path updates of k_route finished before this kernel started)
     for (int x = threadIdx.x; x < KB; x += NT) {
@@ -810,6 +888,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       }
     }
     __syncthreads();
+    FW_STAMP(r, SB, 4 + 3 * min(q, 1));
   }
 }
 
@@ -1278,7 +1357,6 @@ struct fw_engine {
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
   RouteBuf rb{};
-  int32_t* slots = nullptr;                 // batch slice -> pane slot, two parity halves
   unsigned long long* dcounts = nullptr;    // direct-list lengths, two parity halves
   int64_t batches = 0;
   int32_t max_tiles = 0;
@@ -1341,10 +1419,10 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   }
   RouteBuf r = e->rb;
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
-  const size_t agg_lds = e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8;
+  // at least 81 KiB of LDS: one k_aggregate workgroup per CU (the dispatcher would otherwise pair two
+  // of the nb = CU-count workgroups on one CU and leave another idle)
+  const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, 81 * 1024);
   const int par = (int)(e->batches & 1);
-  r.batch_slot = e->slots + par * RT_Q;
-  r.next_slot = e->slots + (1 - par) * RT_Q;
   r.dcount = e->dcounts + par;
   r.next_dcount = e->dcounts + (1 - par);
   hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, e->stream, e->s, b, r);
@@ -1500,19 +1578,20 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (e->routed) {
       e->max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
       const size_t cap = (size_t)e->max_tiles * RT_TILE;
-      e->rb.key = e->alloc<int64_t>(cap);
-      e->rb.val = e->alloc<int64_t>(cap);
+      e->rb.kv = e->alloc<longlong2>(cap);
       e->rb.idx = e->alloc<uint16_t>(cap);
       e->rb.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * e->max_tiles);
-      e->slots = e->alloc<int32_t>(2 * RT_Q);
+      e->rb.hdr = e->alloc<int64_t>((size_t)e->max_tiles * RT_Q);
       e->dcounts = e->alloc<unsigned long long>(2);
       e->rb.dcap = c.max_batch;
       e->rb.dlist = e->alloc<unsigned long long>((size_t)c.max_batch);
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
-      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 8) + 4 * (RT_THREADS / 64);
+      e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
+      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 8) + 4 * 16 + 8 * RT_HS;
       const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-      e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles;
+      e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles + 8 * RT_GS;
+      e->agg_lds = std::max<size_t>(e->agg_lds, 81 * 1024);
       if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
     }
   }
@@ -1566,7 +1645,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(s.stats, 0, 8 * ST_NSTATS, e->stream));
   HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
   if (e->routed) {
-    HIPCHK(e, hipMemsetAsync(e->slots, 0xFF, sizeof(int32_t) * 2 * RT_Q, e->stream));
     HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 16, e->stream));
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1776,6 +1854,14 @@ int fw_get_stats(fw_engine* e, fw_stats* st) {
   st->slices_live = live;
   st->keys_resident = -1;
   st->ingest_form = e->routed ? 2 : 1;
+  return FW_OK;
+}
+
+int fw_debug_stamps(fw_engine* e, int64_t* out, int64_t n) {
+  if (!e || !out) return FW_ERR_INVALID_ARG;
+  if (!e->rb.stamps) return FW_ERR_UNSUPPORTED;
+  HIPCHK(e, hipMemcpyAsync(out, e->rb.stamps, 8 * (size_t)std::min<int64_t>(n, (int64_t)16 << 16), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
   return FW_OK;
 }
 

@@ -184,6 +184,9 @@ int         fw_set_stream(fw_engine* e, void* stream);
 
 /* diagnostics: raw device counters (8 x int64) */
 int         fw_debug_counters(fw_engine* e, int64_t* out8);
+/* diagnostics: per-workgroup phase timestamps of the partitioned ingest (engine created with
+ * FW_DEBUG_AGG & 16 in the environment); n int64 values, 100 MHz realtime clock */
+int         fw_debug_stamps(fw_engine* e, int64_t* out, int64_t n);
 
 /* library version string */
 const char* fw_version(void);

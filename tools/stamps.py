@@ -1,0 +1,36 @@
+"""Diagnostic: per-phase timing of k_route / k_aggregate from in-kernel realtime stamps (FW_DEBUG_AGG=16)."""
+import ctypes, os, sys
+os.environ["FW_DEBUG_AGG"] = str(16 | int(os.environ.get("FW_DEBUG_AGG_EXTRA", "0")))
+import numpy as np, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flink_amd.synth import stream
+from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, WindowEngine, make_config
+cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", True), key_capacity=1 << 16,
+                  max_batch=1 << 22, out_capacity=1 << 21, ingest_mode=2)
+e = WindowEngine(cfg)
+B = 1 << 22
+buf = np.zeros(16 << 16, dtype=np.int64)
+def phases(a, nblk, npts):
+    a = a[: nblk * 8].reshape(nblk, 8)[:, :npts].astype(np.float64)
+    t0 = a[:, 0].min()
+    d = np.diff(a, axis=1) * 10.0  # ns
+    if os.environ.get("STAMP_MAX"):
+        end = (a[:, npts - 1] - t0) * 10
+        print("      max per phase", np.round(d.max(axis=0)), "end p50/p90/max", np.percentile(end, [50, 90, 100]).round())
+        if nblk == 256:
+            m = d[:, 2]
+            print("      main by blockIdx%8:", [round(m[i::8].mean()) for i in range(8)])
+            print("      main by blockIdx//32:", [round(m[i*32:(i+1)*32].mean()) for i in range(8)])
+    return (a[:, 0] - t0).mean() * 10, d.mean(axis=0), (a[:, npts - 1].max() - t0) * 10
+for j in range(6):
+    k, t, v = stream(j * B, B, 1 << 16, 1 << 24, 1_700_000_000_000, device="cuda")
+    torch.cuda.synchronize()
+    e.push(k, t, v)
+    e.sync()
+    e.lib.fw_debug_stamps(e.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), buf.size)
+    sk, d, span = phases(buf, B // 4096, 5)
+    print(f"batch {j} route: start-skew {sk:.0f} ns, load {d[0]:.0f} phaseB {d[1]:.0f} scan {d[2]:.0f} write {d[3]:.0f} | span {span:.0f} ns")
+    sk, d, span = phases(buf[8 << 16:], 256, 5)
+    print(f"        aggregate: start-skew {sk:.0f} ns, ldir {d[0]:.0f} segtab {d[1]:.0f} main {d[2]:.0f} fold {d[3]:.0f} | span {span:.0f} ns")
+    e.advance_watermark(int(t[-1].item()) - 1)
+    e.collect()
