@@ -1043,118 +1043,117 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
 // ------------------------------------------------------------------------------------------------
 // watermark: plan fires/purges from the live slices, fire, purge, mark
 // ------------------------------------------------------------------------------------------------
-struct FireTask {
-  int64_t max_ts;
-  int32_t slots[MAX_K];   // slot of each slice of the window, -1 if not live
-};
-
-struct WmPlan {
-  int32_t n_tasks;
-  int32_t n_purge;
-  int32_t purge_slots[1024];
-};
-
 __device__ __forceinline__ int64_t window_start_n(const Spec& s, int64_t n) {
   return jadd(s.offset, (int64_t)((uint64_t)n * (uint64_t)(s.assigner == FW_TUMBLING ? s.size : s.slide)));
 }
 
-// one block: live slices -> windows with maxTimestamp in (wm_old, wm_new] (owned by their first live
-// slice) and slices whose last window's cleanup time <= wm_new
-__global__ void k_wm_plan(Spec s, int64_t wm_old, int64_t wm_new, FireTask* tasks, int32_t max_tasks, WmPlan* plan) {
-  __shared__ int32_t n_tasks, n_purge;
-  if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; }
+// ------------------------------------------------------------------------------------------------
+// watermark (AbstractStreamOperator.processWatermark :803-808 -> HeapInternalTimerService.advanceWatermark
+// :264-278 -> WindowOperator.onEventTime :336-375), one launch per watermark.  Every workgroup derives
+// the same plan from the live slices (windows with maxTimestamp in (old, new], each owned by its first
+// live slice; slices whose last window's cleanup time <= new), fires those windows over its share of
+// the key ids, then purges its share of the expired slices; the last workgroup to finish frees the
+// slots and records the watermark's position in the output log.
+// ------------------------------------------------------------------------------------------------
+constexpr int WM_THREADS = 1024;
+constexpr int WM_MAXT = 2048;      // windows firing at one watermark
+constexpr int WM_MAXP = 1024;      // slices purged at one watermark (>= P)
+
+template <int VT, int AGG, bool FIRST>
+__global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old, int64_t wm_new, unsigned int* done) {
+  __shared__ int64_t task_n[WM_MAXT];
+  __shared__ int32_t purge[WM_MAXP];
+  __shared__ int32_t slots[MAX_K];
+  __shared__ int32_t n_tasks, n_purge, last;
+  __shared__ int32_t wtot[WM_THREADS / 64];
+  __shared__ unsigned long long base;
+  __shared__ unsigned long long fired;
+  if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; last = 0; fired = 0; }
   __syncthreads();
-  for (int32_t p = threadIdx.x; p < s.P; p += blockDim.x) {
-    int64_t m = s.slice_tag[p];
+  for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) {
+    const int64_t m = s.slice_tag[p];
     if (m == FREE_TAG) continue;
-    int64_t n_hi = floor_div(m, s.R);
-    int64_t n_lo = floor_div(m - s.K, s.R) + 1;
+    const int64_t n_hi = floor_div(m, s.R);
+    const int64_t n_lo = floor_div(m - s.K, s.R) + 1;
     bool purge_now = false;
     for (int64_t n = n_lo; n <= n_hi; ++n) {
-      int64_t start = window_start_n(s, n);
-      int64_t max_ts = jsub(jadd(start, s.size), 1);
-      bool fires = max_ts > wm_old && max_ts <= wm_new;
-      if (fires && s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) purge_now = true;  // tumbling only
+      const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+      const bool fires = max_ts > wm_old && max_ts <= wm_new;
       if (!fires) continue;
-      // owner = first live slice of window n
-      int64_t m0 = n * s.R;
-      bool owner = true;
-      for (int64_t mm = m0; mm < m; ++mm) {
+      if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) purge_now = true;   // tumbling only
+      bool owner = true;                                                    // first live slice of window n
+      for (int64_t mm = n * s.R; mm < m; ++mm) {
         if (s.slice_tag[floor_mod(mm, s.P)] == mm) { owner = false; break; }
       }
       if (!owner) continue;
-      int32_t t = atomicAdd(&n_tasks, 1);
-      if (t >= max_tasks) { set_error(s.err, FW_ERR_CAPACITY); continue; }
-      tasks[t].max_ts = max_ts;
-      for (int k = 0; k < s.K; ++k) {
-        int64_t mm = m0 + k;
-        int32_t pp = (int32_t)floor_mod(mm, s.P);
-        tasks[t].slots[k] = s.slice_tag[pp] == mm ? pp : -1;
-      }
+      const int32_t t = atomicAdd(&n_tasks, 1);
+      if (t < WM_MAXT) task_n[t] = n;
+      else set_error(s.err, FW_ERR_CAPACITY);
     }
-    int64_t last_start = window_start_n(s, n_hi);
-    int64_t ct = cleanup_time(jsub(jadd(last_start, s.size), 1), s.lateness);
+    const int64_t ct = cleanup_time(jsub(jadd(window_start_n(s, n_hi), s.size), 1), s.lateness);
     if (ct <= wm_new) purge_now = true;
     if (purge_now) {
-      int32_t q = atomicAdd(&n_purge, 1);
-      if (q < 1024) plan->purge_slots[q] = p;
+      const int32_t q = atomicAdd(&n_purge, 1);
+      if (q < WM_MAXP) purge[q] = p;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    plan->n_tasks = n_tasks < max_tasks ? n_tasks : max_tasks;
-    plan->n_purge = n_purge < 1024 ? n_purge : 1024;
-  }
-}
-
-template <int VT, int AGG, bool FIRST>
-__global__ __launch_bounds__(BLOCK) void k_fire(Spec s, const FireTask* tasks, const WmPlan* plan) {
-  const int32_t nt = plan->n_tasks;
-  const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+  const int32_t nt = min(n_tasks, WM_MAXT), np = min(n_purge, WM_MAXP);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t gstride = (int64_t)gridDim.x * WM_THREADS;
   LateCombine op;
   for (int32_t t = 0; t < nt; ++t) {
-    const FireTask& task = tasks[t];
-    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < s.stride; k0 += gstride) {
-      int64_t kid = k0 + threadIdx.x;
+    const int64_t n = task_n[t];
+    if (threadIdx.x < s.K) {
+      const int64_t mm = n * s.R + threadIdx.x;
+      const int32_t pp = (int32_t)floor_mod(mm, s.P);
+      slots[threadIdx.x] = s.slice_tag[pp] == mm ? pp : -1;
+    }
+    __syncthreads();
+    const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+    for (int64_t k0 = (int64_t)blockIdx.x * WM_THREADS; k0 < s.stride; k0 += gstride) {
+      const int64_t kid = k0 + threadIdx.x;
       bool any = false;
       LateAcc a;
       a.vt = VT;
       int64_t best_ord = INT64_MAX, f1 = 0;
       if (kid < s.stride) {
         for (int k = 0; k < s.K; ++k) {
-          int32_t p = task.slots[k];
+          const int32_t p = slots[k];
           if (p < 0) continue;
-          int64_t idx = (int64_t)p * s.stride + kid;
+          const int64_t idx = (int64_t)p * s.stride + kid;
           bool pres;
           if (FIRST) {
-            int64_t o = s.c.first[idx];
+            const int64_t o = s.c.first[idx];
             pres = o != INT64_MAX;
             if (pres && o < best_ord) { best_ord = o; f1 = s.c.f1v[idx]; }
           } else {
             pres = s.c.present[idx] != 0;
           }
           if (!pres) continue;
-          LateAcc b = pane_load(s, idx);
+          const LateAcc b = pane_load(s, idx);
           a = any ? op(a, b) : b;
           any = true;
         }
       }
-      unsigned long long pos = wave_append(s.o.count, any);
-      wave_count(&s.stats[ST_FIRED], any);
-      if (any) emit_record(s, pos, kid_key(s, kid), f1, task.max_ts, a);
+      // block-aggregated append: one device atomic per workgroup and chunk
+      const uint64_t bal = __ballot(any);
+      const int32_t rank = __popcll(bal & lanemask_lt());
+      if (lane == 0) wtot[wave] = __popcll(bal);
+      __syncthreads();
+      int32_t off = 0, tot = 0;
+      for (int w = 0; w < WM_THREADS / 64; ++w) { const int32_t c = wtot[w]; off += w < wave ? c : 0; tot += c; }
+      if (threadIdx.x == 0 && tot > 0) { base = atomicAdd(s.o.count, (unsigned long long)tot); fired += tot; }
+      __syncthreads();
+      if (any) emit_record(s, base + off + rank, kid_key(s, kid), f1, max_ts, a);
     }
+    __syncthreads();
   }
-}
-
-// reset purged slices to the empty state and free their slots
-__global__ __launch_bounds__(BLOCK) void k_purge(Spec s, const WmPlan* plan) {
-  const int32_t np = plan->n_purge;
+  // purge this workgroup's share of the expired slices (it fired that share above)
   for (int32_t q = 0; q < np; ++q) {
-    int32_t p = plan->purge_slots[q];
-    const int64_t base = (int64_t)p * s.stride;
-    for (int64_t kid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; kid < s.stride;
-         kid += (int64_t)gridDim.x * blockDim.x) {
-      int64_t idx = base + kid;
+    const int64_t pbase = (int64_t)purge[q] * s.stride;
+    for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < s.stride; kid += gstride) {
+      const int64_t idx = pbase + kid;
       if (s.c.sum) s.c.sum[idx] = 0;
       if (s.c.mn) s.c.mn[idx] = INT64_MAX;
       if (s.c.mx) s.c.mx[idx] = INT64_MIN;
@@ -1162,16 +1161,21 @@ __global__ __launch_bounds__(BLOCK) void k_purge(Spec s, const WmPlan* plan) {
       if (s.first) s.c.first[idx] = INT64_MAX; else s.c.present[idx] = 0;
     }
   }
-}
-
-__global__ void k_free_and_mark(Spec s, const WmPlan* plan, int64_t wm) {
-  // runs after k_purge (stream order): free slots, then record the watermark's position in the log
-  for (int32_t q = threadIdx.x; q < plan->n_purge; q += blockDim.x) s.slice_tag[plan->purge_slots[q]] = FREE_TAG;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long mc = *s.o.mark_count;
+    if (fired) atomicAdd(&s.stats[ST_FIRED], fired);
+    last = atomicAdd(done, 1u) == gridDim.x - 1;   // issued after this workgroup's appends returned
+  }
+  __syncthreads();
+  if (!last) return;
+  // last workgroup: free the purged slots, then record the watermark's position in the log
+  for (int32_t q = threadIdx.x; q < np; q += WM_THREADS) s.slice_tag[purge[q]] = FREE_TAG;
+  if (threadIdx.x == 0) {
+    *done = 0u;
+    const unsigned long long cnt = atomicAdd(s.o.count, 0ull);
+    const unsigned long long mc = *s.o.mark_count;
     if ((int64_t)mc < s.o.mark_capacity) {
-      unsigned long long cnt = *s.o.count;
-      s.o.mark_wm[mc] = wm;
+      s.o.mark_wm[mc] = wm_new;
       s.o.mark_pos[mc] = (int64_t)(cnt < (unsigned long long)s.o.capacity ? cnt : (unsigned long long)s.o.capacity);
       *s.o.mark_count = mc + 1;
     } else {
@@ -1350,10 +1354,7 @@ struct fw_engine {
     timed.push_back({open_phase, open_ev, b, records});
     open_phase = -1;
   }
-  // watermark plan
-  FireTask* tasks = nullptr;
-  int32_t max_tasks = 0;
-  WmPlan* plan = nullptr;
+  unsigned int* wm_done = nullptr;   // k_watermark's workgroup completion counter
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
   RouteBuf rb{};
@@ -1432,9 +1433,9 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
 }
 
 template <int VT, int AGG, bool FIRST>
-static void launch_fire_t(fw_engine* e) {
-  int blocks = (int)std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid);
-  hipLaunchKernelGGL((k_fire<VT, AGG, FIRST>), dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->tasks, e->plan);
+static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + WM_THREADS - 1) / WM_THREADS, e->grid / 8));
+  hipLaunchKernelGGL((k_watermark<VT, AGG, FIRST>), dim3(blocks), dim3(WM_THREADS), 0, e->stream, e->s, wm_old, wm_new, e->wm_done);
 }
 
 // dispatch over (value type, aggregate mask, first-arrival) — the instantiated reduce shapes
@@ -1595,9 +1596,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
     }
   }
-  e->max_tasks = std::max(64, 4 * P);
-  e->tasks = e->alloc<FireTask>((size_t)e->max_tasks);
-  e->plan = e->alloc<WmPlan>(1);
+  e->wm_done = e->alloc<unsigned int>(1);
 
   for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
 
@@ -1644,6 +1643,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(s.err, 0, 4, e->stream));
   HIPCHK(e, hipMemsetAsync(s.stats, 0, 8 * ST_NSTATS, e->stream));
   HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(e->wm_done, 0, 4, e->stream));
   if (e->routed) {
     HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 16, e->stream));
   }
@@ -1764,11 +1764,7 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
     return FW_OK;
   }
   e->phase_begin(FW_PHASE_FIRE);
-  hipLaunchKernelGGL(k_wm_plan, dim3(1), dim3(256), 0, e->stream, e->s, e->cur_wm, wm, e->tasks, e->max_tasks, e->plan);
-  FW_DISPATCH(launch_fire_t, e);
-  int blocks = (int)std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid);
-  hipLaunchKernelGGL(k_purge, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->plan);
-  hipLaunchKernelGGL(k_free_and_mark, dim3(1), dim3(256), 0, e->stream, e->s, e->plan, wm);
+  FW_DISPATCH(launch_watermark_t, e, e->cur_wm, wm);
   e->phase_end(e->s.stride);
   HIPCHK(e, hipGetLastError());
   e->cur_wm = wm;
