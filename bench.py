@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--ingest-mode", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="events in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="no device-time events in the timed loop")
     return ap.parse_args()
 
 
@@ -152,7 +153,7 @@ def main():
     eng.sync()
     torch.cuda.synchronize()
     warm_res = eng.collect()
-    _abi.load_library().fw_set_profiling(eng.h, 1)
+    _abi.load_library().fw_set_profiling(eng.h, 0 if args.no_profile else 1)
     eng.lib.fw_get_profile(eng.h, _abi.FwProfile())  # reset counters
 
     barrier(world)
@@ -220,7 +221,7 @@ def main():
                    "reduce": "Tuple3(a.f0, a.f1, a.f2 + b.f2), f1 = first arrival"},
         "roofline": {"bound": "hbm", "kernel": "k_ingest_direct" if form == 1 else "k_route+k_aggregate", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "bytes_per_event": 24, "ingest_ms_per_launch": ing_ms / max(ing_n, 1),
+                     "bytes_per_event": 24, "ingest_ms_per_batch": ing_ms / max(args.steps, 1),
                      "fire_ms_total": prof.ms[_abi.FW_PHASE_FIRE], "fixup_ms_total": prof.ms[_abi.FW_PHASE_FIXUP],
                      "traffic": traffic, "traffic_unit": "bytes per ingest launch (FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,

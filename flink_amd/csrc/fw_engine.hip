@@ -415,8 +415,8 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
 constexpr int RT_TILE = 4096;
 constexpr int RT_THREADS = 512;
 constexpr int RT_Q = 2;                 // slices per tile routed through LDS (more go to the direct path)
-constexpr int RT_HS = 8;                // tile-local slice set (claims and per-tile routing)
 constexpr int RT_GS = 64;               // distinct routed slices per batch (k_aggregate rounds)
+constexpr int DC_RING = 16;             // direct-list counters, one per batch in flight
 constexpr int AG_THREADS = 1024;
 constexpr int RT_MAX_KB_BITS = 10;      // directory slots per bucket held in LDS by k_aggregate
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
@@ -427,8 +427,8 @@ struct RouteBuf {
   uint16_t* seg;         // [ntiles][nbq + 1] start of each bin's segment in the tile; [nbq] = routed count
   int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
   unsigned long long* dlist;    // direct-path records: (batch index << 32) | (slot << 1) | per-element fire
-  unsigned long long* dcount;   // this batch's direct-list length
-  unsigned long long* next_dcount;
+  unsigned long long* dcount;   // this batch's direct-list length (a ring of DC_RING counters, one per batch)
+  unsigned long long* dcount_reset;   // the counter of batch j + DC_RING/2: zeroed by k_aggregate of batch j
   int64_t dcap;
   long long* stamps;     // diagnostics (FW_DEBUG_AGG & 16): per-workgroup phase timestamps, 8 per workgroup
   int32_t ntiles;
@@ -437,29 +437,15 @@ struct RouteBuf {
 
 #define FW_STAMP(r, base, k) do { if ((r).stamps && threadIdx.x == 0) (r).stamps[(base) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-// Pane-slice slots are a pure function of the slice number (p = floor_mod(m, P)), so claiming one is an
-// idempotent plain store: every claimer of slot p in a batch stores the same m, unless two slices that
-// collide mod P are live at once — the pool is then exhausted (FW_ERR_CAPACITY), which k_aggregate
-// detects from the tile headers after the kernel boundary.  No device-scope atomic on the hot path.
-__device__ __noinline__ void claim_slice_slot(int64_t* slice_tag, int32_t P, int64_t m, int32_t* err) {
-  const int32_t p = (int32_t)floor_mod(m, P);
-  const int64_t tag = slice_tag[p];
-  if (tag == m) return;
-  if (tag == FREE_TAG) slice_tag[p] = m;
-  else set_error(err, FW_ERR_CAPACITY);
-}
-
-// tile-local slice set in LDS: index of slice m, inserting it (and claiming its pane slot) if new;
-// -1 when the set is full
-__device__ __forceinline__ int32_t tile_slice(const Spec& s, int64_t* lset, int64_t m) {
-  for (int q = 0; q < RT_HS; ++q) {
+// tile-local slice set in LDS (RT_Q entries): index of slice m, inserting it if new; -1 when full
+__device__ __forceinline__ int32_t tile_slice(int64_t* lset, int64_t m) {
+  for (int q = 0; q < RT_Q; ++q) {
     const int64_t cur = lset[q];
     if (cur == m) return q;
     if (cur == FREE_TAG) {
       const unsigned long long prev = atomicCAS((unsigned long long*)&lset[q], (unsigned long long)FREE_TAG,
                                                 (unsigned long long)m);
-      if ((int64_t)prev == FREE_TAG) { claim_slice_slot(s.slice_tag, s.P, m, s.err); return q; }
-      if ((int64_t)prev == m) return q;
+      if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) return q;
     }
   }
   return -1;
@@ -505,11 +491,11 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   uint16_t* st_idx = (uint16_t*)(st_kv + RT_TILE);
   int32_t* cnt = (int32_t*)(st_idx + RT_TILE);   // [nbq + 1]
   int32_t* wtot = cnt + (RT_Q * 256 + 8);        // [NT / 64]
-  int64_t* lset = (int64_t*)(wtot + 16);         // [RT_HS] the tile's slices
+  int64_t* lset = (int64_t*)(wtot + 16);         // [RT_Q] the tile's routed slices
   const int64_t base = (int64_t)blockIdx.x * RT_TILE;
   FW_STAMP(r, 0, 0);
   for (int x = threadIdx.x; x <= nbq; x += NT) cnt[x] = 0;
-  if (threadIdx.x < RT_HS) lset[threadIdx.x] = FREE_TAG;
+  if (threadIdx.x < RT_Q) lset[threadIdx.x] = FREE_TAG;
   // phase A: every load of the tile in flight before any dependent work; record (j, e) of this thread
   // is tile index 2 * (j * NT + tid) + e
   int64_t kk[PER], tt[PER], vv[PER];
@@ -538,13 +524,16 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   }
   __syncthreads();   // cnt zeroed, key hashes parked
   FW_STAMP(r, 0, 1);
-  // phase B: per record operator work; the (slice -> slot, batch slice) lookup is cached per wave, as a
-  // wave of an in-order stream stays in one slice
+  // phase B: per record operator work (timestamp, key group, windows, lateness), the record's index in the
+  // tile's slice set (cached per wave, as a wave of an in-order stream stays in one slice) and its
+  // counting-sort rank; the rest join the direct list (rare: per-element fires, slices beyond the tile's
+  // RT_Q, the Long.MIN_VALUE key), applied by the k_aggregate workgroup owning the key's bucket
   int64_t c_m = INT64_MIN;
   int32_t c_q = -1;
   unsigned long long late_pairs = 0;
-  int32_t bin[PER];                   // >= 0 routed bin, -1 not routed
+  int32_t bin[PER];       // routed bin, or -1
   int32_t rank[PER];
+  uint32_t direct_mask = 0, fire_mask = 0;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int64_t i = base + 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
@@ -560,54 +549,61 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     RecWin w;
     w.m = 0; w.n_late = 0; w.n_fire = 0; w.n_windows = 0; w.quirk = false;
     if (ok) {
-      if (r.dbg & 4) { w.m = (int64_t)((double)ts * s.inv_size); w.n_windows = 1; }
-      else w = record_windows(s, ts, b.wm);
+      w = record_windows(s, ts, b.wm);
       if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
     }
     if (ok) late_pairs += (unsigned long long)w.n_late;
     const bool live = ok && (w.n_windows - w.n_late) > 0;
     const bool late_fire = live && w.n_fire > 0;
-    const uint64_t lm = __ballot(live);
+    // routable: its windows neither late nor fired yet, so no watermark up to b.wm fires or purges its slice
+    const bool routable = live && !late_fire && key != EMPTY_KEY;
+    const uint64_t lm = __ballot(routable);
     const int leader = lm ? __ffsll((long long)lm) - 1 : 0;
     const int64_t m0 = __shfl(w.m, leader);
-    const bool uniform = __all(!live || w.m == m0);
+    const bool uniform = __all(!routable || w.m == m0);
     int32_t q = -1;
     if (uniform) {
       if (lm != 0 && m0 != c_m) {   // wave-uniform branch
         int32_t q0 = -1;
-        if ((int)(threadIdx.x & 63) == leader) q0 = tile_slice(s, lset, m0);
+        if ((int)(threadIdx.x & 63) == leader) q0 = tile_slice(lset, m0);
         c_q = __shfl(q0, leader);
         c_m = m0;
       }
-      q = live ? c_q : -1;
-    } else if (live) {
-      q = tile_slice(s, lset, w.m);
+      q = routable ? c_q : -1;
+    } else if (routable) {
+      q = tile_slice(lset, w.m);
     }
     bin[k] = -1;
     rank[k] = 0;
-    const bool routed = live && !late_fire && q >= 0 && q < RT_Q && key != EMPTY_KEY;
-    if (routed) {
+    if (q >= 0) {
       const uint64_t hk = fmix64((uint64_t)key);
       bin[k] = q * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
       rank[k] = atomicAdd(&cnt[bin[k]], 1);
       kk[k] = (int64_t)hk;   // routed records carry the directory hash (a bijection of the key)
-    }
-    // direct path (rare: per-element fires, a slice beyond the batch's RT_Q, the Long.MIN_VALUE key):
-    // listed for k_aggregate, whose workgroup owning the key's bucket applies it
-    const bool direct = live && !routed;
-    const unsigned long long dpos = wave_append(r.dcount, direct);
-    if (direct) {
-      if ((int64_t)dpos < r.dcap) r.dlist[dpos] = ((unsigned long long)i << 1) | (late_fire ? 1ull : 0ull);
-      else set_error(s.err, FW_ERR_CAPACITY);
+    } else if (live) {
+      direct_mask |= 1u << k;
+      if (late_fire) fire_mask |= 1u << k;
     }
   }
   if (__any(late_pairs != 0)) {
     for (int off = 32; off > 0; off >>= 1) late_pairs += __shfl_xor(late_pairs, off);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late_pairs);
   }
+  if (__any(direct_mask != 0)) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int64_t i = base + 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
+      const bool direct = (direct_mask >> k) & 1u;
+      const unsigned long long dpos = wave_append(r.dcount, direct);
+      if (direct) {
+        if ((int64_t)dpos < r.dcap) r.dlist[dpos] = ((unsigned long long)i << 1) | ((fire_mask >> k) & 1u);
+        else set_error(s.err, FW_ERR_CAPACITY);
+      }
+    }
+  }
+  if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
   __syncthreads();
   FW_STAMP(r, 0, 2);
-  if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];
   block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
   uint16_t* seg = r.seg + (int64_t)blockIdx.x * (nbq + 1);
   for (int x = threadIdx.x; x <= nbq; x += NT) seg[x] = (uint16_t)cnt[x];
@@ -644,6 +640,26 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, Rout
   route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(blockIdx.x + 1) * RT_TILE > b.n);
 }
 
+// the bucket's LDS directory-hash table: slot of h, inserting its key (fmix64_inv(h)) into the global
+// directory if absent.  Out of line: taken by a wave only when a lane misses the four probed slots.
+__device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h) {
+  uint32_t x = (uint32_t)h & kbm;
+  for (uint32_t probe = 0; probe <= kbm; ++probe) {
+    const uint64_t cur = lh[x];
+    if (cur == h) return (int32_t)x;
+    if (cur == EMPTY_H) {
+      const int64_t key = (int64_t)fmix64_inv(h);
+      const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[x], (unsigned long long)EMPTY_KEY,
+                                                (unsigned long long)key);
+      const uint64_t now = (int64_t)prev == EMPTY_KEY ? h : fmix64(prev);
+      lh[x] = now;   // only globally confirmed keys enter the cache
+      if (now == h) return (int32_t)x;
+    }
+    x = (x + 1) & kbm;
+  }
+  return -1;
+}
+
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, RouteBuf r, const int64_t* f1col) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -653,12 +669,13 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
   uint64_t* lh = (uint64_t*)smem;                       // [KB] fmix64 of this bucket's directory slice (EMPTY_H = free)
-  int64_t* lsum = (int64_t*)(lh + KB);                  // [KB]
-  int64_t* lmin = lsum + KB;                            // [KB] (AGG 15)
-  int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KB : 0);
-  int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KB : 0);
-  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KB : 0));  // [KB] batch index of the first arrival
-  int32_t* sst = (int32_t*)(lfirst + KB);               // [ntiles] segment start within the tile
+  const int KA = KB + 64;                               // accumulator slots: KB + one dummy per lane
+  int64_t* lsum = (int64_t*)(lh + KB);                  // [KA]
+  int64_t* lmin = lsum + KA;                            // [KA] (AGG 15)
+  int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KA : 0);
+  int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KA : 0);
+  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest tile of the pane
+  int32_t* sst = (int32_t*)(lfirst + KA);               // [ntiles] segment start within the tile
   int32_t* sln = sst + r.ntiles;                        // [ntiles] segment length
   const int64_t dbase = (int64_t)bkt * KB;
   const int64_t SB = (int64_t)8 << 16;
@@ -674,34 +691,23 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   // <= 1/4 keeps nearly every key there); the loop takes the rest and inserts new keys (a global CAS on
   // the key, fmix64_inv(h), confirms every slot before it enters the LDS copy)
   auto find_slow = [&](uint64_t h, uint32_t& kl) -> bool {
-    uint32_t x = (uint32_t)h & kbm;
-    for (uint32_t probe = 0; probe <= kbm; ++probe) {
-      const uint64_t cur = lh[x];
-      if (cur == h) { kl = x; return true; }
-      if (cur == EMPTY_H) {
-        const int64_t key = (int64_t)fmix64_inv(h);
-        const unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[dbase + (int64_t)x],
-                                                  (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-        const uint64_t now = (int64_t)prev == EMPTY_KEY ? h : fmix64(prev);
-        lh[x] = now;   // only globally confirmed keys enter the cache
-        if (now == h) { kl = x; return true; }
-      }
-      x = (x + 1) & kbm;
-    }
-    return false;
+    const int32_t x = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h);
+    if (x < 0) return false;
+    kl = (uint32_t)x;
+    return true;
   };
+  // one record into the bucket's LDS accumulators.  Straight-line on the common path: inactive lanes
+  // update a private dummy slot (KB + lane) instead of being masked off, and the rare miss of the four
+  // probed slots takes one wave-uniform branch to the out-of-line probe/insert
   auto process = [&](bool act, uint64_t h, int64_t v, uint32_t oi) {
-    if (r.dbg & 1) { if (act && h == 0x1234567890ull && v == 3) lsum[0] = (int64_t)oi; return; }
     const uint32_t h0 = (uint32_t)h & kbm;
     const uint64_t a0 = lh[h0], a1 = lh[(h0 + 1) & kbm], a2 = lh[(h0 + 2) & kbm], a3 = lh[(h0 + 3) & kbm];
     uint32_t kl = a0 == h ? h0 : a1 == h ? ((h0 + 1) & kbm) : a2 == h ? ((h0 + 2) & kbm) : ((h0 + 3) & kbm);
-    const bool hit = a0 == h || a1 == h || a2 == h || a3 == h;
-    if (!(r.dbg & 64) && __any(act && !hit)) {
-      if (act && !hit) {
-        if (!find_slow(h, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
-      }
+    const bool miss = act && a0 != h && a1 != h && a2 != h && a3 != h;
+    if (__any(miss)) {
+      if (miss && !find_slow(h, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
     }
-    if (!act || (r.dbg & 32)) return;
+    kl = act ? kl : (uint32_t)KB + (uint32_t)lane;
     if (AGG & FW_AGG_SUM) {
       if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
       else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
@@ -713,10 +719,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   };
 
   const int64_t ord_base = b.ord_base;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *r.next_dcount = 0;   // the other parity half serves the next batch
   // direct-path records of this bucket (listed by k_route): per-element fires join the late list, the
   // rest update their pane with device-scope atomics; no other workgroup touches this bucket's panes,
   // and none of them is a pane the LDS fold below writes (other slice, or the Long.MIN_VALUE key column)
+  // no memset between batches: batch j's counter was zeroed by k_aggregate of batch j - DC_RING/2, whose
+  // counter is no longer read and whose successor k_route starts only after this kernel (event order)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *r.dcount_reset = 0;
   const int64_t nd = min((int64_t)*r.dcount, r.dcap);
   if (nd > 0) {
     for (int64_t x0 = 0; x0 < nd; x0 += NT) {
@@ -774,6 +782,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
 
   // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same set)
   int64_t* gsl = (int64_t*)(sln + r.ntiles);            // [RT_GS]
+  int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
   if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
   __syncthreads();
   for (int t = threadIdx.x; t < r.ntiles; t += NT) {
@@ -796,10 +805,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   for (int g = 0; g < RT_GS; ++g) {
     const int64_t m = gsl[g];
     if (m == FREE_TAG) break;                            // uniform
-    const int32_t p = (int32_t)floor_mod(m, s.P);
-    if (bkt == 0 && threadIdx.x == 0 && s.slice_tag[p] != m) set_error(s.err, FW_ERR_CAPACITY);   // colliding claims
+    // pane-slot claim: authoritative here, after every earlier watermark (engine stream order); slot
+    // p = floor_mod(m, P) is claimed by whichever workgroup comes first, the rest find it taken by m
+    __syncthreads();   // every thread has read the previous round's lclaim
+    if (threadIdx.x == 0) lclaim = slice_slot(s, m);
+    __syncthreads();
+    const int32_t p = lclaim;
+    if (p < 0) { if (threadIdx.x == 0) set_error(s.err, FW_ERR_CAPACITY); continue; }   // slice pool exhausted
     const int q = g;
-    for (int x = threadIdx.x; x < KB; x += NT) {
+    for (int x = threadIdx.x; x < KA; x += NT) {
       lsum[x] = 0;
       if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
       if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
@@ -823,10 +837,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     FW_STAMP(r, SB, 2 + 3 * min(q, 1));
     // each 16-lane group reads one tile's segment, 2 records per lane per round; UR rounds of 4 segments
     // per wave-step, every load issued before any dependent work
+    // lfirst tracks the earliest TILE holding the pane's records (tiles are contiguous ranges of the
+    // batch); the exact first arrival is resolved in the fold, for new panes only, from that tile's segment
     constexpr int UR = 6;
     for (int tb = wave * 4 * UR; tb < r.ntiles; tb += (NT / 64) * 4 * UR) {
       longlong2 ra[UR], rb2[UR];
-      uint32_t ia[UR], ib[UR];
       bool aa[UR], ab[UR];
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
@@ -839,13 +854,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         const int64_t pb = (int64_t)t * RT_TILE + (ab[u] ? st + sub + 16 : 0);
         ra[u] = r.kv[pa];
         rb2[u] = r.kv[pb];
-        ia[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pa] : 0u);
-        ib[u] = (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pb] : 0u);
       }
 #pragma unroll
       for (int u = 0; u < UR; ++u) {
-        process(aa[u], (uint64_t)ra[u].x, ra[u].y, ia[u]);
-        process(ab[u], (uint64_t)rb2[u].x, rb2[u].y, ib[u]);
+        const uint32_t t = (uint32_t)min(tb + u * 4 + grp, r.ntiles - 1);
+        process(aa[u], (uint64_t)ra[u].x, ra[u].y, t);
+        process(ab[u], (uint64_t)rb2[u].x, rb2[u].y, t);
       }
 #pragma unroll
       for (int u = 0; u < UR; ++u) {   // segments longer than 32 records (hot keys, skew)
@@ -857,7 +871,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
             const bool act = j0 + sub < ln;
             const int64_t pp = (int64_t)t * RT_TILE + (act ? sst[t] + j0 + sub : 0);
             const longlong2 rr = r.kv[pp];
-            process(act, (uint64_t)rr.x, rr.y, (uint32_t)(t * RT_TILE) + (FIRST ? (uint32_t)r.idx[pp] : 0u));
+            process(act, (uint64_t)rr.x, rr.y, (uint32_t)t);
           }
         }
       }
@@ -868,7 +882,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     // (direct-path updates of k_route finished before this kernel started)
     for (int x = threadIdx.x; x < KB; x += NT) {
       const uint32_t lf = lfirst[x];
-      if (lf == NO_FIRST || (r.dbg & 2)) continue;
+      if (lf == NO_FIRST) continue;
       const int64_t idx = (int64_t)p * s.stride + dbase + x;
       if (AGG & FW_AGG_SUM) {
         if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[x]);
@@ -878,10 +892,20 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       if (AGG & FW_AGG_MAX) { const int64_t o = s.c.mx[idx]; if (lmax[x] > o) s.c.mx[idx] = lmax[x]; }
       if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[x]);
       if (FIRST) {
-        const int64_t cand = ord_base + (int64_t)lf;
-        if (cand < s.c.first[idx]) {   // first arrival: earlier than any previous batch or direct update
-          s.c.first[idx] = cand;
-          s.c.f1v[idx] = f1col[lf];
+        // first arrival: only a pane not seen before tile lf can change; its earliest record in tile lf
+        // is found by scanning that tile's segment of this bin (records carry their index in the tile)
+        if (ord_base + (int64_t)lf * RT_TILE < s.c.first[idx]) {
+          const uint64_t hx = lh[x];
+          const int64_t tb0 = (int64_t)lf * RT_TILE + sst[lf];
+          int32_t best = RT_TILE;
+          for (int32_t j = 0; j < sln[lf]; ++j) {
+            if ((uint64_t)r.kv[tb0 + j].x == hx) best = min(best, (int32_t)r.idx[tb0 + j]);
+          }
+          const int64_t bi = (int64_t)lf * RT_TILE + best;
+          if (best < RT_TILE && ord_base + bi < s.c.first[idx]) {
+            s.c.first[idx] = ord_base + bi;
+            s.c.f1v[idx] = f1col[bi];
+          }
         }
       } else {
         s.c.present[idx] = 1;
@@ -1305,17 +1329,22 @@ struct fw_engine {
   fw_config cfg{};
   std::string err;
   int32_t sticky = FW_OK;
-  hipStream_t stream = nullptr;       // stream all engine work is ordered on
-  hipStream_t own_stream = nullptr;   // the engine's own stream, if it created one
+  hipStream_t stream = nullptr;       // engine stream: aggregation, watermarks, late path, output
+  hipStream_t rstream = nullptr;      // route stream: k_route of batch j+1 overlaps k_aggregate/k_watermark of j
+  void* client = nullptr;             // producer/consumer stream of the caller (fw_set_stream), or null
+  bool serial = false;                // diagnostics (FW_SERIAL=1): k_route on the engine stream too
+  hipEvent_t ev_in = nullptr;         // client work up to a push (input columns ready)
+  hipEvent_t ev_route[2] = {nullptr, nullptr};   // k_route of the batch with that parity done
+  hipEvent_t ev_agg[2] = {nullptr, nullptr};     // k_aggregate of the batch with that parity done
   Spec s{};
   int64_t cur_wm = INT64_MIN;
   int64_t ordinal = 0;
   int64_t records_in = 0;
   int grid = 0;
   std::vector<void*> allocs;
-  // staging for host-memory pushes
-  int64_t *st_key = nullptr, *st_ts = nullptr, *st_val = nullptr, *st_f1 = nullptr;
-  int32_t* st_hash = nullptr;
+  // staging for host-memory (and misaligned device) pushes, one set per batch parity
+  int64_t *stg_key[2] = {}, *stg_ts[2] = {}, *stg_val[2] = {}, *stg_f1[2] = {};
+  int32_t* stg_hash[2] = {};
   // late path
   unsigned long long *late_key = nullptr, *late_key_sorted = nullptr, *late_count = nullptr, *seg = nullptr;
   unsigned long long *late_idx_in = nullptr, *late_idx_out = nullptr;
@@ -1341,27 +1370,29 @@ struct fw_engine {
   }
   int open_phase = -1;
   hipEvent_t open_ev = nullptr;
-  void phase_begin(int ph) {
+  void phase_begin(int ph, hipStream_t st = nullptr) {
     if (!profiling) return;
     open_phase = ph;
     open_ev = take_event();
-    (void)hipEventRecord(open_ev, stream);
+    (void)hipEventRecord(open_ev, st ? st : stream);
   }
-  void phase_end(int64_t records) {
+  void phase_end(int64_t records, hipStream_t st = nullptr) {
     if (!profiling || open_phase < 0) return;
     hipEvent_t b = take_event();
-    (void)hipEventRecord(b, stream);
+    (void)hipEventRecord(b, st ? st : stream);
     timed.push_back({open_phase, open_ev, b, records});
     open_phase = -1;
   }
   unsigned int* wm_done = nullptr;   // k_watermark's workgroup completion counter
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
-  RouteBuf rb{};
-  unsigned long long* dcounts = nullptr;    // direct-list lengths, two parity halves
+  RouteBuf rb{};                            // fields shared by both parities (dbg, stamps, dcap)
+  RouteBuf rbs[2] = {};                     // routed-batch buffers, one set per batch parity
+  unsigned long long* dcounts = nullptr;    // direct-list lengths, one per parity
   int64_t batches = 0;
   int32_t max_tiles = 0;
   size_t route_lds = 0, agg_lds = 0;
+  int agg_min_lds = 81 * 1024;
   // partition scratch
   int64_t* part_block_counts = nullptr;
   int64_t part_blocks_cap = 0;
@@ -1378,8 +1409,11 @@ struct fw_engine {
     return (T*)p;
   }
   ~fw_engine() {
+    if (rstream) (void)hipStreamSynchronize(rstream);
     if (stream) (void)hipStreamSynchronize(stream);
-    if (own_stream) (void)hipStreamDestroy(own_stream);
+    if (rstream) (void)hipStreamDestroy(rstream);
+    if (stream) (void)hipStreamDestroy(stream);
+    for (hipEvent_t ev : {ev_in, ev_route[0], ev_route[1], ev_agg[0], ev_agg[1]}) if (ev) (void)hipEventDestroy(ev);
     for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
@@ -1409,27 +1443,31 @@ static void launch_ingest_t(fw_engine* e, const BatchIn& b) {
   hipLaunchKernelGGL((k_ingest_direct<VT, AGG, FIRST>), dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b);
 }
 template <int VT, int AGG, bool FIRST>
-static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col) {
+static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col, int par) {
   static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_route<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)e->route_lds);
-    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)e->agg_lds);
-    attr_set = true;
+  if (!attr_set) {   // the largest any engine may ask for
+    (void)hipFuncSetAttribute((const void*)k_route<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;   // both kernels use dynamic LDS only, so the whole 160 KiB is grantable
   }
-  RouteBuf r = e->rb;
+  RouteBuf r = e->rbs[par];
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
+  r.dcount = e->dcounts + (e->batches % DC_RING);
+  r.dcount_reset = e->dcounts + ((e->batches + DC_RING / 2) % DC_RING);
   // at least 81 KiB of LDS: one k_aggregate workgroup per CU (the dispatcher would otherwise pair two
   // of the nb = CU-count workgroups on one CU and leave another idle)
-  const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, 81 * 1024);
-  const int par = (int)(e->batches & 1);
-  r.dcount = e->dcounts + par;
-  r.next_dcount = e->dcounts + (1 - par);
-  hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, e->stream, e->s, b, r);
+  const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, (size_t)e->agg_min_lds);
+  hipStream_t rs = e->serial ? e->stream : e->rstream;
+  e->phase_begin(FW_PHASE_INGEST, rs);
+  hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, rs, e->s, b, r);
+  e->phase_end(b.n, rs);
+  (void)hipEventRecord(e->ev_route[par], rs);
+  (void)hipStreamWaitEvent(e->stream, e->ev_route[par], 0);
+  e->phase_begin(FW_PHASE_INGEST);
   hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b, r,
                      f1col);
-  e->batches++;
+  e->phase_end(0);
+  (void)hipEventRecord(e->ev_agg[par], e->stream);
 }
 
 template <int VT, int AGG, bool FIRST>
@@ -1483,8 +1521,14 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     return unsupported("sliding windows with allowed lateness or PurgingTrigger are not implemented on the slice path");
   HIPCHK(e, hipSetDevice(c.device));
   e->dev = c.device;
-  HIPCHK(e, hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
-  e->stream = e->own_stream;
+  HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  HIPCHK(e, hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking));
+  e->serial = getenv("FW_SERIAL") && atoi(getenv("FW_SERIAL")) != 0;
+  HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
+  for (int q = 0; q < 2; ++q) {
+    HIPCHK(e, hipEventCreateWithFlags(&e->ev_route[q], hipEventDisableTiming));
+    HIPCHK(e, hipEventCreateWithFlags(&e->ev_agg[q], hipEventDisableTiming));
+  }
   hipDeviceProp_t prop;
   HIPCHK(e, hipGetDeviceProperties(&prop, c.device));
   e->grid = prop.multiProcessorCount * 8;
@@ -1563,11 +1607,13 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.err = e->alloc<int32_t>(1);
   s.stats = e->alloc<unsigned long long>(ST_NSTATS);
 
-  e->st_key = e->alloc<int64_t>((size_t)c.max_batch);
-  e->st_ts = e->alloc<int64_t>((size_t)c.max_batch);
-  e->st_val = e->alloc<int64_t>((size_t)c.max_batch);
-  e->st_f1 = e->alloc<int64_t>((size_t)c.max_batch);
-  e->st_hash = e->alloc<int32_t>((size_t)c.max_batch);
+  for (int q = 0; q < 2; ++q) {
+    e->stg_key[q] = e->alloc<int64_t>((size_t)c.max_batch);
+    e->stg_ts[q] = e->alloc<int64_t>((size_t)c.max_batch);
+    e->stg_val[q] = e->alloc<int64_t>((size_t)c.max_batch);
+    e->stg_f1[q] = e->alloc<int64_t>((size_t)c.max_batch);
+    e->stg_hash[q] = e->alloc<int32_t>((size_t)c.max_batch);
+  }
 
   // ingest form: partitioned (LDS pre-aggregation) when a directory bucket fits in LDS and
   // batches are large; direct atomics otherwise
@@ -1579,20 +1625,26 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (e->routed) {
       e->max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
       const size_t cap = (size_t)e->max_tiles * RT_TILE;
-      e->rb.kv = e->alloc<longlong2>(cap);
-      e->rb.idx = e->alloc<uint16_t>(cap);
-      e->rb.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * e->max_tiles);
-      e->rb.hdr = e->alloc<int64_t>((size_t)e->max_tiles * RT_Q);
-      e->dcounts = e->alloc<unsigned long long>(2);
-      e->rb.dcap = c.max_batch;
-      e->rb.dlist = e->alloc<unsigned long long>((size_t)c.max_batch);
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
       e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
-      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 8) + 4 * 16 + 8 * RT_HS;
+      e->rb.dcap = c.max_batch;
+      e->dcounts = e->alloc<unsigned long long>(DC_RING);
+      for (int q = 0; q < 2; ++q) {
+        RouteBuf& r = e->rbs[q];
+        r = e->rb;
+        r.kv = e->alloc<longlong2>(cap);
+        r.idx = e->alloc<uint16_t>(cap);
+        r.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * e->max_tiles);
+        r.hdr = e->alloc<int64_t>((size_t)e->max_tiles * RT_Q);
+        r.dlist = e->alloc<unsigned long long>((size_t)c.max_batch);
+      }
+      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 8) + 4 * 16 + 8 * RT_Q;
       const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-      e->agg_lds = (size_t)KB * (8 * ncols + 4) + 8 * (size_t)e->max_tiles + 8 * RT_GS;
-      e->agg_lds = std::max<size_t>(e->agg_lds, 81 * 1024);
+      e->agg_lds = (size_t)KB * 8 + (size_t)(KB + 64) * (8 * (ncols - 1) + 4) + 8 * (size_t)e->max_tiles + 8 * RT_GS + 16;
+      const char* ml = getenv("FW_AGG_MIN_LDS_KB");
+      e->agg_min_lds = (ml ? atoi(ml) : 81) * 1024;
+      e->agg_lds = std::max<size_t>(e->agg_lds, (size_t)e->agg_min_lds);
       if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
     }
   }
@@ -1645,7 +1697,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(e->wm_done, 0, 4, e->stream));
   if (e->routed) {
-    HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 16, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 8 * DC_RING, e->stream));
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
@@ -1681,23 +1733,32 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (n > e->cfg.max_batch) return fail(e, FW_ERR_CAPACITY, "batch larger than max_batch");
   if (n == 0) return FW_OK;
   HIPCHK(e, hipSetDevice(e->dev));
+  // routed form: the batch's copies and k_route run on the route stream, k_aggregate on the engine
+  // stream; buffers of batch parity par are reused only after k_aggregate of batch j-2 finished
+  const int par = (int)(e->batches & 1);
+  hipStream_t in_stream = e->routed && !e->serial ? e->rstream : e->stream;
+  if (e->routed) HIPCHK(e, hipStreamWaitEvent(in_stream, e->ev_agg[par], 0));
+  if (e->client) {   // input columns are produced on the caller's stream
+    HIPCHK(e, hipEventRecord(e->ev_in, (hipStream_t)e->client));
+    HIPCHK(e, hipStreamWaitEvent(in_stream, e->ev_in, 0));
+  }
   const int64_t *dk = key, *dts = ts, *dv = (const int64_t*)value, *df1 = f1;
   const int32_t* dh = key_hash;
   if (mem == FW_MEM_HOST) {
-    HIPCHK(e, hipMemcpyAsync(e->st_key, key, 8 * n, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->st_ts, ts, 8 * n, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->st_val, value, 8 * n, hipMemcpyHostToDevice, e->stream));
-    dk = e->st_key; dts = e->st_ts; dv = e->st_val;
-    if (key_hash) { HIPCHK(e, hipMemcpyAsync(e->st_hash, key_hash, 4 * n, hipMemcpyHostToDevice, e->stream)); dh = e->st_hash; }
-    if (f1) { HIPCHK(e, hipMemcpyAsync(e->st_f1, f1, 8 * n, hipMemcpyHostToDevice, e->stream)); df1 = e->st_f1; }
+    HIPCHK(e, hipMemcpyAsync(e->stg_key[par], key, 8 * n, hipMemcpyHostToDevice, in_stream));
+    HIPCHK(e, hipMemcpyAsync(e->stg_ts[par], ts, 8 * n, hipMemcpyHostToDevice, in_stream));
+    HIPCHK(e, hipMemcpyAsync(e->stg_val[par], value, 8 * n, hipMemcpyHostToDevice, in_stream));
+    dk = e->stg_key[par]; dts = e->stg_ts[par]; dv = e->stg_val[par];
+    if (key_hash) { HIPCHK(e, hipMemcpyAsync(e->stg_hash[par], key_hash, 4 * n, hipMemcpyHostToDevice, in_stream)); dh = e->stg_hash[par]; }
+    if (f1) { HIPCHK(e, hipMemcpyAsync(e->stg_f1[par], f1, 8 * n, hipMemcpyHostToDevice, in_stream)); df1 = e->stg_f1[par]; }
   }
   if (e->routed && mem == FW_MEM_DEVICE) {
     // k_route streams the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
     auto mis = [](const void* ptr, uintptr_t a) { return ((uintptr_t)ptr & (a - 1)) != 0; };
-    if (mis(dk, 16)) { HIPCHK(e, hipMemcpyAsync(e->st_key, dk, 8 * n, hipMemcpyDeviceToDevice, e->stream)); dk = e->st_key; }
-    if (mis(dts, 16)) { HIPCHK(e, hipMemcpyAsync(e->st_ts, dts, 8 * n, hipMemcpyDeviceToDevice, e->stream)); dts = e->st_ts; }
-    if (mis(dv, 16)) { HIPCHK(e, hipMemcpyAsync(e->st_val, dv, 8 * n, hipMemcpyDeviceToDevice, e->stream)); dv = e->st_val; }
-    if (dh && mis(dh, 8)) { HIPCHK(e, hipMemcpyAsync(e->st_hash, dh, 4 * n, hipMemcpyDeviceToDevice, e->stream)); dh = e->st_hash; }
+    if (mis(dk, 16)) { HIPCHK(e, hipMemcpyAsync(e->stg_key[par], dk, 8 * n, hipMemcpyDeviceToDevice, in_stream)); dk = e->stg_key[par]; }
+    if (mis(dts, 16)) { HIPCHK(e, hipMemcpyAsync(e->stg_ts[par], dts, 8 * n, hipMemcpyDeviceToDevice, in_stream)); dts = e->stg_ts[par]; }
+    if (mis(dv, 16)) { HIPCHK(e, hipMemcpyAsync(e->stg_val[par], dv, 8 * n, hipMemcpyDeviceToDevice, in_stream)); dv = e->stg_val[par]; }
+    if (dh && mis(dh, 8)) { HIPCHK(e, hipMemcpyAsync(e->stg_hash[par], dh, 4 * n, hipMemcpyDeviceToDevice, in_stream)); dh = e->stg_hash[par]; }
   }
   if (!df1) df1 = dts;
   BatchIn b;
@@ -1708,10 +1769,14 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.late_count = e->late_count;
   b.late_capacity = e->late_key ? e->cfg.max_batch : 0;
   b.idx_bits = e->idx_bits;
-  e->phase_begin(FW_PHASE_INGEST);
-  if (e->routed) FW_DISPATCH(launch_routed_t, e, b, df1);
-  else FW_DISPATCH(launch_ingest_t, e, b);
-  e->phase_end(n);
+  if (e->routed) {
+    FW_DISPATCH(launch_routed_t, e, b, df1, par);
+  } else {
+    e->phase_begin(FW_PHASE_INGEST);
+    FW_DISPATCH(launch_ingest_t, e, b);
+    e->phase_end(n);
+  }
+  e->batches++;
   HIPCHK(e, hipGetLastError());
   if (e->s.first && !e->routed) {   // the partitioned form sets f1 in k_aggregate
     e->phase_begin(FW_PHASE_FIXUP);
@@ -1774,6 +1839,7 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
 int fw_sync(fw_engine* e) {
   if (!e) return FW_ERR_INVALID_ARG;
   HIPCHK(e, hipSetDevice(e->dev));
+  HIPCHK(e, hipStreamSynchronize(e->rstream));
   return check_device_error(e);
 }
 
@@ -1871,9 +1937,9 @@ int fw_debug_counters(fw_engine* e, int64_t* out8) {
 int fw_set_stream(fw_engine* e, void* stream) {
   if (!e) return FW_ERR_INVALID_ARG;
   HIPCHK(e, hipSetDevice(e->dev));
+  HIPCHK(e, hipStreamSynchronize(e->rstream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (e->own_stream) { HIPCHK(e, hipStreamDestroy(e->own_stream)); e->own_stream = nullptr; }
-  e->stream = (hipStream_t)stream;
+  e->client = stream;
   return FW_OK;
 }
 
@@ -1922,6 +1988,10 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
     e->part_block_counts = e->alloc<int64_t>((size_t)(nblocks * parallelism));
     if (!e->part_block_counts) return fail(e, FW_ERR_DEVICE, "alloc");
     e->part_blocks_cap = nblocks * parallelism;
+  }
+  if (e->client) {   // the batch is produced on the caller's stream
+    HIPCHK(e, hipEventRecord(e->ev_in, (hipStream_t)e->client));
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_in, 0));
   }
   hipLaunchKernelGGL(k_part_count, dim3((unsigned)nblocks), dim3(BLOCK), 0, e->stream, key, key_hash, n, max_parallelism,
                      parallelism, e->part_block_counts);

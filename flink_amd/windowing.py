@@ -170,6 +170,7 @@ class WindowEngine:
         if rc != 0:
             raise _abi.FwError(rc, self._fn("last_error")(None).decode() or "fw_create failed")
         self.h = h
+        self._inflight = []   # device columns pushed since the last sync/collect (read asynchronously)
 
     def _fn(self, name):
         return getattr(self.lib, f"{self.prefix}_{name}")
@@ -179,7 +180,8 @@ class WindowEngine:
             raise _abi.FwError(rc, self._fn("last_error")(self.h).decode())
 
     def use_stream(self, stream_handle):
-        """Order engine work on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
+        """Make an external HIP stream the producer of pushed columns (e.g. torch.cuda.current_stream().cuda_stream):
+        each push waits for the work enqueued on it so far."""
         if self.prefix == "fw":
             self._check(self._fn("set_stream")(self.h, ctypes.c_void_p(stream_handle)))
             self._stream = stream_handle
@@ -189,11 +191,14 @@ class WindowEngine:
         if self.prefix == "fw":
             mem = _abi.FW_MEM_DEVICE if _is_device(key) else _abi.FW_MEM_HOST
             if mem == _abi.FW_MEM_DEVICE:
-                # device columns are produced on torch's current stream: run the engine on it
+                # device columns are produced on torch's current stream: the engine waits for it at each
+                # push, and reads the columns on its own streams until a later sync/collect, so the
+                # tensors are kept alive until then (torch's allocator does not see the engine's streams)
                 import torch
                 cur = torch.cuda.current_stream(key.device).cuda_stream
                 if getattr(self, "_stream", None) != cur:
                     self.use_stream(cur)
+                self._inflight.append((key, ts, value, key_hash, f1))
             self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n, mem))
         else:
             self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n))
@@ -204,12 +209,14 @@ class WindowEngine:
     def sync(self):
         if self.prefix == "fw":
             self._check(self._fn("sync")(self.h))
+            self._inflight.clear()
 
     def collect(self):
         """Results since the last collect: dict of numpy columns + (mark_wm, mark_pos)."""
         o = _abi.FwOut()
         if self.prefix == "fw":
             self._check(self._fn("collect")(self.h, ctypes.byref(o), _abi.FW_MEM_HOST))
+            self._inflight.clear()
         else:
             self._check(self._fn("collect")(self.h, ctypes.byref(o)))
         n = o.n
