@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--ingest-mode", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="events in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--no-profile", action="store_true", help="no device-time events in the timed loop")
+    ap.add_argument("--prof-steps", type=int, default=8,
+                    help="steps after the timed region run with per-kernel device-time events (roofline); "
+                         "timed events serialise kernels, so the timed region runs without them")
     return ap.parse_args()
 
 
@@ -88,7 +90,7 @@ def cpu_baseline(cfg, n_keys, rate, n):
                       f"watermark every 2^22 events, final MAX_WATERMARK; {fired} windows fired"}
 
 
-def pmc_traffic():
+def pmc_traffic(kernel):
     """HBM bytes per ingest launch from the committed rocprofv3 PMC summary of THIS library build
     (profiles/*_pmc.json, written by tools/summarize_profiles.py from separate FETCH_SIZE / WRITE_SIZE
     passes), or None when no summary matches the library's md5."""
@@ -101,8 +103,11 @@ def pmc_traffic():
             d = json.load(open(f))
         except ValueError:
             continue
-        if d.get("library_md5") == md5 and d.get("ingest_traffic_bytes_per_launch"):
-            return d["ingest_traffic_bytes_per_launch"], os.path.basename(f)
+        if d.get("library_md5") != md5:
+            continue
+        for name, k in d.get("kernels", {}).items():
+            if kernel in name and k.get("hbm_bytes_corrected"):
+                return k["hbm_bytes_corrected"], os.path.basename(f)
     return None, None
 
 
@@ -111,7 +116,7 @@ def main():
     world, rank, local = dist_init(args)
     dev = torch.device("cuda", local)
     n_keys, rate, batch, key_cap = CONFIGS[args.config]
-    total_steps = args.warmup + args.steps
+    total_steps = args.warmup + args.steps + args.prof_steps
 
     from flink_amd.keygroups import compute_key_group_range_for_operator_index
     mp = 128
@@ -153,19 +158,23 @@ def main():
     eng.sync()
     torch.cuda.synchronize()
     warm_res = eng.collect()
-    _abi.load_library().fw_set_profiling(eng.h, 0 if args.no_profile else 1)
-    eng.lib.fw_get_profile(eng.h, _abi.FwProfile())  # reset counters
-
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for j in range(args.warmup, total_steps):
+    for j in range(args.warmup, args.warmup + args.steps):
         step(j)
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()      # device-wide: covers the engine's own streams
     barrier(world)
     dt = time.perf_counter() - t0
+
+    # per-kernel device time on the continuation of the same stream (untimed)
+    eng.lib.fw_set_profiling(eng.h, 1)
+    eng.lib.fw_get_profile(eng.h, _abi.FwProfile())  # reset counters
+    for j in range(args.warmup + args.steps, total_steps):
+        step(j)
     prof = _abi.FwProfile()
     eng.lib.fw_get_profile(eng.h, prof)
+    eng.lib.fw_set_profiling(eng.h, 0)
     eng.sync()
 
     if world > 1:
@@ -197,11 +206,22 @@ def main():
     form = eng.stats()["ingest_form"]
     events = args.steps * batch * world
     value = events / dt
-    ing_ms = prof.ms[_abi.FW_PHASE_INGEST]
-    ing_n = prof.launches[_abi.FW_PHASE_INGEST]
-    ing_rec = prof.records[_abi.FW_PHASE_INGEST]
-    achieved = (24.0 * ing_rec / ing_n) / (ing_ms / ing_n / 1e3) / 1e9 if ing_n else 0.0
-    traffic, traffic_src = pmc_traffic()
+
+    def per(ph):
+        n_ = prof.launches[ph]
+        return (prof.ms[ph] / n_ if n_ else 0.0), (prof.records[ph] / n_ if n_ else 0.0)
+    route_ms, route_rec = per(_abi.FW_PHASE_INGEST)
+    agg_ms, _ = per(_abi.FW_PHASE_AGGREGATE)
+    wm_ms, _ = per(_abi.FW_PHASE_FIRE)
+    # dominant kernel: the one taking the most device time per batch; its algorithmic bytes are SURVEY.md
+    # 8(d)'s 24 B per event (key, ts, value int64) times the events one launch processes
+    names = {"k_route": route_ms, "k_aggregate": agg_ms} if form == 2 else {"k_ingest_direct": route_ms}
+    dom = max(names, key=names.get)
+    dom_ms = names[dom]
+    alg_bytes = 24.0 * route_rec
+    achieved = alg_bytes / (dom_ms / 1e3) / 1e9 if dom_ms else 0.0
+    path_ms = route_ms + agg_ms
+    traffic, traffic_src = pmc_traffic(dom)
     line = {
         "metric": "events/sec (whole node) keyed 1s tumbling sum; % of HBM roofline",
         "value": value,
@@ -219,13 +239,16 @@ def main():
                                f"{rate} events/s event time, watermark every {batch} events per source",
                    "batch_per_gpu": batch, "keys": n_keys, "max_parallelism": mp, "parallelism": f"kg{world}",
                    "reduce": "Tuple3(a.f0, a.f1, a.f2 + b.f2), f1 = first arrival"},
-        "roofline": {"bound": "hbm", "kernel": "k_ingest_direct" if form == 1 else "k_route+k_aggregate", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "bytes_per_event": 24, "ingest_ms_per_batch": ing_ms / max(args.steps, 1),
-                     "fire_ms_total": prof.ms[_abi.FW_PHASE_FIRE], "fixup_ms_total": prof.ms[_abi.FW_PHASE_FIXUP],
-                     "traffic": traffic, "traffic_unit": "bytes per ingest launch (FETCH_SIZE x2 + WRITE_SIZE)",
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc)",
                      "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": 24.0 * ing_rec / ing_n if ing_n else None},
+                     "algorithmic_bytes_per_launch": alg_bytes, "bytes_per_event": 24,
+                     "kernel_ms": {k: v for k, v in names.items()}, "watermark_ms": wm_ms,
+                     "path_achieved": alg_bytes / (path_ms / 1e3) / 1e9 if path_ms else 0.0,
+                     "path_note": "24 B/event over the summed device time of the ingest kernels of one batch",
+                     "device_time_source": f"HIP events around each kernel on its stream, {args.prof_steps} "
+                                           "batches after the timed region"},
         "check": check,
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:

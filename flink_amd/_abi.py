@@ -35,7 +35,7 @@ FW_MEM_DEVICE = 1
 EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sync", "fw_collect",
                     "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
                     "fw_get_profile", "fw_debug_counters", "fw_debug_stamps", "fw_set_stream", "fw_version")
-FW_PHASE_INGEST, FW_PHASE_FIXUP, FW_PHASE_LATE, FW_PHASE_FIRE, FW_NPHASES = 0, 1, 2, 3, 4
+FW_PHASE_INGEST, FW_PHASE_FIXUP, FW_PHASE_LATE, FW_PHASE_FIRE, FW_PHASE_AGGREGATE, FW_NPHASES = 0, 1, 2, 3, 4, 5
 
 _i32, _i64, _p = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
 _pi64 = ctypes.POINTER(ctypes.c_int64)
@@ -57,7 +57,7 @@ class FwOut(ctypes.Structure):
 
 
 class FwProfile(ctypes.Structure):
-    _fields_ = [("ms", ctypes.c_double * 4), ("launches", _i64 * 4), ("records", _i64 * 4)]
+    _fields_ = [("ms", ctypes.c_double * FW_NPHASES), ("launches", _i64 * FW_NPHASES), ("records", _i64 * FW_NPHASES)]
 
 
 class FwStats(ctypes.Structure):

@@ -1359,9 +1359,9 @@ struct fw_engine {
   struct Timed { int phase; hipEvent_t a, b; int64_t records; };
   std::vector<Timed> timed;
   std::vector<hipEvent_t> event_pool;
-  double prof_ms[FW_NPHASES] = {0, 0, 0, 0};
-  int64_t prof_launches[FW_NPHASES] = {0, 0, 0, 0};
-  int64_t prof_records[FW_NPHASES] = {0, 0, 0, 0};
+  double prof_ms[FW_NPHASES] = {};
+  int64_t prof_launches[FW_NPHASES] = {};
+  int64_t prof_records[FW_NPHASES] = {};
   hipEvent_t take_event() {
     hipEvent_t ev = nullptr;
     if (!event_pool.empty()) { ev = event_pool.back(); event_pool.pop_back(); }
@@ -1463,10 +1463,10 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   e->phase_end(b.n, rs);
   (void)hipEventRecord(e->ev_route[par], rs);
   (void)hipStreamWaitEvent(e->stream, e->ev_route[par], 0);
-  e->phase_begin(FW_PHASE_INGEST);
+  e->phase_begin(FW_PHASE_AGGREGATE);
   hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b, r,
                      f1col);
-  e->phase_end(0);
+  e->phase_end(b.n);
   (void)hipEventRecord(e->ev_agg[par], e->stream);
 }
 

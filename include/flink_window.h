@@ -163,13 +163,15 @@ int         fw_partition_by_operator(fw_engine* e, const int64_t* key, const int
                                      int64_t* out_key, int32_t* out_key_hash, int64_t* out_f1,
                                      int64_t* out_ts, void* out_value, int64_t* counts, int64_t* offsets);
 
-/* Device-time accounting (HIP events on the engine's stream around each kernel phase), for the
- * roofline figures of bench.py.  Off by default; enabling it adds event records, not syncs. */
-#define FW_PHASE_INGEST  0   /* per-record ingest (key group, slice, directory, pane update)  */
-#define FW_PHASE_FIXUP   1   /* first-arrival f1 gather for new panes                         */
+/* Device-time accounting (HIP events around each kernel, on the stream it runs on), for the roofline
+ * figures of bench.py.  Off by default; enabling it adds timed event records between kernels, which
+ * serialise them (measure throughput with it off). */
+#define FW_PHASE_INGEST  0   /* per-record ingest: k_route (partitioned form) or k_ingest_direct */
+#define FW_PHASE_FIXUP   1   /* first-arrival f1 gather for new panes (direct form)           */
 #define FW_PHASE_LATE    2   /* per-element fires (allowed lateness > 0)                      */
-#define FW_PHASE_FIRE    3   /* watermark: plan + fire + purge + mark                         */
-#define FW_NPHASES       4
+#define FW_PHASE_FIRE    3   /* watermark: plan + fire + purge + mark (k_watermark)            */
+#define FW_PHASE_AGGREGATE 4 /* partitioned form: per-bucket LDS aggregation (k_aggregate)    */
+#define FW_NPHASES       5
 typedef struct {
   double  ms[FW_NPHASES];        /* accumulated device milliseconds per phase */
   int64_t launches[FW_NPHASES];  /* timed launches per phase                  */

@@ -4,7 +4,7 @@
 # gpurun_out/prof_*; copy the summaries to profiles/.
 REPO="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$REPO"
-ARGS=${PROF_ARGS:-"--steps 16 --warmup 4 --cpu-sample 0 --no-check"}
+ARGS=${PROF_ARGS:-"--steps 16 --warmup 4 --prof-steps 0 --cpu-sample 0 --no-check"}
 export TMPDIR=/tmp
 timeout -k 10 ${T_PROF:-300} rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/prof_trace" -o run -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 gpurun_out/prof_trace.log
