@@ -172,6 +172,7 @@ def main():
     eng.lib.fw_get_profile(eng.h, _abi.FwProfile())  # reset counters
     for j in range(args.warmup + args.steps, total_steps):
         step(j)
+        eng.sync()   # isolate the kernels (no route/aggregate overlap across batches while timing them)
     prof = _abi.FwProfile()
     eng.lib.fw_get_profile(eng.h, prof)
     eng.lib.fw_set_profiling(eng.h, 0)
@@ -248,7 +249,7 @@ def main():
                      "path_achieved": alg_bytes / (path_ms / 1e3) / 1e9 if path_ms else 0.0,
                      "path_note": "24 B/event over the summed device time of the ingest kernels of one batch",
                      "device_time_source": f"HIP events around each kernel on its stream, {args.prof_steps} "
-                                           "batches after the timed region"},
+                                           "batches after the timed region, one batch at a time"},
         "check": check,
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:

@@ -524,16 +524,10 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   }
   __syncthreads();   // cnt zeroed, key hashes parked
   FW_STAMP(r, 0, 1);
-  // phase B: per record operator work (timestamp, key group, windows, lateness), the record's index in the
-  // tile's slice set (cached per wave, as a wave of an in-order stream stays in one slice) and its
-  // counting-sort rank; the rest join the direct list (rare: per-element fires, slices beyond the tile's
-  // RT_Q, the Long.MIN_VALUE key), applied by the k_aggregate workgroup owning the key's bucket
-  int64_t c_m = INT64_MIN;
-  int32_t c_q = -1;
+  // phase B1: per record operator work (timestamp, key group, windows, lateness) — pure ALU; the slice
+  // number replaces the timestamp in tt[]
   unsigned long long late_pairs = 0;
-  int32_t bin[PER];       // routed bin, or -1
-  int32_t rank[PER];
-  uint32_t direct_mask = 0, fire_mask = 0;
+  uint32_t route_mask = 0, direct_mask = 0, fire_mask = 0;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int64_t i = base + 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
@@ -557,32 +551,53 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     const bool late_fire = live && w.n_fire > 0;
     // routable: its windows neither late nor fired yet, so no watermark up to b.wm fires or purges its slice
     const bool routable = live && !late_fire && key != EMPTY_KEY;
-    const uint64_t lm = __ballot(routable);
-    const int leader = lm ? __ffsll((long long)lm) - 1 : 0;
-    const int64_t m0 = __shfl(w.m, leader);
-    const bool uniform = __all(!routable || w.m == m0);
-    int32_t q = -1;
-    if (uniform) {
-      if (lm != 0 && m0 != c_m) {   // wave-uniform branch
-        int32_t q0 = -1;
-        if ((int)(threadIdx.x & 63) == leader) q0 = tile_slice(lset, m0);
-        c_q = __shfl(q0, leader);
-        c_m = m0;
-      }
-      q = routable ? c_q : -1;
-    } else if (routable) {
-      q = tile_slice(lset, w.m);
+    route_mask |= (routable ? 1u : 0u) << k;
+    direct_mask |= (live && !routable ? 1u : 0u) << k;
+    fire_mask |= (late_fire ? 1u : 0u) << k;
+    tt[k] = w.m;
+  }
+  // phase B2: the routed records' index in the tile's slice set — resolved once per wave when all its
+  // routed records share one slice (an in-order stream), per record otherwise — then their bin and
+  // counting-sort rank.  The rest join the direct list (rare: per-element fires, slices beyond the
+  // tile's RT_Q, the Long.MIN_VALUE key), applied by the k_aggregate workgroup owning the key's bucket.
+  int64_t m_ref = INT64_MIN;
+  {
+    const uint64_t lm = __ballot(route_mask != 0);
+    if (lm) {
+      const int leader = __ffsll((long long)lm) - 1;
+      int64_t mine = INT64_MIN;
+#pragma unroll
+      for (int k = PER - 1; k >= 0; --k) if ((route_mask >> k) & 1u) mine = tt[k];
+      m_ref = __shfl(mine, leader);
     }
+  }
+  bool same = true;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) same &= !((route_mask >> k) & 1u) || tt[k] == m_ref;
+  int32_t q_ref = -1;
+  if (__all(same)) {
+    if (m_ref != INT64_MIN && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)__ballot(route_mask != 0)) - 1))
+      q_ref = tile_slice(lset, m_ref);
+    q_ref = __shfl(q_ref, __ffsll((long long)__ballot(route_mask != 0)) - 1);
+  }
+  const bool wave_uniform = __all(same);
+  int32_t bin[PER];       // routed bin, or -1
+  int32_t rank[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
     bin[k] = -1;
     rank[k] = 0;
+    const bool routable = (route_mask >> k) & 1u;
+    int32_t q = -1;
+    if (wave_uniform) q = routable ? q_ref : -1;
+    else if (routable) q = tile_slice(lset, tt[k]);
     if (q >= 0) {
-      const uint64_t hk = fmix64((uint64_t)key);
+      const uint64_t hk = fmix64((uint64_t)kk[k]);
       bin[k] = q * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
       rank[k] = atomicAdd(&cnt[bin[k]], 1);
       kk[k] = (int64_t)hk;   // routed records carry the directory hash (a bijection of the key)
-    } else if (live) {
-      direct_mask |= 1u << k;
-      if (late_fire) fire_mask |= 1u << k;
+    } else if (routable) {
+      direct_mask |= 1u << k;   // the tile's slice set is full
     }
   }
   if (__any(late_pairs != 0)) {
@@ -601,8 +616,8 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
       }
     }
   }
+  __syncthreads();   // every wave's slice claims are in lset
   if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
-  __syncthreads();
   FW_STAMP(r, 0, 2);
   block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
   uint16_t* seg = r.seg + (int64_t)blockIdx.x * (nbq + 1);
