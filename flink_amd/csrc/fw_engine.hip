@@ -199,12 +199,14 @@ struct RecWin {
   int32_t n_late;     // of which late (dropped)
   int32_t n_fire;     // of which not late but maxTimestamp <= watermark (per-element fire)
   bool quirk;         // sliding assignment outside the slice-exact regime
+  int64_t lo, hi;     // the slice's timestamps [lo, hi]: every ts in it gets this same RecWin (lo > hi: none)
 };
 
 struct SlideSpec { int64_t offset, size, slide, g, lateness; double inv_g; int32_t K, R; };
 
 // sliding assignment, out of line (the tumbling case is inlined on the hot path)
-__device__ __noinline__ RecWin record_windows_sliding(SlideSpec s, int64_t ts, int64_t wm) {
+template <bool INL>
+__device__ __forceinline__ RecWin record_windows_sliding_body(const SlideSpec& s, int64_t ts, int64_t wm) {
   RecWin r;
   r.quirk = false;
   r.n_late = 0;
@@ -213,8 +215,13 @@ __device__ __noinline__ RecWin record_windows_sliding(SlideSpec s, int64_t ts, i
   if (x < 0 || jadd(jsub(ts, s.offset), s.slide) < 0) r.quirk = true;   // Java % of a negative numerator
   {
     int64_t q, rem;
-    jdivmod(x, s.g, s.inv_g, q, rem);
+    if (INL) jdivmod_inl(x, s.g, s.inv_g, q, rem);
+    else jdivmod(x, s.g, s.inv_g, q, rem);
     r.m = q - 1;
+    // ts' in [ts - rem, ts - rem + g) shares q; x >= 0 makes the quirk test monotone over that range
+    r.lo = jsub(ts, rem);
+    r.hi = jadd(r.lo, s.g - 1);
+    if (r.quirk || r.hi < r.lo) { r.lo = 1; r.hi = 0; }
   }
   int64_t n_hi = floor_div(r.m, s.R);
   int64_t n_lo = floor_div(r.m - s.K, s.R) + 1;
@@ -228,22 +235,34 @@ __device__ __noinline__ RecWin record_windows_sliding(SlideSpec s, int64_t ts, i
   }
   return r;
 }
+__device__ __noinline__ RecWin record_windows_sliding(SlideSpec s, int64_t ts, int64_t wm) {
+  return record_windows_sliding_body<false>(s, ts, wm);
+}
 
+
+template <bool INL = false>
 __device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int64_t wm) {
-  if (s.assigner != FW_TUMBLING)
-    return record_windows_sliding(SlideSpec{s.offset, s.size, s.slide, s.g, s.lateness, s.inv_g, s.K, s.R}, ts, wm);
+  if (s.assigner != FW_TUMBLING) {
+    const SlideSpec ss{s.offset, s.size, s.slide, s.g, s.lateness, s.inv_g, s.K, s.R};
+    return INL ? record_windows_sliding_body<true>(ss, ts, wm) : record_windows_sliding(ss, ts, wm);
+  }
   RecWin r;
   r.quirk = false;
   r.n_late = 0;
   r.n_fire = 0;
   int64_t x = jadd(jsub(ts, s.offset), s.size);
   int64_t q, rem;
-  jdivmod(x, s.size, s.inv_size, q, rem);
+  if (INL) jdivmod_inl(x, s.size, s.inv_size, q, rem);
+  else jdivmod(x, s.size, s.inv_size, q, rem);
   r.m = q - 1;                                                 // start = offset + m * size
   int64_t start = jsub(ts, rem);                               // getWindowStartWithOffset
   int64_t max_ts = jsub(jadd(start, s.size), 1);               // TimeWindow.maxTimestamp
   int64_t ct = cleanup_time(max_ts, s.lateness);
   r.n_windows = 1;
+  // ts' in [start, max_ts] shares the window when x >= 0 (a negative x is Java's truncating-% regime)
+  r.lo = start;
+  r.hi = max_ts;
+  if (x < 0 || max_ts < start) { r.lo = 1; r.hi = 0; }
   if (ct <= wm) r.n_late = 1;
   else if (max_ts <= wm) r.n_fire = 1;
   return r;
@@ -437,6 +456,13 @@ struct RouteBuf {
 
 #define FW_STAMP(r, base, k) do { if ((r).stamps && threadIdx.x == 0) (r).stamps[(base) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
+// a wave-uniform 64-bit value moved to scalar registers
+__device__ __forceinline__ int64_t uniform64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // tile-local slice set in LDS (RT_Q entries): index of slice m, inserting it if new; -1 when full
 __device__ __forceinline__ int32_t tile_slice(int64_t* lset, int64_t m) {
   for (int q = 0; q < RT_Q; ++q) {
@@ -528,6 +554,27 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   // number replaces the timestamp in tt[]
   unsigned long long late_pairs = 0;
   uint32_t route_mask = 0, direct_mask = 0, fire_mask = 0;
+  // the wave's reference slice: assignment of its first record, valid for every record whose timestamp
+  // lies in the same slice (a wave of an in-order stream nearly always does); the others take the
+  // full per-record path.  Bounded away from the int64 edges so no wrap happens inside the range.
+  RecWin w0;
+  w0.m = 0; w0.n_late = 0; w0.n_fire = 0; w0.n_windows = 0; w0.quirk = false; w0.lo = 1; w0.hi = 0;
+  {
+    const int64_t i0 = base + 2 * (int)threadIdx.x;
+    const bool c0 = (!tail || i0 < b.n) && tt[0] > -(1LL << 61) && tt[0] < (1LL << 61);
+    const uint64_t cm = __ballot(c0);
+    if (cm && s.size < (1LL << 60)) {
+      const int64_t ts0 = uniform64(__shfl(tt[0], __ffsll((long long)cm) - 1));
+      w0 = record_windows(s, ts0, b.wm);
+      w0.m = uniform64(w0.m); w0.lo = uniform64(w0.lo); w0.hi = uniform64(w0.hi);
+      w0.n_late = __builtin_amdgcn_readfirstlane(w0.n_late);
+      w0.n_fire = __builtin_amdgcn_readfirstlane(w0.n_fire);
+      w0.n_windows = __builtin_amdgcn_readfirstlane(w0.n_windows);
+    }
+  }
+  // a subtask owning every key group cannot see a foreign key: skip the murmur range check
+  const bool all_kg = s.kg_start == 0 && s.kg_end == s.mp - 1;
+  uint32_t slow_mask = 0;   // records outside the wave's reference slice
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int64_t i = base + 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
@@ -535,26 +582,58 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     const int64_t key = kk[k], ts = tt[k];
     bool ok = valid;
     if (ok && ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
-    if (ok) {
+    if (ok && !all_kg) {
       const int32_t h = b.key_hash ? lhash[i - base] : long_hash_code(key);
       const int32_t kg = record_key_group(s, h);   // AbstractKeyedStateBackend.setCurrentKey :167-170
       if (kg < s.kg_start || kg > s.kg_end) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
     }
-    RecWin w;
-    w.m = 0; w.n_late = 0; w.n_fire = 0; w.n_windows = 0; w.quirk = false;
-    if (ok) {
-      w = record_windows(s, ts, b.wm);
-      if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
-    }
-    if (ok) late_pairs += (unsigned long long)w.n_late;
-    const bool live = ok && (w.n_windows - w.n_late) > 0;
-    const bool late_fire = live && w.n_fire > 0;
+    const bool fast = ok && ts >= w0.lo && ts <= w0.hi;
+    slow_mask |= (ok && !fast ? 1u : 0u) << k;
+    if (fast) late_pairs += (unsigned long long)w0.n_late;
+    const bool live = fast && (w0.n_windows - w0.n_late) > 0;
+    const bool late_fire = live && w0.n_fire > 0;
     // routable: its windows neither late nor fired yet, so no watermark up to b.wm fires or purges its slice
     const bool routable = live && !late_fire && key != EMPTY_KEY;
     route_mask |= (routable ? 1u : 0u) << k;
     direct_mask |= (live && !routable ? 1u : 0u) << k;
     fire_mask |= (late_fire ? 1u : 0u) << k;
-    tt[k] = w.m;
+    tt[k] = w0.m;
+  }
+  // the full assignment for the rest: one call-free copy of the code (a call would make the register
+  // allocator spill the tile around it), timestamps re-read from the input, results through LDS
+  if (__any(slow_mask != 0)) {
+    int64_t* sm = (int64_t*)st_kv + RT_TILE / 2;     // [RT_TILE] slice numbers, after the parked key hashes
+    int32_t* sf = (int32_t*)(sm + RT_TILE);          // [RT_TILE] flags: live | late_fire << 1 | n_late << 2
+#pragma unroll 1
+    for (int k = 0; k < PER; ++k) {
+      if ((slow_mask >> k) & 1u) {
+        const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
+        const int64_t ts = b.ts[base + t];
+        const RecWin w = record_windows<true>(s, ts, b.wm);
+        int32_t f = 0;
+        if (w.quirk && s.assigner == FW_SLIDING) set_error(s.err, FW_ERR_UNSUPPORTED);
+        else {
+          const bool live = (w.n_windows - w.n_late) > 0;
+          f = (live ? 1 : 0) | (live && w.n_fire > 0 ? 2 : 0) | (w.n_late << 2);
+        }
+        sm[t] = w.m;
+        sf[t] = f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if ((slow_mask >> k) & 1u) {
+        const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
+        const int32_t f = sf[t];
+        late_pairs += (unsigned long long)(f >> 2);
+        const bool live = f & 1, late_fire = (f & 2) != 0;
+        const bool routable = live && !late_fire && kk[k] != EMPTY_KEY;
+        route_mask |= (routable ? 1u : 0u) << k;
+        direct_mask |= (live && !routable ? 1u : 0u) << k;
+        fire_mask |= (late_fire ? 1u : 0u) << k;
+        tt[k] = sm[t];
+      }
+    }
   }
   // phase B2: the routed records' index in the tile's slice set — resolved once per wave when all its
   // routed records share one slice (an in-order stream), per record otherwise — then their bin and

@@ -87,6 +87,17 @@ FW_HD void jdivmod(int64_t x, int64_t d, double inv_d, int64_t& q, int64_t& r) {
   r = w.r;
 }
 
+// jdivmod with the wide case inline (no call): for kernels whose register budget a call would spill
+FW_HD void jdivmod_inl(int64_t x, int64_t d, double inv_d, int64_t& q, int64_t& r) {
+  const int64_t lim = (int64_t)1 << 52;
+  if (x > -lim && x < lim && d < lim) {
+    jdivmod(x, d, inv_d, q, r);
+    return;
+  }
+  q = x / d;
+  r = x - q * d;
+}
+
 // floor division / modulo on int64 (slice numbering; not Java semantics, internal indexing)
 FW_HD int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b, r = a % b;

@@ -184,6 +184,25 @@ def test_extreme_keys_and_timestamps(hip, oracle_engine, mode):
     eg.close(); eo.close()
 
 
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("size,offset", [(1000, -300), (700, 0), (1000, 250)])
+def test_tumbling_negative_timestamps_dense(hip, oracle_engine, mode, size, offset):
+    """In-order and shuffled runs across ts < offset - size, where Java's truncating % assigns a window
+    not containing ts (TimeWindow.java:239-241): the per-wave slice shortcut must not apply there."""
+    from flink_amd.windowing import TumblingEventTimeWindows
+    n = 120_000
+    i = np.arange(n, dtype=np.int64)
+    ts = -40_000 + (i * 80_000) // n
+    mix = (i // 4096) % 3 == 1                       # every third tile shuffled within +-3 s
+    rng = np.random.default_rng(7)
+    ts[mix] += rng.integers(-3000, 3000, mix.sum())
+    keys = rng.integers(0, 3000, n).astype(np.int64)
+    vals = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(size, offset), ("sum", "count"), lateness=2000,
+                max_open_slices=64)
+    _run_both(hip, oracle_engine, cfg, keys, ts, vals, 8192, 1000, ["sum_i64", "count"])
+
+
 def test_missing_timestamp_fails(hip):
     from flink_amd import _abi
     from flink_amd.windowing import TumblingEventTimeWindows
