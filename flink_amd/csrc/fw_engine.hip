@@ -416,6 +416,13 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f
   }
 }
 
+// a wave-uniform 64-bit value moved to scalar registers
+__device__ __forceinline__ int64_t uniform64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // ------------------------------------------------------------------------------------------------
 // ingest, partitioned form.  Two kernels per batch:
 //  k_route      one workgroup per tile of RT_TILE records: streams the tile's columns in with 16-B
@@ -455,13 +462,6 @@ struct RouteBuf {
 };
 
 #define FW_STAMP(r, base, k) do { if ((r).stamps && threadIdx.x == 0) (r).stamps[(base) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-
-// a wave-uniform 64-bit value moved to scalar registers
-__device__ __forceinline__ int64_t uniform64(int64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 // tile-local slice set in LDS (RT_Q entries): index of slice m, inserting it if new; -1 when full
 __device__ __forceinline__ int32_t tile_slice(int64_t* lset, int64_t m) {
@@ -1564,6 +1564,20 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   (void)hipEventRecord(e->ev_agg[par], e->stream);
 }
 
+// no window of the assigner has its maxTimestamp or its cleanup time in (old, new]: the advance fires
+// and purges nothing (a live slice's fire and cleanup times lie above the watermark it was created
+// under), only the watermark's mark is due.  Conservative near the int64 edges.
+static bool wm_quiet(const Spec& s, int64_t old_wm, int64_t new_wm) {
+  const int64_t lim = (int64_t)1 << 61;
+  if (old_wm <= -lim || new_wm >= lim || s.lateness >= lim || s.size >= lim || s.offset <= -lim || s.offset >= lim)
+    return false;
+  const __int128 d = s.assigner == FW_TUMBLING ? s.size : s.slide;
+  auto fdiv = [](__int128 x, __int128 y) { __int128 q = x / y; if (x % y != 0 && x < 0) --q; return q; };
+  auto crosses = [&](__int128 a) { return fdiv((__int128)new_wm - a, d) != fdiv((__int128)old_wm - a, d); };
+  const __int128 a = (__int128)s.offset + s.size - 1;   // maxTimestamp of window n is a + n * d
+  return !crosses(a) && !crosses(a + s.lateness);
+}
+
 template <int VT, int AGG, bool FIRST>
 static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + WM_THREADS - 1) / WM_THREADS, e->grid / 8));
@@ -1611,6 +1625,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (c.value_type != FW_VALUE_I64 && c.value_type != FW_VALUE_F64) return bad("bad value type");
   if ((c.agg_mask & ~15) != 0 || c.agg_mask == 0) return bad("bad aggregate mask");
   if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
+  if (c.ingest_mode < 0 || c.ingest_mode > 2) return bad("bad ingest mode");
   if (c.assigner == FW_SLIDING && (c.allowed_lateness > 0 || c.trigger != FW_TRIGGER_EVENT_TIME))
     return unsupported("sliding windows with allowed lateness or PurgingTrigger are not implemented on the slice path");
   HIPCHK(e, hipSetDevice(c.device));
@@ -1917,9 +1932,10 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   if (!e) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
   HIPCHK(e, hipSetDevice(e->dev));
-  if (wm <= e->cur_wm) {
+  if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
     hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
     HIPCHK(e, hipGetLastError());
+    if (wm > e->cur_wm) e->cur_wm = wm;
     return FW_OK;
   }
   e->phase_begin(FW_PHASE_FIRE);
