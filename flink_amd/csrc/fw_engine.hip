@@ -432,8 +432,8 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 //               table of segment starts.  Records that cannot be routed (per-element fires, a third
 //               slice in one batch, the Long.MIN_VALUE key) take the direct path after the scatter.
 //  k_aggregate  one workgroup per directory bucket: owns every pane of that bucket for this batch,
-//               gathers the bucket's segment from every tile (16-lane groups, 4 segments per wave
-//               instruction), resolves keys in an LDS copy of the bucket's directory slice, reduces with
+//               gathers the bucket's segment from every tile (the segments concatenated, one record
+//               per lane), resolves keys in an LDS copy of the bucket's directory slice, reduces with
 //               LDS atomics and folds each touched pane into the dense columns once.
 // No device-scope atomic per record: the routed form is bounded by HBM traffic, not the memory-side
 // atomic rate (tools/microbench/ingest_mb.hip: ~24 G random 8-B atomics/s chip-wide).
@@ -444,6 +444,9 @@ constexpr int RT_Q = 2;                 // slices per tile routed through LDS (m
 constexpr int RT_GS = 64;               // distinct routed slices per batch (k_aggregate rounds)
 constexpr int DC_RING = 16;             // direct-list counters, one per batch in flight
 constexpr int AG_THREADS = 1024;
+constexpr int AG_WIN = 8;              // k_aggregate: directory slots probed without a branch
+constexpr int AG_CHS = 1024;           // k_aggregate wave steps (64 records each) tabulated per chunk
+constexpr int AG_MAXPER = 17;          // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
 constexpr int RT_MAX_KB_BITS = 10;      // directory slots per bucket held in LDS by k_aggregate
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
@@ -477,12 +480,12 @@ __device__ __forceinline__ int32_t tile_slice(int64_t* lset, int64_t m) {
   return -1;
 }
 
-// exclusive scan of a[0..n) in place (n <= 8 * blockDim.x), contiguous chunks per thread
-template <int NT>
+// exclusive scan of a[0..n) in place (n <= MAXPER * blockDim.x), contiguous chunks per thread
+template <int NT, int MAXPER = 8>
 __device__ __forceinline__ void block_scan_excl(int32_t* a, int n, int32_t* wtot) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int per = (n + NT - 1) / NT;
-  int32_t loc[8];
+  int32_t loc[MAXPER];
   int32_t sum = 0;
   for (int i = 0; i < per; ++i) {
     const int x = threadIdx.x * per + i;
@@ -768,17 +771,30 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   int64_t* lmin = lsum + KA;                            // [KA] (AGG 15)
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KA : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KA : 0);
-  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest tile of the pane
+  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest record (tile << 12 | index)
   int32_t* sst = (int32_t*)(lfirst + KA);               // [ntiles] segment start within the tile
-  int32_t* sln = sst + r.ntiles;                        // [ntiles] segment length
+  int32_t* off = sst + r.ntiles;                        // [ntiles + 1] segment lengths, then their exclusive prefix
+  int32_t* step_tile = off + r.ntiles + 1;              // [AG_CHS] tile holding the first record of each step
+  int32_t* awtot = step_tile + AG_CHS;                  // [16] scan scratch
   const int64_t dbase = (int64_t)bkt * KB;
   const int64_t SB = (int64_t)8 << 16;
   FW_STAMP(r, SB, 0);
+  // issued together with the directory-slice load: this thread's tile header and the bucket's segment
+  // bounds in both bin groups of that tile (tiles beyond the first NT are read where they are used)
+  int64_t ph[RT_Q] = {FREE_TAG, FREE_TAG};
+  uint32_t pseg[RT_Q] = {0u, 0u};   // segment start | end << 16
+  if ((int)threadIdx.x < r.ntiles) {
+    const uint16_t* seg = r.seg + (int64_t)threadIdx.x * (nbq + 1);
+#pragma unroll
+    for (int q = 0; q < RT_Q; ++q) {
+      ph[q] = r.hdr[(int64_t)threadIdx.x * RT_Q + q];
+      pseg[q] = (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16);
+    }
+  }
   for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
   __syncthreads();
   FW_STAMP(r, SB, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int grp = lane >> 4, sub = lane & 15;
 
   // directory hash -> slot in this bucket.  Linear probing keeps a key within the run that starts at
   // its home slot, so the first four slots are compared without branching (the directory's load factor
@@ -791,13 +807,23 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     return true;
   };
   // one record into the bucket's LDS accumulators.  Straight-line on the common path: inactive lanes
-  // update a private dummy slot (KB + lane) instead of being masked off, and the rare miss of the four
-  // probed slots takes one wave-uniform branch to the out-of-line probe/insert
+  // update a private dummy slot (KB + lane) instead of being masked off, and a miss of the AG_WIN probed
+  // slots takes one wave-uniform branch to the out-of-line probe/insert.  The window covers the
+  // displacements linear probing produces at the directory's load factor <= 1/4 (a key 8 or more
+  // slots from home: ~6e-5 of them, so a wave takes the branch ~0.4 % of the time; at 4 slots it
+  // was ~18 %, which cost a third of the kernel)
   auto process = [&](bool act, uint64_t h, int64_t v, uint32_t oi) {
     const uint32_t h0 = (uint32_t)h & kbm;
-    const uint64_t a0 = lh[h0], a1 = lh[(h0 + 1) & kbm], a2 = lh[(h0 + 2) & kbm], a3 = lh[(h0 + 3) & kbm];
-    uint32_t kl = a0 == h ? h0 : a1 == h ? ((h0 + 1) & kbm) : a2 == h ? ((h0 + 2) & kbm) : ((h0 + 3) & kbm);
-    const bool miss = act && a0 != h && a1 != h && a2 != h && a3 != h;
+    uint32_t kl = h0;
+    bool found = false;
+#pragma unroll
+    for (int j = AG_WIN - 1; j >= 0; --j) {   // the nearest match wins
+      const uint32_t x = (h0 + j) & kbm;
+      const bool m = lh[x] == h;
+      kl = m ? x : kl;
+      found |= m;
+    }
+    const bool miss = act && !found;
     if (__any(miss)) {
       if (miss && !find_slow(h, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
     }
@@ -875,13 +901,13 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   }
 
   // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same set)
-  int64_t* gsl = (int64_t*)(sln + r.ntiles);            // [RT_GS]
+  int64_t* gsl = (int64_t*)(((uintptr_t)(awtot + 16) + 7) & ~(uintptr_t)7);   // [RT_GS]
   int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
   if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
   __syncthreads();
   for (int t = threadIdx.x; t < r.ntiles; t += NT) {
     for (int qq = 0; qq < RT_Q; ++qq) {
-      const int64_t m = r.hdr[(int64_t)t * RT_Q + qq];
+      const int64_t m = t == (int)threadIdx.x ? ph[qq] : r.hdr[(int64_t)t * RT_Q + qq];
       if (m == FREE_TAG) break;
       int g = 0;
       for (; g < RT_GS; ++g) {
@@ -915,60 +941,96 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       lfirst[x] = NO_FIRST;
     }
     for (int t = threadIdx.x; t < r.ntiles; t += NT) {
-      const int64_t h0 = r.hdr[(int64_t)t * RT_Q], h1 = r.hdr[(int64_t)t * RT_Q + 1];
-      const int ql = h0 == m ? 0 : (h1 == m ? 1 : -1);
       int32_t a0 = 0, a1 = 0;
-      if (ql >= 0) {
-        const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
-        const int bin = ql * s.nb + bkt;
-        a0 = seg[bin];
-        a1 = seg[bin + 1];
-      }
-      sst[t] = a0;
-      sln[t] = a1 - a0;
-    }
-    __syncthreads();
-    FW_STAMP(r, SB, 2 + 3 * min(q, 1));
-    // each 16-lane group reads one tile's segment, 2 records per lane per round; UR rounds of 4 segments
-    // per wave-step, every load issued before any dependent work
-    // lfirst tracks the earliest TILE holding the pane's records (tiles are contiguous ranges of the
-    // batch); the exact first arrival is resolved in the fold, for new panes only, from that tile's segment
-    constexpr int UR = 6;
-    for (int tb = wave * 4 * UR; tb < r.ntiles; tb += (NT / 64) * 4 * UR) {
-      longlong2 ra[UR], rb2[UR];
-      bool aa[UR], ab[UR];
-#pragma unroll
-      for (int u = 0; u < UR; ++u) {
-        const int tt = tb + u * 4 + grp;
-        const int t = min(tt, r.ntiles - 1);
-        const int32_t st = sst[t], ln = tt < r.ntiles ? sln[t] : 0;
-        aa[u] = sub < ln;
-        ab[u] = sub + 16 < ln;
-        const int64_t pa = (int64_t)t * RT_TILE + (aa[u] ? st + sub : 0);        // inactive lanes read the tile's first slot
-        const int64_t pb = (int64_t)t * RT_TILE + (ab[u] ? st + sub + 16 : 0);
-        ra[u] = r.kv[pa];
-        rb2[u] = r.kv[pb];
-      }
-#pragma unroll
-      for (int u = 0; u < UR; ++u) {
-        const uint32_t t = (uint32_t)min(tb + u * 4 + grp, r.ntiles - 1);
-        process(aa[u], (uint64_t)ra[u].x, ra[u].y, t);
-        process(ab[u], (uint64_t)rb2[u].x, rb2[u].y, t);
-      }
-#pragma unroll
-      for (int u = 0; u < UR; ++u) {   // segments longer than 32 records (hot keys, skew)
-        const int tt = tb + u * 4 + grp;
-        const int32_t ln = tt < r.ntiles ? sln[tt] : 0;
-        if (__any(ln > 32)) {
-          const int t = min(tt, r.ntiles - 1);
-          for (int j0 = 32; __any(j0 < ln); j0 += 16) {
-            const bool act = j0 + sub < ln;
-            const int64_t pp = (int64_t)t * RT_TILE + (act ? sst[t] + j0 + sub : 0);
-            const longlong2 rr = r.kv[pp];
-            process(act, (uint64_t)rr.x, rr.y, (uint32_t)t);
-          }
+      if (t == (int)threadIdx.x) {
+        const int ql = ph[0] == m ? 0 : (ph[1] == m ? 1 : -1);
+        if (ql >= 0) { a0 = (int32_t)(pseg[ql] & 0xFFFFu); a1 = (int32_t)(pseg[ql] >> 16); }
+      } else {
+        const int64_t h0 = r.hdr[(int64_t)t * RT_Q], h1 = r.hdr[(int64_t)t * RT_Q + 1];
+        const int ql = h0 == m ? 0 : (h1 == m ? 1 : -1);
+        if (ql >= 0) {
+          const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
+          const int bin = ql * s.nb + bkt;
+          a0 = seg[bin];
+          a1 = seg[bin + 1];
         }
       }
+      sst[t] = a0;
+      off[t] = a1 - a0;
+    }
+    if (threadIdx.x == 0) off[r.ntiles] = 0;
+    __syncthreads();
+    block_scan_excl<NT, AG_MAXPER>(off, r.ntiles + 1, awtot);   // off[ntiles] = the bucket's records of slice m
+    const int32_t R = off[r.ntiles];
+    FW_STAMP(r, SB, 2 + 3 * min(q, 1));
+    // dense assignment: the bucket's records of slice m, concatenated over the tiles in order (record
+    // rr lies in the tile t with off[t] <= rr < off[t + 1]), are taken 64 at a time, one per lane, in
+    // wave steps; the tile of each step's first record is tabulated per chunk of AG_CHS steps, a lane
+    // walks forward from it (a step spans ~4 segments at 256 buckets), and every load of a wave's UR
+    // steps is issued before any of them is processed.  lfirst keeps the pane's earliest record of the
+    // batch as (tile << 12 | index in the tile): tiles are consecutive ranges of the batch
+    constexpr int UR = 3;
+    for (int32_t cb = 0; cb < R; cb += AG_CHS * 64) {   // uniform
+      for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+        const int32_t o = off[t], l = off[t + 1] - o;
+        if (l == 0) continue;
+        const int32_t s_lo = max(0, (o - cb + 63) >> 6), s_hi = min(AG_CHS, (o + l - cb + 63) >> 6);
+        for (int32_t st = s_lo; st < s_hi; ++st) step_tile[st] = t;
+      }
+      __syncthreads();
+      const int32_t nsteps = min(AG_CHS, (R - cb + 63) >> 6);
+      // one group = UR steps of this wave: addresses from the step table, loads issued, nothing waited on
+      auto load_group = [&](int32_t s0, longlong2* rv, uint32_t* ri, bool* ra) {
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+          const int32_t st = s0 + u;
+          const int32_t rr = cb + 64 * st + lane;
+          ra[u] = st < nsteps && rr < R;
+          int32_t t = 0;
+          int64_t pos = 0;   // inactive lanes read tile 0's first slot
+          if (ra[u]) {
+            t = step_tile[st];
+            while (off[t + 1] <= rr) ++t;
+            pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
+          }
+          rv[u] = r.kv[pos];
+          ri[u] = ((uint32_t)t << 12) | (FIRST ? (uint32_t)r.idx[pos] : 0u);
+        }
+      };
+      // software pipelined: the next group's loads are in flight while this group updates LDS (two
+      // register sets, the loop unrolled by two so that both stay in registers)
+      longlong2 rvA[UR], rvB[UR];
+      uint32_t riA[UR], riB[UR];
+      bool raA[UR], raB[UR];
+      constexpr int32_t G = (NT / 64) * UR;
+      int32_t s0 = wave * UR;
+      if (s0 < nsteps) load_group(s0, rvA, riA, raA);
+      while (s0 < nsteps) {   // wave-uniform
+        if (s0 + G < nsteps) load_group(s0 + G, rvB, riB, raB);
+        if (r.dbg & 1) {   // diagnostics: loads only
+          int64_t x = 0;
+#pragma unroll
+          for (int u = 0; u < UR; ++u) x ^= rvA[u].x ^ rvA[u].y ^ riA[u];
+          if (x == 0x123456789) lsum[KB + lane] = x;
+        } else {
+#pragma unroll
+          for (int u = 0; u < UR; ++u) process(raA[u], (uint64_t)rvA[u].x, rvA[u].y, riA[u]);
+        }
+        s0 += G;
+        if (s0 >= nsteps) break;
+        if (s0 + G < nsteps) load_group(s0 + G, rvA, riA, raA);
+        if (r.dbg & 1) {   // diagnostics: loads only
+          int64_t x = 0;
+#pragma unroll
+          for (int u = 0; u < UR; ++u) x ^= rvB[u].x ^ rvB[u].y ^ riB[u];
+          if (x == 0x123456789) lsum[KB + lane] = x;
+        } else {
+#pragma unroll
+          for (int u = 0; u < UR; ++u) process(raB[u], (uint64_t)rvB[u].x, rvB[u].y, riB[u]);
+        }
+        s0 += G;
+      }
+      __syncthreads();   // the next chunk rewrites step_tile
     }
     __syncthreads();
     FW_STAMP(r, SB, 3 + 3 * min(q, 1));
@@ -986,20 +1048,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       if (AGG & FW_AGG_MAX) { const int64_t o = s.c.mx[idx]; if (lmax[x] > o) s.c.mx[idx] = lmax[x]; }
       if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[x]);
       if (FIRST) {
-        // first arrival: only a pane not seen before tile lf can change; its earliest record in tile lf
-        // is found by scanning that tile's segment of this bin (records carry their index in the tile)
-        if (ord_base + (int64_t)lf * RT_TILE < s.c.first[idx]) {
-          const uint64_t hx = lh[x];
-          const int64_t tb0 = (int64_t)lf * RT_TILE + sst[lf];
-          int32_t best = RT_TILE;
-          for (int32_t j = 0; j < sln[lf]; ++j) {
-            if ((uint64_t)r.kv[tb0 + j].x == hx) best = min(best, (int32_t)r.idx[tb0 + j]);
-          }
-          const int64_t bi = (int64_t)lf * RT_TILE + best;
-          if (best < RT_TILE && ord_base + bi < s.c.first[idx]) {
-            s.c.first[idx] = ord_base + bi;
-            s.c.f1v[idx] = f1col[bi];
-          }
+        // first arrival: the pane's earliest routed record of the batch
+        const int64_t bi = (int64_t)(lf >> 12) * RT_TILE + (lf & (RT_TILE - 1));
+        if (ord_base + bi < s.c.first[idx]) {
+          s.c.first[idx] = ord_base + bi;
+          s.c.f1v[idx] = f1col[bi];
         }
       } else {
         s.c.present[idx] = 1;
@@ -1750,7 +1803,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       }
       e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 8) + 4 * 16 + 8 * RT_Q;
       const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-      e->agg_lds = (size_t)KB * 8 + (size_t)(KB + 64) * (8 * (ncols - 1) + 4) + 8 * (size_t)e->max_tiles + 8 * RT_GS + 16;
+      e->agg_lds = (size_t)KB * 8 + (size_t)(KB + 64) * (8 * (ncols - 1) + 4) + 8 * (size_t)e->max_tiles + 4 +
+                   4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 16;
       const char* ml = getenv("FW_AGG_MIN_LDS_KB");
       e->agg_min_lds = (ml ? atoi(ml) : 81) * 1024;
       e->agg_lds = std::max<size_t>(e->agg_lds, (size_t)e->agg_min_lds);
