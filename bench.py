@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--ingest-mode", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=1 << 25, help="events in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="diagnostics: run the keyBy exchange (partition + RCCL all-to-all + MIN all-reduce) at N=1 too")
     ap.add_argument("--prof-steps", type=int, default=8,
                     help="steps after the timed region run with per-kernel device-time events (roofline); "
                          "timed events serialise kernels, so the timed region runs without them")
@@ -61,10 +63,15 @@ def dist_init(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.force_exchange:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -124,7 +131,7 @@ def main():
     reduce_fn = ReduceFunction(("sum",), "i64", keep_first_f1=True)
     windows_in_run = (total_steps * batch * world) // rate + 2
     cfg = make_config(TumblingEventTimeWindows.of(1000), reduce_fn, max_parallelism=mp, key_group_range=kg,
-                      device=local, key_capacity=key_cap, max_batch=batch * (2 if world > 1 else 1),
+                      device=local, key_capacity=key_cap, max_batch=batch * (2 if world > 1 or args.force_exchange else 1),
                       out_capacity=int(min(windows_in_run * key_cap // max(world, 1) * 2 + 4096, 1 << 27)),
                       ingest_mode=args.ingest_mode)
     eng = WindowEngine(cfg)
@@ -140,7 +147,7 @@ def main():
     torch.cuda.synchronize()
 
     exch = None
-    if world > 1:
+    if world > 1 or args.force_exchange:
         from flink_amd.keyby import KeyByExchange
         exch = KeyByExchange(eng, world, rank, mp, batch, dev)
 
@@ -257,7 +264,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if world > 1 or args.force_exchange:
         import torch.distributed as dist
         dist.destroy_process_group()
 

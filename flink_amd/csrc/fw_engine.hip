@@ -93,7 +93,6 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int32_t P;
   int64_t stride;   // D + 1
   int64_t* slice_tag;
-  int32_t* touched;
   Cols c;
   OutLog o;
   int32_t* err;
@@ -278,7 +277,9 @@ __device__ __forceinline__ int32_t record_key_group(const Spec& s, int32_t key_h
 // ingest, direct form: every (record, slice) update is a device-scope atomic on the dense columns.
 // ------------------------------------------------------------------------------------------------
 template <int VT, int AGG, bool FIRST>
-__device__ __forceinline__ void pane_update(const Spec& s, int64_t idx, int64_t vbits, int64_t ord) {
+// returns true for exactly one record of a pane absent before the launch (FIRST: the min-ordinal
+// atomic that found the pane empty)
+__device__ __forceinline__ bool pane_update(const Spec& s, int64_t idx, int64_t vbits, int64_t ord) {
   if (AGG & FW_AGG_SUM) {
     if (VT == FW_VALUE_I64) {
       atomicAdd((unsigned long long*)&s.c.sum[idx], (unsigned long long)vbits);
@@ -300,10 +301,11 @@ __device__ __forceinline__ void pane_update(const Spec& s, int64_t idx, int64_t 
     // first arrival = min ordinal; values only decrease within a kernel, so a stale load that is
     // already below our ordinal proves we are not first
     int64_t cur = s.c.first[idx];
-    if (ord < cur) atomicMin((long long*)&s.c.first[idx], (long long)ord);
+    if (ord < cur) return atomicMin((long long*)&s.c.first[idx], (long long)ord) == INT64_MAX;
   } else {
     if (s.c.present[idx] == 0) s.c.present[idx] = 1;
   }
+  return false;
 }
 
 struct BatchIn {
@@ -319,6 +321,10 @@ struct BatchIn {
   unsigned long long* late_count;
   int64_t late_capacity;
   int32_t idx_bits;
+  // direct form with first arrival: panes created by the batch, for the f1 fix-up
+  int64_t* new_list;
+  unsigned long long* new_count;
+  int64_t new_capacity;
 };
 
 template <int VT, int AGG, bool FIRST>
@@ -395,25 +401,34 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
         live = false;
       }
     }
+    bool fresh = false;
+    int64_t idx = 0;
     if (live) {
-      int64_t idx = (int64_t)p * s.stride + kid;
-      pane_update<VT, AGG, FIRST>(s, idx, v, b.ord_base + i);
-      if (s.touched[p] == 0) s.touched[p] = 1;
+      idx = (int64_t)p * s.stride + kid;
+      fresh = pane_update<VT, AGG, FIRST>(s, idx, v, b.ord_base + i);
+    }
+    if (FIRST) {   // list the panes this batch created: their f1 is taken from the batch after the launch
+      const unsigned long long pos = wave_append(b.new_count, fresh);
+      if (fresh) {
+        if ((int64_t)pos < b.new_capacity) b.new_list[pos] = idx;
+        else set_error(s.err, FW_ERR_CAPACITY);
+      }
     }
   }
 }
 
-// after ingest: record f1 of panes whose first arrival lies in this batch
-__global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* f1col, int64_t ord_base, int64_t n) {
-  for (int32_t p = 0; p < s.P; ++p) {
-    if (s.touched[p] == 0) continue;
-    const int64_t base = (int64_t)p * s.stride;
-    for (int64_t kid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; kid < s.stride;
-         kid += (int64_t)gridDim.x * blockDim.x) {
-      int64_t ord = s.c.first[base + kid];
-      if (ord >= ord_base && ord < ord_base + n) s.c.f1v[base + kid] = f1col[ord - ord_base];
-    }
+// after the direct ingest: f1 of the panes the batch created (listed by k_ingest_direct), from the
+// batch's column; clears the other batch parity's list counter (used next by the following batch)
+__global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* list, const unsigned long long* count,
+                                                       unsigned long long* count_next, const int64_t* f1col,
+                                                       int64_t ord_base, int64_t n, int64_t cap) {
+  const int64_t nl = min((int64_t)*count, cap);
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nl; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t idx = list[j];
+    const int64_t o = s.c.first[idx] - ord_base;
+    if (o >= 0 && o < n) s.c.f1v[idx] = f1col[o];
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *count_next = 0;
 }
 
 // a wave-uniform 64-bit value moved to scalar registers
@@ -1395,20 +1410,46 @@ __global__ __launch_bounds__(BLOCK) void k_part_count(const int64_t* key, const 
   for (int d = threadIdx.x; d < par; d += blockDim.x) block_counts[(int64_t)blockIdx.x * par + d] = cnt[d];
 }
 
-// single block: exclusive scan over (dest, block) -> per-block write offsets; totals
-__global__ void k_part_scan(int64_t* block_counts, int64_t nblocks, int32_t par, int64_t* counts, int64_t* offsets) {
-  if (threadIdx.x != 0) return;
-  int64_t run = 0;
+// one workgroup: per destination d (in order), an exclusive scan of the blocks' counts (column d of
+// [nblocks][par]) into per-block write offsets, after the totals of destinations 0..d-1; totals and
+// destination offsets out
+constexpr int PART_SCAN_THREADS = 1024;
+__global__ __launch_bounds__(PART_SCAN_THREADS) void k_part_scan(int64_t* block_counts, int64_t nblocks, int32_t par,
+                                                                  int64_t* counts, int64_t* offsets) {
+  __shared__ int64_t wtot[PART_SCAN_THREADS / 64];
+  __shared__ int64_t base;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t per = (nblocks + PART_SCAN_THREADS - 1) / PART_SCAN_THREADS;
+  const int64_t b0 = (int64_t)threadIdx.x * per, b1 = min(b0 + per, nblocks);
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
   for (int32_t d = 0; d < par; ++d) {
-    offsets[d] = run;
-    int64_t tot = 0;
-    for (int64_t b = 0; b < nblocks; ++b) {
-      int64_t c = block_counts[b * par + d];
+    int64_t sum = 0;
+    for (int64_t b = b0; b < b1; ++b) sum += block_counts[b * par + d];
+    int64_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int64_t run = base + incl - sum, total = 0;
+    for (int w = 0; w < PART_SCAN_THREADS / 64; ++w) {
+      run += w < wave ? wtot[w] : 0;
+      total += wtot[w];
+    }
+    for (int64_t b = b0; b < b1; ++b) {
+      const int64_t c = block_counts[b * par + d];
       block_counts[b * par + d] = run;
       run += c;
-      tot += c;
     }
-    counts[d] = tot;
+    __syncthreads();   // every thread has read base and wtot
+    if (threadIdx.x == 0) {
+      counts[d] = total;
+      offsets[d] = base;
+      base += total;
+    }
+    __syncthreads();
   }
 }
 
@@ -1541,6 +1582,8 @@ struct fw_engine {
   size_t route_lds = 0, agg_lds = 0;
   int agg_min_lds = 81 * 1024;
   // partition scratch
+  int64_t* new_list = nullptr;                // direct form with first arrival: panes created per batch
+  unsigned long long* new_counts = nullptr;   // one list length per batch parity
   int64_t* part_block_counts = nullptr;
   int64_t part_blocks_cap = 0;
   // host output copies
@@ -1737,7 +1780,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.dir_keys = e->alloc<int64_t>((size_t)s.D);
   s.dir_min_used = e->alloc<int32_t>(1);
   s.slice_tag = e->alloc<int64_t>((size_t)P);
-  s.touched = e->alloc<int32_t>((size_t)P);
   const size_t cells = (size_t)P * (size_t)s.stride;
   s.c.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>(cells) : nullptr;
   s.c.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(cells) : nullptr;
@@ -1812,6 +1854,10 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     }
   }
   e->wm_done = e->alloc<unsigned int>(1);
+  if (s.first && !e->routed) {
+    e->new_list = e->alloc<int64_t>((size_t)c.max_batch);
+    e->new_counts = e->alloc<unsigned long long>(2);
+  }
 
   for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
 
@@ -1852,7 +1898,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   launch_fill(e, s.c.first, INT64_MAX, (int64_t)cells);
   if (s.c.present) HIPCHK(e, hipMemsetAsync(s.c.present, 0, cells, e->stream));
   HIPCHK(e, hipMemsetAsync(s.dir_min_used, 0, 4, e->stream));
-  HIPCHK(e, hipMemsetAsync(s.touched, 0, 4 * (size_t)P, e->stream));
   HIPCHK(e, hipMemsetAsync(o.count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(o.mark_count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(s.err, 0, 4, e->stream));
@@ -1862,6 +1907,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->routed) {
     HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 8 * DC_RING, e->stream));
   }
+  if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
   *out = e;
@@ -1932,6 +1978,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.late_count = e->late_count;
   b.late_capacity = e->late_key ? e->cfg.max_batch : 0;
   b.idx_bits = e->idx_bits;
+  b.new_list = e->new_list;
+  b.new_count = e->new_counts ? e->new_counts + par : nullptr;
+  b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
   if (e->routed) {
     FW_DISPATCH(launch_routed_t, e, b, df1, par);
   } else {
@@ -1943,11 +1992,11 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   HIPCHK(e, hipGetLastError());
   if (e->s.first && !e->routed) {   // the partitioned form sets f1 in k_aggregate
     e->phase_begin(FW_PHASE_FIXUP);
-    hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
-                       e->stream, e->s, df1, e->ordinal, n);
-    e->phase_end(e->s.stride);
+    hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
+                       e->stream, e->s, e->new_list, e->new_counts + par, e->new_counts + (par ^ 1), df1, e->ordinal, n,
+                       e->cfg.max_batch);
+    e->phase_end(n);
   }
-  if (!e->routed) HIPCHK(e, hipMemsetAsync(e->s.touched, 0, 4 * (size_t)e->s.P, e->stream));
   if (e->cfg.allowed_lateness > 0) {
     // per-element fires: need the count on the host to size the sort
     unsigned long long nl = 0;
@@ -2153,14 +2202,13 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
     if (!e->part_block_counts) return fail(e, FW_ERR_DEVICE, "alloc");
     e->part_blocks_cap = nblocks * parallelism;
   }
-  if (e->client) {   // the batch is produced on the caller's stream
-    HIPCHK(e, hipEventRecord(e->ev_in, (hipStream_t)e->client));
-    HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_in, 0));
-  }
-  hipLaunchKernelGGL(k_part_count, dim3((unsigned)nblocks), dim3(BLOCK), 0, e->stream, key, key_hash, n, max_parallelism,
+  // with a caller stream set (fw_set_stream) the partition runs on it, ordered after the producer of the
+  // batch and before whatever consumes the packed output there (the exchange); otherwise on the engine's
+  hipStream_t ps = e->client ? (hipStream_t)e->client : e->stream;
+  hipLaunchKernelGGL(k_part_count, dim3((unsigned)nblocks), dim3(BLOCK), 0, ps, key, key_hash, n, max_parallelism,
                      parallelism, e->part_block_counts);
-  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, e->stream, e->part_block_counts, nblocks, parallelism, counts, offsets);
-  hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblocks), dim3(BLOCK), 0, e->stream, key, key_hash, f1, ts,
+  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PART_SCAN_THREADS), 0, ps, e->part_block_counts, nblocks, parallelism, counts, offsets);
+  hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblocks), dim3(BLOCK), 0, ps, key, key_hash, f1, ts,
                      (const int64_t*)value, n, max_parallelism, parallelism, e->part_block_counts, out_key, out_key_hash,
                      out_f1, out_ts, (int64_t*)out_value);
   HIPCHK(e, hipGetLastError());

@@ -29,10 +29,12 @@ class KeyByExchange:
         self.cuda = self.device.type == "cuda"
         if self.cuda:
             z = lambda dt=torch.int64: torch.empty(batch, dtype=dt, device=self.device)
-            self.s_key, self.s_ts, self.s_val, self.s_f1 = z(), z(), z(), z()
-            self.s_hash = z(torch.int32)
+            self.s_key, self.s_ts, self.s_val = z(), z(), z()
             self.counts = torch.zeros(world, dtype=torch.int64, device=self.device)
             self.offsets = torch.zeros(world, dtype=torch.int64, device=self.device)
+            self.recv_counts = torch.zeros(world, dtype=torch.int64, device=self.device)
+            # the engine enqueues its partition on torch's stream, so the exchange below is ordered after it
+            self.eng.use_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _route_cuda(self, k, t, v):
         n = k.numel()
@@ -42,7 +44,6 @@ class KeyByExchange:
                                                    P(self.counts), P(self.offsets))
         if rc != 0:
             raise RuntimeError(f"fw_partition_by_operator failed: {rc}")
-        self.eng.sync()                       # partition runs on the engine's stream
         return self.s_key[:n], self.s_ts[:n], self.s_val[:n], self.counts
 
     def _route_host(self, k, t, v):
@@ -55,14 +56,23 @@ class KeyByExchange:
     def exchange(self, k, t, v):
         """Route a source batch to the key-group owners; returns this rank's received (key, ts, value)."""
         sk, st, sv, counts = self._route_cuda(k, t, v) if self.cuda else self._route_host(k, t, v)
-        recv_counts = torch.empty_like(counts)
+        recv_counts = self.recv_counts if self.cuda else torch.empty_like(counts)
         dist.all_to_all_single(recv_counts, counts)
-        send_splits = counts.tolist()
-        recv_splits = recv_counts.tolist()
-        packed = torch.stack([sk, st, sv.view(torch.int64)], dim=1)
-        out = torch.empty((sum(recv_splits), 3), dtype=torch.int64, device=packed.device)
-        dist.all_to_all_single(out, packed, recv_splits, send_splits)
-        return out[:, 0].contiguous(), out[:, 1].contiguous(), out[:, 2].contiguous().view(v.dtype)
+        splits = torch.stack([counts, recv_counts]).tolist()   # the one host synchronisation of the exchange
+        send_splits, recv_splits = splits
+        m = sum(recv_splits)
+        if not self.cuda:
+            packed = torch.stack([sk, st, sv.view(torch.int64)], dim=1)
+            out = torch.empty((m, 3), dtype=torch.int64)
+            dist.all_to_all_single(out, packed, recv_splits, send_splits)
+            return out[:, 0].contiguous(), out[:, 1].contiguous(), out[:, 2].contiguous().view(v.dtype)
+        # one all-to-all per column straight into fresh engine input columns (no packing or unpacking copy);
+        # fresh because the engine reads pushed columns asynchronously and keeps them referenced until its
+        # next sync / collect (WindowEngine._inflight), so a column is never overwritten while in use
+        rk, rt, rv = (torch.empty(m, dtype=torch.int64, device=self.device) for _ in range(3))
+        for dst, src in ((rk, sk), (rt, st), (rv, sv.view(torch.int64))):
+            dist.all_to_all_single(dst, src, recv_splits, send_splits)
+        return rk, rt, rv.view(v.dtype)
 
     def align_watermark(self, wm_local):
         """Min over all input channels (StreamInputProcessor.java:147-161)."""

@@ -152,7 +152,7 @@ int         fw_get_stats(fw_engine* e, fw_stats* st);
 const char* fw_last_error(const fw_engine* e);
 void        fw_destroy(fw_engine* e);
 
-/* Key-group routing for the multi-GPU keyBy exchange
+/* Key-group routing for the multi-GPU keyBy exchange (enqueued on the caller stream when fw_set_stream set one)
  * (KeyGroupStreamPartitioner.selectChannels, SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65;
  *  KeyGroupRangeAssignment.assignKeyToParallelOperator, KeyGroupRangeAssignment.java:40-42,105-107).
  * Counting-sorts n records by destination operator index into out_* (device pointers) and writes
