@@ -1405,7 +1405,24 @@ __global__ __launch_bounds__(BLOCK) void k_part_count(const int64_t* key, const 
   for (int d = threadIdx.x; d < par; d += blockDim.x) cnt[d] = 0;
   __syncthreads();
   int64_t lo = (int64_t)blockIdx.x * PART_CHUNK, hi = lo + PART_CHUNK < n ? lo + PART_CHUNK : n;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd((unsigned long long*)&cnt[route(key, kh, i, mp, par)], 1ull);
+  // per-thread private counts of its records' destinations (few destinations: a thread's records are
+  // counted in registers when par <= 8, then one LDS atomic per thread and destination)
+  if (par <= 8) {
+    int32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const int32_t d = route(key, kh, i, mp, par);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) c[q] += d == q ? 1 : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      int32_t x = c[q];
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);   // wave total
+      if ((threadIdx.x & 63) == 0 && x != 0) atomicAdd((unsigned long long*)&cnt[q], (unsigned long long)x);
+    }
+  } else {
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd((unsigned long long*)&cnt[route(key, kh, i, mp, par)], 1ull);
+  }
   __syncthreads();
   for (int d = threadIdx.x; d < par; d += blockDim.x) block_counts[(int64_t)blockIdx.x * par + d] = cnt[d];
 }
@@ -1519,15 +1536,19 @@ struct fw_engine {
   int32_t sticky = FW_OK;
   hipStream_t stream = nullptr;       // engine stream: aggregation, watermarks, late path, output
   hipStream_t rstream = nullptr;      // route stream: k_route of batch j+1 overlaps k_aggregate/k_watermark of j
-  void* client = nullptr;             // producer/consumer stream of the caller (fw_set_stream), or null
+  void* client = nullptr;             // producer/consumer stream of the caller (fw_set_stream)
+  bool has_client = false;            // set by fw_set_stream; the handle itself may be 0 (the null stream)
   bool serial = false;                // diagnostics (FW_SERIAL=1): k_route on the engine stream too
   hipEvent_t ev_in = nullptr;         // client work up to a push (input columns ready)
+  static constexpr int NCONS = 8;
+  hipEvent_t ev_consumed[NCONS] = {};  // per push (ring): every read of that push's input columns done
   hipEvent_t ev_route[2] = {nullptr, nullptr};   // k_route of the batch with that parity done
   hipEvent_t ev_agg[2] = {nullptr, nullptr};     // k_aggregate of the batch with that parity done
   Spec s{};
   int64_t cur_wm = INT64_MIN;
   int64_t ordinal = 0;
   int64_t records_in = 0;
+  int64_t pushes = 0;                 // non-empty pushes (ev_consumed ring position)
   int grid = 0;
   std::vector<void*> allocs;
   // staging for host-memory (and misaligned device) pushes, one set per batch parity
@@ -1604,6 +1625,7 @@ struct fw_engine {
     if (rstream) (void)hipStreamDestroy(rstream);
     if (stream) (void)hipStreamDestroy(stream);
     for (hipEvent_t ev : {ev_in, ev_route[0], ev_route[1], ev_agg[0], ev_agg[1]}) if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : ev_consumed) if (ev) (void)hipEventDestroy(ev);
     for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
@@ -1730,6 +1752,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking));
   e->serial = getenv("FW_SERIAL") && atoi(getenv("FW_SERIAL")) != 0;
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
+  for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (int q = 0; q < 2; ++q) {
     HIPCHK(e, hipEventCreateWithFlags(&e->ev_route[q], hipEventDisableTiming));
     HIPCHK(e, hipEventCreateWithFlags(&e->ev_agg[q], hipEventDisableTiming));
@@ -1947,7 +1970,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   const int par = (int)(e->batches & 1);
   hipStream_t in_stream = e->routed && !e->serial ? e->rstream : e->stream;
   if (e->routed) HIPCHK(e, hipStreamWaitEvent(in_stream, e->ev_agg[par], 0));
-  if (e->client) {   // input columns are produced on the caller's stream
+  if (e->has_client) {   // input columns are produced on the caller's stream
     HIPCHK(e, hipEventRecord(e->ev_in, (hipStream_t)e->client));
     HIPCHK(e, hipStreamWaitEvent(in_stream, e->ev_in, 0));
   }
@@ -2026,8 +2049,19 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     }
   }
   HIPCHK(e, hipGetLastError());
+  // every reader of this push's columns (k_route, k_aggregate's direct records, the f1 fix-up, the late
+  // path) is ordered before this point of the engine stream
+  HIPCHK(e, hipEventRecord(e->ev_consumed[(e->pushes++) % fw_engine::NCONS], e->stream));
   e->ordinal += n;
   e->records_in += n;
+  return FW_OK;
+}
+
+int fw_stream_wait_input(fw_engine* e, void* stream, int32_t back) {
+  if (!e || back < 0 || back >= fw_engine::NCONS) return FW_ERR_INVALID_ARG;
+  if (back >= e->pushes) return FW_OK;   // no such push
+  HIPCHK(e, hipSetDevice(e->dev));
+  HIPCHK(e, hipStreamWaitEvent((hipStream_t)stream, e->ev_consumed[(e->pushes - 1 - back) % fw_engine::NCONS], 0));
   return FW_OK;
 }
 
@@ -2153,6 +2187,7 @@ int fw_set_stream(fw_engine* e, void* stream) {
   HIPCHK(e, hipStreamSynchronize(e->rstream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   e->client = stream;
+  e->has_client = true;
   return FW_OK;
 }
 
@@ -2204,7 +2239,7 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
   }
   // with a caller stream set (fw_set_stream) the partition runs on it, ordered after the producer of the
   // batch and before whatever consumes the packed output there (the exchange); otherwise on the engine's
-  hipStream_t ps = e->client ? (hipStream_t)e->client : e->stream;
+  hipStream_t ps = e->has_client ? (hipStream_t)e->client : e->stream;
   hipLaunchKernelGGL(k_part_count, dim3((unsigned)nblocks), dim3(BLOCK), 0, ps, key, key_hash, n, max_parallelism,
                      parallelism, e->part_block_counts);
   hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PART_SCAN_THREADS), 0, ps, e->part_block_counts, nblocks, parallelism, counts, offsets);

@@ -33,6 +33,11 @@ class KeyByExchange:
             self.counts = torch.zeros(world, dtype=torch.int64, device=self.device)
             self.offsets = torch.zeros(world, dtype=torch.int64, device=self.device)
             self.recv_counts = torch.zeros(world, dtype=torch.int64, device=self.device)
+            self.RING = 3
+            self.ring = [None] * self.RING
+            self.pushed_at = [None] * self.RING   # engine push index that last read each set
+            self.steps = self.pushes = 0
+            self.pending_slot = None
             # the engine enqueues its partition on torch's stream, so the exchange below is ordered after it
             self.eng.use_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -66,10 +71,23 @@ class KeyByExchange:
             out = torch.empty((m, 3), dtype=torch.int64)
             dist.all_to_all_single(out, packed, recv_splits, send_splits)
             return out[:, 0].contiguous(), out[:, 1].contiguous(), out[:, 2].contiguous().view(v.dtype)
-        # one all-to-all per column straight into fresh engine input columns (no packing or unpacking copy);
-        # fresh because the engine reads pushed columns asynchronously and keeps them referenced until its
-        # next sync / collect (WindowEngine._inflight), so a column is never overwritten while in use
-        rk, rt, rv = (torch.empty(m, dtype=torch.int64, device=self.device) for _ in range(3))
+        # one all-to-all per column straight into the engine's input columns (no packing or unpacking
+        # copy), from a ring of RING column sets: before a set is rewritten, torch's stream waits on the
+        # device for the engine to have read it (fw_stream_wait_input), no host synchronisation
+        slot = self.steps % self.RING
+        cols = self.ring[slot]
+        if cols is None or cols[0].numel() < m:
+            if cols is not None:
+                self.eng.sync()   # growing: the old set is dropped only once nothing reads it
+            cap = max(m, int(1.25 * k.numel()))
+            cols = self.ring[slot] = [torch.empty(cap, dtype=torch.int64, device=self.device) for _ in range(3)]
+        elif self.pushed_at[slot] is not None:
+            back = self.pushes - 1 - self.pushed_at[slot]
+            if back < 8:
+                self.eng.wait_input(torch.cuda.current_stream(self.device).cuda_stream, back)
+        self.steps += 1
+        self.pending_slot = slot
+        rk, rt, rv = (x[:m] for x in cols)
         for dst, src in ((rk, sk), (rt, st), (rv, sv.view(torch.int64))):
             dist.all_to_all_single(dst, src, recv_splits, send_splits)
         return rk, rt, rv.view(v.dtype)
@@ -83,5 +101,8 @@ class KeyByExchange:
     def step(self, k, t, v, wm_local):
         rk, rt, rv = self.exchange(k, t, v)
         if rk.numel():
-            self.eng.push(rk, rt, rv)
+            self.eng.push(rk, rt, rv, keep_alive=False)   # the ring keeps the columns (see exchange)
+            if self.cuda:
+                self.pushed_at[self.pending_slot] = self.pushes
+                self.pushes += 1
         self.eng.advance_watermark(self.align_watermark(wm_local))

@@ -186,7 +186,12 @@ class WindowEngine:
             self._check(self._fn("set_stream")(self.h, ctypes.c_void_p(stream_handle)))
             self._stream = stream_handle
 
-    def push(self, key, ts, value, key_hash=None, f1=None):
+    def wait_input(self, stream_handle, back):
+        """Make an external HIP stream wait (on the device) until the engine has read the columns of the push
+        made `back` non-empty pushes ago (fw_stream_wait_input)."""
+        self._check(self._fn("stream_wait_input")(self.h, ctypes.c_void_p(stream_handle), back))
+
+    def push(self, key, ts, value, key_hash=None, f1=None, keep_alive=True):
         n = len(key)
         if self.prefix == "fw":
             mem = _abi.FW_MEM_DEVICE if _is_device(key) else _abi.FW_MEM_HOST
@@ -198,7 +203,8 @@ class WindowEngine:
                 cur = torch.cuda.current_stream(key.device).cuda_stream
                 if getattr(self, "_stream", None) != cur:
                     self.use_stream(cur)
-                self._inflight.append((key, ts, value, key_hash, f1))
+                if keep_alive:
+                    self._inflight.append((key, ts, value, key_hash, f1))
             self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n, mem))
         else:
             self._check(self._fn("push_batch")(self.h, _ptr(key), _ptr(key_hash), _ptr(f1), _ptr(ts), _ptr(value), n))

@@ -180,9 +180,14 @@ typedef struct {
 int         fw_set_profiling(fw_engine* e, int32_t enable);
 int         fw_get_profile(fw_engine* e, fw_profile* out);   /* synchronises; resets the counters */
 
-/* Order all engine work on the caller's HIP stream (hipStream_t), e.g. the stream that produced
- * device-resident input columns, instead of the engine's own stream.  Synchronises first. */
+/* Make the caller's HIP stream (hipStream_t; 0 = the null stream) the producer of device-resident input
+ * columns: every push waits for the work enqueued on it so far, and fw_partition_by_operator runs on it.
+ * Synchronises first. */
 int         fw_set_stream(fw_engine* e, void* stream);
+/* Make `stream` wait (device-side, no host synchronisation) until the engine has finished reading the
+ * input columns of the non-empty push made `back` pushes ago (0 = the latest, at most 7), so that a caller
+ * recycling column buffers never overwrites one the engine still reads. */
+int         fw_stream_wait_input(fw_engine* e, void* stream, int32_t back);
 
 /* diagnostics: raw device counters (8 x int64) */
 int         fw_debug_counters(fw_engine* e, int64_t* out8);
