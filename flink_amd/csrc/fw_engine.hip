@@ -776,7 +776,12 @@ template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, RouteBuf r, const int64_t* f1col) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = AG_THREADS;
-  const int bkt = blockIdx.x;
+  // XCD-aware bucket order: workgroups are dealt to the 8 XCDs round-robin, so XCD x runs the
+  // contiguous bucket range [x * nb/8, (x + 1) * nb/8).  Neighbouring buckets' segments share the
+  // 128-B lines at their boundaries (records and first-arrival indices alike); with both readers on one
+  // XCD the second read hits that XCD's L2 instead of going back to HBM
+  const int bkt = (s.nb % 8 == 0 && !(r.dbg & 32)) ? (int)(blockIdx.x % 8) * (s.nb / 8) + (int)(blockIdx.x / 8)
+                                                    : (int)blockIdx.x;
   const int nbq = RT_Q * s.nb;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
@@ -805,6 +810,20 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       ph[q] = r.hdr[(int64_t)threadIdx.x * RT_Q + q];
       pseg[q] = (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16);
     }
+  }
+  // also in flight with the directory slice: the direct-list length and the slot claim of tile 0's first
+  // routed slice (nearly always the batch's only one; slice_slot is idempotent, so claiming it before
+  // the round that uses it changes nothing).  The accumulators are cleared meanwhile; each fold resets
+  // the entries it consumed for the next round
+  const int64_t nd = min((int64_t)*r.dcount, r.dcap);
+  int32_t pre_p = -1;
+  if (threadIdx.x == 0 && r.ntiles > 0 && ph[0] != FREE_TAG) pre_p = slice_slot(s, ph[0]);
+  for (int x = threadIdx.x; x < KA; x += NT) {
+    lsum[x] = 0;
+    if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
+    if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
+    if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
+    lfirst[x] = NO_FIRST;
   }
   for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
   __syncthreads();
@@ -860,7 +879,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   // no memset between batches: batch j's counter was zeroed by k_aggregate of batch j - DC_RING/2, whose
   // counter is no longer read and whose successor k_route starts only after this kernel (event order)
   if (blockIdx.x == 0 && threadIdx.x == 0) *r.dcount_reset = 0;
-  const int64_t nd = min((int64_t)*r.dcount, r.dcap);
   if (nd > 0) {
     for (int64_t x0 = 0; x0 < nd; x0 += NT) {
       const int64_t x = x0 + threadIdx.x;
@@ -920,20 +938,33 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
   if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
   __syncthreads();
-  for (int t = threadIdx.x; t < r.ntiles; t += NT) {
-    for (int qq = 0; qq < RT_Q; ++qq) {
-      const int64_t m = t == (int)threadIdx.x ? ph[qq] : r.hdr[(int64_t)t * RT_Q + qq];
-      if (m == FREE_TAG) break;
-      int g = 0;
-      for (; g < RT_GS; ++g) {
-        const int64_t cur = gsl[g];
-        if (cur == m) break;
-        if (cur == FREE_TAG) {
-          const unsigned long long prev = atomicCAS((unsigned long long*)&gsl[g], (unsigned long long)FREE_TAG, (unsigned long long)m);
-          if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) break;
-        }
+  auto gsl_insert = [&](int64_t m) {
+    int g = 0;
+    for (; g < RT_GS; ++g) {
+      const int64_t cur = gsl[g];
+      if (cur == m) break;
+      if (cur == FREE_TAG) {
+        const unsigned long long prev = atomicCAS((unsigned long long*)&gsl[g], (unsigned long long)FREE_TAG, (unsigned long long)m);
+        if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) break;
       }
-      if (g == RT_GS) set_error(s.err, FW_ERR_CAPACITY);   // more distinct slices in one batch than RT_GS
+    }
+    if (g == RT_GS) set_error(s.err, FW_ERR_CAPACITY);   // more distinct slices in one batch than RT_GS
+  };
+  // the first NT tiles from registers (ph = FREE_TAG beyond ntiles): a lane whose slice equals its left
+  // neighbour's leaves the insert to it, so a wave of an in-order stream inserts once, not 64 times
+  // (same-address LDS atomics serialise)
+#pragma unroll
+  for (int qq = 0; qq < RT_Q; ++qq) {
+    const int64_t m = ph[qq];
+    const int64_t left = __shfl_up(m, 1);
+    const bool dup = (threadIdx.x & 63) != 0 && left == m;
+    if (m != FREE_TAG && !dup) gsl_insert(m);
+  }
+  for (int t = NT + threadIdx.x; t < r.ntiles; t += NT) {
+    for (int qq = 0; qq < RT_Q; ++qq) {
+      const int64_t m = r.hdr[(int64_t)t * RT_Q + qq];
+      if (m == FREE_TAG) break;
+      gsl_insert(m);
     }
   }
   __syncthreads();
@@ -943,18 +974,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     // pane-slot claim: authoritative here, after every earlier watermark (engine stream order); slot
     // p = floor_mod(m, P) is claimed by whichever workgroup comes first, the rest find it taken by m
     __syncthreads();   // every thread has read the previous round's lclaim
-    if (threadIdx.x == 0) lclaim = slice_slot(s, m);
+    if (threadIdx.x == 0) lclaim = (pre_p >= 0 && m == ph[0]) ? pre_p : slice_slot(s, m);
     __syncthreads();
     const int32_t p = lclaim;
     if (p < 0) { if (threadIdx.x == 0) set_error(s.err, FW_ERR_CAPACITY); continue; }   // slice pool exhausted
     const int q = g;
-    for (int x = threadIdx.x; x < KA; x += NT) {
-      lsum[x] = 0;
-      if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
-      if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
-      if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
-      lfirst[x] = NO_FIRST;
-    }
     for (int t = threadIdx.x; t < r.ntiles; t += NT) {
       int32_t a0 = 0, a1 = 0;
       if (t == (int)threadIdx.x) {
@@ -1072,6 +1096,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       } else {
         s.c.present[idx] = 1;
       }
+      // cleared for the next round (untouched entries still are; the per-lane dummies are never read)
+      lsum[x] = 0;
+      if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
+      if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
+      if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
+      lfirst[x] = NO_FIRST;
     }
     __syncthreads();
     FW_STAMP(r, SB, 4 + 3 * min(q, 1));
