@@ -35,7 +35,8 @@ FW_MEM_DEVICE = 1
 EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sync", "fw_collect",
                     "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
                     "fw_get_profile", "fw_debug_counters", "fw_debug_stamps", "fw_set_stream", "fw_stream_wait_input",
-                    "fw_version")
+                    "fw_version", "fw_snapshot_kg", "fw_restore_kg")
+FW_SNAP_MAGIC, FW_SNAP_HEADER_WORDS, FW_SNAP_ENTRY_WORDS = 0x31474b5746574b, 12, 8
 FW_PHASE_INGEST, FW_PHASE_FIXUP, FW_PHASE_LATE, FW_PHASE_FIRE, FW_PHASE_AGGREGATE, FW_NPHASES = 0, 1, 2, 3, 4, 5
 
 _i32, _i64, _p = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
@@ -85,6 +86,8 @@ def declare(lib, prefix="fw"):
         "debug_counters": (_i32, [_p, _p]),
         "set_stream": (_i32, [_p, _p]),
         "stream_wait_input": (_i32, [_p, _p, _i32]),
+        "snapshot_kg": (_i32, [_p, _i32, _p, _i64, P(_i64)]),
+        "restore_kg": (_i32, [_p, _i32, _p, _i64]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}", None)

@@ -1418,6 +1418,27 @@ __global__ void k_fill_i64(int64_t* p, int64_t v, int64_t n) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// checkpoint restore: one thread per snapshot entry (FW_SNAP_ENTRY_WORDS int64 words) inserts the key
+// into the directory, claims the slice's slot and writes the pane — readStateTableForKeyGroup
+// (HeapKeyedStateBackend.java:318-349) putting (namespace, key) -> state into the state table
+// ------------------------------------------------------------------------------------------------
+__global__ void k_restore(Spec s, const int64_t* ent, int64_t n) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t* x = ent + j * FW_SNAP_ENTRY_WORDS;
+    const int64_t kid = dir_find_or_insert(s, x[1]);
+    const int32_t p = slice_slot(s, x[0]);
+    if (kid < 0 || p < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+    const int64_t idx = (int64_t)p * s.stride + kid;
+    s.c.sum[idx] = x[2];
+    if (s.c.mn) s.c.mn[idx] = x[3];
+    if (s.c.mx) s.c.mx[idx] = x[4];
+    if (s.c.cnt) s.c.cnt[idx] = x[5];
+    if (s.first) { s.c.first[idx] = x[6]; s.c.f1v[idx] = x[7]; }
+    else s.c.present[idx] = 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // keyBy routing (multi-GPU exchange): stable counting sort of records by operator index
 // KeyGroupStreamPartitioner.selectChannels (SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65)
 // ------------------------------------------------------------------------------------------------
@@ -1577,6 +1598,11 @@ struct fw_engine {
   Spec s{};
   int64_t cur_wm = INT64_MIN;
   int64_t ordinal = 0;
+  bool used_key_hash = false;         // a push carried Java key hashes: key groups are not derivable from keys
+  bool restored = false;              // fw_restore_kg was called (fixes the watermark of every later restore)
+  // fw_snapshot_kg: entries of every key group, built once per engine state (state_epoch)
+  int64_t state_epoch = 0, snap_epoch = -1;
+  std::vector<std::vector<int64_t>> snap_kg;
   int64_t records_in = 0;
   int64_t pushes = 0;                 // non-empty pushes (ev_consumed ring position)
   int grid = 0;
@@ -1995,6 +2021,8 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (n > e->cfg.max_batch) return fail(e, FW_ERR_CAPACITY, "batch larger than max_batch");
   if (n == 0) return FW_OK;
   HIPCHK(e, hipSetDevice(e->dev));
+  if (key_hash) e->used_key_hash = true;
+  e->state_epoch++;
   // routed form: the batch's copies and k_route run on the route stream, k_aggregate on the engine
   // stream; buffers of batch parity par are reused only after k_aggregate of batch j-2 finished
   const int par = (int)(e->batches & 1);
@@ -2099,6 +2127,7 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   if (!e) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
   HIPCHK(e, hipSetDevice(e->dev));
+  e->state_epoch++;
   if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
     hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
     HIPCHK(e, hipGetLastError());
@@ -2253,6 +2282,147 @@ int fw_get_profile(fw_engine* e, fw_profile* out) {
 const char* fw_last_error(const fw_engine* e) { return e ? e->err.c_str() : g_create_error.c_str(); }
 
 void fw_destroy(fw_engine* e) { delete e; }
+
+// key group of a Long key (KeyGroupRangeAssignment.assignToKeyGroup :51-64 over Long.hashCode)
+static int32_t host_key_group(const fw::Spec& s, int64_t key) {
+  return fw::key_group_for_hash(fw::long_hash_code(key), s.mp);
+}
+
+// an argument the call rejects: reported like a failure but, unlike one, leaves the engine usable
+static int reject(fw_engine* e, int code, const std::string& msg) {
+  e->err = msg;
+  return code;
+}
+
+static void snap_header(const fw_engine* e, int32_t kg, int64_t n, int64_t* h) {
+  const fw_config& c = e->cfg;
+  const int64_t w[FW_SNAP_HEADER_WORDS] = {FW_SNAP_MAGIC, 1, kg, n, e->cur_wm, c.assigner, c.size,
+                                          c.assigner == FW_SLIDING ? c.slide : c.size, c.offset, c.value_type,
+                                          c.agg_mask, c.keep_first_f1 ? 1 : 0};
+  memcpy(h, w, sizeof(w));
+}
+
+// every key group's entries, from one copy of the directory and the live slices' columns.  The heap
+// backend walks its per-key-group maps instead (HeapKeyedStateBackend.java:196-212); here the panes of
+// all key groups sit in one dense table, so one pass sorts them into key groups
+static int build_snapshot(fw_engine* e) {
+  if (e->snap_epoch == e->state_epoch) return FW_OK;
+  const fw::Spec& s = e->s;
+  HIPCHK(e, hipStreamSynchronize(e->rstream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int rc = check_device_error(e);
+  if (rc) return rc;
+  std::vector<int64_t> keys((size_t)s.D), tags((size_t)s.P);
+  int32_t min_used = 0;
+  HIPCHK(e, hipMemcpy(keys.data(), s.dir_keys, 8 * (size_t)s.D, hipMemcpyDeviceToHost));
+  HIPCHK(e, hipMemcpy(tags.data(), s.slice_tag, 8 * (size_t)s.P, hipMemcpyDeviceToHost));
+  HIPCHK(e, hipMemcpy(&min_used, s.dir_min_used, 4, hipMemcpyDeviceToHost));
+  const int32_t mp = s.mp;
+  std::vector<int32_t> kid_kg((size_t)s.stride, -1);
+  for (int64_t k = 0; k < s.D; ++k)
+    if (keys[k] != fw::EMPTY_KEY) kid_kg[k] = host_key_group(s, keys[k]);
+  if (min_used) kid_kg[s.D] = host_key_group(s, fw::EMPTY_KEY);
+  e->snap_kg.assign((size_t)mp, {});
+  const size_t st = (size_t)s.stride;
+  std::vector<int64_t> sum(st), mn, mx, cnt, first, f1v;
+  std::vector<uint8_t> present;
+  for (int32_t p = 0; p < s.P; ++p) {
+    const int64_t m = tags[p];
+    if (m == fw::FREE_TAG) continue;
+    const size_t off = (size_t)p * st;
+    auto get = [&](std::vector<int64_t>& v, const int64_t* col) -> hipError_t {
+      if (!col) return hipSuccess;
+      v.resize(st);
+      return hipMemcpy(v.data(), col + off, 8 * st, hipMemcpyDeviceToHost);
+    };
+    HIPCHK(e, get(sum, s.c.sum));
+    HIPCHK(e, get(mn, s.c.mn));
+    HIPCHK(e, get(mx, s.c.mx));
+    HIPCHK(e, get(cnt, s.c.cnt));
+    if (s.first) {
+      HIPCHK(e, get(first, s.c.first));
+      HIPCHK(e, get(f1v, s.c.f1v));
+    } else {
+      present.resize(st);
+      HIPCHK(e, hipMemcpy(present.data(), s.c.present + off, st, hipMemcpyDeviceToHost));
+    }
+    for (size_t k = 0; k < st; ++k) {
+      const bool pres = s.first ? first[k] != INT64_MAX : present[k] != 0;
+      if (!pres || kid_kg[k] < 0) continue;
+      const int64_t key = (int64_t)k == s.D ? fw::EMPTY_KEY : keys[k];
+      const int64_t ent[FW_SNAP_ENTRY_WORDS] = {
+          m, key, sum[k], s.c.mn ? mn[k] : INT64_MAX, s.c.mx ? mx[k] : INT64_MIN, s.c.cnt ? cnt[k] : 0,
+          s.first ? first[k] - e->ordinal : -1, s.first ? f1v[k] : 0};
+      auto& v = e->snap_kg[(size_t)kid_kg[k]];
+      v.insert(v.end(), ent, ent + FW_SNAP_ENTRY_WORDS);
+    }
+  }
+  e->snap_epoch = e->state_epoch;
+  return FW_OK;
+}
+
+int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* len) {
+  if (!e || !len) return FW_ERR_INVALID_ARG;
+  if (e->sticky) return e->sticky;
+  if (kg < e->s.kg_start || kg > e->s.kg_end)   // HeapInternalTimerService.restoreTimersForKeyGroup's check
+    return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
+  if (e->used_key_hash)
+    return reject(e, FW_ERR_UNSUPPORTED, "snapshot needs Long keys (a push carried Java key hashes)");
+  HIPCHK(e, hipSetDevice(e->dev));
+  int rc = build_snapshot(e);
+  if (rc) return rc;
+  const std::vector<int64_t>& v = e->snap_kg[(size_t)kg];
+  const int64_t n = (int64_t)v.size() / FW_SNAP_ENTRY_WORDS;
+  *len = 8 * (FW_SNAP_HEADER_WORDS + (int64_t)v.size());
+  if (!buf) return FW_OK;
+  if (cap < *len) return reject(e, FW_ERR_CAPACITY, "snapshot buffer too small");
+  snap_header(e, kg, n, (int64_t*)buf);
+  if (!v.empty()) memcpy((int64_t*)buf + FW_SNAP_HEADER_WORDS, v.data(), 8 * v.size());
+  return FW_OK;
+}
+
+int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
+  if (!e || !buf) return FW_ERR_INVALID_ARG;
+  if (e->sticky) return e->sticky;
+  if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
+  if (len < 8 * FW_SNAP_HEADER_WORDS) return reject(e, FW_ERR_INVALID_ARG, "snapshot blob too short");
+  const int64_t* h = (const int64_t*)buf;
+  int64_t ref[FW_SNAP_HEADER_WORDS];
+  snap_header(e, kg, h[3], ref);
+  if (h[0] != FW_SNAP_MAGIC || h[1] != 1) return reject(e, FW_ERR_INVALID_ARG, "not a key-group snapshot (magic/version)");
+  if (h[2] != kg) return reject(e, FW_ERR_INVALID_ARG, "snapshot holds key group " + std::to_string(h[2]));
+  for (int w = 5; w < FW_SNAP_HEADER_WORDS; ++w)
+    if (h[w] != ref[w]) return reject(e, FW_ERR_INVALID_ARG, "snapshot of a different window/reduce configuration");
+  if (kg < e->s.kg_start || kg > e->s.kg_end)
+    return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
+  const int64_t n = h[3];
+  if (n < 0 || len != 8 * (FW_SNAP_HEADER_WORDS + n * FW_SNAP_ENTRY_WORDS))
+    return reject(e, FW_ERR_INVALID_ARG, "snapshot blob length does not match its entry count");
+  if (e->restored && h[4] != e->cur_wm)
+    return reject(e, FW_ERR_INVALID_ARG, "key groups checkpointed at different watermarks");
+  const int64_t* ent = h + FW_SNAP_HEADER_WORDS;
+  for (int64_t j = 0; j < n; ++j)
+    if (host_key_group(e->s, ent[j * FW_SNAP_ENTRY_WORDS + 1]) != kg)
+      return reject(e, FW_ERR_KEY_GROUP, "snapshot entry key outside its key group");
+  HIPCHK(e, hipSetDevice(e->dev));
+  e->restored = true;
+  e->cur_wm = h[4];
+  e->state_epoch++;
+  if (n == 0) return FW_OK;
+  int64_t* d = nullptr;
+  HIPCHK(e, hipMalloc(&d, 8 * (size_t)n * FW_SNAP_ENTRY_WORDS));
+  hipError_t r = hipMemcpyAsync(d, ent, 8 * (size_t)n * FW_SNAP_ENTRY_WORDS, hipMemcpyHostToDevice, e->stream);
+  if (r == hipSuccess) {
+    const int blocks = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, 1024);
+    hipLaunchKernelGGL(fw::k_restore, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, d, n);
+    r = hipGetLastError();
+  }
+  const hipError_t r2 = hipStreamSynchronize(e->stream);
+  (void)hipFree(d);
+  HIPCHK(e, r);
+  HIPCHK(e, r2);
+  return check_device_error(e);
+}
 
 int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,
                              const int64_t* ts, const void* value, int64_t n, int32_t max_parallelism,

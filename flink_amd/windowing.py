@@ -240,6 +240,20 @@ class WindowEngine:
             self._fn("clear_output")(self.h)
         return res
 
+    def snapshot_kg(self, kg):
+        """State of key group kg as one blob (fw_snapshot_kg; HeapKeyedStateBackend.writeStateTableForKeyGroup
+        + HeapInternalTimerService.snapshotTimersForKeyGroup)."""
+        n = ctypes.c_int64()
+        self._check(self._fn("snapshot_kg")(self.h, kg, None, 0, ctypes.byref(n)))
+        buf = np.zeros(n.value // 8, dtype=np.int64)
+        self._check(self._fn("snapshot_kg")(self.h, kg, _ptr(buf), n.value, ctypes.byref(n)))
+        return buf.tobytes()
+
+    def restore_kg(self, kg, blob):
+        """Load a key group's blob before the first push (fw_restore_kg; readStateTableForKeyGroup)."""
+        buf = np.frombuffer(blob, dtype=np.int64).copy()
+        self._check(self._fn("restore_kg")(self.h, kg, _ptr(buf), len(blob)))
+
     def stats(self):
         st = _abi.FwStats()
         self._check(self._fn("get_stats")(self.h, ctypes.byref(st)))
@@ -369,6 +383,24 @@ class WindowOperator:
         while pos < res["n"]:
             self.output.append(self._record(res, pos))
             pos += 1
+
+    def snapshotState(self):
+        """{key group: blob} for this subtask's key groups (AbstractStreamOperator.snapshotState
+        :367-391 writes the keyed state and the timers of each key group of the local range).  Buffered
+        records are handed to the engine first, as the task flushes before the barrier."""
+        self._flush()
+        if self._key_names:
+            raise _abi.FwError(_abi.FW_ERR_UNSUPPORTED, "snapshot needs Long keys")
+        lo, hi = self.config.kg_start, self.config.kg_end
+        return {kg: self.engine.snapshot_kg(kg) for kg in range(lo, hi + 1)}
+
+    def initializeState(self, state):
+        """Restore the blobs of the local key groups (AbstractStreamOperator.initializeState :405-425 reads
+        only the key groups of the new range: StateAssignmentOperation hands each subtask its share)."""
+        lo, hi = self.config.kg_start, self.config.kg_end
+        for kg, blob in sorted(state.items()):
+            if lo <= kg <= hi:
+                self.engine.restore_kg(kg, blob)
 
     def getOutput(self):
         return self.output

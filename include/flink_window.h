@@ -152,6 +152,34 @@ int         fw_get_stats(fw_engine* e, fw_stats* st);
 const char* fw_last_error(const fw_engine* e);
 void        fw_destroy(fw_engine* e);
 
+/* ---- checkpoint state per key group ----
+ * fw_snapshot_kg <- HeapKeyedStateBackend.snapshot / writeStateTableForKeyGroup
+ *                   flink-runtime/.../runtime/state/heap/HeapKeyedStateBackend.java:164-249
+ *                   + HeapInternalTimerService.snapshotTimersForKeyGroup   SJ/api/operators/HeapInternalTimerService.java:285-310
+ *                   (called per key group from AbstractStreamOperator.snapshotState, AbstractStreamOperator.java:367-391)
+ * fw_restore_kg  <- HeapKeyedStateBackend.restorePartitionedState / readStateTableForKeyGroup :251-349
+ *                   + HeapInternalTimerService.restoreTimersForKeyGroup :319-345 (AbstractStreamOperator.java:405-425)
+ * One blob per key group: FW_SNAP_HEADER_WORDS int64 header words, then n entries of FW_SNAP_ENTRY_WORDS
+ * int64 words, native byte order:
+ *   header  [0] FW_SNAP_MAGIC  [1] version (1)  [2] key group  [3] n entries  [4] watermark of the snapshot
+ *           [5] assigner  [6] size  [7] slide  [8] offset  [9] value_type  [10] agg_mask  [11] keep_first_f1
+ *   entry   [0] slice number m (namespace: the window [m*size+offset, +size) for tumbling; the slice
+ *               [m*g+offset, +g), g = gcd(size, slide), of which every window is made for sliding)
+ *           [1] key  [2] sum  [3] min  [4] max  [5] count (double bits / Math.min-max codes for FW_VALUE_F64)
+ *           [6] first-arrival order (negative, relative to the end of the snapshot's stream)  [7] f1
+ * Timers are implicit, as in the engine: a pane's trigger timer is pending iff its window's maxTimestamp is
+ * above the snapshot watermark, its cleanup timer iff it is present at all.  Blobs restored into one engine
+ * must carry the same watermark (an aligned checkpoint: every window subtask has seen the same
+ * watermarks, which keyBy broadcasts to all of them).  Restore is allowed only before the first push,
+ * like initializeState before open.  Keys must be Long keys (no key_hash column was ever pushed).
+ * fw_snapshot_kg with buf == NULL (or cap too small) stores the required size in *len and returns
+ * FW_OK (NULL) or FW_ERR_CAPACITY. */
+#define FW_SNAP_MAGIC         0x31474b5746574bLL   /* "KWFWKG1" */
+#define FW_SNAP_HEADER_WORDS  12
+#define FW_SNAP_ENTRY_WORDS   8
+int         fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* len);
+int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len);
+
 /* Key-group routing for the multi-GPU keyBy exchange (enqueued on the caller stream when fw_set_stream set one)
  * (KeyGroupStreamPartitioner.selectChannels, SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65;
  *  KeyGroupRangeAssignment.assignKeyToParallelOperator, KeyGroupRangeAssignment.java:40-42,105-107).
