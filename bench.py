@@ -170,6 +170,7 @@ def main():
     t0 = time.perf_counter()
     for j in range(args.warmup, args.warmup + args.steps):
         step(j)
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (host-bound if close to dt)
     torch.cuda.synchronize()      # device-wide: covers the engine's own streams
     barrier(world)
     dt = time.perf_counter() - t0
@@ -258,6 +259,7 @@ def main():
                      "device_time_source": f"HIP events around each kernel on its stream, {args.prof_steps} "
                                            "batches after the timed region, one batch at a time"},
         "check": check,
+        "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         line["cpu_baseline"] = cpu_baseline(cfg, n_keys, rate, args.cpu_sample)

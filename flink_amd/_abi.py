@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libflink_window.so")
+# FW_LIBRARY: another build of the same engine (A/B measurements of two builds in one run)
+LIB_PATH = os.environ.get("FW_LIBRARY") or os.path.join(HERE, "lib", "libflink_window.so")
 
 # return codes
 FW_OK = 0

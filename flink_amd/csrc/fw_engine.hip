@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     // walks forward from it (a step spans ~4 segments at 256 buckets), and every load of a wave's UR
     // steps is issued before any of them is processed.  lfirst keeps the pane's earliest record of the
     // batch as (tile << 12 | index in the tile): tiles are consecutive ranges of the batch
-    constexpr int UR = 3;
+    constexpr int UR = 2;
     for (int32_t cb = 0; cb < R; cb += AG_CHS * 64) {   // uniform
       for (int t = threadIdx.x; t < r.ntiles; t += NT) {
         const int32_t o = off[t], l = off[t + 1] - o;
