@@ -91,3 +91,13 @@ def test_window_assigner_factories_use_java_remainder():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(RuntimeError, match="not built"):
         _abi.open_library(str(tmp_path / "nope.so"))
+
+
+def test_snapshot_layout_constants_match_header():
+    """The key-group snapshot blob layout (fw_snapshot_kg / fw_restore_kg) seen by ctypes is the
+    header's: magic, header and entry word counts."""
+    src = open(HEADER).read()
+    defs = dict(re.findall(r"#define (FW_SNAP_[A-Z_]+)\s+(0x[0-9a-fA-F]+|\d+)", src))
+    assert int(defs["FW_SNAP_MAGIC"], 0) == _abi.FW_SNAP_MAGIC
+    assert int(defs["FW_SNAP_HEADER_WORDS"]) == _abi.FW_SNAP_HEADER_WORDS
+    assert int(defs["FW_SNAP_ENTRY_WORDS"]) == _abi.FW_SNAP_ENTRY_WORDS
