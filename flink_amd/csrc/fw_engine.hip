@@ -859,7 +859,21 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     }
     const bool miss = act && !found;
     if (__any(miss)) {
-      if (miss && !find_slow(h, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
+      // second window, still inline: the few keys displaced 8+ slots cluster in a few buckets, where a
+      // call on every such wave (its live registers saved around it) doubled the bucket's time
+      // (tools/stamps.py: the slowest workgroups were always the same buckets)
+      bool found2 = false;
+#pragma unroll
+      for (int j = 2 * AG_WIN - 1; j >= AG_WIN; --j) {
+        const uint32_t x = (h0 + j) & kbm;
+        const bool m = lh[x] == h;
+        kl = (miss && m) ? x : kl;
+        found2 |= m;
+      }
+      const bool miss2 = miss && !found2;
+      if (__any(miss2)) {
+        if (miss2 && !find_slow(h, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
+      }
     }
     kl = act ? kl : (uint32_t)KB + (uint32_t)lane;
     if (AGG & FW_AGG_SUM) {

@@ -19,6 +19,10 @@ def phases(a, nblk, npts):
         print("      max per phase", np.round(d.max(axis=0)), "end p50/p90/max", np.percentile(end, [50, 90, 100]).round())
         if nblk == 256:
             m = d[:, 2]
+            st = (a[:, 0] - t0) * 10
+            slow = np.argsort(end)[-6:][::-1]
+            print("      slowest blocks (blockIdx, start ns, main ns, end ns):",
+                  [(int(b), round(st[b]), round(m[b]), round(end[b])) for b in slow])
             print("      main by blockIdx%8:", [round(m[i::8].mean()) for i in range(8)])
             print("      main by blockIdx//32:", [round(m[i*32:(i+1)*32].mean()) for i in range(8)])
     return (a[:, 0] - t0).mean() * 10, d.mean(axis=0), (a[:, npts - 1].max() - t0) * 10
