@@ -479,6 +479,12 @@ struct RouteBuf {
   int32_t dbg;
 };
 
+// Non-temporal access of the streamed columns, a bit mask: 1 = k_route's input loads (on: k_route 43 ->
+// 41 us per 4 Mi-event batch), 2 = k_aggregate's gathers of the routed records, 4 = k_route's stores of
+// them (both measured slower: k_aggregate 36 -> 38-40 us, the intermediate is re-read from the cache)
+#ifndef FW_ROUTE_NT
+#define FW_ROUTE_NT 1
+#endif
 #define FW_STAMP(r, base, k) do { if ((r).stamps && threadIdx.x == 0) (r).stamps[(base) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 // tile-local slice set in LDS (RT_Q entries): index of slice m, inserting it if new; -1 when full
@@ -548,9 +554,17 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   for (int j = 0; j < V; ++j) {
     const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
     if (!tail) {
+#if FW_ROUTE_NT & 1
+      // streamed once per batch: non-temporal, so the routed intermediate k_aggregate reads next keeps the cache
+      typedef long long v2i64 __attribute__((ext_vector_type(2)));
+      const v2i64 a = __builtin_nontemporal_load((const v2i64*)(b.key + i));
+      const v2i64 c = __builtin_nontemporal_load((const v2i64*)(b.ts + i));
+      const v2i64 d = __builtin_nontemporal_load((const v2i64*)(b.val + i));
+#else
       const longlong2 a = *(const longlong2*)(b.key + i);
       const longlong2 c = *(const longlong2*)(b.ts + i);
       const longlong2 d = *(const longlong2*)(b.val + i);
+#endif
       kk[2 * j] = a.x; kk[2 * j + 1] = a.y;
       tt[2 * j] = c.x; tt[2 * j + 1] = c.y;
       vv[2 * j] = d.x; vv[2 * j + 1] = d.y;
@@ -733,7 +747,16 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
 #pragma unroll 2
   for (int k = 0; k < PER; ++k) {
     const int32_t pos = k * NT + (int)threadIdx.x;
+#if FW_ROUTE_NT & 4
+    if (pos < total) {
+      typedef long long v2i64 __attribute__((ext_vector_type(2)));
+      const longlong2 x = st_kv[pos];
+      v2i64 g; g.x = x.x; g.y = x.y;
+      __builtin_nontemporal_store(g, (v2i64*)(r.kv + base + pos));
+    }
+#else
     if (pos < total) r.kv[base + pos] = st_kv[pos];
+#endif
   }
   if (FIRST) {
 #pragma unroll
@@ -1046,7 +1069,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
             while (off[t + 1] <= rr) ++t;
             pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
           }
+#if FW_ROUTE_NT & 2
+          {
+            typedef long long v2i64 __attribute__((ext_vector_type(2)));
+            const v2i64 g = __builtin_nontemporal_load((const v2i64*)(r.kv + pos));
+            rv[u] = make_longlong2(g.x, g.y);
+          }
+#else
           rv[u] = r.kv[pos];
+#endif
           ri[u] = ((uint32_t)t << 12) | (FIRST ? (uint32_t)r.idx[pos] : 0u);
         }
       };
