@@ -1,17 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark: keyed 1 s tumbling event-time long-sum (BASELINE.json metric), events/s whole node.
 
-Workload (SURVEY.md §8d, config C1 — BASELINE.json configs[1] asks for 10M keys on one GPU; the
-metric itself is quoted on the C1 job, which is what this measures at N=1 unless --config c2):
+Workload.  Default config C1, the job BASELINE.json's metric is quoted on:
   keyBy(0).window(TumblingEventTimeWindows.of(1 s)).reduce((a, b) -> Tuple3(a.f0, a.f1, a.f2 + b.f2))
   over Tuple3<Long key, Long ts, Long value>; 64K uniform keys; R = 2^24 events per event-time
   second; a punctuated watermark (max ts seen - 1) after every batch of 2^22 events.
-A step = one batch of 2^22 events pushed through the engine + its watermark (fire/purge).
+Other configs (--config): c2 = the same at 10M keys (R = 2^26); c3 = sliding 10 s / 1 s windows,
+double values, sum/min/max/count; c4 = Zipf(1.2) keys, timestamps up to 200 ms out of order, watermark
+lag 50 ms, allowed lateness 100 ms (per-element late fires), sum/count.
+A step = one batch of 2^22 events per GPU pushed through the engine + its watermark (fire/purge).
 Inputs are generated on the GPU and resident in HBM before the timed region.
 
 Multi-GPU (torchrun, one process per GPU): every rank is a source subtask producing its own 2^22
 events per step (weak scaling); records are routed to the key-group owner (maxParallelism 128) by
 the keyBy exchange (HIP partition kernel + RCCL all-to-all) and the watermark is the min over ranks.
+
+Roofline: algorithmic bytes per step = 24 B x events + 96 B (112 B for C3) x fired
+panes; the headline `achieved` divides them by the whole step time (ms_per_step), so every kernel of
+the path and the gaps between them count.  Per-kernel device times (HIP events on the stream each runs
+on, measured after the timed region) and the PMC HBM traffic of the committed rocprofv3 summary of this
+library build are reported beside it.
 
 Prints ONE JSON line (rank 0).
 """
@@ -29,16 +37,26 @@ sys.path.insert(0, ROOT)
 
 from flink_amd import _abi  # noqa: E402
 from flink_amd.synth import stream  # noqa: E402
-from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, WindowEngine, make_config  # noqa: E402
+from flink_amd.windowing import (ReduceFunction, SlidingEventTimeWindows, TumblingEventTimeWindows,  # noqa: E402
+                                 WindowEngine, make_config)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 LONG_MAX = (1 << 63) - 1
 T0 = 1_700_000_000_000     # epoch ms, aligned to the window size
 
 CONFIGS = {
-    # name: (n_keys, rate events/s of event time, batch, key_capacity)
-    "c1": (1 << 16, 1 << 24, 1 << 22, 1 << 16),
-    "c2": (10_000_000, 1 << 26, 1 << 22, 10_000_000),
+    "c1": dict(keys=1 << 16, rate=1 << 24, batch=1 << 22, key_cap=1 << 16, window=("tumbling", 1000),
+               reduce=(("sum",), "i64"), zipf=None, ooo=0, wm_lag=1, lateness=0, pane_bytes=96,
+               desc="tumbling 1s event-time long-sum, f1 = first arrival"),
+    "c2": dict(keys=10_000_000, rate=1 << 26, batch=1 << 22, key_cap=10_000_000, window=("tumbling", 1000),
+               reduce=(("sum",), "i64"), zipf=None, ooo=0, wm_lag=1, lateness=0, pane_bytes=96,
+               desc="tumbling 1s event-time long-sum at 10M keys, f1 = first arrival"),
+    "c3": dict(keys=1 << 16, rate=1 << 24, batch=1 << 22, key_cap=1 << 16, window=("sliding", 10_000, 1000),
+               reduce=(("sum", "min", "max", "count"), "f64"), zipf=None, ooo=0, wm_lag=1, lateness=0, pane_bytes=112,
+               desc="sliding 10s/1s event-time windows, double sum/min/max/count, f1 = first arrival"),
+    "c4": dict(keys=1 << 16, rate=1 << 24, batch=1 << 22, key_cap=1 << 16, window=("tumbling", 1000),
+               reduce=(("sum", "count"), "i64"), zipf=1.2, ooo=200, wm_lag=50, lateness=100, pane_bytes=96,
+               desc="Zipf(1.2) keys, ts up to 200 ms out of order, watermark lag 50 ms, allowed lateness 100 ms"),
 }
 
 
@@ -56,6 +74,8 @@ def parse():
     ap.add_argument("--prof-steps", type=int, default=8,
                     help="steps after the timed region run with per-kernel device-time events (roofline); "
                          "timed events serialise kernels, so the timed region runs without them")
+    ap.add_argument("--h2d-steps", type=int, default=8,
+                    help="steps after the timed region pushed from pinned host columns (PCIe-inclusive rate; 0 = skip)")
     return ap.parse_args()
 
 
@@ -83,24 +103,25 @@ def barrier(world):
         dist.barrier()
 
 
-def cpu_baseline(cfg, n_keys, rate, n):
+def cpu_baseline(cfg, C, n):
     """The oracle as a p-subtask CPU job (key-group partitioned threads) on a bounded sample."""
     from oracle import oracle
     cores = min(16, len(os.sched_getaffinity(0)))
-    keys, ts, vals = (t.numpy() for t in stream(0, n, n_keys, rate, T0, device="cpu"))
+    keys, ts, vals = (t.numpy() for t in stream(0, n, C["keys"], C["rate"], T0, device="cpu",
+                                                 value_type=C["reduce"][1], zipf=C["zipf"], ooo=C["ooo"]))
     oracle.load()
     t = time.perf_counter()
-    fired, _ = oracle.run_parallel(cfg, cores, keys, ts, vals, 1 << 22, 1, LONG_MAX)
+    fired, _ = oracle.run_parallel(cfg, cores, keys, ts, vals, C["batch"], C["wm_lag"], LONG_MAX)
     dt = time.perf_counter() - t
     return {"value": n / dt, "unit": "events/s", "cores": cores, "kind": "port",
             "sample": f"first {n} events of the same stream, {cores} key-group subtasks (oracle/fw_oracle.cpp), "
-                      f"watermark every 2^22 events, final MAX_WATERMARK; {fired} windows fired"}
+                      f"watermark every {C['batch']} events, final MAX_WATERMARK; {fired} windows fired"}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per ingest launch from the committed rocprofv3 PMC summary of THIS library build
-    (profiles/*_pmc.json, written by tools/summarize_profiles.py from separate FETCH_SIZE / WRITE_SIZE
-    passes), or None when no summary matches the library's md5."""
+def pmc_traffic():
+    """HBM bytes per launch of every engine kernel from the committed rocprofv3 PMC summary of THIS
+    library build (profiles/*_pmc.json, written by tools/summarize_profiles.py from separate FETCH_SIZE /
+    WRITE_SIZE passes): ({kernel name: bytes}, file), or ({}, None) when no summary matches the library's md5."""
     import glob
     import hashlib
     lib = os.path.join(ROOT, "flink_amd", "lib", "libflink_window.so")
@@ -112,35 +133,52 @@ def pmc_traffic(kernel):
             continue
         if d.get("library_md5") != md5:
             continue
-        for name, k in d.get("kernels", {}).items():
-            if kernel in name and k.get("hbm_bytes_corrected"):
-                return k["hbm_bytes_corrected"], os.path.basename(f)
-    return None, None
+        return {n: k["hbm_bytes_corrected"] for n, k in d.get("kernels", {}).items()
+                if k.get("hbm_bytes_corrected")}, os.path.basename(f)
+    return {}, None
+
+
+def traffic_of(pmc, short):
+    for name, b in pmc.items():
+        if f"::{short}" in name:
+            return b
+    return None
 
 
 def main():
     args = parse()
     world, rank, local = dist_init(args)
     dev = torch.device("cuda", local)
-    n_keys, rate, batch, key_cap = CONFIGS[args.config]
-    total_steps = args.warmup + args.steps + args.prof_steps
+    C = CONFIGS[args.config]
+    n_keys, rate, batch, key_cap = C["keys"], C["rate"], C["batch"], C["key_cap"]
+    fields, vt = C["reduce"]
+    total_steps = args.warmup + args.steps + args.prof_steps + args.h2d_steps
 
     from flink_amd.keygroups import compute_key_group_range_for_operator_index
     mp = 128
     kg = compute_key_group_range_for_operator_index(mp, world, rank)
-    reduce_fn = ReduceFunction(("sum",), "i64", keep_first_f1=True)
+    reduce_fn = ReduceFunction(fields, vt, keep_first_f1=True)
+    if C["window"][0] == "tumbling":
+        assigner = TumblingEventTimeWindows.of(C["window"][1])
+        windows_per_record = 1
+    else:
+        assigner = SlidingEventTimeWindows.of(C["window"][1], C["window"][2])
+        windows_per_record = C["window"][1] // C["window"][2]
     windows_in_run = (total_steps * batch * world) // rate + 2
-    cfg = make_config(TumblingEventTimeWindows.of(1000), reduce_fn, max_parallelism=mp, key_group_range=kg,
+    out_cap = windows_in_run * windows_per_record * key_cap // max(world, 1) * 2 + 4096
+    if C["lateness"]:
+        out_cap += total_steps * batch // 4
+    cfg = make_config(assigner, reduce_fn, allowed_lateness=C["lateness"], max_parallelism=mp, key_group_range=kg,
                       device=local, key_capacity=key_cap, max_batch=batch * (2 if world > 1 or args.force_exchange else 1),
-                      out_capacity=int(min(windows_in_run * key_cap // max(world, 1) * 2 + 4096, 1 << 27)),
-                      ingest_mode=args.ingest_mode)
+                      out_capacity=int(min(out_cap, 1 << 27)), ingest_mode=args.ingest_mode)
     eng = WindowEngine(cfg)
 
     # resident synthetic input: rank r is source subtask r; its i-th event is global index i*world + r
     # (the interleaving keeps event time aligned across sources)
     cols = []
-    for j in range(total_steps):
-        k, t, v = stream(j * batch * world, batch * world, n_keys, rate, T0, device=dev)
+    for j in range(args.warmup + args.steps + args.prof_steps):
+        k, t, v = stream(j * batch * world, batch * world, n_keys, rate, T0, device=dev, value_type=vt,
+                         zipf=C["zipf"], ooo=C["ooo"])
         if world > 1:
             k, t, v = k[rank::world].contiguous(), t[rank::world].contiguous(), v[rank::world].contiguous()
         cols.append((k, t, v))
@@ -151,40 +189,75 @@ def main():
         from flink_amd.keyby import KeyByExchange
         exch = KeyByExchange(eng, world, rank, mp, batch, dev)
 
-    def step(j):
-        k, t, v = cols[j]
-        wm_local = int(T0 + (((j + 1) * batch * world - 1) * 1000) // rate) - 1   # max ts seen - 1
+    def wm_of(j):
+        # source watermark after batch j: max ts seen - lag (BoundedOutOfOrdernessTimestampExtractor)
+        return int(T0 + (((j + 1) * batch * world - 1) * 1000) // rate) - C["wm_lag"]
+
+    def step(j, k, t, v):
         if exch is None:
             eng.push(k, t, v)
-            eng.advance_watermark(wm_local)
+            eng.advance_watermark(wm_of(j))
         else:
-            exch.step(k, t, v, wm_local)
+            exch.step(k, t, v, wm_of(j))
+
+    def drain():
+        if exch is not None:
+            exch.flush()   # the pipelined exchange's outstanding batches
 
     for j in range(args.warmup):
-        step(j)
+        step(j, *cols[j])
+    drain()
     eng.sync()
     torch.cuda.synchronize()
-    warm_res = eng.collect()
+    collected = [eng.collect()]
+    st0 = eng.stats()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(args.warmup, args.warmup + args.steps):
-        step(j)
+        step(j, *cols[j])
+    drain()
     t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (host-bound if close to dt)
     torch.cuda.synchronize()      # device-wide: covers the engine's own streams
     barrier(world)
     dt = time.perf_counter() - t0
+    st1 = eng.stats()
+    fired_per_step = (st1["panes_fired"] - st0["panes_fired"]) / args.steps
+    collected.append(eng.collect())
 
     # per-kernel device time on the continuation of the same stream (untimed)
     eng.lib.fw_set_profiling(eng.h, 1)
     eng.lib.fw_get_profile(eng.h, _abi.FwProfile())  # reset counters
-    for j in range(args.warmup + args.steps, total_steps):
-        step(j)
+    j0 = args.warmup + args.steps
+    for j in range(j0, j0 + args.prof_steps):
+        step(j, *cols[j])
+        drain()
         eng.sync()   # isolate the kernels (no route/aggregate overlap across batches while timing them)
     prof = _abi.FwProfile()
     eng.lib.fw_get_profile(eng.h, prof)
     eng.lib.fw_set_profiling(eng.h, 0)
     eng.sync()
+    collected.append(eng.collect())
+
+    # PCIe-inclusive ingest: the same kind of batch pushed from pinned host columns (FW_MEM_HOST)
+    h2d = None
+    if args.h2d_steps > 0 and exch is None:
+        j0 = args.warmup + args.steps + args.prof_steps
+        host = []
+        for j in range(j0, j0 + args.h2d_steps):
+            k, t, v = stream(j * batch, batch, n_keys, rate, T0, device=dev, value_type=vt, zipf=C["zipf"], ooo=C["ooo"])
+            host.append(tuple(x.cpu().pin_memory() for x in (k, t, v)))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for j, (k, t, v) in enumerate(host):
+            eng.push(k, t, v)
+            eng.advance_watermark(wm_of(j0 + j))
+        eng.sync()
+        dth = time.perf_counter() - t1
+        h2d = {"value": args.h2d_steps * batch / dth, "unit": "events/s", "steps": args.h2d_steps,
+               "note": "pinned host key/ts/value columns -> fw_push_batch(FW_MEM_HOST): hipMemcpyAsync to HBM, then "
+                       "the same kernels; PCIe-inclusive, never the headline value"}
+        collected.append(eng.collect())
 
     if world > 1:
         import torch.distributed as dist
@@ -192,45 +265,68 @@ def main():
         dist.all_reduce(t_all, op=dist.ReduceOp.MAX)
         dt = float(t_all.item())
 
-    # --- correctness property (untimed): after MAX_WATERMARK every record has fired exactly once,
-    # so the wrapping sum of fired sums equals the wrapping sum of all values pushed (checksum of checksums)
+    # --- correctness property (untimed).  After MAX_WATERMARK every record has fired exactly once per
+    # window: C1/C2 wrapping sum of fired sums = wrapping sum of all values pushed (checksum of
+    # checksums); C3 sum of fired counts = windows per record x records
     check = "skipped"
-    if not args.no_check:
-        mask = (1 << 64) - 1
-        res = eng.collect()
+    if not args.no_check and C["lateness"] == 0:
         eng.advance_watermark(LONG_MAX)
-        res2 = eng.collect()
-        fired = int(np.concatenate([warm_res["sum_i64"], res["sum_i64"], res2["sum_i64"]]).astype(np.uint64).sum(dtype=np.uint64)) & mask
-        pushed = 0
-        for k, t, v in cols:
-            pushed = (pushed + (int(v.sum().item()) & mask)) & mask      # int64 tensor sums wrap
+        collected.append(eng.collect())
+        pushed_cols = [c for c in cols] + ([] if h2d is None else [tuple(x for x in hc) for hc in host])
+        if vt == "i64":
+            mask = (1 << 64) - 1
+            fired = int(np.concatenate([r["sum_i64"] for r in collected]).astype(np.uint64).sum(dtype=np.uint64)) & mask
+            pushed = 0
+            for k, t, v in pushed_cols:
+                pushed = (pushed + (int(v.sum().item()) & mask)) & mask      # int64 tensor sums wrap
+        else:
+            fired = int(np.concatenate([r["count"] for r in collected]).sum())
+            pushed = windows_per_record * sum(int(k.numel()) for k, t, v in pushed_cols)
         if world > 1:
             import torch.distributed as dist
             signed = lambda x: x - (1 << 64) if x >= (1 << 63) else x
             x = torch.tensor([signed(fired), signed(pushed)], dtype=torch.int64, device=dev)
             dist.all_reduce(x)
-            fired, pushed = int(x[0].item()) & mask, int(x[1].item()) & mask
+            fired, pushed = int(x[0].item()) & ((1 << 64) - 1), int(x[1].item()) & ((1 << 64) - 1)
         check = "ok" if fired == pushed else "MISMATCH"
 
-    form = eng.stats()["ingest_form"]
+    stats = eng.stats()
+    form = stats["ingest_form"]
     events = args.steps * batch * world
     value = events / dt
+    ms_step = dt * 1e3 / args.steps
 
     def per(ph):
         n_ = prof.launches[ph]
-        return (prof.ms[ph] / n_ if n_ else 0.0), (prof.records[ph] / n_ if n_ else 0.0)
-    route_ms, route_rec = per(_abi.FW_PHASE_INGEST)
+        return (prof.ms[ph] / n_ if n_ else 0.0), n_
+    route_ms, _ = per(_abi.FW_PHASE_INGEST)
     agg_ms, _ = per(_abi.FW_PHASE_AGGREGATE)
-    wm_ms, _ = per(_abi.FW_PHASE_FIRE)
-    # dominant kernel: the one taking the most device time per batch; its algorithmic bytes are SURVEY.md
-    # 8(d)'s 24 B per event (key, ts, value int64) times the events one launch processes
-    names = {"k_route": route_ms, "k_aggregate": agg_ms} if form == 2 else {"k_ingest_direct": route_ms}
-    dom = max(names, key=names.get)
-    dom_ms = names[dom]
-    alg_bytes = 24.0 * route_rec
-    achieved = alg_bytes / (dom_ms / 1e3) / 1e9 if dom_ms else 0.0
-    path_ms = route_ms + agg_ms
-    traffic, traffic_src = pmc_traffic(dom)
+    wm_ms, wm_n = per(_abi.FW_PHASE_FIRE)
+    late_ms, late_n = per(_abi.FW_PHASE_LATE)
+    wm_per_step = wm_n / max(args.prof_steps, 1)
+    # algorithmic bytes: 24 B per event (key, ts, value) + per fired pane 96 B (C3: 112 B)
+    ev_gpu = batch
+    alg_step = 24.0 * ev_gpu + C["pane_bytes"] * fired_per_step / max(world, 1)
+    achieved = alg_step / (ms_step / 1e3) / 1e9
+    pmc, pmc_src = pmc_traffic()
+    kernels = {}
+    names = [("k_route", route_ms, 1.0), ("k_aggregate", agg_ms, 1.0)] if form == 2 else [("k_ingest_direct", route_ms, 1.0)]
+    names.append(("k_watermark", wm_ms, wm_per_step))
+    for name, ms, per_step in names:
+        tr = traffic_of(pmc, name)
+        kernels[name] = {"ms": ms, "launches_per_step": per_step,
+                         "achieved_GBs": (24.0 * ev_gpu / (ms / 1e3) / 1e9) if ms and name != "k_watermark" else None,
+                         "traffic_bytes_per_launch": tr}
+        if kernels[name]["achieved_GBs"]:
+            kernels[name]["frac"] = kernels[name]["achieved_GBs"] / HBM_PEAK_GBS
+    if late_n:
+        kernels["late_path"] = {"ms": late_ms, "launches_per_step": late_n / max(args.prof_steps, 1)}
+    ingest = [n for n, _, _ in names if n != "k_watermark"]
+    dom = max(ingest, key=lambda n: kernels[n]["ms"])
+    traffic_step = None
+    if pmc and all(kernels[n]["traffic_bytes_per_launch"] for n in ingest):
+        traffic_step = sum(kernels[n]["traffic_bytes_per_launch"] * kernels[n]["launches_per_step"] for n in kernels
+                           if kernels[n].get("traffic_bytes_per_launch"))
     line = {
         "metric": "events/sec (whole node) keyed 1s tumbling sum; % of HBM roofline",
         "value": value,
@@ -238,31 +334,36 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt * 1e3 / args.steps,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int64",
+        "dtype": "int64" if vt == "i64" else "f64",
         "data": "synthetic (splitmix64 counter stream, SURVEY.md §8d), resident in HBM",
-        "config": {"workload": f"{args.config}: tumbling 1s event-time long-sum, {n_keys} keys, "
-                               f"{rate} events/s event time, watermark every {batch} events per source",
+        "config": {"workload": f"{args.config}: {C['desc']}, {n_keys} keys, {rate} events/s event time, "
+                               f"watermark every {batch} events per source",
                    "batch_per_gpu": batch, "keys": n_keys, "max_parallelism": mp, "parallelism": f"kg{world}",
-                   "reduce": "Tuple3(a.f0, a.f1, a.f2 + b.f2), f1 = first arrival"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc)",
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": alg_bytes, "bytes_per_event": 24,
-                     "kernel_ms": {k: v for k, v in names.items()}, "watermark_ms": wm_ms,
-                     "path_achieved": alg_bytes / (path_ms / 1e3) / 1e9 if path_ms else 0.0,
-                     "path_note": "24 B/event over the summed device time of the ingest kernels of one batch",
+                   "reduce": f"{'/'.join(fields)} over {vt}, f1 = first arrival"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_step,
+                     "scope": "whole step: algorithmic bytes of one batch (24 B/event + pane bytes x fired panes) "
+                              "over ms_per_step, every kernel and gap included",
+                     "algorithmic_bytes_per_step": alg_step, "fired_panes_per_step": fired_per_step,
+                     "traffic_unit": "HBM bytes per step: sum over kernels of PMC bytes per launch (FETCH_SIZE x2 + "
+                                     "WRITE_SIZE, rocprofv3 --pmc) x launches per step",
+                     "traffic_ratio": (traffic_step / alg_step) if traffic_step else None,
+                     "traffic_source": pmc_src,
+                     "dominant_kernel": dom, "kernels": kernels,
                      "device_time_source": f"HIP events around each kernel on its stream, {args.prof_steps} "
                                            "batches after the timed region, one batch at a time"},
         "check": check,
+        "stats": {k: stats[k] for k in ("records_in", "records_late", "panes_fired", "late_fires", "ingest_form")},
         "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
     }
+    if h2d is not None:
+        line["h2d_ingest"] = h2d
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        line["cpu_baseline"] = cpu_baseline(cfg, n_keys, rate, args.cpu_sample)
+        line["cpu_baseline"] = cpu_baseline(cfg, C, args.cpu_sample)
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()

@@ -110,18 +110,6 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {  // MurmurHash3 finalis
   return k;
 }
 
-// inverse of fmix64 (fmix64 is a bijection on 64-bit words): k ^= k >> 33 is an involution, and the
-// multipliers are odd, so their inverses mod 2^64 exist
-__device__ __forceinline__ uint64_t fmix64_inv(uint64_t h) {
-  h ^= h >> 33;
-  h *= 0x9cb4b2f8129337dbull;
-  h ^= h >> 33;
-  h *= 0x4f74430c22a54005ull;
-  h ^= h >> 33;
-  return h;
-}
-constexpr uint64_t EMPTY_H = 0x8f780810af31a493ull;   // fmix64(Long.MIN_VALUE): the hash of an empty slot
-
 __device__ __forceinline__ uint64_t lanemask_lt() { return __lanemask_lt(); }
 
 // wave-aggregated counter add; returns this lane's slot (only meaningful where pred)
@@ -140,31 +128,52 @@ __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
     atomicAdd(ctr, (unsigned long long)__popcll(mask));
 }
 
-// key -> kid (directory slot).  Entries go EMPTY -> key once and never change until engine reset, so
-// a plain (possibly stale) load can only under-report, which the CAS then corrects.  Probing stays
-// inside the key's home bucket of 2^kb_bits slots, so every kid of a key lies in the bucket its hash
-// names: the partitioned ingest (k_route / k_aggregate) owns whole buckets exclusively.
-__device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key) {
+// key -> kid (directory slot).  Group probing inside the key's home bucket of 2^kb_bits slots: the
+// aligned group of DIR_GROUP slots (32 B) holding the key's home slot first, then the following groups,
+// wrapping inside the bucket; a key takes the first slot in that order that was EMPTY when it arrived.
+// At the directory's load factor <= 1/4 a group overflows for ~0.4 % of keys, so a lookup is nearly
+// always one 32-B read (k_route does it for every routed record, against an L2-resident directory).
+// Entries go EMPTY -> key once and never change until engine reset, so a plain (possibly stale) load
+// can only under-report, which the CAS then corrects; a key found EMPTY at slot j cannot sit at a later
+// slot.  Every kid of a key lies in the bucket its hash names: the partitioned ingest (k_route /
+// k_aggregate) owns whole buckets exclusively.
+constexpr int DIR_GROUP = 4;
+__device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
+                                                         int32_t kb_bits, int64_t D, int64_t key) {
   if (key == EMPTY_KEY) {
-    if (s.dir_min_used[0] == 0) s.dir_min_used[0] = 1;
-    return s.D;
+    if (dir_min_used[0] == 0) dir_min_used[0] = 1;
+    return D;
   }
-  const uint64_t home = fmix64((uint64_t)key) & s.dir_mask;
-  const uint64_t kbm = (1ull << s.kb_bits) - 1;
+  const uint64_t home = fmix64((uint64_t)key) & dir_mask;
+  const uint64_t kbm = (1ull << kb_bits) - 1;
   const uint64_t base = home & ~kbm;
-  uint64_t off = home & kbm;
-  for (uint64_t probe = 0; probe <= kbm; ++probe) {
-    const uint64_t h = base + off;
-    int64_t cur = s.dir_keys[h];
-    if (cur == key) return (int64_t)h;
-    if (cur == EMPTY_KEY) {
-      unsigned long long prev = atomicCAS((unsigned long long*)&s.dir_keys[h], (unsigned long long)EMPTY_KEY,
-                                          (unsigned long long)key);
-      if ((int64_t)prev == EMPTY_KEY || (int64_t)prev == key) return (int64_t)h;
+  uint64_t g = home & kbm & ~(uint64_t)(DIR_GROUP - 1);
+  for (uint64_t probe = 0; probe <= kbm; probe += DIR_GROUP) {
+    for (int j = 0; j < DIR_GROUP; ++j) {
+      const uint64_t h = base + g + j;
+      const int64_t cur = dir_keys[h];
+      if (cur == key) return (int64_t)h;
+      if (cur == EMPTY_KEY) {
+        const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[h], (unsigned long long)EMPTY_KEY,
+                                                  (unsigned long long)key);
+        if ((int64_t)prev == EMPTY_KEY || (int64_t)prev == key) return (int64_t)h;
+      }
     }
-    off = (off + 1) & kbm;
+    g = (g + DIR_GROUP) & kbm;
   }
   return -1;
+}
+__device__ __noinline__ int64_t dir_find_or_insert_call(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
+                                                        int32_t kb_bits, int64_t D, int64_t key) {
+  return dir_find_or_insert_at(dir_keys, dir_min_used, dir_mask, kb_bits, D, key);
+}
+// inline: the direct form's per-record lookup
+__device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key) {
+  return dir_find_or_insert_at(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key);
+}
+// out of line: the rare lookups of the partitioned form (new keys, direct-list records) and restore
+__device__ __forceinline__ int64_t dir_lookup(const Spec& s, int64_t key) {
+  return dir_find_or_insert_call(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key);
 }
 
 // slice number m -> slot p, claiming a FREE slot.  Returns -1 when slot p holds another live slice.
@@ -442,35 +451,38 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 // ingest, partitioned form.  Two kernels per batch:
 //  k_route      one workgroup per tile of RT_TILE records: streams the tile's columns in with 16-B
 //               loads, does the per-record operator work (key group check, window/slice, lateness),
-//               counting-sorts the routable records through LDS by bin = (batch slice q, directory
-//               bucket) and writes the tile back bin-sorted (key, value, index-in-tile) with a per-tile
-//               table of segment starts.  Records that cannot be routed (per-element fires, a third
-//               slice in one batch, the Long.MIN_VALUE key) take the direct path after the scatter.
+//               resolves each routable record's directory slot (one 32-B group read of the L2-resident
+//               directory; new keys are inserted there), counting-sorts the routable records through LDS
+//               by bin = (tile slice q, directory bucket) and writes the tile back bin-sorted as 12-B
+//               records (value, slot-in-bucket << 12 | index-in-tile) with a per-tile table of segment
+//               starts.  Records that cannot be routed (per-element fires, slices beyond the tile's RT_Q,
+//               the Long.MIN_VALUE key) join the direct list.
 //  k_aggregate  one workgroup per directory bucket: owns every pane of that bucket for this batch,
 //               gathers the bucket's segment from every tile (the segments concatenated, one record
-//               per lane), resolves keys in an LDS copy of the bucket's directory slice, reduces with
-//               LDS atomics and folds each touched pane into the dense columns once.
-// No device-scope atomic per record: the routed form is bounded by HBM traffic, not the memory-side
-// atomic rate (tools/microbench/ingest_mb.hip: ~24 G random 8-B atomics/s chip-wide).
+//               per lane), reduces with LDS atomics indexed by the routed slot (no key compare left),
+//               adds the bucket's direct records the same way and folds each touched pane into the
+//               dense columns once, with plain loads and stores.
+// No device-scope atomic per record, and 48 B of HBM traffic per event (24 in, 12 out, 12 back in).
 // ------------------------------------------------------------------------------------------------
 constexpr int RT_TILE = 4096;
 constexpr int RT_THREADS = 512;
-constexpr int RT_Q = 2;                 // slices per tile routed through LDS (more go to the direct path)
-constexpr int RT_GS = 64;               // distinct routed slices per batch (k_aggregate rounds)
+constexpr int RT_Q = 4;                 // slices per tile routed through LDS (more go to the direct list)
+constexpr int RT_GS = 64;               // distinct slices per batch (k_aggregate rounds)
+constexpr int RT_MAXNB = 256;           // directory buckets the route table holds
 constexpr int DC_RING = 16;             // direct-list counters, one per batch in flight
 constexpr int AG_THREADS = 1024;
-constexpr int AG_WIN = 8;              // k_aggregate: directory slots probed without a branch
-constexpr int AG_CHS = 1024;           // k_aggregate wave steps (64 records each) tabulated per chunk
-constexpr int AG_MAXPER = 17;          // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
-constexpr int RT_MAX_KB_BITS = 10;      // directory slots per bucket held in LDS by k_aggregate
+constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
+constexpr int AG_MAXPER = 17;           // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
+constexpr int RT_MAX_KB_BITS = 13;      // directory slots per bucket whose accumulators k_aggregate holds in LDS
+constexpr int IDX_BITS = 12;            // record index within a tile (RT_TILE = 2^12)
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
-  longlong2* kv;         // [ntiles][RT_TILE] routed records (fmix64(key), value), each tile sorted by bin
-  uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
+  int64_t* val;          // [ntiles][RT_TILE] routed values (int64 or double bits), each tile sorted by bin
+  uint32_t* meta;        // [ntiles][RT_TILE] directory slot within the bucket << 12 | record index within the tile
   uint16_t* seg;         // [ntiles][nbq + 1] start of each bin's segment in the tile; [nbq] = routed count
   int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
-  unsigned long long* dlist;    // direct-path records: (batch index << 32) | (slot << 1) | per-element fire
+  unsigned long long* dlist;    // direct-list records: (batch index << 1) | per-element fire
   unsigned long long* dcount;   // this batch's direct-list length (a ring of DC_RING counters, one per batch)
   unsigned long long* dcount_reset;   // the counter of batch j + DC_RING/2: zeroed by k_aggregate of batch j
   int64_t dcap;
@@ -479,9 +491,8 @@ struct RouteBuf {
   int32_t dbg;
 };
 
-// Non-temporal access of the streamed columns, a bit mask: 1 = k_route's input loads (on: k_route 43 ->
-// 41 us per 4 Mi-event batch), 2 = k_aggregate's gathers of the routed records, 4 = k_route's stores of
-// them (both measured slower: k_aggregate 36 -> 38-40 us, the intermediate is re-read from the cache)
+// Non-temporal access of the streamed columns, a bit mask: 1 = k_route's input loads (streamed once per
+// batch, so they do not evict the directory and the routed records k_aggregate reads next)
 #ifndef FW_ROUTE_NT
 #define FW_ROUTE_NT 1
 #endif
@@ -530,6 +541,16 @@ __device__ __forceinline__ void block_scan_excl(int32_t* a, int n, int32_t* wtot
   __syncthreads();
 }
 
+// LDS layout of k_route (bytes): [0, 48K) per-record staging, reused phase by phase (each phase's
+// entries are written and read by the thread owning the record, so no barrier separates them):
+//   phase A/B1   key hashes int32[4096] at 0 (optional column)
+//   slow path    flags int32[4096] at 0 (the record's key hash is read before), slice numbers int64[4096] at 16K
+//   directory    slots of the records that missed their home group, uint32[4096] at 0
+//   scatter      values int64[4096] at 0, meta uint32[4096] at 32K (after the barriers of the scan)
+// then the bin counters, the scan scratch and the tile's slice set.
+constexpr size_t RT_LDS_STAGE = (size_t)RT_TILE * 12;
+constexpr size_t RT_LDS = RT_LDS_STAGE + 4 * (size_t)(RT_Q * RT_MAXNB + 8) + 4 * 16 + 8 * RT_Q;
+
 template <int VT, int AGG, bool FIRST>
 __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, const RouteBuf& r, unsigned char* smem,
                                            const bool tail) {
@@ -537,25 +558,25 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   constexpr int PER = RT_TILE / NT;     // records per thread
   constexpr int V = PER / 2;            // 16-B vectors per column per thread
   const int nbq = RT_Q * s.nb;
-  longlong2* st_kv = (longlong2*)smem;
-  uint16_t* st_idx = (uint16_t*)(st_kv + RT_TILE);
-  int32_t* cnt = (int32_t*)(st_idx + RT_TILE);   // [nbq + 1]
-  int32_t* wtot = cnt + (RT_Q * 256 + 8);        // [NT / 64]
-  int64_t* lset = (int64_t*)(wtot + 16);         // [RT_Q] the tile's routed slices
+  int64_t* st_val = (int64_t*)smem;
+  uint32_t* st_meta = (uint32_t*)(smem + (size_t)RT_TILE * 8);
+  int32_t* cnt = (int32_t*)(smem + RT_LDS_STAGE);   // [nbq + 1]
+  int32_t* wtot = cnt + (RT_Q * RT_MAXNB + 8);      // [NT / 64]
+  int64_t* lset = (int64_t*)(wtot + 16);            // [RT_Q] the tile's routed slices
+  int32_t* lhash = (int32_t*)smem;                  // Java key hashes (optional column)
   const int64_t base = (int64_t)blockIdx.x * RT_TILE;
+  const uint64_t kbm = (1ull << s.kb_bits) - 1;
   FW_STAMP(r, 0, 0);
   for (int x = threadIdx.x; x <= nbq; x += NT) cnt[x] = 0;
   if (threadIdx.x < RT_Q) lset[threadIdx.x] = FREE_TAG;
   // phase A: every load of the tile in flight before any dependent work; record (j, e) of this thread
   // is tile index 2 * (j * NT + tid) + e
   int64_t kk[PER], tt[PER], vv[PER];
-  int32_t* lhash = (int32_t*)st_kv;     // Java key hashes (optional column) parked in st_kv until the scatter
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
     if (!tail) {
 #if FW_ROUTE_NT & 1
-      // streamed once per batch: non-temporal, so the routed intermediate k_aggregate reads next keeps the cache
       typedef long long v2i64 __attribute__((ext_vector_type(2)));
       const v2i64 a = __builtin_nontemporal_load((const v2i64*)(b.key + i));
       const v2i64 c = __builtin_nontemporal_load((const v2i64*)(b.ts + i));
@@ -580,7 +601,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
       }
     }
   }
-  __syncthreads();   // cnt zeroed, key hashes parked
+  __syncthreads();   // cnt and lset initialised
   FW_STAMP(r, 0, 1);
   // phase B1: per record operator work (timestamp, key group, windows, lateness) — pure ALU; the slice
   // number replaces the timestamp in tt[]
@@ -634,8 +655,8 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   // the full assignment for the rest: one call-free copy of the code (a call would make the register
   // allocator spill the tile around it), timestamps re-read from the input, results through LDS
   if (__any(slow_mask != 0)) {
-    int64_t* sm = (int64_t*)st_kv + RT_TILE / 2;     // [RT_TILE] slice numbers, after the parked key hashes
-    int32_t* sf = (int32_t*)(sm + RT_TILE);          // [RT_TILE] flags: live | late_fire << 1 | n_late << 2
+    int32_t* sf = (int32_t*)smem;                            // [RT_TILE] flags: live | late_fire << 1 | n_late << 2
+    int64_t* sm = (int64_t*)(smem + (size_t)RT_TILE * 4);    // [RT_TILE] slice numbers
 #pragma unroll 1
     for (int k = 0; k < PER; ++k) {
       if ((slow_mask >> k) & 1u) {
@@ -668,9 +689,9 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     }
   }
   // phase B2: the routed records' index in the tile's slice set — resolved once per wave when all its
-  // routed records share one slice (an in-order stream), per record otherwise — then their bin and
-  // counting-sort rank.  The rest join the direct list (rare: per-element fires, slices beyond the
-  // tile's RT_Q, the Long.MIN_VALUE key), applied by the k_aggregate workgroup owning the key's bucket.
+  // routed records share one slice (an in-order stream), per record otherwise.  The rest join the direct
+  // list (rare: per-element fires, slices beyond the tile's RT_Q, the Long.MIN_VALUE key), applied by
+  // the k_aggregate workgroup owning the key's bucket.
   int64_t m_ref = INT64_MIN;
   {
     const uint64_t lm = __ballot(route_mask != 0);
@@ -692,23 +713,82 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     q_ref = __shfl(q_ref, __ffsll((long long)__ballot(route_mask != 0)) - 1);
   }
   const bool wave_uniform = __all(same);
+  int32_t qq[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const bool routable = (route_mask >> k) & 1u;
+    int32_t q = -1;
+    if (wave_uniform) q = routable ? q_ref : -1;
+    else if (routable) q = tile_slice(lset, tt[k]);
+    qq[k] = q;
+    if (routable && q < 0) {   // the tile's slice set is full
+      route_mask &= ~(1u << k);
+      direct_mask |= 1u << k;
+    }
+  }
+  // phase B3: directory slot of every routed record — the aligned 4-slot group holding its home slot,
+  // two 16-B loads from the L2-resident directory, four records' loads in flight at a time; the keys not
+  // found there (first sight of a key, or an overflowed group) take the probe/insert loop below
+  uint32_t slot[PER];
+  uint32_t miss_mask = 0;
+#pragma unroll
+  for (int h4 = 0; h4 < PER; h4 += 4) {
+    longlong2 ga[4], gb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = h4 + u;
+      const uint64_t hk = fmix64((uint64_t)kk[k]);
+      const int64_t g = (int64_t)(hk & s.dir_mask & ~(uint64_t)(DIR_GROUP - 1));
+      const longlong2* gp = (const longlong2*)(s.dir_keys + (((route_mask >> k) & 1u) ? g : 0));
+      if (r.dbg & 64) { ga[u] = make_longlong2(kk[k], 0); gb[u] = make_longlong2(0, 0); continue; }   // ablation: no probe
+      ga[u] = gp[0];
+      gb[u] = (r.dbg & 128) ? make_longlong2(0, 0) : gp[1];   // ablation: first half only
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = h4 + u;
+      const int64_t key = kk[k];
+      const uint32_t g = (uint32_t)(fmix64((uint64_t)key) & kbm & ~(uint64_t)(DIR_GROUP - 1));
+      uint32_t sl = NO_FIRST;
+      sl = gb[u].y == key ? g + 3 : sl;
+      sl = gb[u].x == key ? g + 2 : sl;
+      sl = ga[u].y == key ? g + 1 : sl;
+      sl = ga[u].x == key ? g : sl;
+      slot[k] = sl;
+      miss_mask |= (((route_mask >> k) & 1u) && sl == NO_FIRST ? 1u : 0u) << k;
+    }
+  }
+  if (__any(miss_mask != 0)) {
+    uint32_t* ms = (uint32_t*)smem;   // [RT_TILE] slots of the missed records
+#pragma unroll 1
+    for (int k = 0; k < PER; ++k) {
+      if ((miss_mask >> k) & 1u) {
+        const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
+        const int64_t kid = dir_lookup(s, b.key[base + t]);
+        if (kid < 0) set_error(s.err, FW_ERR_CAPACITY);
+        ms[t] = kid < 0 ? NO_FIRST : (uint32_t)((uint64_t)kid & kbm);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if ((miss_mask >> k) & 1u) {
+        const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
+        slot[k] = ms[t];
+        if (slot[k] == NO_FIRST) route_mask &= ~(1u << k);   // directory bucket full: reported above
+      }
+    }
+  }
+  // bins and counting-sort ranks
   int32_t bin[PER];       // routed bin, or -1
   int32_t rank[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     bin[k] = -1;
     rank[k] = 0;
-    const bool routable = (route_mask >> k) & 1u;
-    int32_t q = -1;
-    if (wave_uniform) q = routable ? q_ref : -1;
-    else if (routable) q = tile_slice(lset, tt[k]);
-    if (q >= 0) {
+    if ((route_mask >> k) & 1u) {
       const uint64_t hk = fmix64((uint64_t)kk[k]);
-      bin[k] = q * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
+      bin[k] = qq[k] * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
       rank[k] = atomicAdd(&cnt[bin[k]], 1);
-      kk[k] = (int64_t)hk;   // routed records carry the directory hash (a bijection of the key)
-    } else if (routable) {
-      direct_mask |= 1u << k;   // the tile's slice set is full
     }
   }
   if (__any(late_pairs != 0)) {
@@ -727,7 +807,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
       }
     }
   }
-  __syncthreads();   // every wave's slice claims are in lset
+  __syncthreads();   // every wave's slice claims are in lset, every staging read is done
   if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
   FW_STAMP(r, 0, 2);
   block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
@@ -737,33 +817,25 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   for (int k = 0; k < PER; ++k) {
     if (bin[k] >= 0) {
       const int32_t pos = cnt[bin[k]] + rank[k];
-      st_kv[pos] = make_longlong2(kk[k], vv[k]);
-      st_idx[pos] = (uint16_t)(2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1));
+      st_val[pos] = vv[k];
+      st_meta[pos] = (slot[k] << IDX_BITS) | (uint32_t)(2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1));
     }
   }
   __syncthreads();
   FW_STAMP(r, 0, 3);
   const int32_t total = cnt[nbq];
-#pragma unroll 2
-  for (int k = 0; k < PER; ++k) {
-    const int32_t pos = k * NT + (int)threadIdx.x;
-#if FW_ROUTE_NT & 4
-    if (pos < total) {
-      typedef long long v2i64 __attribute__((ext_vector_type(2)));
-      const longlong2 x = st_kv[pos];
-      v2i64 g; g.x = x.x; g.y = x.y;
-      __builtin_nontemporal_store(g, (v2i64*)(r.kv + base + pos));
-    }
-#else
-    if (pos < total) r.kv[base + pos] = st_kv[pos];
-#endif
-  }
-  if (FIRST) {
+  // write-out: 16-B stores of the values (two per lane), 16-B stores of the meta words (four per lane)
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
-      if (pos < total) *(uint32_t*)(r.idx + base + pos) = *(const uint32_t*)(st_idx + pos);
-    }
+  for (int j = 0; j < V; ++j) {
+    const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
+    if (pos + 1 < total) *(longlong2*)(r.val + base + pos) = *(const longlong2*)(st_val + pos);
+    else if (pos < total) r.val[base + pos] = st_val[pos];
+  }
+#pragma unroll
+  for (int j = 0; j < PER / 4; ++j) {
+    const int32_t pos = 4 * (j * NT + (int)threadIdx.x);
+    if (pos + 3 < total) *(uint4*)(r.meta + base + pos) = *(const uint4*)(st_meta + pos);
+    else for (int e = 0; e < 4; ++e) if (pos + e < total) r.meta[base + pos + e] = st_meta[pos + e];
   }
   FW_STAMP(r, 0, 4);
 }
@@ -775,24 +847,18 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, Rout
   route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(blockIdx.x + 1) * RT_TILE > b.n);
 }
 
-// the bucket's LDS directory-hash table: slot of h, inserting its key (fmix64_inv(h)) into the global
-// directory if absent.  Out of line: taken by a wave only when a lane misses the four probed slots.
-__device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h) {
-  uint32_t x = (uint32_t)h & kbm;
-  for (uint32_t probe = 0; probe <= kbm; ++probe) {
-    const uint64_t cur = lh[x];
-    if (cur == h) return (int32_t)x;
-    if (cur == EMPTY_H) {
-      const int64_t key = (int64_t)fmix64_inv(h);
-      const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[x], (unsigned long long)EMPTY_KEY,
-                                                (unsigned long long)key);
-      const uint64_t now = (int64_t)prev == EMPTY_KEY ? h : fmix64(prev);
-      lh[x] = now;   // only globally confirmed keys enter the cache
-      if (now == h) return (int32_t)x;
-    }
-    x = (x + 1) & kbm;
+// one record into the bucket's LDS accumulators at slot kl
+template <int VT, int AGG>
+__device__ __forceinline__ void acc_add(int64_t* lsum, int64_t* lmin, int64_t* lmax, int64_t* lcnt, uint32_t* lfirst,
+                                        uint32_t kl, int64_t v, uint32_t oi) {
+  if (AGG & FW_AGG_SUM) {
+    if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
+    else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
   }
-  return -1;
+  if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
+  if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
+  if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
+  atomicMin(&lfirst[kl], oi);   // earliest record of the batch: the first arrival, and the "touched" mark
 }
 
 template <int VT, int AGG, bool FIRST>
@@ -801,46 +867,36 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   constexpr int NT = AG_THREADS;
   // XCD-aware bucket order: workgroups are dealt to the 8 XCDs round-robin, so XCD x runs the
   // contiguous bucket range [x * nb/8, (x + 1) * nb/8).  Neighbouring buckets' segments share the
-  // 128-B lines at their boundaries (records and first-arrival indices alike); with both readers on one
-  // XCD the second read hits that XCD's L2 instead of going back to HBM
+  // 128-B lines at their boundaries; with both readers on one XCD the second read hits that XCD's L2
   const int bkt = (s.nb % 8 == 0 && !(r.dbg & 32)) ? (int)(blockIdx.x % 8) * (s.nb / 8) + (int)(blockIdx.x / 8)
                                                     : (int)blockIdx.x;
   const int nbq = RT_Q * s.nb;
   const int KB = 1 << s.kb_bits;
-  const uint32_t kbm = (uint32_t)KB - 1;
-  uint64_t* lh = (uint64_t*)smem;                       // [KB] fmix64 of this bucket's directory slice (EMPTY_H = free)
-  const int KA = KB + 64;                               // accumulator slots: KB + one dummy per lane
-  int64_t* lsum = (int64_t*)(lh + KB);                  // [KA]
-  int64_t* lmin = lsum + KA;                            // [KA] (AGG 15)
+  const int KA = KB + 65;                               // accumulators: KB slots, one dummy per lane, the MIN key
+  const uint32_t KMIN = (uint32_t)KB + 64;              // slot of the Long.MIN_VALUE key (kid D, bucket 0)
+  int64_t* lsum = (int64_t*)smem;                       // [KA]
+  int64_t* lmin = lsum + KA;
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KA : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KA : 0);
-  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest record (tile << 12 | index)
-  int32_t* sst = (int32_t*)(lfirst + KA);               // [ntiles] segment start within the tile
+  uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest record (batch index)
+  int32_t* sst = (int32_t*)(lfirst + ((KA + 3) & ~3));  // [ntiles] segment start within the tile
   int32_t* off = sst + r.ntiles;                        // [ntiles + 1] segment lengths, then their exclusive prefix
   int32_t* step_tile = off + r.ntiles + 1;              // [AG_CHS] tile holding the first record of each step
   int32_t* awtot = step_tile + AG_CHS;                  // [16] scan scratch
+  int64_t* gsl = (int64_t*)(((uintptr_t)(awtot + 16) + 7) & ~(uintptr_t)7);   // [RT_GS] the batch's slices
+  int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
   const int64_t dbase = (int64_t)bkt * KB;
   const int64_t SB = (int64_t)8 << 16;
   FW_STAMP(r, SB, 0);
-  // issued together with the directory-slice load: this thread's tile header and the bucket's segment
-  // bounds in both bin groups of that tile (tiles beyond the first NT are read where they are used)
-  int64_t ph[RT_Q] = {FREE_TAG, FREE_TAG};
-  uint32_t pseg[RT_Q] = {0u, 0u};   // segment start | end << 16
-  if ((int)threadIdx.x < r.ntiles) {
-    const uint16_t* seg = r.seg + (int64_t)threadIdx.x * (nbq + 1);
-#pragma unroll
-    for (int q = 0; q < RT_Q; ++q) {
-      ph[q] = r.hdr[(int64_t)threadIdx.x * RT_Q + q];
-      pseg[q] = (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16);
-    }
-  }
-  // also in flight with the directory slice: the direct-list length and the slot claim of tile 0's first
-  // routed slice (nearly always the batch's only one; slice_slot is idempotent, so claiming it before
-  // the round that uses it changes nothing).  The accumulators are cleared meanwhile; each fold resets
-  // the entries it consumed for the next round
   const int64_t nd = min((int64_t)*r.dcount, r.dcap);
+  // claimed early (slice_slot is idempotent): the slot of tile 0's first routed slice, nearly always the
+  // batch's only one
+  int64_t m_pre = FREE_TAG;
   int32_t pre_p = -1;
-  if (threadIdx.x == 0 && r.ntiles > 0 && ph[0] != FREE_TAG) pre_p = slice_slot(s, ph[0]);
+  if (threadIdx.x == 0 && r.ntiles > 0) {
+    m_pre = r.hdr[0];
+    if (m_pre != FREE_TAG) pre_p = slice_slot(s, m_pre);
+  }
   for (int x = threadIdx.x; x < KA; x += NT) {
     lsum[x] = 0;
     if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
@@ -848,133 +904,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
     lfirst[x] = NO_FIRST;
   }
-  for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
-  __syncthreads();
-  FW_STAMP(r, SB, 1);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-
-  // directory hash -> slot in this bucket.  Linear probing keeps a key within the run that starts at
-  // its home slot, so the first four slots are compared without branching (the directory's load factor
-  // <= 1/4 keeps nearly every key there); the loop takes the rest and inserts new keys (a global CAS on
-  // the key, fmix64_inv(h), confirms every slot before it enters the LDS copy)
-  auto find_slow = [&](uint64_t h, uint32_t& kl) -> bool {
-    const int32_t x = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h);
-    if (x < 0) return false;
-    kl = (uint32_t)x;
-    return true;
-  };
-  // one record into the bucket's LDS accumulators.  Straight-line on the common path: inactive lanes
-  // update a private dummy slot (KB + lane) instead of being masked off, and a miss of the AG_WIN probed
-  // slots takes one wave-uniform branch to the out-of-line probe/insert.  The window covers the
-  // displacements linear probing produces at the directory's load factor <= 1/4 (a key 8 or more
-  // slots from home: ~6e-5 of them, so a wave takes the branch ~0.4 % of the time; at 4 slots it
-  // was ~18 %, which cost a third of the kernel)
-  auto process = [&](bool act, uint64_t h, int64_t v, uint32_t oi) {
-    const uint32_t h0 = (uint32_t)h & kbm;
-    uint32_t kl = h0;
-    bool found = false;
-#pragma unroll
-    for (int j = AG_WIN - 1; j >= 0; --j) {   // the nearest match wins
-      const uint32_t x = (h0 + j) & kbm;
-      const bool m = lh[x] == h;
-      kl = m ? x : kl;
-      found |= m;
-    }
-    const bool miss = act && !found;
-    if (__any(miss)) {
-      // second window, still inline: the few keys displaced 8+ slots cluster in a few buckets, where a
-      // call on every such wave (its live registers saved around it) doubled the bucket's time
-      // (tools/stamps.py: the slowest workgroups were always the same buckets)
-      bool found2 = false;
-#pragma unroll
-      for (int j = 2 * AG_WIN - 1; j >= AG_WIN; --j) {
-        const uint32_t x = (h0 + j) & kbm;
-        const bool m = lh[x] == h;
-        kl = (miss && m) ? x : kl;
-        found2 |= m;
-      }
-      const bool miss2 = miss && !found2;
-      if (__any(miss2)) {
-        if (miss2 && !find_slow(h, kl)) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
-      }
-    }
-    kl = act ? kl : (uint32_t)KB + (uint32_t)lane;
-    if (AGG & FW_AGG_SUM) {
-      if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
-      else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
-    }
-    if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
-    if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
-    if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
-    atomicMin(&lfirst[kl], oi);
-  };
-
-  const int64_t ord_base = b.ord_base;
-  // direct-path records of this bucket (listed by k_route): per-element fires join the late list, the
-  // rest update their pane with device-scope atomics; no other workgroup touches this bucket's panes,
-  // and none of them is a pane the LDS fold below writes (other slice, or the Long.MIN_VALUE key column)
+  if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
   // no memset between batches: batch j's counter was zeroed by k_aggregate of batch j - DC_RING/2, whose
   // counter is no longer read and whose successor k_route starts only after this kernel (event order)
   if (blockIdx.x == 0 && threadIdx.x == 0) *r.dcount_reset = 0;
-  if (nd > 0) {
-    for (int64_t x0 = 0; x0 < nd; x0 += NT) {
-      const int64_t x = x0 + threadIdx.x;
-      const unsigned long long ent = x < nd ? r.dlist[x] : 0ull;
-      const int64_t i = (int64_t)(ent >> 1);
-      const bool fire = (ent & 1ull) != 0;
-      const int64_t key = x < nd ? b.key[i] : 0;
-      bool mine = x < nd && (key == EMPTY_KEY ? bkt == 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) == bkt);
-      int64_t kid = -1;
-      int32_t p = -1;
-      if (mine) {
-        p = slice_slot(s, record_windows(s, b.ts[i], b.wm).m);   // claimed by k_route unless its tile set overflowed
-        if (p < 0) { set_error(s.err, FW_ERR_CAPACITY); mine = false; }
-      }
-      if (mine) {
-        uint32_t kl = 0;
-        if (key == EMPTY_KEY) { kid = dir_find_or_insert(s, key); }
-        else if (find_slow(fmix64((uint64_t)key), kl)) kid = dbase + kl;
-        if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); mine = false; }
-      }
-      const bool want = mine && fire && b.late_key != nullptr;
-      const unsigned long long pos = wave_append(b.late_count, want);
-      if (want) {
-        if ((int64_t)pos < b.late_capacity) {
-          const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
-          b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
-        } else {
-          set_error(s.err, FW_ERR_CAPACITY);
-        }
-      }
-      if (mine && !fire) pane_update<VT, AGG, FIRST>(s, (int64_t)p * s.stride + kid, b.val[i], ord_base + i);
-    }
-    __syncthreads();
-    if (FIRST) {   // f1 of panes whose first arrival is a direct record of this batch
-      for (int64_t x = threadIdx.x; x < nd; x += NT) {
-        const unsigned long long ent = r.dlist[x];
-        if (ent & 1ull) continue;
-        const int64_t i = (int64_t)(ent >> 1);
-        const int64_t key = b.key[i];
-        if (key == EMPTY_KEY ? bkt != 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) != bkt) continue;
-        uint32_t kl = 0;
-        int64_t kid = -1;
-        if (key == EMPTY_KEY) kid = s.D;
-        else if (find_slow(fmix64((uint64_t)key), kl)) kid = dbase + kl;
-        if (kid < 0) continue;
-        const int32_t p = (int32_t)floor_mod(record_windows(s, b.ts[i], b.wm).m, s.P);
-        const int64_t idx = (int64_t)p * s.stride + kid;
-        if (__hip_atomic_load(&s.c.first[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ord_base + i)
-          s.c.f1v[idx] = f1col[i];
-      }
-    }
-    __syncthreads();
-  }
-
-  // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same set)
-  int64_t* gsl = (int64_t*)(((uintptr_t)(awtot + 16) + 7) & ~(uintptr_t)7);   // [RT_GS]
-  int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
-  if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
   __syncthreads();
+  FW_STAMP(r, SB, 1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ord_base = b.ord_base;
   auto gsl_insert = [&](int64_t m) {
     int g = 0;
     for (; g < RT_GS; ++g) {
@@ -987,21 +924,40 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     }
     if (g == RT_GS) set_error(s.err, FW_ERR_CAPACITY);   // more distinct slices in one batch than RT_GS
   };
-  // the first NT tiles from registers (ph = FREE_TAG beyond ntiles): a lane whose slice equals its left
-  // neighbour's leaves the insert to it, so a wave of an in-order stream inserts once, not 64 times
-  // (same-address LDS atomics serialise)
-#pragma unroll
-  for (int qq = 0; qq < RT_Q; ++qq) {
-    const int64_t m = ph[qq];
-    const int64_t left = __shfl_up(m, 1);
-    const bool dup = (threadIdx.x & 63) != 0 && left == m;
-    if (m != FREE_TAG && !dup) gsl_insert(m);
+  // direct-list records of this bucket: per-element fires join the late list (k_late_* apply them after
+  // this kernel, in arrival order); the others are added in the round of their slice below
+  auto direct_mine = [&](int64_t key) {
+    return key == EMPTY_KEY ? bkt == 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) == bkt;
+  };
+  for (int64_t x = threadIdx.x; x < nd; x += NT) {
+    const unsigned long long ent = r.dlist[x];
+    const int64_t i = (int64_t)(ent >> 1);
+    const int64_t key = b.key[i];
+    if (!direct_mine(key)) continue;
+    const int64_t m = record_windows(s, b.ts[i], b.wm).m;
+    if (!(ent & 1ull)) { gsl_insert(m); continue; }
+    if (b.late_key == nullptr) continue;
+    const int32_t p = slice_slot(s, m);
+    const int64_t kid = dir_lookup(s, key);
+    if (p < 0 || kid < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+    const unsigned long long pos = atomicAdd(b.late_count, 1ull);
+    if ((int64_t)pos < b.late_capacity) {
+      const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
+      b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
+    } else {
+      set_error(s.err, FW_ERR_CAPACITY);
+    }
   }
-  for (int t = NT + threadIdx.x; t < r.ntiles; t += NT) {
-    for (int qq = 0; qq < RT_Q; ++qq) {
-      const int64_t m = r.hdr[(int64_t)t * RT_Q + qq];
-      if (m == FREE_TAG) break;
-      gsl_insert(m);
+  // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same
+  // set).  A lane whose slice equals its left neighbour's leaves the insert to it, so a wave of an
+  // in-order stream inserts once, not 64 times (same-address LDS atomics serialise)
+  for (int t0 = 0; t0 < r.ntiles; t0 += NT) {   // uniform
+    const int t = t0 + (int)threadIdx.x;
+    for (int q = 0; q < RT_Q; ++q) {
+      const int64_t m = t < r.ntiles ? r.hdr[(int64_t)t * RT_Q + q] : FREE_TAG;
+      const int64_t left = __shfl_up(m, 1);
+      const bool dup = lane != 0 && left == m;
+      if (m != FREE_TAG && !dup) gsl_insert(m);
     }
   }
   __syncthreads();
@@ -1011,24 +967,18 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     // pane-slot claim: authoritative here, after every earlier watermark (engine stream order); slot
     // p = floor_mod(m, P) is claimed by whichever workgroup comes first, the rest find it taken by m
     __syncthreads();   // every thread has read the previous round's lclaim
-    if (threadIdx.x == 0) lclaim = (pre_p >= 0 && m == ph[0]) ? pre_p : slice_slot(s, m);
+    if (threadIdx.x == 0) lclaim = (pre_p >= 0 && m == m_pre) ? pre_p : slice_slot(s, m);
     __syncthreads();
     const int32_t p = lclaim;
     if (p < 0) { if (threadIdx.x == 0) set_error(s.err, FW_ERR_CAPACITY); continue; }   // slice pool exhausted
-    const int q = g;
     for (int t = threadIdx.x; t < r.ntiles; t += NT) {
       int32_t a0 = 0, a1 = 0;
-      if (t == (int)threadIdx.x) {
-        const int ql = ph[0] == m ? 0 : (ph[1] == m ? 1 : -1);
-        if (ql >= 0) { a0 = (int32_t)(pseg[ql] & 0xFFFFu); a1 = (int32_t)(pseg[ql] >> 16); }
-      } else {
-        const int64_t h0 = r.hdr[(int64_t)t * RT_Q], h1 = r.hdr[(int64_t)t * RT_Q + 1];
-        const int ql = h0 == m ? 0 : (h1 == m ? 1 : -1);
-        if (ql >= 0) {
+      for (int q = 0; q < RT_Q; ++q) {
+        if (r.hdr[(int64_t)t * RT_Q + q] == m) {
           const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
-          const int bin = ql * s.nb + bkt;
-          a0 = seg[bin];
-          a1 = seg[bin + 1];
+          a0 = seg[q * s.nb + bkt];
+          a1 = seg[q * s.nb + bkt + 1];
+          break;
         }
       }
       sst[t] = a0;
@@ -1038,13 +988,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     __syncthreads();
     block_scan_excl<NT, AG_MAXPER>(off, r.ntiles + 1, awtot);   // off[ntiles] = the bucket's records of slice m
     const int32_t R = off[r.ntiles];
-    FW_STAMP(r, SB, 2 + 3 * min(q, 1));
+    FW_STAMP(r, SB, 2 + 3 * min(g, 1));
     // dense assignment: the bucket's records of slice m, concatenated over the tiles in order (record
     // rr lies in the tile t with off[t] <= rr < off[t + 1]), are taken 64 at a time, one per lane, in
     // wave steps; the tile of each step's first record is tabulated per chunk of AG_CHS steps, a lane
     // walks forward from it (a step spans ~4 segments at 256 buckets), and every load of a wave's UR
-    // steps is issued before any of them is processed.  lfirst keeps the pane's earliest record of the
-    // batch as (tile << 12 | index in the tile): tiles are consecutive ranges of the batch
+    // steps is issued before any of them is processed
     constexpr int UR = 2;
     for (int32_t cb = 0; cb < R; cb += AG_CHS * 64) {   // uniform
       for (int t = threadIdx.x; t < r.ntiles; t += NT) {
@@ -1056,100 +1005,99 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       __syncthreads();
       const int32_t nsteps = min(AG_CHS, (R - cb + 63) >> 6);
       // one group = UR steps of this wave: addresses from the step table, loads issued, nothing waited on
-      auto load_group = [&](int32_t s0, longlong2* rv, uint32_t* ri, bool* ra) {
+      auto load_group = [&](int32_t s0, int64_t* rv, uint32_t* rm, uint32_t* rt) {
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
           const int32_t st = s0 + u;
           const int32_t rr = cb + 64 * st + lane;
-          ra[u] = st < nsteps && rr < R;
+          const bool act = st < nsteps && rr < R;
           int32_t t = 0;
           int64_t pos = 0;   // inactive lanes read tile 0's first slot
-          if (ra[u]) {
+          if (act) {
             t = step_tile[st];
             while (off[t + 1] <= rr) ++t;
             pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
           }
-#if FW_ROUTE_NT & 2
-          {
-            typedef long long v2i64 __attribute__((ext_vector_type(2)));
-            const v2i64 g = __builtin_nontemporal_load((const v2i64*)(r.kv + pos));
-            rv[u] = make_longlong2(g.x, g.y);
-          }
-#else
-          rv[u] = r.kv[pos];
-#endif
-          ri[u] = ((uint32_t)t << 12) | (FIRST ? (uint32_t)r.idx[pos] : 0u);
+          rv[u] = r.val[pos];
+          rm[u] = r.meta[pos];
+          rt[u] = act ? (uint32_t)t : NO_FIRST;
+        }
+      };
+      auto process_group = [&](const int64_t* rv, const uint32_t* rm, const uint32_t* rt) {
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+          const bool act = rt[u] != NO_FIRST;
+          const uint32_t kl = act ? rm[u] >> IDX_BITS : (uint32_t)KB + (uint32_t)lane;
+          const uint32_t oi = act ? (rt[u] << IDX_BITS) | (rm[u] & ((1u << IDX_BITS) - 1)) : 0u;
+          acc_add<VT, AGG>(lsum, lmin, lmax, lcnt, lfirst, kl, rv[u], oi);
         }
       };
       // software pipelined: the next group's loads are in flight while this group updates LDS (two
       // register sets, the loop unrolled by two so that both stay in registers)
-      longlong2 rvA[UR], rvB[UR];
-      uint32_t riA[UR], riB[UR];
-      bool raA[UR], raB[UR];
+      int64_t rvA[UR], rvB[UR];
+      uint32_t rmA[UR], rmB[UR], rtA[UR], rtB[UR];
       constexpr int32_t G = (NT / 64) * UR;
       int32_t s0 = wave * UR;
-      if (s0 < nsteps) load_group(s0, rvA, riA, raA);
+      if (s0 < nsteps) load_group(s0, rvA, rmA, rtA);
       while (s0 < nsteps) {   // wave-uniform
-        if (s0 + G < nsteps) load_group(s0 + G, rvB, riB, raB);
-        if (r.dbg & 1) {   // diagnostics: loads only
-          int64_t x = 0;
-#pragma unroll
-          for (int u = 0; u < UR; ++u) x ^= rvA[u].x ^ rvA[u].y ^ riA[u];
-          if (x == 0x123456789) lsum[KB + lane] = x;
-        } else {
-#pragma unroll
-          for (int u = 0; u < UR; ++u) process(raA[u], (uint64_t)rvA[u].x, rvA[u].y, riA[u]);
-        }
+        if (s0 + G < nsteps) load_group(s0 + G, rvB, rmB, rtB);
+        process_group(rvA, rmA, rtA);
         s0 += G;
         if (s0 >= nsteps) break;
-        if (s0 + G < nsteps) load_group(s0 + G, rvA, riA, raA);
-        if (r.dbg & 1) {   // diagnostics: loads only
-          int64_t x = 0;
-#pragma unroll
-          for (int u = 0; u < UR; ++u) x ^= rvB[u].x ^ rvB[u].y ^ riB[u];
-          if (x == 0x123456789) lsum[KB + lane] = x;
-        } else {
-#pragma unroll
-          for (int u = 0; u < UR; ++u) process(raB[u], (uint64_t)rvB[u].x, rvB[u].y, riB[u]);
-        }
+        if (s0 + G < nsteps) load_group(s0 + G, rvA, rmA, rtA);
+        process_group(rvB, rmB, rtB);
         s0 += G;
       }
       __syncthreads();   // the next chunk rewrites step_tile
     }
-    __syncthreads();
-    FW_STAMP(r, SB, 3 + 3 * min(q, 1));
-    // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
-    // (direct-path updates of k_route finished before this kernel started)
-    for (int x = threadIdx.x; x < KB; x += NT) {
-      const uint32_t lf = lfirst[x];
-      if (lf == NO_FIRST) continue;
-      const int64_t idx = (int64_t)p * s.stride + dbase + x;
-      if (AGG & FW_AGG_SUM) {
-        if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[x]);
-        else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(lsum[x]));
+    // this bucket's direct records of slice m (rare): the same accumulators, ordered by batch index
+    if (nd > 0) {
+      for (int64_t x = threadIdx.x; x < nd; x += NT) {
+        const unsigned long long ent = r.dlist[x];
+        if (ent & 1ull) continue;
+        const int64_t i = (int64_t)(ent >> 1);
+        const int64_t key = b.key[i];
+        if (!direct_mine(key) || record_windows(s, b.ts[i], b.wm).m != m) continue;
+        const int64_t kid = dir_lookup(s, key);
+        if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+        const uint32_t kl = key == EMPTY_KEY ? KMIN : (uint32_t)(kid - dbase);
+        acc_add<VT, AGG>(lsum, lmin, lmax, lcnt, lfirst, kl, b.val[i], (uint32_t)i);
       }
-      if (AGG & FW_AGG_MIN) { const int64_t o = s.c.mn[idx]; if (lmin[x] < o) s.c.mn[idx] = lmin[x]; }
-      if (AGG & FW_AGG_MAX) { const int64_t o = s.c.mx[idx]; if (lmax[x] > o) s.c.mx[idx] = lmax[x]; }
-      if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[x]);
+    }
+    __syncthreads();
+    FW_STAMP(r, SB, 3 + 3 * min(g, 1));
+    // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
+    for (int x = threadIdx.x; x <= KB; x += NT) {
+      if (x == KB && bkt != 0) continue;
+      const uint32_t xl = x < KB ? (uint32_t)x : KMIN;
+      const uint32_t lf = lfirst[xl];
+      if (lf == NO_FIRST) continue;
+      const int64_t idx = (int64_t)p * s.stride + (x < KB ? dbase + x : s.D);
+      if (AGG & FW_AGG_SUM) {
+        if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[xl]);
+        else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(lsum[xl]));
+      }
+      if (AGG & FW_AGG_MIN) { const int64_t o = s.c.mn[idx]; if (lmin[xl] < o) s.c.mn[idx] = lmin[xl]; }
+      if (AGG & FW_AGG_MAX) { const int64_t o = s.c.mx[idx]; if (lmax[xl] > o) s.c.mx[idx] = lmax[xl]; }
+      if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[xl]);
       if (FIRST) {
-        // first arrival: the pane's earliest routed record of the batch
-        const int64_t bi = (int64_t)(lf >> 12) * RT_TILE + (lf & (RT_TILE - 1));
-        if (ord_base + bi < s.c.first[idx]) {
-          s.c.first[idx] = ord_base + bi;
-          s.c.f1v[idx] = f1col[bi];
+        // first arrival: the pane's earliest record of the batch, if the pane is new
+        if (ord_base + (int64_t)lf < s.c.first[idx]) {
+          s.c.first[idx] = ord_base + (int64_t)lf;
+          s.c.f1v[idx] = f1col[lf];
         }
       } else {
         s.c.present[idx] = 1;
       }
       // cleared for the next round (untouched entries still are; the per-lane dummies are never read)
-      lsum[x] = 0;
-      if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
-      if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
-      if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
-      lfirst[x] = NO_FIRST;
+      lsum[xl] = 0;
+      if (AGG & FW_AGG_MIN) lmin[xl] = INT64_MAX;
+      if (AGG & FW_AGG_MAX) lmax[xl] = INT64_MIN;
+      if (AGG & FW_AGG_COUNT) lcnt[xl] = 0;
+      lfirst[xl] = NO_FIRST;
     }
     __syncthreads();
-    FW_STAMP(r, SB, 4 + 3 * min(q, 1));
+    FW_STAMP(r, SB, 4 + 3 * min(g, 1));
   }
 }
 
@@ -1470,7 +1418,7 @@ __global__ void k_fill_i64(int64_t* p, int64_t v, int64_t n) {
 __global__ void k_restore(Spec s, const int64_t* ent, int64_t n) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t* x = ent + j * FW_SNAP_ENTRY_WORDS;
-    const int64_t kid = dir_find_or_insert(s, x[1]);
+    const int64_t kid = dir_lookup(s, x[1]);
     const int32_t p = slice_slot(s, x[0]);
     if (kid < 0 || p < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
     const int64_t idx = (int64_t)p * s.stride + kid;
@@ -1943,16 +1891,23 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->stg_hash[q] = e->alloc<int32_t>((size_t)c.max_batch);
   }
 
-  // ingest form: partitioned (LDS pre-aggregation) when a directory bucket fits in LDS and
-  // batches are large; direct atomics otherwise
+  // ingest form: partitioned (LDS pre-aggregation) when a directory bucket's accumulators fit in LDS
+  // and batches are large; direct atomics otherwise
   {
     const int KB = 1 << s.kb_bits;
-    const bool fits = s.kb_bits <= RT_MAX_KB_BITS && c.max_batch >= 4096 && c.max_batch <= (1ll << 26);
-    if (c.ingest_mode == 2 && !fits) return unsupported("partitioned ingest needs <= 1024 directory slots per bucket");
+    const int32_t max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
+    const int nacc = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
+    const size_t KA = (size_t)KB + 65;
+    const size_t agg_need = KA * 8 * nacc + ((KA + 3) & ~(size_t)3) * 4 + 8 * (size_t)max_tiles + 4 +
+                            4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8;
+    const bool fits = s.kb_bits <= RT_MAX_KB_BITS && s.nb <= RT_MAXNB && agg_need <= 160 * 1024 &&
+                      c.max_batch >= RT_TILE && c.max_batch <= (1ll << 26);
+    if (c.ingest_mode == 2 && !fits)
+      return unsupported("partitioned ingest needs <= 8192 directory slots per bucket (key_capacity <= 512 Ki)");
     e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && c.max_batch >= (1 << 16));
     if (e->routed) {
-      e->max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
-      const size_t cap = (size_t)e->max_tiles * RT_TILE;
+      e->max_tiles = max_tiles;
+      const size_t cap = (size_t)max_tiles * RT_TILE;
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
       e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
@@ -1961,20 +1916,16 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       for (int q = 0; q < 2; ++q) {
         RouteBuf& r = e->rbs[q];
         r = e->rb;
-        r.kv = e->alloc<longlong2>(cap);
-        r.idx = e->alloc<uint16_t>(cap);
-        r.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * e->max_tiles);
-        r.hdr = e->alloc<int64_t>((size_t)e->max_tiles * RT_Q);
+        r.val = e->alloc<int64_t>(cap);
+        r.meta = e->alloc<uint32_t>(cap);
+        r.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * max_tiles);
+        r.hdr = e->alloc<int64_t>((size_t)max_tiles * RT_Q);
         r.dlist = e->alloc<unsigned long long>((size_t)c.max_batch);
       }
-      e->route_lds = (size_t)RT_TILE * (8 + 8 + 2) + 4 * (size_t)(RT_Q * 256 + 8) + 4 * 16 + 8 * RT_Q;
-      const int ncols = 2 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-      e->agg_lds = (size_t)KB * 8 + (size_t)(KB + 64) * (8 * (ncols - 1) + 4) + 8 * (size_t)e->max_tiles + 4 +
-                   4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 16;
+      e->route_lds = RT_LDS;
       const char* ml = getenv("FW_AGG_MIN_LDS_KB");
       e->agg_min_lds = (ml ? atoi(ml) : 81) * 1024;
-      e->agg_lds = std::max<size_t>(e->agg_lds, (size_t)e->agg_min_lds);
-      if (e->agg_lds > 160 * 1024) return unsupported("partitioned ingest: aggregate LDS too large");
+      e->agg_lds = agg_need;   // at launch: less the unused tiles, at least agg_min_lds
     }
   }
   e->wm_done = e->alloc<unsigned int>(1);

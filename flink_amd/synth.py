@@ -3,8 +3,11 @@
 Counter-based: record i of a stream is a pure function of (seed, i) through splitmix64, so the GPU
 engine, the CPU oracle and a Java SourceFunction can all produce identical streams.
   key   = splitmix64(seed_key ^ i) & (n_keys - 1)           (n_keys a power of two), or % n_keys
+          Zipf(s): inverse CDF of ranks 1..n_keys at u = (splitmix64(seed_key ^ i) >> 11) / 2^53
   ts    = t0 + (i * 1000) // rate                            (rate = events per event-time second)
+          out of order by D: minus splitmix64(3 ^ i) % (D + 1)
   value = (int64) splitmix64(seed_val ^ i)                   full range: the long sums wrap
+          doubles: (splitmix64(seed_val ^ i) >> 11) / 2^53   in [0, 1)
 """
 import torch
 
@@ -25,14 +28,31 @@ def splitmix64(x):
     return z ^ _lsr(z, 31)
 
 
-def stream(start, n, n_keys, rate, t0=0, seed_key=1, seed_val=2, device="cpu", value_type="i64"):
+_zipf_cdf = {}
+
+
+def zipf_cdf(n_keys, s, device):
+    k = (n_keys, s, str(device))
+    if k not in _zipf_cdf:
+        ranks = torch.arange(1, n_keys + 1, dtype=torch.float64)
+        cdf = torch.cumsum(ranks ** -s, 0)
+        _zipf_cdf[k] = (cdf / cdf[-1]).to(device)
+    return _zipf_cdf[k]
+
+
+def stream(start, n, n_keys, rate, t0=0, seed_key=1, seed_val=2, device="cpu", value_type="i64", zipf=None, ooo=0):
     i = torch.arange(start, start + n, dtype=torch.int64, device=device)
     hk = splitmix64(i ^ seed_key)
-    if n_keys & (n_keys - 1) == 0:
+    if zipf is not None:
+        u = _lsr(hk, 11).to(torch.float64) / float(1 << 53)
+        keys = torch.clamp(torch.searchsorted(zipf_cdf(n_keys, zipf, device), u), max=n_keys - 1)
+    elif n_keys & (n_keys - 1) == 0:
         keys = hk & (n_keys - 1)
     else:
         keys = torch.remainder(_lsr(hk, 1), n_keys)
     ts = t0 + torch.div(i * 1000, rate, rounding_mode="floor")
+    if ooo:
+        ts = ts - torch.remainder(_lsr(splitmix64(i ^ 3), 1), ooo + 1)
     hv = splitmix64(i ^ seed_val)
     if value_type == "i64":
         vals = hv

@@ -28,6 +28,36 @@ def _free_port():
     return p
 
 
+def _local_wm(j, r, t_part):
+    """Source r's watermark after its batch j: max ts - 1 - 37 r, with regressions (rank 1 every 5th
+    step) and repeats (rank 0 every 4th step) that the channel valve must swallow."""
+    wm = int(t_part.max()) - 1 - 37 * r
+    if r == 1 and j % 5 == 3:
+        wm -= 4000
+    if r == 0 and j % 4 == 1 and j > 0:
+        wm = -(1 << 63) + 5
+    return wm
+
+
+def expected_forwarded(world, steps, batch):
+    """StreamInputProcessor.java:147-161 over the world's source channels, one forward per step at most."""
+    from flink_amd.keyby import ChannelWatermarks
+    from flink_amd.synth import stream
+    valve = ChannelWatermarks(world)
+    out = []
+    for j in range(steps):
+        _, t, _ = stream(j * batch * world, batch * world, 3000, 1 << 13)
+        fwd = None
+        for r in range(world):
+            x = valve.on_watermark(r, _local_wm(j, r, t[r::world]))
+            fwd = x if x is not None else fwd
+        out.append(fwd)
+    return out
+
+
+STEPS, BATCH = 12, 4096
+
+
 def _worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -35,6 +65,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from harness import epochs_of
     from flink_amd.keyby import KeyByExchange
     from flink_amd.keygroups import compute_key_group_range_for_operator_index
     from flink_amd.synth import stream
@@ -46,26 +77,15 @@ def _worker(rank, world, port, q):
                       key_capacity=4096, max_batch=1 << 14, out_capacity=1 << 18)
     eng = OracleEngine(cfg)
     ex = KeyByExchange(eng, world, rank, 128, 1 << 13, "cpu")
-    batch = 4096
-    rows = []
-    for j in range(12):
-        k, t, v = stream(j * batch * world, batch * world, 3000, 1 << 13)
+    results = []
+    for j in range(STEPS):
+        k, t, v = stream(j * BATCH * world, BATCH * world, 3000, 1 << 13)
         k, t, v = k[rank::world].contiguous(), t[rank::world].contiguous(), v[rank::world].contiguous()
-        # local watermark lags a bit differently per source: the aligned one is their min
-        wm_local = int(t.max()) - 1 - 37 * rank
-        rk, rt, rv = ex.exchange(k, t, v)
-        if rk.numel():
-            eng.push(rk.numpy(), rt.numpy(), rv.numpy())
-        wm = ex.align_watermark(wm_local)
-        _, tall, _ = stream(j * batch * world, batch * world, 3000, 1 << 13)
-        assert wm == min(int(tall[r::world].max()) - 1 - 37 * r for r in range(world))
-        eng.advance_watermark(wm)
-        r = eng.collect()
-        rows += list(zip(r["key"].tolist(), r["ts"].tolist(), r["sum_i64"].tolist(), r["count"].tolist()))
+        ex.step(k, t, v, _local_wm(j, rank, t))
+        results.append(eng.collect())
     eng.advance_watermark(LONG_MAX)
-    r = eng.collect()
-    rows += list(zip(r["key"].tolist(), r["ts"].tolist(), r["sum_i64"].tolist(), r["count"].tolist()))
-    q.put((rank, rows))
+    results.append(eng.collect())
+    q.put((rank, epochs_of(results, ["sum_i64", "count"]), ex.emitted))
     dist.destroy_process_group()
 
 
@@ -77,26 +97,42 @@ def test_keyby_exchange_two_ranks(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = {}
+    got, emitted = {}, {}
     for _ in range(world):
-        rank, rows = q.get(timeout=240)
-        got[rank] = rows
+        rank, ep, em = q.get(timeout=240)
+        got[rank], emitted[rank] = ep, em
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    union = sorted(got[0] + got[1])
+    exp = expected_forwarded(world, STEPS, BATCH)
+    assert any(e is None for e in exp), "the stream must exercise non-increasing aligned watermarks"
+    forwarded = [e for e in exp if e is not None]
+    # every window subtask forwards exactly the valve's watermarks (positions included)
+    for r in range(world):
+        assert emitted[r] == forwarded
+        assert [w for w, _ in got[r]] == forwarded + [LONG_MAX]
     # every key lands on exactly one subtask
-    assert not ({r[0] for r in got[0]} & {r[0] for r in got[1]})
+    keys = [{rec[0] for _, recs in got[r] for rec in recs} for r in range(world)]
+    assert not (keys[0] & keys[1])
 
+    # one subtask over the whole stream, fed the same forwarded watermarks after the same batches
+    from harness import epochs_of
     from flink_amd.synth import stream
     from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, make_config
     from oracle.oracle import OracleEngine
     cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "count")), key_capacity=4096,
                       max_batch=1 << 17, out_capacity=1 << 18)
     e = OracleEngine(cfg)
-    k, t, v = stream(0, 12 * 4096 * world, 3000, 1 << 13)
-    e.push(k.numpy(), t.numpy(), v.numpy())
+    res = []
+    for j in range(STEPS):
+        k, t, v = stream(j * BATCH * world, BATCH * world, 3000, 1 << 13)
+        e.push(k.numpy(), t.numpy(), v.numpy())
+        if exp[j] is not None:
+            e.advance_watermark(exp[j])
+        res.append(e.collect())
     e.advance_watermark(LONG_MAX)
-    r = e.collect()
-    ref = sorted(zip(r["key"].tolist(), r["ts"].tolist(), r["sum_i64"].tolist(), r["count"].tolist()))
+    res.append(e.collect())
+    ref = epochs_of(res, ["sum_i64", "count"])
+    union = [(w, sorted(got[0][i][1] + got[1][i][1])) for i, (w, _) in enumerate(got[0])]
     assert union == ref
+    assert sum(len(r) for _, r in ref) > 0
