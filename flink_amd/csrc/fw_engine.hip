@@ -110,6 +110,18 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {  // MurmurHash3 finalis
   return k;
 }
 
+// inverse of fmix64 (fmix64 is a bijection on 64-bit words): k ^= k >> 33 is an involution, and the
+// multipliers are odd, so their inverses mod 2^64 exist
+__device__ __forceinline__ uint64_t fmix64_inv(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0x9cb4b2f8129337dbull;
+  h ^= h >> 33;
+  h *= 0x4f74430c22a54005ull;
+  h ^= h >> 33;
+  return h;
+}
+constexpr uint64_t EMPTY_H = 0x8f780810af31a493ull;   // fmix64(Long.MIN_VALUE): the hash of an empty slot
+
 __device__ __forceinline__ uint64_t lanemask_lt() { return __lanemask_lt(); }
 
 // wave-aggregated counter add; returns this lane's slot (only meaningful where pred)
@@ -128,16 +140,12 @@ __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
     atomicAdd(ctr, (unsigned long long)__popcll(mask));
 }
 
-// key -> kid (directory slot).  Group probing inside the key's home bucket of 2^kb_bits slots: the
-// aligned group of DIR_GROUP slots (32 B) holding the key's home slot first, then the following groups,
-// wrapping inside the bucket; a key takes the first slot in that order that was EMPTY when it arrived.
-// At the directory's load factor <= 1/4 a group overflows for ~0.4 % of keys, so a lookup is nearly
-// always one 32-B read (k_route does it for every routed record, against an L2-resident directory).
-// Entries go EMPTY -> key once and never change until engine reset, so a plain (possibly stale) load
-// can only under-report, which the CAS then corrects; a key found EMPTY at slot j cannot sit at a later
-// slot.  Every kid of a key lies in the bucket its hash names: the partitioned ingest (k_route /
-// k_aggregate) owns whole buckets exclusively.
-constexpr int DIR_GROUP = 4;
+// key -> kid (directory slot).  Linear probing inside the key's home bucket of 2^kb_bits slots, so
+// every kid of a key lies in the bucket its hash names: the partitioned ingest (k_route / k_aggregate)
+// owns whole buckets exclusively, and k_aggregate probes an LDS copy of the bucket with the same
+// sequence.  Entries go EMPTY -> key once and never change until engine reset, so a plain (possibly
+// stale) load can only under-report, which the CAS then corrects; a key found EMPTY at slot j cannot
+// sit at a later slot.
 __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
                                                          int32_t kb_bits, int64_t D, int64_t key) {
   if (key == EMPTY_KEY) {
@@ -147,19 +155,17 @@ __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int3
   const uint64_t home = fmix64((uint64_t)key) & dir_mask;
   const uint64_t kbm = (1ull << kb_bits) - 1;
   const uint64_t base = home & ~kbm;
-  uint64_t g = home & kbm & ~(uint64_t)(DIR_GROUP - 1);
-  for (uint64_t probe = 0; probe <= kbm; probe += DIR_GROUP) {
-    for (int j = 0; j < DIR_GROUP; ++j) {
-      const uint64_t h = base + g + j;
-      const int64_t cur = dir_keys[h];
-      if (cur == key) return (int64_t)h;
-      if (cur == EMPTY_KEY) {
-        const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[h], (unsigned long long)EMPTY_KEY,
-                                                  (unsigned long long)key);
-        if ((int64_t)prev == EMPTY_KEY || (int64_t)prev == key) return (int64_t)h;
-      }
+  uint64_t off = home & kbm;
+  for (uint64_t probe = 0; probe <= kbm; ++probe) {
+    const uint64_t h = base + off;
+    const int64_t cur = dir_keys[h];
+    if (cur == key) return (int64_t)h;
+    if (cur == EMPTY_KEY) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[h], (unsigned long long)EMPTY_KEY,
+                                                (unsigned long long)key);
+      if ((int64_t)prev == EMPTY_KEY || (int64_t)prev == key) return (int64_t)h;
     }
-    g = (g + DIR_GROUP) & kbm;
+    off = (off + 1) & kbm;
   }
   return -1;
 }
@@ -451,35 +457,37 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 // ingest, partitioned form.  Two kernels per batch:
 //  k_route      one workgroup per tile of RT_TILE records: streams the tile's columns in with 16-B
 //               loads, does the per-record operator work (key group check, window/slice, lateness),
-//               resolves each routable record's directory slot (one 32-B group read of the L2-resident
-//               directory; new keys are inserted there), counting-sorts the routable records through LDS
-//               by bin = (tile slice q, directory bucket) and writes the tile back bin-sorted as 12-B
-//               records (value, slot-in-bucket << 12 | index-in-tile) with a per-tile table of segment
-//               starts.  Records that cannot be routed (per-element fires, slices beyond the tile's RT_Q,
-//               the Long.MIN_VALUE key) join the direct list.
+//               counting-sorts the routable records through LDS by bin = (tile slice q, directory
+//               bucket) and writes the tile back bin-sorted as (fmix64(key), value) + the 2-B index of
+//               the record in its tile, with a per-tile table of segment starts.  Records that cannot be
+//               routed (per-element fires, slices beyond the tile's RT_Q, the Long.MIN_VALUE key) join
+//               the direct list.
 //  k_aggregate  one workgroup per directory bucket: owns every pane of that bucket for this batch,
 //               gathers the bucket's segment from every tile (the segments concatenated, one record
-//               per lane), reduces with LDS atomics indexed by the routed slot (no key compare left),
-//               adds the bucket's direct records the same way and folds each touched pane into the
-//               dense columns once, with plain loads and stores.
-// No device-scope atomic per record, and 48 B of HBM traffic per event (24 in, 12 out, 12 back in).
+//               per lane), resolves keys in an LDS copy of the bucket's directory slice, reduces with
+//               LDS atomics, adds the bucket's direct records the same way and folds each touched pane
+//               into the dense columns once, with plain loads and stores (it is their only writer).
+// No device-scope atomic per record.  (A variant that resolved the directory slot in k_route and routed
+// 12-B records measured slower: the per-record probe of the global directory cost k_route more than the
+// 6 B/event it saved)
 // ------------------------------------------------------------------------------------------------
 constexpr int RT_TILE = 4096;
 constexpr int RT_THREADS = 512;
-constexpr int RT_Q = 4;                 // slices per tile routed through LDS (more go to the direct list)
+constexpr int RT_Q = 2;                 // slices per tile routed through LDS (more go to the direct list)
 constexpr int RT_GS = 64;               // distinct slices per batch (k_aggregate rounds)
 constexpr int RT_MAXNB = 256;           // directory buckets the route table holds
 constexpr int DC_RING = 16;             // direct-list counters, one per batch in flight
 constexpr int AG_THREADS = 1024;
+constexpr int AG_WIN = 8;               // k_aggregate: directory slots probed without a branch
 constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
 constexpr int AG_MAXPER = 17;           // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
-constexpr int RT_MAX_KB_BITS = 13;      // directory slots per bucket whose accumulators k_aggregate holds in LDS
+constexpr int RT_MAX_KB_BITS = 12;      // directory slots per bucket that k_aggregate holds in LDS
 constexpr int IDX_BITS = 12;            // record index within a tile (RT_TILE = 2^12)
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
-  int64_t* val;          // [ntiles][RT_TILE] routed values (int64 or double bits), each tile sorted by bin
-  uint32_t* meta;        // [ntiles][RT_TILE] directory slot within the bucket << 12 | record index within the tile
+  longlong2* kv;         // [ntiles][RT_TILE] routed records (fmix64(key), value), each tile sorted by bin
+  uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
   uint16_t* seg;         // [ntiles][nbq + 1] start of each bin's segment in the tile; [nbq] = routed count
   int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
   unsigned long long* dlist;    // direct-list records: (batch index << 1) | per-element fire
@@ -491,8 +499,9 @@ struct RouteBuf {
   int32_t dbg;
 };
 
-// Non-temporal access of the streamed columns, a bit mask: 1 = k_route's input loads (streamed once per
-// batch, so they do not evict the directory and the routed records k_aggregate reads next)
+// Non-temporal access of the streamed columns, a bit mask: 1 = k_route's input loads (on: k_route 43 ->
+// 41 us per 4 Mi-event batch), 2 = k_aggregate's gathers of the routed records, 4 = k_route's stores of
+// them (both measured slower: the intermediate is re-read from the cache)
 #ifndef FW_ROUTE_NT
 #define FW_ROUTE_NT 1
 #endif
@@ -541,15 +550,12 @@ __device__ __forceinline__ void block_scan_excl(int32_t* a, int n, int32_t* wtot
   __syncthreads();
 }
 
-// LDS layout of k_route (bytes): [0, 48K) per-record staging, reused phase by phase (each phase's
-// entries are written and read by the thread owning the record, so no barrier separates them):
-//   phase A/B1   key hashes int32[4096] at 0 (optional column)
-//   slow path    flags int32[4096] at 0 (the record's key hash is read before), slice numbers int64[4096] at 16K
-//   directory    slots of the records that missed their home group, uint32[4096] at 0
-//   scatter      values int64[4096] at 0, meta uint32[4096] at 32K (after the barriers of the scan)
-// then the bin counters, the scan scratch and the tile's slice set.
-constexpr size_t RT_LDS_STAGE = (size_t)RT_TILE * 12;
-constexpr size_t RT_LDS = RT_LDS_STAGE + 4 * (size_t)(RT_Q * RT_MAXNB + 8) + 4 * 16 + 8 * RT_Q;
+// LDS layout of k_route (bytes): [0, 64K) staging of the bin-sorted records (fmix64(key), value); before
+// the scatter the same bytes hold, entry by entry of the thread owning the record (no barrier needed):
+// the key hashes int32[4096] at 0 (optional column), and for records outside their wave's reference slice
+// their slice numbers int64[4096] at 16K and flags int32[4096] at 48K.  Then [64K, 72K) the sorted records'
+// index in the tile, the bin counters, the scan scratch and the tile's slice set.
+constexpr size_t RT_LDS = (size_t)RT_TILE * (16 + 2) + 4 * (size_t)(RT_Q * RT_MAXNB + 8) + 4 * 16 + 8 * RT_Q;
 
 template <int VT, int AGG, bool FIRST>
 __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, const RouteBuf& r, unsigned char* smem,
@@ -558,14 +564,13 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   constexpr int PER = RT_TILE / NT;     // records per thread
   constexpr int V = PER / 2;            // 16-B vectors per column per thread
   const int nbq = RT_Q * s.nb;
-  int64_t* st_val = (int64_t*)smem;
-  uint32_t* st_meta = (uint32_t*)(smem + (size_t)RT_TILE * 8);
-  int32_t* cnt = (int32_t*)(smem + RT_LDS_STAGE);   // [nbq + 1]
-  int32_t* wtot = cnt + (RT_Q * RT_MAXNB + 8);      // [NT / 64]
-  int64_t* lset = (int64_t*)(wtot + 16);            // [RT_Q] the tile's routed slices
-  int32_t* lhash = (int32_t*)smem;                  // Java key hashes (optional column)
+  longlong2* st_kv = (longlong2*)smem;
+  uint16_t* st_idx = (uint16_t*)(st_kv + RT_TILE);
+  int32_t* cnt = (int32_t*)(st_idx + RT_TILE);     // [nbq + 1]
+  int32_t* wtot = cnt + (RT_Q * RT_MAXNB + 8);     // [NT / 64]
+  int64_t* lset = (int64_t*)(wtot + 16);           // [RT_Q] the tile's routed slices
+  int32_t* lhash = (int32_t*)smem;                 // Java key hashes (optional column)
   const int64_t base = (int64_t)blockIdx.x * RT_TILE;
-  const uint64_t kbm = (1ull << s.kb_bits) - 1;
   FW_STAMP(r, 0, 0);
   for (int x = threadIdx.x; x <= nbq; x += NT) cnt[x] = 0;
   if (threadIdx.x < RT_Q) lset[threadIdx.x] = FREE_TAG;
@@ -577,6 +582,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
     if (!tail) {
 #if FW_ROUTE_NT & 1
+      // streamed once per batch: non-temporal, so the routed intermediate k_aggregate reads next keeps the cache
       typedef long long v2i64 __attribute__((ext_vector_type(2)));
       const v2i64 a = __builtin_nontemporal_load((const v2i64*)(b.key + i));
       const v2i64 c = __builtin_nontemporal_load((const v2i64*)(b.ts + i));
@@ -655,8 +661,8 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   // the full assignment for the rest: one call-free copy of the code (a call would make the register
   // allocator spill the tile around it), timestamps re-read from the input, results through LDS
   if (__any(slow_mask != 0)) {
-    int32_t* sf = (int32_t*)smem;                            // [RT_TILE] flags: live | late_fire << 1 | n_late << 2
-    int64_t* sm = (int64_t*)(smem + (size_t)RT_TILE * 4);    // [RT_TILE] slice numbers
+    int64_t* sm = (int64_t*)(smem + (size_t)RT_TILE * 4);        // [RT_TILE] slice numbers
+    int32_t* sf = (int32_t*)(smem + (size_t)RT_TILE * 12);       // [RT_TILE] flags: live | late_fire << 1 | n_late << 2
 #pragma unroll 1
     for (int k = 0; k < PER; ++k) {
       if ((slow_mask >> k) & 1u) {
@@ -689,9 +695,9 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     }
   }
   // phase B2: the routed records' index in the tile's slice set — resolved once per wave when all its
-  // routed records share one slice (an in-order stream), per record otherwise.  The rest join the direct
-  // list (rare: per-element fires, slices beyond the tile's RT_Q, the Long.MIN_VALUE key), applied by
-  // the k_aggregate workgroup owning the key's bucket.
+  // routed records share one slice (an in-order stream), per record otherwise — then their bin and
+  // counting-sort rank.  The rest join the direct list (rare: per-element fires, slices beyond the
+  // tile's RT_Q, the Long.MIN_VALUE key), applied by the k_aggregate workgroup owning the key's bucket.
   int64_t m_ref = INT64_MIN;
   {
     const uint64_t lm = __ballot(route_mask != 0);
@@ -713,82 +719,23 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     q_ref = __shfl(q_ref, __ffsll((long long)__ballot(route_mask != 0)) - 1);
   }
   const bool wave_uniform = __all(same);
-  int32_t qq[PER];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const bool routable = (route_mask >> k) & 1u;
-    int32_t q = -1;
-    if (wave_uniform) q = routable ? q_ref : -1;
-    else if (routable) q = tile_slice(lset, tt[k]);
-    qq[k] = q;
-    if (routable && q < 0) {   // the tile's slice set is full
-      route_mask &= ~(1u << k);
-      direct_mask |= 1u << k;
-    }
-  }
-  // phase B3: directory slot of every routed record — the aligned 4-slot group holding its home slot,
-  // two 16-B loads from the L2-resident directory, four records' loads in flight at a time; the keys not
-  // found there (first sight of a key, or an overflowed group) take the probe/insert loop below
-  uint32_t slot[PER];
-  uint32_t miss_mask = 0;
-#pragma unroll
-  for (int h4 = 0; h4 < PER; h4 += 4) {
-    longlong2 ga[4], gb[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = h4 + u;
-      const uint64_t hk = fmix64((uint64_t)kk[k]);
-      const int64_t g = (int64_t)(hk & s.dir_mask & ~(uint64_t)(DIR_GROUP - 1));
-      const longlong2* gp = (const longlong2*)(s.dir_keys + (((route_mask >> k) & 1u) ? g : 0));
-      if (r.dbg & 64) { ga[u] = make_longlong2(kk[k], 0); gb[u] = make_longlong2(0, 0); continue; }   // ablation: no probe
-      ga[u] = gp[0];
-      gb[u] = (r.dbg & 128) ? make_longlong2(0, 0) : gp[1];   // ablation: first half only
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = h4 + u;
-      const int64_t key = kk[k];
-      const uint32_t g = (uint32_t)(fmix64((uint64_t)key) & kbm & ~(uint64_t)(DIR_GROUP - 1));
-      uint32_t sl = NO_FIRST;
-      sl = gb[u].y == key ? g + 3 : sl;
-      sl = gb[u].x == key ? g + 2 : sl;
-      sl = ga[u].y == key ? g + 1 : sl;
-      sl = ga[u].x == key ? g : sl;
-      slot[k] = sl;
-      miss_mask |= (((route_mask >> k) & 1u) && sl == NO_FIRST ? 1u : 0u) << k;
-    }
-  }
-  if (__any(miss_mask != 0)) {
-    uint32_t* ms = (uint32_t*)smem;   // [RT_TILE] slots of the missed records
-#pragma unroll 1
-    for (int k = 0; k < PER; ++k) {
-      if ((miss_mask >> k) & 1u) {
-        const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
-        const int64_t kid = dir_lookup(s, b.key[base + t]);
-        if (kid < 0) set_error(s.err, FW_ERR_CAPACITY);
-        ms[t] = kid < 0 ? NO_FIRST : (uint32_t)((uint64_t)kid & kbm);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      if ((miss_mask >> k) & 1u) {
-        const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
-        slot[k] = ms[t];
-        if (slot[k] == NO_FIRST) route_mask &= ~(1u << k);   // directory bucket full: reported above
-      }
-    }
-  }
-  // bins and counting-sort ranks
   int32_t bin[PER];       // routed bin, or -1
   int32_t rank[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     bin[k] = -1;
     rank[k] = 0;
-    if ((route_mask >> k) & 1u) {
+    const bool routable = (route_mask >> k) & 1u;
+    int32_t q = -1;
+    if (wave_uniform) q = routable ? q_ref : -1;
+    else if (routable) q = tile_slice(lset, tt[k]);
+    if (q >= 0) {
       const uint64_t hk = fmix64((uint64_t)kk[k]);
-      bin[k] = qq[k] * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
+      bin[k] = q * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
       rank[k] = atomicAdd(&cnt[bin[k]], 1);
+      kk[k] = (int64_t)hk;   // routed records carry the directory hash (a bijection of the key)
+    } else if (routable) {
+      direct_mask |= 1u << k;   // the tile's slice set is full
     }
   }
   if (__any(late_pairs != 0)) {
@@ -817,25 +764,24 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   for (int k = 0; k < PER; ++k) {
     if (bin[k] >= 0) {
       const int32_t pos = cnt[bin[k]] + rank[k];
-      st_val[pos] = vv[k];
-      st_meta[pos] = (slot[k] << IDX_BITS) | (uint32_t)(2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1));
+      st_kv[pos] = make_longlong2(kk[k], vv[k]);
+      st_idx[pos] = (uint16_t)(2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1));
     }
   }
   __syncthreads();
   FW_STAMP(r, 0, 3);
   const int32_t total = cnt[nbq];
-  // write-out: 16-B stores of the values (two per lane), 16-B stores of the meta words (four per lane)
-#pragma unroll
-  for (int j = 0; j < V; ++j) {
-    const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
-    if (pos + 1 < total) *(longlong2*)(r.val + base + pos) = *(const longlong2*)(st_val + pos);
-    else if (pos < total) r.val[base + pos] = st_val[pos];
+#pragma unroll 2
+  for (int k = 0; k < PER; ++k) {
+    const int32_t pos = k * NT + (int)threadIdx.x;
+    if (pos < total) r.kv[base + pos] = st_kv[pos];
   }
+  if (FIRST) {
 #pragma unroll
-  for (int j = 0; j < PER / 4; ++j) {
-    const int32_t pos = 4 * (j * NT + (int)threadIdx.x);
-    if (pos + 3 < total) *(uint4*)(r.meta + base + pos) = *(const uint4*)(st_meta + pos);
-    else for (int e = 0; e < 4; ++e) if (pos + e < total) r.meta[base + pos + e] = st_meta[pos + e];
+    for (int j = 0; j < V; ++j) {
+      const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
+      if (pos < total) *(uint32_t*)(r.idx + base + pos) = *(const uint32_t*)(st_idx + pos);
+    }
   }
   FW_STAMP(r, 0, 4);
 }
@@ -845,6 +791,27 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, Rout
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // every tile but the last is whole, so its 16-B loads need no bounds (uniform branch)
   route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(blockIdx.x + 1) * RT_TILE > b.n);
+}
+
+// the bucket's LDS directory-hash table: slot of h, inserting its key (fmix64_inv(h)) into the global
+// directory if absent (the same linear probe sequence as dir_find_or_insert).  Out of line: taken by a
+// wave only when a lane misses the probed windows.
+__device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h) {
+  uint32_t x = (uint32_t)h & kbm;
+  for (uint32_t probe = 0; probe <= kbm; ++probe) {
+    const uint64_t cur = lh[x];
+    if (cur == h) return (int32_t)x;
+    if (cur == EMPTY_H) {
+      const int64_t key = (int64_t)fmix64_inv(h);
+      const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[x], (unsigned long long)EMPTY_KEY,
+                                                (unsigned long long)key);
+      const uint64_t now = (int64_t)prev == EMPTY_KEY ? h : fmix64(prev);
+      lh[x] = now;   // only globally confirmed keys enter the cache
+      if (now == h) return (int32_t)x;
+    }
+    x = (x + 1) & kbm;
+  }
+  return -1;
 }
 
 // one record into the bucket's LDS accumulators at slot kl
@@ -861,6 +828,13 @@ __device__ __forceinline__ void acc_add(int64_t* lsum, int64_t* lmin, int64_t* l
   atomicMin(&lfirst[kl], oi);   // earliest record of the batch: the first arrival, and the "touched" mark
 }
 
+// LDS bytes k_aggregate needs for buckets of 2^kb_bits slots and ntiles tiles
+__host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_t ntiles) {
+  return (size_t)8 * ((size_t)1 << kb_bits) + ((size_t)(1 << kb_bits) + 65) * 8 * nacc +
+         ((((size_t)(1 << kb_bits) + 65) + 3) & ~(size_t)3) * 4 + (size_t)12 * RT_Q * ntiles + 8 * (size_t)ntiles + 4 +
+         4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8;
+}
+
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, RouteBuf r, const int64_t* f1col) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -872,14 +846,18 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
                                                     : (int)blockIdx.x;
   const int nbq = RT_Q * s.nb;
   const int KB = 1 << s.kb_bits;
+  const uint32_t kbm = (uint32_t)KB - 1;
   const int KA = KB + 65;                               // accumulators: KB slots, one dummy per lane, the MIN key
   const uint32_t KMIN = (uint32_t)KB + 64;              // slot of the Long.MIN_VALUE key (kid D, bucket 0)
-  int64_t* lsum = (int64_t*)smem;                       // [KA]
+  uint64_t* lh = (uint64_t*)smem;                       // [KB] fmix64 of this bucket's directory slice (EMPTY_H = free)
+  int64_t* lsum = (int64_t*)(lh + KB);                  // [KA]
   int64_t* lmin = lsum + KA;
   int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KA : 0);
   int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KA : 0);
   uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest record (batch index)
-  int32_t* sst = (int32_t*)(lfirst + ((KA + 3) & ~3));  // [ntiles] segment start within the tile
+  int64_t* lhdr = (int64_t*)(lfirst + ((KA + 3) & ~3)); // [ntiles][RT_Q] the tiles' routed slices
+  uint32_t* lseg = (uint32_t*)(lhdr + (int64_t)r.ntiles * RT_Q);   // [ntiles][RT_Q] this bucket's segment start | end << 16
+  int32_t* sst = (int32_t*)(lseg + (int64_t)r.ntiles * RT_Q);     // [ntiles] segment start within the tile
   int32_t* off = sst + r.ntiles;                        // [ntiles + 1] segment lengths, then their exclusive prefix
   int32_t* step_tile = off + r.ntiles + 1;              // [AG_CHS] tile holding the first record of each step
   int32_t* awtot = step_tile + AG_CHS;                  // [16] scan scratch
@@ -888,6 +866,21 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   const int64_t dbase = (int64_t)bkt * KB;
   const int64_t SB = (int64_t)8 << 16;
   FW_STAMP(r, SB, 0);
+  // every tile's header and this bucket's segment bounds in each of its bin groups, plus the bucket's
+  // directory slice, into LDS: all loads independent, one round trip
+  for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+    const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
+    int64_t h[RT_Q];
+    uint32_t sg[RT_Q];
+#pragma unroll
+    for (int q = 0; q < RT_Q; ++q) {
+      h[q] = r.hdr[(int64_t)t * RT_Q + q];
+      sg[q] = (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16);
+    }
+#pragma unroll
+    for (int q = 0; q < RT_Q; ++q) { lhdr[t * RT_Q + q] = h[q]; lseg[t * RT_Q + q] = sg[q]; }
+  }
+  for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
   const int64_t nd = min((int64_t)*r.dcount, r.dcap);
   // claimed early (slice_slot is idempotent): the slot of tile 0's first routed slice, nearly always the
   // batch's only one
@@ -954,13 +947,50 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   for (int t0 = 0; t0 < r.ntiles; t0 += NT) {   // uniform
     const int t = t0 + (int)threadIdx.x;
     for (int q = 0; q < RT_Q; ++q) {
-      const int64_t m = t < r.ntiles ? r.hdr[(int64_t)t * RT_Q + q] : FREE_TAG;
+      const int64_t m = t < r.ntiles ? lhdr[t * RT_Q + q] : FREE_TAG;
       const int64_t left = __shfl_up(m, 1);
       const bool dup = lane != 0 && left == m;
       if (m != FREE_TAG && !dup) gsl_insert(m);
     }
   }
   __syncthreads();
+
+  // directory hash -> slot in this bucket.  Linear probing keeps a key within the run that starts at
+  // its home slot, so the first AG_WIN slots are compared without branching (the directory's load factor
+  // <= 1/4 keeps nearly every key there); a second inline window takes the few displaced further, the
+  // out-of-line probe the rest and new keys (a global CAS on the key, fmix64_inv(h), confirms every slot
+  // before it enters the LDS copy)
+  auto probe = [&](bool& act, uint64_t h) -> uint32_t {
+    const uint32_t h0 = (uint32_t)h & kbm;
+    uint32_t kl = h0;
+    bool found = false;
+#pragma unroll
+    for (int j = AG_WIN - 1; j >= 0; --j) {   // the nearest match wins
+      const uint32_t x = (h0 + j) & kbm;
+      const bool m = lh[x] == h;
+      kl = m ? x : kl;
+      found |= m;
+    }
+    const bool miss = act && !found;
+    if (__any(miss)) {
+      bool found2 = false;
+#pragma unroll
+      for (int j = 2 * AG_WIN - 1; j >= AG_WIN; --j) {
+        const uint32_t x = (h0 + j) & kbm;
+        const bool m = lh[x] == h;
+        kl = (miss && m) ? x : kl;
+        found2 |= m;
+      }
+      const bool miss2 = miss && !found2;
+      if (__any(miss2) && miss2) {
+        const int32_t x = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h);
+        if (x < 0) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
+        else kl = (uint32_t)x;
+      }
+    }
+    return kl;
+  };
+
   for (int g = 0; g < RT_GS; ++g) {
     const int64_t m = gsl[g];
     if (m == FREE_TAG) break;                            // uniform
@@ -973,12 +1003,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     if (p < 0) { if (threadIdx.x == 0) set_error(s.err, FW_ERR_CAPACITY); continue; }   // slice pool exhausted
     for (int t = threadIdx.x; t < r.ntiles; t += NT) {
       int32_t a0 = 0, a1 = 0;
+#pragma unroll
       for (int q = 0; q < RT_Q; ++q) {
-        if (r.hdr[(int64_t)t * RT_Q + q] == m) {
-          const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
-          a0 = seg[q * s.nb + bkt];
-          a1 = seg[q * s.nb + bkt + 1];
-          break;
+        if (lhdr[t * RT_Q + q] == m) {
+          const uint32_t sg = lseg[t * RT_Q + q];
+          a0 = (int32_t)(sg & 0xFFFFu);
+          a1 = (int32_t)(sg >> 16);
         }
       }
       sst[t] = a0;
@@ -1005,47 +1035,47 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       __syncthreads();
       const int32_t nsteps = min(AG_CHS, (R - cb + 63) >> 6);
       // one group = UR steps of this wave: addresses from the step table, loads issued, nothing waited on
-      auto load_group = [&](int32_t s0, int64_t* rv, uint32_t* rm, uint32_t* rt) {
+      auto load_group = [&](int32_t s0, longlong2* rv, uint32_t* ri, bool* ra) {
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
           const int32_t st = s0 + u;
           const int32_t rr = cb + 64 * st + lane;
-          const bool act = st < nsteps && rr < R;
+          ra[u] = st < nsteps && rr < R;
           int32_t t = 0;
           int64_t pos = 0;   // inactive lanes read tile 0's first slot
-          if (act) {
+          if (ra[u]) {
             t = step_tile[st];
             while (off[t + 1] <= rr) ++t;
             pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
           }
-          rv[u] = r.val[pos];
-          rm[u] = r.meta[pos];
-          rt[u] = act ? (uint32_t)t : NO_FIRST;
+          rv[u] = r.kv[pos];
+          ri[u] = ((uint32_t)t << IDX_BITS) | (FIRST ? (uint32_t)r.idx[pos] : 0u);
         }
       };
-      auto process_group = [&](const int64_t* rv, const uint32_t* rm, const uint32_t* rt) {
+      auto process_group = [&](const longlong2* rv, const uint32_t* ri, const bool* ra) {
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
-          const bool act = rt[u] != NO_FIRST;
-          const uint32_t kl = act ? rm[u] >> IDX_BITS : (uint32_t)KB + (uint32_t)lane;
-          const uint32_t oi = act ? (rt[u] << IDX_BITS) | (rm[u] & ((1u << IDX_BITS) - 1)) : 0u;
-          acc_add<VT, AGG>(lsum, lmin, lmax, lcnt, lfirst, kl, rv[u], oi);
+          bool act = ra[u];
+          uint32_t kl = probe(act, (uint64_t)rv[u].x);
+          kl = act ? kl : (uint32_t)KB + (uint32_t)lane;   // inactive lanes update a private dummy slot
+          acc_add<VT, AGG>(lsum, lmin, lmax, lcnt, lfirst, kl, rv[u].y, ri[u]);
         }
       };
       // software pipelined: the next group's loads are in flight while this group updates LDS (two
       // register sets, the loop unrolled by two so that both stay in registers)
-      int64_t rvA[UR], rvB[UR];
-      uint32_t rmA[UR], rmB[UR], rtA[UR], rtB[UR];
+      longlong2 rvA[UR], rvB[UR];
+      uint32_t riA[UR], riB[UR];
+      bool raA[UR], raB[UR];
       constexpr int32_t G = (NT / 64) * UR;
       int32_t s0 = wave * UR;
-      if (s0 < nsteps) load_group(s0, rvA, rmA, rtA);
+      if (s0 < nsteps) load_group(s0, rvA, riA, raA);
       while (s0 < nsteps) {   // wave-uniform
-        if (s0 + G < nsteps) load_group(s0 + G, rvB, rmB, rtB);
-        process_group(rvA, rmA, rtA);
+        if (s0 + G < nsteps) load_group(s0 + G, rvB, riB, raB);
+        process_group(rvA, riA, raA);
         s0 += G;
         if (s0 >= nsteps) break;
-        if (s0 + G < nsteps) load_group(s0 + G, rvA, rmA, rtA);
-        process_group(rvB, rmB, rtB);
+        if (s0 + G < nsteps) load_group(s0 + G, rvA, riA, raA);
+        process_group(rvB, riB, raB);
         s0 += G;
       }
       __syncthreads();   // the next chunk rewrites step_tile
@@ -1058,9 +1088,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         const int64_t i = (int64_t)(ent >> 1);
         const int64_t key = b.key[i];
         if (!direct_mine(key) || record_windows(s, b.ts[i], b.wm).m != m) continue;
-        const int64_t kid = dir_lookup(s, key);
-        if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
-        const uint32_t kl = key == EMPTY_KEY ? KMIN : (uint32_t)(kid - dbase);
+        uint32_t kl = KMIN;
+        if (key != EMPTY_KEY) {
+          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, fmix64((uint64_t)key));
+          if (x2 < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+          kl = (uint32_t)x2;
+        } else {
+          (void)dir_lookup(s, key);   // marks the Long.MIN_VALUE key's column in use
+        }
         acc_add<VT, AGG>(lsum, lmin, lmax, lcnt, lfirst, kl, b.val[i], (uint32_t)i);
       }
     }
@@ -1894,16 +1929,13 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   // ingest form: partitioned (LDS pre-aggregation) when a directory bucket's accumulators fit in LDS
   // and batches are large; direct atomics otherwise
   {
-    const int KB = 1 << s.kb_bits;
     const int32_t max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
     const int nacc = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-    const size_t KA = (size_t)KB + 65;
-    const size_t agg_need = KA * 8 * nacc + ((KA + 3) & ~(size_t)3) * 4 + 8 * (size_t)max_tiles + 4 +
-                            4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8;
+    const size_t agg_need = agg_lds_bytes(s.kb_bits, nacc, max_tiles);
     const bool fits = s.kb_bits <= RT_MAX_KB_BITS && s.nb <= RT_MAXNB && agg_need <= 160 * 1024 &&
                       c.max_batch >= RT_TILE && c.max_batch <= (1ll << 26);
     if (c.ingest_mode == 2 && !fits)
-      return unsupported("partitioned ingest needs <= 8192 directory slots per bucket (key_capacity <= 512 Ki)");
+      return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
     e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && c.max_batch >= (1 << 16));
     if (e->routed) {
       e->max_tiles = max_tiles;
@@ -1916,8 +1948,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       for (int q = 0; q < 2; ++q) {
         RouteBuf& r = e->rbs[q];
         r = e->rb;
-        r.val = e->alloc<int64_t>(cap);
-        r.meta = e->alloc<uint32_t>(cap);
+        r.kv = e->alloc<longlong2>(cap);
+        r.idx = e->alloc<uint16_t>(cap);
         r.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * max_tiles);
         r.hdr = e->alloc<int64_t>((size_t)max_tiles * RT_Q);
         r.dlist = e->alloc<unsigned long long>((size_t)c.max_batch);
