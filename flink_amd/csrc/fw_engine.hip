@@ -471,8 +471,11 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 // 12-B records measured slower: the per-record probe of the global directory cost k_route more than the
 // 6 B/event it saved)
 // ------------------------------------------------------------------------------------------------
-constexpr int RT_TILE = 4096;
-constexpr int RT_THREADS = 512;
+#ifndef FW_RT_TILE_LOG
+#define FW_RT_TILE_LOG 12
+#endif
+constexpr int RT_TILE = 1 << FW_RT_TILE_LOG;  // records per k_route tile
+constexpr int RT_THREADS = RT_TILE / 8;      // eight records per thread
 constexpr int RT_Q = 2;                 // slices per tile routed through LDS (more go to the direct list)
 constexpr int RT_GS = 64;               // distinct slices per batch (k_aggregate rounds)
 constexpr int RT_MAXNB = 256;           // directory buckets the route table holds
@@ -482,7 +485,7 @@ constexpr int AG_WIN = 8;               // k_aggregate: directory slots probed w
 constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
 constexpr int AG_MAXPER = 17;           // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
 constexpr int RT_MAX_KB_BITS = 12;      // directory slots per bucket that k_aggregate holds in LDS
-constexpr int IDX_BITS = 12;            // record index within a tile (RT_TILE = 2^12)
+constexpr int IDX_BITS = FW_RT_TILE_LOG; // record index within a tile
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 
 struct RouteBuf {
@@ -552,9 +555,10 @@ __device__ __forceinline__ void block_scan_excl(int32_t* a, int n, int32_t* wtot
 
 // LDS layout of k_route (bytes): [0, 64K) staging of the bin-sorted records (fmix64(key), value); before
 // the scatter the same bytes hold, entry by entry of the thread owning the record (no barrier needed):
-// the key hashes int32[4096] at 0 (optional column), and for records outside their wave's reference slice
-// their slice numbers int64[4096] at 16K and flags int32[4096] at 48K.  Then [64K, 72K) the sorted records'
-// index in the tile, the bin counters, the scan scratch and the tile's slice set.
+// the key hashes int32[RT_TILE] at 0 (optional column), and for records outside their wave's reference
+// slice their slice numbers int64[RT_TILE] at 4 RT_TILE and flags int32[RT_TILE] at 12 RT_TILE.  Then the
+// sorted records' index in the tile (uint16[RT_TILE]), the bin counters, the scan scratch and the tile's
+// slice set.
 constexpr size_t RT_LDS = (size_t)RT_TILE * (16 + 2) + 4 * (size_t)(RT_Q * RT_MAXNB + 8) + 4 * 16 + 8 * RT_Q;
 
 template <int VT, int AGG, bool FIRST>
@@ -1933,7 +1937,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     const int nacc = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
     const size_t agg_need = agg_lds_bytes(s.kb_bits, nacc, max_tiles);
     const bool fits = s.kb_bits <= RT_MAX_KB_BITS && s.nb <= RT_MAXNB && agg_need <= 160 * 1024 &&
-                      c.max_batch >= RT_TILE && c.max_batch <= (1ll << 26);
+                      c.max_batch <= (1ll << 26);
     if (c.ingest_mode == 2 && !fits)
       return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
     e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && c.max_batch >= (1 << 16));
