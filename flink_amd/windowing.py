@@ -316,16 +316,26 @@ class WindowOperator:
         self._key_ids, self._key_names = {}, {}
         self.output = []
 
-    # keys: int (Long) keys pass through; other keys (e.g. String) are interned and carry hashCode()
+    # keys: int (Long) keys pass through with Long.hashCode; String keys are interned to dense ids and
+    # carry String.hashCode(), which is what KeyGroupRangeAssignment hashes (KeyGroupRangeAssignment.java:51-64).
+    # One operator takes one key type (a keyed stream has one key type), so interned ids never meet Long keys.
     def _key(self, k):
         if isinstance(k, (int, np.integer)) and not isinstance(k, bool):
+            if self._key_ids:
+                raise TypeError("a keyed stream has one key type: Long key after String keys")
+            self._long_keys = True
             return int(k), None
+        if not isinstance(k, str):
+            raise TypeError(f"key type {type(k).__name__} is not supported (Long or String keys: their Java "
+                            "hashCode() decides the key group)")
+        if getattr(self, "_long_keys", False):
+            raise TypeError("a keyed stream has one key type: String key after Long keys")
         kid = self._key_ids.get(k)
         if kid is None:
             kid = len(self._key_ids) + 1
             self._key_ids[k] = kid
             self._key_names[kid] = k
-        return kid, java_string_hash(k) if isinstance(k, str) else hash(k) & 0x7FFFFFFF
+        return kid, java_string_hash(k)
 
     def processElement(self, record):
         v = record.value
