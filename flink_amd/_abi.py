@@ -27,6 +27,10 @@ FW_AGG_SUM = 1
 FW_AGG_MIN = 2
 FW_AGG_MAX = 4
 FW_AGG_COUNT = 8
+FW_AGG_MAXBY = 16
+FW_AGG_MINBY = 32
+FW_AGGF_COMPARABLE = 1
+FW_AGGF_BY_LAST = 2
 FW_VALUE_I64 = 0
 FW_VALUE_F64 = 1
 FW_MEM_HOST = 0
@@ -50,7 +54,7 @@ class FwConfig(ctypes.Structure):
                 ("allowed_lateness", _i64), ("value_type", _i32), ("agg_mask", _i32), ("keep_first_f1", _i32),
                 ("max_parallelism", _i32), ("kg_start", _i32), ("kg_end", _i32), ("device", _i32),
                 ("max_open_slices", _i32), ("key_capacity", _i64), ("max_batch", _i64), ("out_capacity", _i64),
-                ("ingest_mode", _i32), ("reserved", _i32)]
+                ("ingest_mode", _i32), ("agg_flags", _i32)]
 
 
 class FwOut(ctypes.Structure):

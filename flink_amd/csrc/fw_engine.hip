@@ -82,6 +82,9 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int32_t mp, kg_start, kg_end;
   int32_t mp_mask;  // mp - 1 when mp is a power of two, else 0
   int32_t vt, agg, first;
+  int32_t cmpto;    // min/max of doubles in Double.compareTo order (ComparableAggregator), else Math.min/max
+  int32_t by;       // 0, FW_AGG_MAXBY or FW_AGG_MINBY: the extremal record (value, f1) is the result
+  int32_t by_last;  // maxBy/minBy tie rule: the later record (first = false)
   // directory
   int64_t* dir_keys;
   int32_t* dir_min_used;
@@ -203,6 +206,20 @@ __device__ __noinline__ int32_t slice_slot_at(int64_t* slice_tag, int32_t P, int
 }
 __device__ __forceinline__ int32_t slice_slot(const Spec& s, int64_t m) { return slice_slot_at(s.slice_tag, s.P, m); }
 
+// orderable codes of a value for the min / max columns: int64 values as they are; doubles in Math.min /
+// Math.max order, or Double.compareTo order for ComparableAggregator (.min/.max with FW_AGGF_COMPARABLE,
+// and always for maxBy/minBy)
+__device__ __forceinline__ int64_t min_code(int32_t vt, bool cmpto, int64_t v) {
+  if (vt == FW_VALUE_I64) return v;
+  const double d = __longlong_as_double(v);
+  return cmpto ? f64_cmp_code(d) : f64_min_code(d);
+}
+__device__ __forceinline__ int64_t max_code(int32_t vt, bool cmpto, int64_t v) {
+  if (vt == FW_VALUE_I64) return v;
+  const double d = __longlong_as_double(v);
+  return cmpto ? f64_cmp_code(d) : f64_max_code(d);
+}
+
 // Window bookkeeping for one record, following SlidingEventTimeWindows.assignWindows (:64-77) /
 // TumblingEventTimeWindows.assignWindows (:59-68).  Produces the record's slice number m and how many
 // of its windows are late (WindowOperator.isLate :470-472) or already fired (EventTimeTrigger.onElement
@@ -304,12 +321,10 @@ __device__ __forceinline__ bool pane_update(const Spec& s, int64_t idx, int64_t 
     }
   }
   if (AGG & FW_AGG_MIN) {
-    int64_t code = VT == FW_VALUE_I64 ? vbits : f64_min_code(__longlong_as_double(vbits));
-    atomicMin((long long*)&s.c.mn[idx], (long long)code);
+    atomicMin((long long*)&s.c.mn[idx], (long long)min_code(VT, s.cmpto, vbits));
   }
   if (AGG & FW_AGG_MAX) {
-    int64_t code = VT == FW_VALUE_I64 ? vbits : f64_max_code(__longlong_as_double(vbits));
-    atomicMax((long long*)&s.c.mx[idx], (long long)code);
+    atomicMax((long long*)&s.c.mx[idx], (long long)max_code(VT, s.cmpto, vbits));
   }
   if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&s.c.cnt[idx], 1ull);
   if (FIRST) {
@@ -818,23 +833,47 @@ __device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys
   return -1;
 }
 
-// one record into the bucket's LDS accumulators at slot kl
+// the bucket's LDS accumulators
+struct AggLds {
+  int64_t *sum, *mn, *mx, *cnt;
+  uint32_t* first;   // earliest record of the batch (batch index): the first arrival, and the "touched" mark
+  uint32_t* ord;     // maxBy / minBy: batch index of the extremal record
+};
+
+// one record into the bucket's LDS accumulators at slot kl.  maxBy / minBy take two passes over the
+// records (no lock: a (value, ordinal) pair cannot be updated by one atomic): pass 0 the extremal value
+// in Double.compareTo (Long) order, pass 1 among the records holding it the earliest (first) or latest
+// (last) batch index — ComparableAggregator MAXBY/MINBY with the tie rule (ComparableAggregator.java:74-81)
 template <int VT, int AGG>
-__device__ __forceinline__ void acc_add(int64_t* lsum, int64_t* lmin, int64_t* lmax, int64_t* lcnt, uint32_t* lfirst,
-                                        uint32_t kl, int64_t v, uint32_t oi) {
-  if (AGG & FW_AGG_SUM) {
-    if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&lsum[kl], (unsigned long long)v);
-    else unsafeAtomicAdd((double*)&lsum[kl], __longlong_as_double(v));
+__device__ __forceinline__ void acc_add(const AggLds& L, bool cmpto, bool by_last, int pass, uint32_t kl, int64_t v,
+                                        uint32_t oi) {
+  constexpr bool MAXBY = (AGG & FW_AGG_MAXBY) != 0, MINBY = (AGG & FW_AGG_MINBY) != 0;
+  if (MAXBY || MINBY) {
+    const int64_t code = VT == FW_VALUE_I64 ? v : f64_cmp_code(__longlong_as_double(v));
+    int64_t* ext = MAXBY ? L.mx : L.mn;
+    if (pass == 0) {
+      if (MAXBY) atomicMax((long long*)&ext[kl], (long long)code);
+      else atomicMin((long long*)&ext[kl], (long long)code);
+      atomicMin(&L.first[kl], oi);
+    } else if (ext[kl] == code) {
+      if (by_last) atomicMax(&L.ord[kl], oi);
+      else atomicMin(&L.ord[kl], oi);
+    }
+    return;
   }
-  if (AGG & FW_AGG_MIN) atomicMin((long long*)&lmin[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v))));
-  if (AGG & FW_AGG_MAX) atomicMax((long long*)&lmax[kl], (long long)(VT == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v))));
-  if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&lcnt[kl], 1ull);
-  atomicMin(&lfirst[kl], oi);   // earliest record of the batch: the first arrival, and the "touched" mark
+  if (AGG & FW_AGG_SUM) {
+    if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&L.sum[kl], (unsigned long long)v);
+    else unsafeAtomicAdd((double*)&L.sum[kl], __longlong_as_double(v));
+  }
+  if (AGG & FW_AGG_MIN) atomicMin((long long*)&L.mn[kl], (long long)min_code(VT, cmpto, v));
+  if (AGG & FW_AGG_MAX) atomicMax((long long*)&L.mx[kl], (long long)max_code(VT, cmpto, v));
+  if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&L.cnt[kl], 1ull);
+  atomicMin(&L.first[kl], oi);   // earliest record of the batch: the first arrival, and the "touched" mark
 }
 
 // LDS bytes k_aggregate needs for buckets of 2^kb_bits slots and ntiles tiles
-__host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_t ntiles) {
-  return (size_t)8 * ((size_t)1 << kb_bits) + ((size_t)(1 << kb_bits) + 65) * 8 * nacc +
+__host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_t ntiles, bool by) {
+  return (size_t)8 * ((size_t)1 << kb_bits) + ((size_t)(1 << kb_bits) + 65) * (8 * nacc + (by ? 4 : 0)) +
          ((((size_t)(1 << kb_bits) + 65) + 3) & ~(size_t)3) * 4 + (size_t)12 * RT_Q * ntiles + 8 * (size_t)ntiles + 4 +
          4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8;
 }
@@ -854,12 +893,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   const int KA = KB + 65;                               // accumulators: KB slots, one dummy per lane, the MIN key
   const uint32_t KMIN = (uint32_t)KB + 64;              // slot of the Long.MIN_VALUE key (kid D, bucket 0)
   uint64_t* lh = (uint64_t*)smem;                       // [KB] fmix64 of this bucket's directory slice (EMPTY_H = free)
+  constexpr bool MAXBY = (AGG & FW_AGG_MAXBY) != 0, MINBY = (AGG & FW_AGG_MINBY) != 0, BY = MAXBY || MINBY;
+  constexpr bool HAS_MIN = (AGG & FW_AGG_MIN) || MINBY, HAS_MAX = (AGG & FW_AGG_MAX) || MAXBY;
   int64_t* lsum = (int64_t*)(lh + KB);                  // [KA]
   int64_t* lmin = lsum + KA;
-  int64_t* lmax = lmin + ((AGG & FW_AGG_MIN) ? KA : 0);
-  int64_t* lcnt = lmax + ((AGG & FW_AGG_MAX) ? KA : 0);
+  int64_t* lmax = lmin + (HAS_MIN ? KA : 0);
+  int64_t* lcnt = lmax + (HAS_MAX ? KA : 0);
   uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest record (batch index)
-  int64_t* lhdr = (int64_t*)(lfirst + ((KA + 3) & ~3)); // [ntiles][RT_Q] the tiles' routed slices
+  uint32_t* lord = lfirst + ((KA + 3) & ~3);            // [KA] maxBy/minBy: the extremal record (batch index)
+  int64_t* lhdr = (int64_t*)(lord + (BY ? ((KA + 3) & ~3) : 0)); // [ntiles][RT_Q] the tiles' routed slices
   uint32_t* lseg = (uint32_t*)(lhdr + (int64_t)r.ntiles * RT_Q);   // [ntiles][RT_Q] this bucket's segment start | end << 16
   int32_t* sst = (int32_t*)(lseg + (int64_t)r.ntiles * RT_Q);     // [ntiles] segment start within the tile
   int32_t* off = sst + r.ntiles;                        // [ntiles + 1] segment lengths, then their exclusive prefix
@@ -896,11 +938,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   }
   for (int x = threadIdx.x; x < KA; x += NT) {
     lsum[x] = 0;
-    if (AGG & FW_AGG_MIN) lmin[x] = INT64_MAX;
-    if (AGG & FW_AGG_MAX) lmax[x] = INT64_MIN;
+    if (HAS_MIN) lmin[x] = INT64_MAX;
+    if (HAS_MAX) lmax[x] = INT64_MIN;
     if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
     lfirst[x] = NO_FIRST;
+    if (BY) lord[x] = s.by_last ? 0u : NO_FIRST;
   }
+  const AggLds L{lsum, lmin, lmax, lcnt, lfirst, lord};
+  const bool cmpto = s.cmpto != 0, by_last = s.by_last != 0;
   if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
   // no memset between batches: batch j's counter was zeroed by k_aggregate of batch j - DC_RING/2, whose
   // counter is no longer read and whose successor k_route starts only after this kernel (event order)
@@ -1029,6 +1074,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     // walks forward from it (a step spans ~4 segments at 256 buckets), and every load of a wave's UR
     // steps is issued before any of them is processed
     constexpr int UR = 2;
+    constexpr int NPASS = BY ? 2 : 1;
+    for (int pass = 0; pass < NPASS; ++pass) {
     for (int32_t cb = 0; cb < R; cb += AG_CHS * 64) {   // uniform
       for (int t = threadIdx.x; t < r.ntiles; t += NT) {
         const int32_t o = off[t], l = off[t + 1] - o;
@@ -1062,7 +1109,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
           bool act = ra[u];
           uint32_t kl = probe(act, (uint64_t)rv[u].x);
           kl = act ? kl : (uint32_t)KB + (uint32_t)lane;   // inactive lanes update a private dummy slot
-          acc_add<VT, AGG>(lsum, lmin, lmax, lcnt, lfirst, kl, rv[u].y, ri[u]);
+          acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, rv[u].y, ri[u]);
         }
       };
       // software pipelined: the next group's loads are in flight while this group updates LDS (two
@@ -1100,10 +1147,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         } else {
           (void)dir_lookup(s, key);   // marks the Long.MIN_VALUE key's column in use
         }
-        acc_add<VT, AGG>(lsum, lmin, lmax, lcnt, lfirst, kl, b.val[i], (uint32_t)i);
+        acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, b.val[i], (uint32_t)i);
       }
     }
     __syncthreads();
+    }   // passes
     FW_STAMP(r, SB, 3 + 3 * min(g, 1));
     // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
     for (int x = threadIdx.x; x <= KB; x += NT) {
@@ -1119,7 +1167,22 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       if (AGG & FW_AGG_MIN) { const int64_t o = s.c.mn[idx]; if (lmin[xl] < o) s.c.mn[idx] = lmin[xl]; }
       if (AGG & FW_AGG_MAX) { const int64_t o = s.c.mx[idx]; if (lmax[xl] > o) s.c.mx[idx] = lmax[xl]; }
       if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[xl]);
-      if (FIRST) {
+      if (BY) {
+        // the batch's extremal record against the pane's (an earlier arrival: a tie keeps it under
+        // "first", takes the batch's under "last"); its ordinal in the count column, its f1 in f1v
+        int64_t* col = MAXBY ? s.c.mx : s.c.mn;
+        const int64_t code = MAXBY ? lmax[xl] : lmin[xl];
+        const uint32_t lo = lord[xl];
+        const int64_t cur = col[idx];
+        const bool present = s.c.first[idx] != INT64_MAX;
+        if (!present || (MAXBY ? code > cur : code < cur) || (code == cur && by_last)) {
+          col[idx] = code;
+          s.c.cnt[idx] = ord_base + (int64_t)lo;
+          s.c.f1v[idx] = f1col[lo];
+        }
+        if (ord_base + (int64_t)lf < s.c.first[idx]) s.c.first[idx] = ord_base + (int64_t)lf;
+        lord[xl] = by_last ? 0u : NO_FIRST;
+      } else if (FIRST) {
         // first arrival: the pane's earliest record of the batch, if the pane is new
         if (ord_base + (int64_t)lf < s.c.first[idx]) {
           s.c.first[idx] = ord_base + (int64_t)lf;
@@ -1130,8 +1193,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       }
       // cleared for the next round (untouched entries still are; the per-lane dummies are never read)
       lsum[xl] = 0;
-      if (AGG & FW_AGG_MIN) lmin[xl] = INT64_MAX;
-      if (AGG & FW_AGG_MAX) lmax[xl] = INT64_MIN;
+      if (HAS_MIN) lmin[xl] = INT64_MAX;
+      if (HAS_MAX) lmax[xl] = INT64_MIN;
       if (AGG & FW_AGG_COUNT) lcnt[xl] = 0;
       lfirst[xl] = NO_FIRST;
     }
@@ -1147,11 +1210,24 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
 struct LateAcc {
   int64_t sum;    // int64 or double bits
   int64_t mn, mx, cnt;
+  int64_t ord, f1;  // maxBy / minBy: the extremal record's arrival ordinal and f1
   int32_t vt;
-  __host__ __device__ LateAcc() : sum(0), mn(INT64_MAX), mx(INT64_MIN), cnt(0), vt(0) {}
+  int32_t by;       // 0, or FW_AGG_MAXBY / FW_AGG_MINBY, | 1 for the last-tie rule
+  __host__ __device__ LateAcc() : sum(0), mn(INT64_MAX), mx(INT64_MIN), cnt(0), ord(INT64_MAX), f1(0), vt(0), by(0) {}
 };
+// ComparableAggregator.reduce for MAXBY / MINBY (ComparableAggregator.java:74-81): the extremal record;
+// on a tie the earlier one (first) or the later one — decided by arrival ordinal, not argument order
+__device__ __forceinline__ const LateAcc& by_select(const LateAcc& a, const LateAcc& b) {
+  const bool maxby = (a.by & FW_AGG_MAXBY) != 0, last = (a.by & 1) != 0;
+  const int64_t ca = maxby ? a.mx : a.mn, cb = maxby ? b.mx : b.mn;
+  bool take_b;
+  if (ca != cb) take_b = maxby ? cb > ca : cb < ca;
+  else take_b = last ? b.ord > a.ord : b.ord < a.ord;
+  return take_b ? b : a;
+}
 struct LateCombine {
   __device__ LateAcc operator()(const LateAcc& a, const LateAcc& b) const {
+    if (a.by) return by_select(a, b);
     LateAcc r;
     r.vt = a.vt;
     if (a.vt == FW_VALUE_I64) {
@@ -1167,7 +1243,8 @@ struct LateCombine {
 };
 
 __global__ void k_late_prepare(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
-                               const int64_t* val, unsigned long long* seg, LateAcc* acc, int64_t* headpos) {
+                               const int64_t* val, unsigned long long* seg, LateAcc* acc, int64_t* headpos,
+                               const int64_t* f1col, int64_t ord_base) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nl) return;
   unsigned long long k = sorted_key[j];
@@ -1178,9 +1255,12 @@ __global__ void k_late_prepare(Spec s, const unsigned long long* sorted_key, int
   LateAcc a;
   a.vt = s.vt;
   a.sum = v;
-  a.mn = s.vt == FW_VALUE_I64 ? v : f64_min_code(__longlong_as_double(v));
-  a.mx = s.vt == FW_VALUE_I64 ? v : f64_max_code(__longlong_as_double(v));
+  a.mn = min_code(s.vt, s.cmpto, v);
+  a.mx = max_code(s.vt, s.cmpto, v);
   a.cnt = 1;
+  a.by = s.by ? (s.by | (s.by_last ? 1 : 0)) : 0;
+  a.ord = ord_base + i;
+  a.f1 = f1col[i];
   acc[j] = a;
 }
 
@@ -1195,6 +1275,12 @@ __device__ __forceinline__ LateAcc pane_load(const Spec& s, int64_t idx) {
   a.mn = s.c.mn ? s.c.mn[idx] : INT64_MAX;
   a.mx = s.c.mx ? s.c.mx[idx] : INT64_MIN;
   a.cnt = s.c.cnt ? s.c.cnt[idx] : 0;
+  if (s.by) {   // the extremal record: ordinal in the count column, its f1 in f1v
+    a.by = s.by | (s.by_last ? 1 : 0);
+    a.ord = a.cnt;
+    a.cnt = 0;
+    a.f1 = s.c.f1v[idx];
+  }
   return a;
 }
 
@@ -1238,7 +1324,9 @@ __global__ void k_late_emit(Spec s, const unsigned long long* sorted_key, int64_
   else if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) out = base_present ? op(pane_load(s, idx), acc[j]) : acc[j];
   else out = base_present ? op(pane_load(s, idx), scanned[j]) : scanned[j];
   int64_t f1 = 0;
-  if (s.first) {
+  if (s.by) {
+    f1 = out.f1;   // maxBy / minBy: the extremal record's
+  } else if (s.first) {
     // first arrival: the pane's if it existed, else the segment head (purging: the record itself
     // unless it is the head of a segment over an existing pane)
     int64_t i_self = (int64_t)(sorted_key[j] & ((1ull << idx_bits) - 1));
@@ -1279,10 +1367,11 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
   if (s.c.sum) s.c.sum[idx] = st.sum;
   if (s.c.mn) s.c.mn[idx] = st.mn;
   if (s.c.mx) s.c.mx[idx] = st.mx;
-  if (s.c.cnt) s.c.cnt[idx] = st.cnt;
+  if (s.c.cnt) s.c.cnt[idx] = s.by ? st.ord : st.cnt;
+  if (s.by) s.c.f1v[idx] = st.f1;
   if (!base_present) {
     int64_t ih = (int64_t)(sorted_key[headpos[j]] & ((1ull << idx_bits) - 1));
-    if (s.first) { s.c.first[idx] = ord_base + ih; s.c.f1v[idx] = f1col[ih]; }
+    if (s.first) { s.c.first[idx] = ord_base + ih; if (!s.by) s.c.f1v[idx] = f1col[ih]; }
     else s.c.present[idx] = 1;
   }
   (void)p;
@@ -1393,7 +1482,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       for (int w = 0; w < WM_THREADS / 64; ++w) { const int32_t c = wtot[w]; off += w < wave ? c : 0; tot += c; }
       if (threadIdx.x == 0 && tot > 0) { base = atomicAdd(s.o.count, (unsigned long long)tot); fired += tot; }
       __syncthreads();
-      if (any) emit_record(s, base + off + rank, kid_key(s, kid), f1, max_ts, a);
+      if (any) emit_record(s, base + off + rank, kid_key(s, kid), s.by ? a.f1 : f1, max_ts, a);
     }
     __syncthreads();
   }
@@ -1461,7 +1550,7 @@ __global__ void k_restore(Spec s, const int64_t* ent, int64_t n) {
     const int32_t p = slice_slot(s, x[0]);
     if (kid < 0 || p < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
     const int64_t idx = (int64_t)p * s.stride + kid;
-    s.c.sum[idx] = x[2];
+    if (s.c.sum) s.c.sum[idx] = x[2];
     if (s.c.mn) s.c.mn[idx] = x[3];
     if (s.c.mx) s.c.mx[idx] = x[4];
     if (s.c.cnt) s.c.cnt[idx] = x[5];
@@ -1798,12 +1887,16 @@ static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
     if (_s.vt == FW_VALUE_I64) {                                                                 \
       switch (_s.agg) {                                                                          \
         case 1: if (_f) FN<0, 1, true>(e, ##__VA_ARGS__); else FN<0, 1, false>(e, ##__VA_ARGS__); break;   \
+        case 16: FN<0, 16, true>(e, ##__VA_ARGS__); break;                                       \
+        case 32: FN<0, 32, true>(e, ##__VA_ARGS__); break;                                       \
         case 15: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
         default: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
       }                                                                                          \
     } else {                                                                                     \
       switch (_s.agg) {                                                                          \
         case 1: if (_f) FN<1, 1, true>(e, ##__VA_ARGS__); else FN<1, 1, false>(e, ##__VA_ARGS__); break;   \
+        case 16: FN<1, 16, true>(e, ##__VA_ARGS__); break;                                       \
+        case 32: FN<1, 32, true>(e, ##__VA_ARGS__); break;                                       \
         default: if (_f) FN<1, 15, true>(e, ##__VA_ARGS__); else FN<1, 15, false>(e, ##__VA_ARGS__); break; \
       }                                                                                          \
     }                                                                                            \
@@ -1829,7 +1922,11 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       c.kg_end >= c.max_parallelism)
     return bad("bad key-group range");
   if (c.value_type != FW_VALUE_I64 && c.value_type != FW_VALUE_F64) return bad("bad value type");
-  if ((c.agg_mask & ~15) != 0 || c.agg_mask == 0) return bad("bad aggregate mask");
+  const bool by = (c.agg_mask & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;
+  if ((c.agg_mask & ~63) != 0 || c.agg_mask == 0 || (by && c.agg_mask != FW_AGG_MAXBY && c.agg_mask != FW_AGG_MINBY))
+    return bad("bad aggregate mask (maxBy / minBy return the whole record and combine with nothing else)");
+  if ((c.agg_flags & ~(FW_AGGF_COMPARABLE | FW_AGGF_BY_LAST)) != 0) return bad("bad aggregate flags");
+  if (by && c.ingest_mode == 1) return unsupported("maxBy / minBy run on the partitioned ingest form (ingest_mode 0 or 2)");
   if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
   if (c.ingest_mode < 0 || c.ingest_mode > 2) return bad("bad ingest mode");
   if (c.assigner == FW_SLIDING && (c.allowed_lateness > 0 || c.trigger != FW_TRIGGER_EVENT_TIME))
@@ -1867,8 +1964,11 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.kg_start = c.kg_start;
   s.kg_end = c.kg_end;
   s.vt = c.value_type;
-  s.agg = c.agg_mask == FW_AGG_SUM ? FW_AGG_SUM : 15;   // instantiated reduce shapes
-  s.first = c.keep_first_f1 ? 1 : 0;
+  s.agg = by ? c.agg_mask : (c.agg_mask == FW_AGG_SUM ? FW_AGG_SUM : 15);   // instantiated reduce shapes
+  s.by = by ? c.agg_mask : 0;
+  s.by_last = (c.agg_flags & FW_AGGF_BY_LAST) ? 1 : 0;
+  s.cmpto = by || (c.agg_flags & FW_AGGF_COMPARABLE) ? 1 : 0;
+  s.first = c.keep_first_f1 || by ? 1 : 0;   // maxBy/minBy: the pane's presence and the extremal f1
 
   // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys): short linear-probe sequences
   s.D = next_pow2(std::max<int64_t>((c.key_capacity <= (1 << 20) ? 4 : 2) * c.key_capacity, 64));
@@ -1893,9 +1993,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.slice_tag = e->alloc<int64_t>((size_t)P);
   const size_t cells = (size_t)P * (size_t)s.stride;
   s.c.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>(cells) : nullptr;
-  s.c.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(cells) : nullptr;
-  s.c.mx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>(cells) : nullptr;
-  s.c.cnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>(cells) : nullptr;
+  s.c.mn = (s.agg & (FW_AGG_MIN | FW_AGG_MINBY)) ? e->alloc<int64_t>(cells) : nullptr;
+  s.c.mx = (s.agg & (FW_AGG_MAX | FW_AGG_MAXBY)) ? e->alloc<int64_t>(cells) : nullptr;
+  s.c.cnt = (s.agg & FW_AGG_COUNT) || by ? e->alloc<int64_t>(cells) : nullptr;   // maxBy/minBy: the extremal ordinal
   if (s.first) {
     s.c.first = e->alloc<int64_t>(cells);
     s.c.f1v = e->alloc<int64_t>(cells);
@@ -1911,8 +2011,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   o.f1 = s.first ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
   o.ts = e->alloc<int64_t>((size_t)o.capacity);
   o.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
-  o.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
-  o.mx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.mn = (s.agg & (FW_AGG_MIN | FW_AGG_MINBY)) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.mx = (s.agg & (FW_AGG_MAX | FW_AGG_MAXBY)) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
   o.cnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
   o.count = e->alloc<unsigned long long>(1);
   o.mark_capacity = 1 << 16;
@@ -1934,13 +2034,15 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   // and batches are large; direct atomics otherwise
   {
     const int32_t max_tiles = (int32_t)((c.max_batch + RT_TILE - 1) / RT_TILE);
-    const int nacc = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-    const size_t agg_need = agg_lds_bytes(s.kb_bits, nacc, max_tiles);
+    const int nacc = 1 + ((s.agg & (FW_AGG_MIN | FW_AGG_MINBY)) ? 1 : 0) + ((s.agg & (FW_AGG_MAX | FW_AGG_MAXBY)) ? 1 : 0) +
+                     ((s.agg & FW_AGG_COUNT) ? 1 : 0);
+    const size_t agg_need = agg_lds_bytes(s.kb_bits, nacc, max_tiles, by);
     const bool fits = s.kb_bits <= RT_MAX_KB_BITS && s.nb <= RT_MAXNB && agg_need <= 160 * 1024 &&
                       c.max_batch <= (1ll << 26);
     if (c.ingest_mode == 2 && !fits)
       return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
-    e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && c.max_batch >= (1 << 16));
+    e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by));
+    if (by && !e->routed) return unsupported("maxBy / minBy need the partitioned ingest form (key_capacity <= 256 Ki)");
     if (e->routed) {
       e->max_tiles = max_tiles;
       const size_t cap = (size_t)max_tiles * RT_TILE;
@@ -2122,7 +2224,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
       HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, e->late_key, e->late_key_sorted, (size_t)nl, 0, 64, e->stream));
       int blocks = (int)((nl + BLOCK - 1) / BLOCK);
       hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
-                         e->idx_bits, dv, e->seg, e->late_acc, e->headpos);
+                         e->idx_bits, dv, e->seg, e->late_acc, e->headpos, df1, e->ordinal);
       tb = e->temp_bytes;
       HIPCHK(e, rocprim::inclusive_scan(e->temp, tb, e->headpos, e->headpos_scan, (size_t)nl,
                                         rocprim::maximum<int64_t>(), e->stream));
@@ -2226,8 +2328,8 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
   // only the fields the reduce function asked for
   const int32_t um = e->cfg.agg_mask;
   if (!(um & FW_AGG_SUM)) { o->sum_i64 = nullptr; o->sum_f64 = nullptr; }
-  if (!(um & FW_AGG_MIN)) { o->min_i64 = nullptr; o->min_f64 = nullptr; }
-  if (!(um & FW_AGG_MAX)) { o->max_i64 = nullptr; o->max_f64 = nullptr; }
+  if (!(um & (FW_AGG_MIN | FW_AGG_MINBY))) { o->min_i64 = nullptr; o->min_f64 = nullptr; }
+  if (!(um & (FW_AGG_MAX | FW_AGG_MAXBY))) { o->max_i64 = nullptr; o->max_f64 = nullptr; }
   if (!(um & FW_AGG_COUNT)) o->count = nullptr;
   // the log restarts; device pointers handed out above stay valid until the next enqueue
   HIPCHK(e, hipMemsetAsync(L.count, 0, 8, e->stream));
@@ -2383,7 +2485,8 @@ static int build_snapshot(fw_engine* e) {
       if (!pres || kid_kg[k] < 0) continue;
       const int64_t key = (int64_t)k == s.D ? fw::EMPTY_KEY : keys[k];
       const int64_t ent[FW_SNAP_ENTRY_WORDS] = {
-          m, key, sum[k], s.c.mn ? mn[k] : INT64_MAX, s.c.mx ? mx[k] : INT64_MIN, s.c.cnt ? cnt[k] : 0,
+          m, key, sum[k], s.c.mn ? mn[k] : INT64_MAX, s.c.mx ? mx[k] : INT64_MIN,
+          s.c.cnt ? (s.by ? cnt[k] - e->ordinal : cnt[k]) : 0,
           s.first ? first[k] - e->ordinal : -1, s.first ? f1v[k] : 0};
       auto& v = e->snap_kg[(size_t)kid_kg[k]];
       v.insert(v.end(), ent, ent + FW_SNAP_ENTRY_WORDS);

@@ -120,6 +120,15 @@ FW_HD int64_t f64_max_code(double x) {
   int64_t b; __builtin_memcpy(&b, &x, 8);
   return b >= 0 ? b : (b ^ INT64_MAX);
 }
+// Orderable encoding for Double.compareTo (JDK: doubleToLongBits order — every NaN equal and above
+// +inf, -0.0 < +0.0), the order of ComparableAggregator's Comparator (Comparator.java:45-105).  The NaN
+// is canonicalised as doubleToLongBits does, so it decodes as the canonical quiet NaN.
+FW_HD int64_t f64_cmp_code(double x) {
+  int64_t b;
+  if (x != x) b = 0x7ff8000000000000ll;
+  else __builtin_memcpy(&b, &x, 8);
+  return b >= 0 ? b : (b ^ INT64_MAX);
+}
 FW_HD double f64_from_code(int64_t c) {
   if (c == INT64_MIN || c == INT64_MAX) {  // a NaN won (canonical quiet NaN)
     uint64_t nan = 0x7ff8000000000000ull; double d; __builtin_memcpy(&d, &nan, 8); return d;

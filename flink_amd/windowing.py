@@ -90,17 +90,28 @@ class ReduceFunction:
 
     A record is (key, f1, value).  reduce(value1 = stored, value2 = new) returns value1 with
     sum = v1 + v2, min = Math.min, max = Math.max, count = c1 + c2; f1 stays value1's (first arrival).
+    comparable=True orders min/max by Double.compareTo instead (ComparableAggregator .min/.max).
+    "maxBy" / "minBy" return the extremal record itself, value and f1 (ComparableAggregator MAXBY/MINBY,
+    ComparableAggregator.java:74-81), a tie keeping the earlier record when first=True.
     `SumReducer()` is WindowOperatorTest.SumReducer (WindowOperatorTest.java:2245-2252).
     """
-    FIELDS = {"sum": _abi.FW_AGG_SUM, "min": _abi.FW_AGG_MIN, "max": _abi.FW_AGG_MAX, "count": _abi.FW_AGG_COUNT}
+    FIELDS = {"sum": _abi.FW_AGG_SUM, "min": _abi.FW_AGG_MIN, "max": _abi.FW_AGG_MAX, "count": _abi.FW_AGG_COUNT,
+              "maxBy": _abi.FW_AGG_MAXBY, "minBy": _abi.FW_AGG_MINBY}
+    COLUMN = {"sum": "sum", "min": "min", "max": "max", "count": "count", "maxBy": "max", "minBy": "min"}
 
-    def __init__(self, fields=("sum",), value_type="i64", keep_first_f1=False):
+    def __init__(self, fields=("sum",), value_type="i64", keep_first_f1=False, comparable=False, first=True):
         self.fields = tuple(fields)
         self.mask = 0
         for f in self.fields:
             self.mask |= self.FIELDS[f]
+        self.by = bool(self.mask & (_abi.FW_AGG_MAXBY | _abi.FW_AGG_MINBY))
+        if self.by and len(self.fields) != 1:
+            raise ValueError("maxBy / minBy return the whole record and combine with no other field")
         self.value_type = value_type
-        self.keep_first_f1 = keep_first_f1
+        self.keep_first_f1 = keep_first_f1 or self.by   # maxBy/minBy: the extremal record's f1
+        self.comparable = comparable
+        self.first = first
+        self.flags = (_abi.FW_AGGF_COMPARABLE if comparable else 0) | (0 if first else _abi.FW_AGGF_BY_LAST)
 
     @property
     def vt(self):
@@ -109,6 +120,32 @@ class ReduceFunction:
 
 def SumReducer(value_type="i64"):
     return ReduceFunction(("sum",), value_type)
+
+
+class Aggregations:
+    """The built-in window aggregations of WindowedStream (WindowedStream.java:523-713) over the record's
+    value field: sum (SumAggregator), min/max (ComparableAggregator MIN/MAX: value1's other fields, the
+    field set to the extremum in compareTo order) and minBy/maxBy (the extremal record)."""
+
+    @staticmethod
+    def sum(value_type="i64"):
+        return ReduceFunction(("sum",), value_type, keep_first_f1=True)
+
+    @staticmethod
+    def min(value_type="i64"):
+        return ReduceFunction(("min",), value_type, keep_first_f1=True, comparable=True)
+
+    @staticmethod
+    def max(value_type="i64"):
+        return ReduceFunction(("max",), value_type, keep_first_f1=True, comparable=True)
+
+    @staticmethod
+    def minBy(value_type="i64", first=True):
+        return ReduceFunction(("minBy",), value_type, first=first)
+
+    @staticmethod
+    def maxBy(value_type="i64", first=True):
+        return ReduceFunction(("maxBy",), value_type, first=first)
 
 
 # ------------------------------------------------------------------ stream elements
@@ -294,6 +331,7 @@ def make_config(assigner, reduce_function, trigger=None, allowed_lateness=0, max
     c.max_batch = max_batch
     c.out_capacity = out_capacity
     c.ingest_mode = ingest_mode
+    c.agg_flags = getattr(reduce_function, "flags", 0)
     return c
 
 
@@ -377,8 +415,8 @@ class WindowOperator:
         if self.reduce.keep_first_f1:
             vals.append(int(res["f1"][i]))
         for f in self.reduce.fields:
-            col = res[{"sum": "sum", "min": "min", "max": "max", "count": "count"}[f] +
-                      ("" if f == "count" else ("_i64" if self.reduce.value_type == "i64" else "_f64"))]
+            c = ReduceFunction.COLUMN[f]
+            col = res[c + ("" if c == "count" else ("_i64" if self.reduce.value_type == "i64" else "_f64"))]
             vals.append(col[i].item())
         return StreamRecord(tuple([key] + vals), int(res["ts"][i]))
 

@@ -71,11 +71,23 @@ extern "C" {
  *   max   = Math.max(value1.max, value2.max)
  *   count = value1.count + value2.count            (each record starts at 1)
  *   f1    = value1.f1                              (first arrival into the pane: SumAggregator.java:64-72)
+ * FW_AGG_MAXBY / FW_AGG_MINBY instead return the extremal record (value and f1).
  */
 #define FW_AGG_SUM    1
 #define FW_AGG_MIN    2
 #define FW_AGG_MAX    4
 #define FW_AGG_COUNT  8
+/* ComparableAggregator MAXBY / MINBY (SJ/api/functions/aggregation/ComparableAggregator.java:66-90,
+ * Comparator.java:45-105): the result is the whole extremal record — its value (in the max / min column)
+ * and its f1 — ties resolved by FW_AGGF_BY_LAST (first = keep value1, the earlier record).  Used alone. */
+#define FW_AGG_MAXBY  16
+#define FW_AGG_MINBY  32
+
+/* agg_flags */
+#define FW_AGGF_COMPARABLE  1  /* min/max order doubles by Double.compareTo (ComparableAggregator .min/.max:
+                                  NaN above +inf, -0.0 < +0.0) instead of Math.min/max (NaN wins); long
+                                  values order the same either way.  MAXBY/MINBY always use compareTo. */
+#define FW_AGGF_BY_LAST     2  /* maxBy/minBy(pos, first = false): a tie takes the later record */
 
 #define FW_VALUE_I64  0
 #define FW_VALUE_F64  1
@@ -105,7 +117,7 @@ typedef struct {
   int64_t max_batch;         /* max records per fw_push_batch                                   */
   int64_t out_capacity;      /* max fired records between two fw_collect calls                  */
   int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate     */
-  int32_t reserved;
+  int32_t agg_flags;         /* OR of FW_AGGF_*                                                 */
 } fw_config;
 
 /* Output between two collects: records and watermark marks.  Records [mark_pos[i-1], mark_pos[i])

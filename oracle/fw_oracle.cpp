@@ -25,7 +25,9 @@
 //   InternalTimer               SJ/api/operators/InternalTimer.java:59-86
 //   processWatermark            SJ/api/operators/AbstractStreamOperator.java:803-808
 //   reduce functions            SJ/api/functions/aggregation/SumAggregator.java:64-72, SumFunction.java:60-77,
-//                               JDK Math.min/Math.max (double), Long arithmetic (wrapping)
+//                               JDK Math.min/Math.max (double), Long arithmetic (wrapping),
+//                               ComparableAggregator.java:66-90 + Comparator.java:45-105 (min/max/minBy/maxBy
+//                               over Comparable fields: Long.compareTo, Double.compareTo)
 //
 // Java semantics kept: wrapping int32/int64 arithmetic (done in unsigned), logical >>>, truncating %,
 // Long.MIN_VALUE-timestamp error, cleanup-time overflow clamp, arrival-order left fold.
@@ -118,6 +120,19 @@ double javaMax(double a, double b) {
   return (a >= b) ? a : b;
 }
 
+// JDK Double.compare(a, b): doubleToLongBits order (every NaN equal, above +inf; -0.0 < +0.0)
+int64_t doubleOrderKey(double x) {
+  int64_t b;
+  if (x != x) b = 0x7ff8000000000000ll;   // doubleToLongBits canonicalises NaN
+  else std::memcpy(&b, &x, 8);
+  return b >= 0 ? b : (b ^ INT64_MAX);
+}
+int javaDoubleCompare(double a, double b) {
+  const int64_t x = doubleOrderKey(a), y = doubleOrderKey(b);
+  return x < y ? -1 : (x == y ? 0 : 1);
+}
+int javaLongCompare(int64_t a, int64_t b) { return a < b ? -1 : (a == b ? 0 : 1); }
+
 struct Config {
   fw_config c;
   int64_t size() const { return c.size; }
@@ -126,6 +141,15 @@ struct Config {
 // ReduceFunction.reduce(value1 = stored, value2 = incoming); non-aggregated fields from value1
 // (SumAggregator.java:64-72 copies value1; user lambdas of the form Tuple.of(a.f0, a.f1, ...) likewise).
 Acc reduceFn(const fw_config& c, const Acc& v1, const Acc& v2) {
+  if (c.agg_mask == FW_AGG_MAXBY || c.agg_mask == FW_AGG_MINBY) {
+    // ComparableAggregator.reduce, byAggregate (ComparableAggregator.java:74-81): the field is the record's
+    // value; Comparator MaxBy/MinBy.isExtremal (Comparator.java:60-93) -> 1 / 0 / -1
+    const int cmp = c.value_type == FW_VALUE_I64 ? javaLongCompare(v1.max_i, v2.max_i) : javaDoubleCompare(v1.max_d, v2.max_d);
+    const int ext = c.agg_mask == FW_AGG_MAXBY ? (cmp > 0 ? 1 : (cmp == 0 ? 0 : -1)) : (cmp < 0 ? 1 : (cmp == 0 ? 0 : -1));
+    const bool first = (c.agg_flags & FW_AGGF_BY_LAST) == 0;
+    if (ext == 0) return first ? v1 : v2;
+    return ext == 1 ? v1 : v2;
+  }
   Acc r = v1;
   if (c.value_type == FW_VALUE_I64) {
     r.sum_i = jlong_add(v1.sum_i, v2.sum_i);                 // SumFunction.LongSum :60-66
@@ -133,8 +157,15 @@ Acc reduceFn(const fw_config& c, const Acc& v1, const Acc& v2) {
     r.max_i = v1.max_i >= v2.max_i ? v1.max_i : v2.max_i;     // Math.max(long,long)
   } else {
     r.sum_d = v1.sum_d + v2.sum_d;                            // SumFunction.DoubleSum :68-77
-    r.min_d = javaMin(v1.min_d, v2.min_d);
-    r.max_d = javaMax(v1.max_d, v2.max_d);
+    if (c.agg_flags & FW_AGGF_COMPARABLE) {
+      // ComparableAggregator MIN / MAX (not byAggregate): value1's field becomes o2 unless o1 is
+      // extremal (MinComparator / MaxComparator.isExtremal, Comparator.java:45-56,95-105)
+      r.min_d = javaDoubleCompare(v1.min_d, v2.min_d) < 0 ? v1.min_d : v2.min_d;
+      r.max_d = javaDoubleCompare(v1.max_d, v2.max_d) > 0 ? v1.max_d : v2.max_d;
+    } else {
+      r.min_d = javaMin(v1.min_d, v2.min_d);
+      r.max_d = javaMax(v1.max_d, v2.max_d);
+    }
   }
   r.count = jlong_add(v1.count, v2.count);
   return r;
