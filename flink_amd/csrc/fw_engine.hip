@@ -351,11 +351,40 @@ struct BatchIn {
   unsigned long long* late_count;
   int64_t late_capacity;
   int32_t idx_bits;
+  // sliding windows: one fire element per (record, window in its lateness period past maxTimestamp)
+  unsigned long long* fire_key;   // (window pane id << idx_bits) | idx, window pane = floor_mod(n, P) * stride + kid
+  unsigned long long* fire_count;
+  int64_t fire_capacity;
   // direct form with first arrival: panes created by the batch, for the f1 fix-up
   int64_t* new_list;
   unsigned long long* new_count;
   int64_t new_capacity;
 };
+
+__device__ __forceinline__ int64_t window_start_n(const Spec& s, int64_t n) {
+  return jadd(s.offset, (int64_t)((uint64_t)n * (uint64_t)(s.assigner == FW_TUMBLING ? s.size : s.slide)));
+}
+
+// a record whose slice belongs to a window in its allowed lateness past its maxTimestamp (EventTimeTrigger
+// .onElement FIRE, EventTimeTrigger.java:38-40; WindowOperator.java:317-325): its slice update joins the
+// commit list (applied in arrival order by k_late_commit); for sliding windows every such window of the
+// record also gets a fire element (tumbling: the slice is the window, the commit list serves as both)
+__device__ void late_append(const Spec& s, const BatchIn& b, int32_t p, int64_t kid, int64_t m, int64_t i) {
+  const unsigned long long pos = atomicAdd(b.late_count, 1ull);
+  const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
+  if ((int64_t)pos < b.late_capacity) b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
+  else set_error(s.err, FW_ERR_CAPACITY);
+  if (s.assigner != FW_SLIDING) return;
+  const int64_t n_hi = floor_div(m, s.R), n_lo = floor_div(m - s.K, s.R) + 1;
+  for (int64_t n = n_lo; n <= n_hi; ++n) {
+    const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+    if (max_ts > b.wm || cleanup_time(max_ts, s.lateness) <= b.wm) continue;   // not fired yet / late (dropped)
+    const unsigned long long wpane = (unsigned long long)floor_mod(n, s.P) * (unsigned long long)s.stride + (unsigned long long)kid;
+    const unsigned long long fpos = atomicAdd(b.fire_count, 1ull);
+    if ((int64_t)fpos < b.fire_capacity) b.fire_key[fpos] = (wpane << b.idx_bits) | (unsigned long long)i;
+    else set_error(s.err, FW_ERR_CAPACITY);
+  }
+}
 
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
@@ -418,18 +447,9 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
       kid = dir_find_or_insert(s, key);
       if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
     }
-    if (b.late_key) {  // kernel argument: uniform
-      const bool want = live && late_fire;
-      unsigned long long pos = wave_append(b.late_count, want);
-      if (want) {
-        if ((int64_t)pos < b.late_capacity) {
-          unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
-          b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
-        } else {
-          set_error(s.err, FW_ERR_CAPACITY);
-        }
-        live = false;
-      }
+    if (b.late_key && live && late_fire) {
+      late_append(s, b, p, kid, w.m, i);
+      live = false;
     }
     bool fresh = false;
     int64_t idx = 0;
@@ -982,13 +1002,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     const int32_t p = slice_slot(s, m);
     const int64_t kid = dir_lookup(s, key);
     if (p < 0 || kid < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
-    const unsigned long long pos = atomicAdd(b.late_count, 1ull);
-    if ((int64_t)pos < b.late_capacity) {
-      const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
-      b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
-    } else {
-      set_error(s.err, FW_ERR_CAPACITY);
-    }
+    late_append(s, b, p, kid, m, i);
   }
   // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same
   // set).  A lane whose slice equals its left neighbour's leaves the insert to it, so a wave of an
@@ -1352,8 +1366,10 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
   if (!tail) return;
   int64_t idx = (int64_t)pane;
   int32_t p = (int32_t)(pane / (unsigned long long)s.stride);
-  if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) {
-    // FIRE_AND_PURGE after the last element: pane cleared (AbstractHeapState.clear)
+  if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) {
+    // FIRE_AND_PURGE after the last element: pane cleared (AbstractHeapState.clear).  (Sliding: the slice
+    // also feeds windows that have not fired; a purged window's later per-element fires emit the record
+    // alone, k_fire_emit)
     if (s.c.sum) s.c.sum[idx] = 0;
     if (s.c.mn) s.c.mn[idx] = INT64_MAX;
     if (s.c.mx) s.c.mx[idx] = INT64_MIN;
@@ -1377,12 +1393,58 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
   (void)p;
 }
 
+// sliding windows: one result per fire element (record, window) in (window, arrival) order — the window's
+// contents when the record was added: its slices' states before this batch's per-element records (+) the
+// prefix of the window's late records up to this one.  PurgingTrigger: the window was purged by its
+// watermark fire and by every per-element fire since (FIRE_AND_PURGE), so the result is the record alone.
+__global__ void k_fire_emit(Spec s, const unsigned long long* sorted_key, int64_t nf, int32_t idx_bits,
+                            const unsigned long long* seg, const LateAcc* acc, const LateAcc* scanned,
+                            const int64_t* f1col, const int64_t* tscol, int64_t wm, const int64_t* headpos) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = j < nf;
+  const unsigned long long pos = wave_append(s.o.count, act);
+  if (!act) return;
+  const unsigned long long wpane = seg[j];
+  const int32_t wp = (int32_t)(wpane / (unsigned long long)s.stride);
+  const int64_t kid = (int64_t)(wpane % (unsigned long long)s.stride);
+  const int64_t i_self = (int64_t)(sorted_key[j] & ((1ull << idx_bits) - 1));
+  // the window: the one of the record's windows with slot wp (its windows span fewer than P numbers)
+  const int64_t m = record_windows(s, tscol[i_self], wm).m;
+  const int64_t n_hi = floor_div(m, s.R), n_lo = floor_div(m - s.K, s.R) + 1;
+  int64_t n = n_lo;
+  for (int64_t x = n_lo; x <= n_hi; ++x) if (floor_mod(x, s.P) == wp) n = x;
+  const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+  LateAcc out;
+  int64_t f1 = f1col[i_self];
+  if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) {
+    out = acc[j];
+  } else {
+    LateCombine op;
+    bool any = false;
+    LateAcc base;
+    int64_t best = INT64_MAX, bf1 = 0;
+    for (int k = 0; k < s.K; ++k) {
+      const int64_t mm = n * s.R + k;
+      const int32_t pp = (int32_t)floor_mod(mm, s.P);
+      if (s.slice_tag[pp] != mm) continue;
+      const int64_t idx = (int64_t)pp * s.stride + kid;
+      if (!pane_present(s, idx)) continue;
+      if (s.first && s.c.first[idx] < best) { best = s.c.first[idx]; bf1 = s.c.f1v[idx]; }
+      const LateAcc bb = pane_load(s, idx);
+      base = any ? op(base, bb) : bb;
+      any = true;
+    }
+    out = any ? op(base, scanned[j]) : scanned[j];
+    // first arrival: the window's earliest slice record, else the head of this window's late records
+    f1 = any ? bf1 : f1col[(int64_t)(sorted_key[headpos[j]] & ((1ull << idx_bits) - 1))];
+  }
+  if (s.by) f1 = out.f1;
+  emit_record(s, pos, kid_key(s, kid), f1, max_ts, out);
+}
+
 // ------------------------------------------------------------------------------------------------
 // watermark: plan fires/purges from the live slices, fire, purge, mark
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t window_start_n(const Spec& s, int64_t n) {
-  return jadd(s.offset, (int64_t)((uint64_t)n * (uint64_t)(s.assigner == FW_TUMBLING ? s.size : s.slide)));
-}
 
 // ------------------------------------------------------------------------------------------------
 // watermark (AbstractStreamOperator.processWatermark :803-808 -> HeapInternalTimerService.advanceWatermark
@@ -1417,7 +1479,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
       const bool fires = max_ts > wm_old && max_ts <= wm_new;
       if (!fires) continue;
-      if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) purge_now = true;   // tumbling only
+      if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) purge_now = true;   // the slice is the window
       bool owner = true;                                                    // first live slice of window n
       for (int64_t mm = n * s.R; mm < m; ++mm) {
         if (s.slice_tag[floor_mod(mm, s.P)] == mm) { owner = false; break; }
@@ -1733,6 +1795,8 @@ struct fw_engine {
   int32_t* stg_hash[2] = {};
   // late path
   unsigned long long *late_key = nullptr, *late_key_sorted = nullptr, *late_count = nullptr, *seg = nullptr;
+  unsigned long long *fire_key = nullptr, *fire_count = nullptr;   // sliding: per-element fire elements
+  int64_t fire_cap = 0;
   unsigned long long *late_idx_in = nullptr, *late_idx_out = nullptr;
   LateAcc *late_acc = nullptr, *late_scan = nullptr;
   int64_t *headpos = nullptr, *headpos_scan = nullptr;
@@ -1929,8 +1993,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (by && c.ingest_mode == 1) return unsupported("maxBy / minBy run on the partitioned ingest form (ingest_mode 0 or 2)");
   if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
   if (c.ingest_mode < 0 || c.ingest_mode > 2) return bad("bad ingest mode");
-  if (c.assigner == FW_SLIDING && (c.allowed_lateness > 0 || c.trigger != FW_TRIGGER_EVENT_TIME))
-    return unsupported("sliding windows with allowed lateness or PurgingTrigger are not implemented on the slice path");
   HIPCHK(e, hipSetDevice(c.device));
   e->dev = c.device;
   HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
@@ -2079,8 +2141,14 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->idx_bits = bits_for((uint64_t)c.max_batch);
     int pane_bits = bits_for((uint64_t)P * (uint64_t)s.stride);
     if (e->idx_bits + pane_bits > 64) { delete e; return FW_ERR_UNSUPPORTED; }
-    size_t nb = (size_t)c.max_batch;
-    e->late_key = e->alloc<unsigned long long>(nb);
+    // sliding: a late record fires once per window of its slice in its lateness period
+    if (c.assigner == FW_SLIDING) e->fire_cap = c.max_batch * (int64_t)((s.K + s.R - 1) / s.R);
+    const size_t nb = (size_t)std::max<int64_t>(c.max_batch, e->fire_cap);
+    if (e->fire_cap) {
+      e->fire_key = e->alloc<unsigned long long>((size_t)e->fire_cap);
+      e->fire_count = e->alloc<unsigned long long>(1);
+    }
+    e->late_key = e->alloc<unsigned long long>((size_t)c.max_batch);
     e->late_key_sorted = e->alloc<unsigned long long>(nb);
     e->late_count = e->alloc<unsigned long long>(1);
     e->seg = e->alloc<unsigned long long>(nb);
@@ -2089,11 +2157,10 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->headpos = e->alloc<int64_t>(nb);
     e->headpos_scan = e->alloc<int64_t>(nb);
     size_t t1 = 0, t2 = 0, t3 = 0;
-    (void)rocprim::radix_sort_keys(nullptr, t1, e->late_key, e->late_key_sorted, (size_t)c.max_batch, 0, 64, e->stream);
-    (void)rocprim::deterministic_inclusive_scan_by_key(nullptr, t2, e->seg, e->late_acc, e->late_scan, (size_t)c.max_batch,
+    (void)rocprim::radix_sort_keys(nullptr, t1, e->late_key, e->late_key_sorted, nb, 0, 64, e->stream);
+    (void)rocprim::deterministic_inclusive_scan_by_key(nullptr, t2, e->seg, e->late_acc, e->late_scan, nb,
                                                  LateCombine(), rocprim::equal_to<unsigned long long>(), e->stream);
-    (void)rocprim::inclusive_scan(nullptr, t3, e->headpos, e->headpos_scan, (size_t)c.max_batch,
-                                  rocprim::maximum<int64_t>(), e->stream);
+    (void)rocprim::inclusive_scan(nullptr, t3, e->headpos, e->headpos_scan, nb, rocprim::maximum<int64_t>(), e->stream);
     e->temp_bytes = std::max(std::max(t1, t2), t3);
     e->temp = e->alloc<char>(e->temp_bytes);
     for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
@@ -2116,6 +2183,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(s.err, 0, 4, e->stream));
   HIPCHK(e, hipMemsetAsync(s.stats, 0, 8 * ST_NSTATS, e->stream));
   HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
+  if (e->fire_count) HIPCHK(e, hipMemsetAsync(e->fire_count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(e->wm_done, 0, 4, e->stream));
   if (e->routed) {
     HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 8 * DC_RING, e->stream));
@@ -2193,6 +2261,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.late_count = e->late_count;
   b.late_capacity = e->late_key ? e->cfg.max_batch : 0;
   b.idx_bits = e->idx_bits;
+  b.fire_key = e->fire_key;
+  b.fire_count = e->fire_count;
+  b.fire_capacity = e->fire_cap;
   b.new_list = e->new_list;
   b.new_count = e->new_counts ? e->new_counts + par : nullptr;
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
@@ -2213,32 +2284,51 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     e->phase_end(n);
   }
   if (e->cfg.allowed_lateness > 0) {
-    // per-element fires: need the count on the host to size the sort
-    unsigned long long nl = 0;
+    // per-element fires: the list lengths on the host size the sorts
+    unsigned long long nl = 0, nf = 0;
     HIPCHK(e, hipMemcpyAsync(&nl, e->late_count, 8, hipMemcpyDeviceToHost, e->stream));
+    if (e->fire_count) HIPCHK(e, hipMemcpyAsync(&nf, e->fire_count, 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (nl > (unsigned long long)e->cfg.max_batch) nl = e->cfg.max_batch;
-    if (nl > 0) {
-      e->phase_begin(FW_PHASE_LATE);
+    if (nf > (unsigned long long)e->fire_cap) nf = e->fire_cap;
+    const bool sliding = e->cfg.assigner == FW_SLIDING;
+    if (nl > 0 || nf > 0) e->phase_begin(FW_PHASE_LATE);
+    // sort by (pane, arrival), per-pane inclusive scan of the records' accumulators in arrival order
+    auto sorted_scan = [&](unsigned long long* keys, unsigned long long n) -> int {
       size_t tb = e->temp_bytes;
-      HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, e->late_key, e->late_key_sorted, (size_t)nl, 0, 64, e->stream));
-      int blocks = (int)((nl + BLOCK - 1) / BLOCK);
-      hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
+      HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, keys, e->late_key_sorted, (size_t)n, 0, 64, e->stream));
+      const int blocks = (int)((n + BLOCK - 1) / BLOCK);
+      hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)n,
                          e->idx_bits, dv, e->seg, e->late_acc, e->headpos, df1, e->ordinal);
       tb = e->temp_bytes;
-      HIPCHK(e, rocprim::inclusive_scan(e->temp, tb, e->headpos, e->headpos_scan, (size_t)nl,
+      HIPCHK(e, rocprim::inclusive_scan(e->temp, tb, e->headpos, e->headpos_scan, (size_t)n,
                                         rocprim::maximum<int64_t>(), e->stream));
       tb = e->temp_bytes;
-      HIPCHK(e, rocprim::deterministic_inclusive_scan_by_key(e->temp, tb, e->seg, e->late_acc, e->late_scan, (size_t)nl,
+      HIPCHK(e, rocprim::deterministic_inclusive_scan_by_key(e->temp, tb, e->seg, e->late_acc, e->late_scan, (size_t)n,
                                                              LateCombine(), rocprim::equal_to<unsigned long long>(), e->stream));
-      hipLaunchKernelGGL(k_late_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
-                         e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, e->ordinal, e->headpos_scan);
+      return FW_OK;
+    };
+    if (nf > 0) {   // sliding: the fires first, against the slices before this batch's late records
+      if (int rc = sorted_scan(e->fire_key, nf)) return rc;
+      hipLaunchKernelGGL(k_fire_emit, dim3((unsigned)((nf + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, e->stream, e->s,
+                         e->late_key_sorted, (int64_t)nf, e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, dts,
+                         e->cur_wm, e->headpos_scan);
+      e->late_fires_host += (int64_t)nf;
+      HIPCHK(e, hipMemsetAsync(e->fire_count, 0, 8, e->stream));
+    }
+    if (nl > 0) {
+      if (int rc = sorted_scan(e->late_key, nl)) return rc;
+      const int blocks = (int)((nl + BLOCK - 1) / BLOCK);
+      if (!sliding) {
+        hipLaunchKernelGGL(k_late_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
+                           e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, e->ordinal, e->headpos_scan);
+        e->late_fires_host += (int64_t)nl;
+      }
       hipLaunchKernelGGL(k_late_commit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
                          e->idx_bits, e->seg, e->late_scan, df1, e->ordinal, e->headpos_scan);
-      e->phase_end((int64_t)nl);
-      e->late_fires_host += (int64_t)nl;
       HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
     }
+    if (nl > 0 || nf > 0) e->phase_end((int64_t)(nl + nf));
   }
   HIPCHK(e, hipGetLastError());
   // every reader of this push's columns (k_route, k_aggregate's direct records, the f1 fix-up, the late

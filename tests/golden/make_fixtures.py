@@ -167,6 +167,39 @@ FIXTURES.append(fixture(
                               out("key2", 1, 2009)]}]))
 
 
+# HAND-DERIVED (no reference test runs sliding windows with allowed lateness > 0): WOT:1104-1161
+# testLateness's input over SlidingEventTimeWindows.of(3 s, 1 s), lateness 500, SumReducer, worked out
+# step by step from WindowOperator.processElement / onEventTime (WindowOperator.java:302-375, isLate
+# :470-472, cleanupTime :511-514), EventTimeTrigger (:37-52) and PurgingTrigger (:47-55):
+#  500   -> windows [0,3000) [-1000,2000) [-2000,1000)
+#  wm 1500  fires [-2000,1000) = 1 @999 (cleanup 1499 passes too)
+#  1300  -> [1000,4000) [0,3000) [-1000,2000), none late, none fires (all maxTs > 1500)
+#  wm 2300  fires [-1000,2000) = 2 @1999
+#  1997  -> same three windows, none late (cleanups 2499/3499/4499 > 2300); [-1000,2000) has maxTs
+#           1999 <= 2300: the element FIRES it -> 3 (accumulating), or 1 (purging: the watermark fire
+#           purged it, so it holds only this element)
+#  wm 6000  cleanup of [-1000,2000) (no output), fires [0,3000) = 3 @2999, [1000,4000) = 2 @3999
+#  1998  -> all three windows late (cleanup <= 6000): dropped;  wm 7000 nothing
+_SL_EVENTS = [rec("key2", 1, 500), wm(1500), rec("key2", 1, 1300), wm(2300), rec("key2", 1, 1997), wm(6000),
+              rec("key2", 1, 1998), wm(7000)]
+FIXTURES.append(fixture(
+    "sliding_lateness", "hand-derived: WindowOperatorTest.java:1104-1161 inputs, sliding 3s/1s, lateness 500, EventTimeTrigger",
+    cfg("sliding", 3000, 1000, lateness=500),
+    _SL_EVENTS,
+    [{"wm": 1500, "records": [out("key2", 1, 999)]},
+     {"wm": 2300, "records": [out("key2", 2, 1999)]},
+     {"wm": 6000, "records": [out("key2", 3, 1999), out("key2", 3, 2999), out("key2", 2, 3999)]},
+     {"wm": 7000, "records": []}]))
+FIXTURES.append(fixture(
+    "sliding_lateness_purging", "hand-derived: WindowOperatorTest.java:1104-1161 inputs, sliding 3s/1s, lateness 500, PurgingTrigger",
+    cfg("sliding", 3000, 1000, lateness=500, trigger="purging_event_time"),
+    _SL_EVENTS,
+    [{"wm": 1500, "records": [out("key2", 1, 999)]},
+     {"wm": 2300, "records": [out("key2", 2, 1999)]},
+     {"wm": 6000, "records": [out("key2", 1, 1999), out("key2", 3, 2999), out("key2", 2, 3999)]},
+     {"wm": 7000, "records": []}]))
+
+
 def closed_form(name, source, size, slide):
     """EventTimeWindowCheckpointingITCase (flink-tests/.../test/checkpointing/...): FailingSource
     :495-579 emits, for next = 0..2999, (key i, next) @ ts=next for keys 0..99, then Watermark(next);

@@ -23,7 +23,8 @@ def load_golden(name):
 
 WINDOW_FIXTURES = ["sliding_reduce", "tumbling_reduce", "lateness_purging", "cleanup_time_overflow",
                    "drop_late_tumbling", "drop_late_sliding", "cleanup_timer_empty_state", "tumbling_offset",
-                   "sliding_offset", "itcase_tumbling_closed_form", "itcase_sliding_closed_form"]
+                   "sliding_offset", "itcase_tumbling_closed_form", "itcase_sliding_closed_form",
+                   "sliding_lateness", "sliding_lateness_purging"]
 
 
 def fixture_config(c, **kw):

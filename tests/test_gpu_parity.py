@@ -115,6 +115,34 @@ def test_sliding_uneven_slide(hip, oracle_engine, mode):
     _run_both(hip, oracle_engine, cfg, keys, ts, vals, 3000, 500, ["sum_i64", "count"])
 
 
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("purging", [False, True], ids=["event_time", "purging"])
+def test_sliding_allowed_lateness(hip, oracle_engine, mode, purging):
+    """Sliding 3 s / 1 s, allowed lateness 500, out-of-order input behind the watermark: per-element fires
+    of every window of a late record's slice in its lateness period (WindowOperator.java:302-333,
+    EventTimeTrigger.java:38-40); PurgingTrigger purges each window at every fire (PurgingTrigger.java:47-55)."""
+    from flink_amd.windowing import EventTimeTrigger, PurgingTrigger, SlidingEventTimeWindows
+    keys, ts, vals = gen_stream(120_000, 800, rate=1 << 14, ooo=900)
+    trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else None
+    cfg = _cfgm(mode, SlidingEventTimeWindows.of(3000, 1000), ("sum", "max", "count"), first=True, lateness=500,
+                trigger=trig)
+    sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 3000, 300, ["sum_i64", "max_i64", "count"], first=True)
+    assert so["late_fires"] > 0 and sg["late_fires"] == so["late_fires"]
+    assert sg["records_late"] == so["records_late"] and so["records_late"] > 0
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_sliding_lateness_double_uneven(hip, oracle_engine, mode):
+    """size not a multiple of slide (slices of gcd), doubles, lateness longer than a slide."""
+    from flink_amd.windowing import SlidingEventTimeWindows
+    keys, ts, vals = gen_stream(80_000, 300, rate=1 << 13, ooo=1500, value_type="f64", t0=1_700_000_000_123)
+    cfg = _cfgm(mode, SlidingEventTimeWindows.of(2500, 1000, 300), ("sum", "min", "max", "count"), "f64", True,
+                lateness=1200)
+    sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 4000, 400, ["sum_f64", "min_f64", "max_f64", "count"],
+                       first=True, rel=1e-9)
+    assert so["late_fires"] > 0 and sg["late_fires"] == so["late_fires"]
+
+
 def test_sliding_negative_timestamp_quirk_is_rejected(hip):
     """Java's % on a negative (ts - offset + slide) makes SlidingEventTimeWindows assign a window that
     does not contain ts (TimeWindow.java:239-241); the slice path reports it instead of diverging."""
