@@ -148,6 +148,43 @@ class Aggregations:
         return ReduceFunction(("maxBy",), value_type, first=first)
 
 
+# ------------------------------------------------------------------ windows / window functions
+class TimeWindow:
+    """[start, end); maxTimestamp() = end - 1 (SJ/api/windowing/windows/TimeWindow.java:41-62)."""
+    __slots__ = ("start", "end")
+
+    def __init__(self, start, end):
+        self.start, self.end = start, end
+
+    def getStart(self):
+        return self.start
+
+    def getEnd(self):
+        return self.end
+
+    def maxTimestamp(self):
+        return self.end - 1
+
+    def __eq__(self, o):
+        return isinstance(o, TimeWindow) and (self.start, self.end) == (o.start, o.end)
+
+    def __hash__(self):
+        return hash((self.start, self.end))
+
+    def __repr__(self):
+        return f"TimeWindow{{start={self.start}, end={self.end}}}"
+
+
+class Collector:
+    """org.apache.flink.util.Collector: what a WindowFunction emits."""
+
+    def __init__(self):
+        self.items = []
+
+    def collect(self, record):
+        self.items.append(record)
+
+
 # ------------------------------------------------------------------ stream elements
 class StreamRecord:
     __slots__ = ("value", "timestamp")
@@ -342,11 +379,19 @@ class WindowOperator:
     processWatermark(Watermark) hands the buffered epoch to the engine, advances the watermark and
     appends the fired results followed by the watermark to the output (AbstractStreamOperator
     .processWatermark :803-808: timers fire, then the watermark is forwarded).
+    `window_function`: WindowedStream.reduce(reduceFunction, windowFunction) / apply(reduce, function)
+    (WindowedStream.java:347-425): the reduce runs on the GPU, the window function on the host for every
+    fired pane, as InternalSingleValueWindowFunction does (InternalSingleValueWindowFunction.java:51-53):
+    apply(key, TimeWindow, [reduced value], Collector), each collected element timestamped with
+    window.maxTimestamp() (TimestampedCollector, WindowOperator.java:435-438).  A plain callable with the
+    same arguments works too.
     `engine_factory(config)` lets the tests run the oracle behind the same surface.
     """
 
-    def __init__(self, assigner, reduce_function, trigger=None, allowed_lateness=0, engine_factory=None, **kw):
+    def __init__(self, assigner, reduce_function, trigger=None, allowed_lateness=0, engine_factory=None,
+                 window_function=None, **kw):
         self.assigner = assigner
+        self.window_function = window_function
         self.reduce = reduce_function
         self.config = make_config(assigner, reduce_function, trigger, allowed_lateness, **kw)
         self.engine = (engine_factory or WindowEngine)(self.config)
@@ -418,18 +463,26 @@ class WindowOperator:
             c = ReduceFunction.COLUMN[f]
             col = res[c + ("" if c == "count" else ("_i64" if self.reduce.value_type == "i64" else "_f64"))]
             vals.append(col[i].item())
-        return StreamRecord(tuple([key] + vals), int(res["ts"][i]))
+        ts = int(res["ts"][i])
+        value = tuple([key] + vals)
+        if self.window_function is None:
+            return [StreamRecord(value, ts)]
+        out = Collector()
+        window = TimeWindow(ts + 1 - self.assigner.size, ts + 1)
+        apply = getattr(self.window_function, "apply", self.window_function)
+        apply(key, window, [value], out)
+        return [StreamRecord(x, ts) for x in out.items]
 
     def _drain(self):
         res = self.engine.collect()
         pos = 0
         for wm, mp in zip(res["mark_wm"], res["mark_pos"]):
             while pos < mp:
-                self.output.append(self._record(res, pos))
+                self.output.extend(self._record(res, pos))
                 pos += 1
             self.output.append(Watermark(int(wm)))
         while pos < res["n"]:
-            self.output.append(self._record(res, pos))
+            self.output.extend(self._record(res, pos))
             pos += 1
 
     def snapshotState(self):
