@@ -103,6 +103,9 @@ struct Spec {  // window specification + reduce + subtask, passed by value
 };
 
 __device__ __forceinline__ void set_error(int32_t* err, int32_t code) { atomicCAS(err, 0, code); }
+// a capacity error, with the id of the site that raised it first (fw_debug_counters word 7: diagnostics)
+#define cap_error(s, site) do { set_error((s).err, FW_ERR_CAPACITY); \
+    atomicCAS(&(s).stats[7], 0ull, (unsigned long long)(site)); } while (0)
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {  // MurmurHash3 finaliser: directory hash
   k ^= k >> 33;
@@ -373,7 +376,7 @@ __device__ void late_append(const Spec& s, const BatchIn& b, int32_t p, int64_t 
   const unsigned long long pos = atomicAdd(b.late_count, 1ull);
   const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
   if ((int64_t)pos < b.late_capacity) b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
-  else set_error(s.err, FW_ERR_CAPACITY);
+  else cap_error(s, 1);
   if (s.assigner != FW_SLIDING) return;
   const int64_t n_hi = floor_div(m, s.R), n_lo = floor_div(m - s.K, s.R) + 1;
   for (int64_t n = n_lo; n <= n_hi; ++n) {
@@ -382,7 +385,7 @@ __device__ void late_append(const Spec& s, const BatchIn& b, int32_t p, int64_t 
     const unsigned long long wpane = (unsigned long long)floor_mod(n, s.P) * (unsigned long long)s.stride + (unsigned long long)kid;
     const unsigned long long fpos = atomicAdd(b.fire_count, 1ull);
     if ((int64_t)fpos < b.fire_capacity) b.fire_key[fpos] = (wpane << b.idx_bits) | (unsigned long long)i;
-    else set_error(s.err, FW_ERR_CAPACITY);
+    else cap_error(s, 2);
   }
 }
 
@@ -441,11 +444,11 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
     } else if (live) {
       p = slice_slot(s, w.m);
     }
-    if (live && p < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
+    if (live && p < 0) { cap_error(s, 3); live = false; }
     int64_t kid = -1;
     if (live) {
       kid = dir_find_or_insert(s, key);
-      if (kid < 0) { set_error(s.err, FW_ERR_CAPACITY); live = false; }
+      if (kid < 0) { cap_error(s, 4); live = false; }
     }
     if (b.late_key && live && late_fire) {
       late_append(s, b, p, kid, w.m, i);
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
       const unsigned long long pos = wave_append(b.new_count, fresh);
       if (fresh) {
         if ((int64_t)pos < b.new_capacity) b.new_list[pos] = idx;
-        else set_error(s.err, FW_ERR_CAPACITY);
+        else cap_error(s, 5);
       }
     }
   }
@@ -495,8 +498,8 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 //               counting-sorts the routable records through LDS by bin = (tile slice q, directory
 //               bucket) and writes the tile back bin-sorted as (fmix64(key), value) + the 2-B index of
 //               the record in its tile, with a per-tile table of segment starts.  Records that cannot be
-//               routed (per-element fires, slices beyond the tile's RT_Q, the Long.MIN_VALUE key) join
-//               the direct list.
+//               routed by slice (slices beyond the tile's RT_Q, the Long.MIN_VALUE key) and per-element
+//               fires go to two more bin groups per bucket, so each bucket's workgroup finds its own.
 //  k_aggregate  one workgroup per directory bucket: owns every pane of that bucket for this batch,
 //               gathers the bucket's segment from every tile (the segments concatenated, one record
 //               per lane), resolves keys in an LDS copy of the bucket's directory slice, reduces with
@@ -514,7 +517,8 @@ constexpr int RT_THREADS = RT_TILE / 8;      // eight records per thread
 constexpr int RT_Q = 2;                 // slices per tile routed through LDS (more go to the direct list)
 constexpr int RT_GS = 64;               // distinct slices per batch (k_aggregate rounds)
 constexpr int RT_MAXNB = 256;           // directory buckets the route table holds
-constexpr int DC_RING = 16;             // direct-list counters, one per batch in flight
+constexpr int RT_GROUPS = RT_Q + 2;     // bin groups per bucket: RT_Q routed slices, then the direct records
+                                        // (any other slice, the Long.MIN_VALUE key) and the per-element fires
 constexpr int AG_THREADS = 1024;
 constexpr int AG_WIN = 8;               // k_aggregate: directory slots probed without a branch
 constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
@@ -526,12 +530,8 @@ constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 struct RouteBuf {
   longlong2* kv;         // [ntiles][RT_TILE] routed records (fmix64(key), value), each tile sorted by bin
   uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
-  uint16_t* seg;         // [ntiles][nbq + 1] start of each bin's segment in the tile; [nbq] = routed count
+  uint16_t* seg;         // [ntiles][RT_GROUPS * nb + 1] start of each bin's segment in the tile; [last] = count
   int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
-  unsigned long long* dlist;    // direct-list records: (batch index << 1) | per-element fire
-  unsigned long long* dcount;   // this batch's direct-list length (a ring of DC_RING counters, one per batch)
-  unsigned long long* dcount_reset;   // the counter of batch j + DC_RING/2: zeroed by k_aggregate of batch j
-  int64_t dcap;
   long long* stamps;     // diagnostics (FW_DEBUG_AGG & 16): per-workgroup phase timestamps, 8 per workgroup
   int32_t ntiles;
   int32_t dbg;
@@ -594,7 +594,7 @@ __device__ __forceinline__ void block_scan_excl(int32_t* a, int n, int32_t* wtot
 // slice their slice numbers int64[RT_TILE] at 4 RT_TILE and flags int32[RT_TILE] at 12 RT_TILE.  Then the
 // sorted records' index in the tile (uint16[RT_TILE]), the bin counters, the scan scratch and the tile's
 // slice set.
-constexpr size_t RT_LDS = (size_t)RT_TILE * (16 + 2) + 4 * (size_t)(RT_Q * RT_MAXNB + 8) + 4 * 16 + 8 * RT_Q;
+constexpr size_t RT_LDS = (size_t)RT_TILE * (16 + 2) + 4 * (size_t)(RT_GROUPS * RT_MAXNB + 8) + 4 * 16 + 8 * RT_Q + 8;
 
 template <int VT, int AGG, bool FIRST>
 __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, const RouteBuf& r, unsigned char* smem,
@@ -602,17 +602,19 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   constexpr int NT = RT_THREADS;
   constexpr int PER = RT_TILE / NT;     // records per thread
   constexpr int V = PER / 2;            // 16-B vectors per column per thread
-  const int nbq = RT_Q * s.nb;
+  const int nbq = RT_GROUPS * s.nb;
   longlong2* st_kv = (longlong2*)smem;
   uint16_t* st_idx = (uint16_t*)(st_kv + RT_TILE);
   int32_t* cnt = (int32_t*)(st_idx + RT_TILE);     // [nbq + 1]
-  int32_t* wtot = cnt + (RT_Q * RT_MAXNB + 8);     // [NT / 64]
+  int32_t* wtot = cnt + (RT_GROUPS * RT_MAXNB + 8); // [NT / 64]
   int64_t* lset = (int64_t*)(wtot + 16);           // [RT_Q] the tile's routed slices
+  int32_t* any_direct = (int32_t*)(lset + RT_Q);   // the tile has direct-group records
   int32_t* lhash = (int32_t*)smem;                 // Java key hashes (optional column)
   const int64_t base = (int64_t)blockIdx.x * RT_TILE;
   FW_STAMP(r, 0, 0);
   for (int x = threadIdx.x; x <= nbq; x += NT) cnt[x] = 0;
   if (threadIdx.x < RT_Q) lset[threadIdx.x] = FREE_TAG;
+  if (threadIdx.x == 0) *any_direct = 0;
   // phase A: every load of the tile in flight before any dependent work; record (j, e) of this thread
   // is tile index 2 * (j * NT + tid) + e
   int64_t kk[PER], tt[PER], vv[PER];
@@ -735,8 +737,9 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   }
   // phase B2: the routed records' index in the tile's slice set — resolved once per wave when all its
   // routed records share one slice (an in-order stream), per record otherwise — then their bin and
-  // counting-sort rank.  The rest join the direct list (rare: per-element fires, slices beyond the
-  // tile's RT_Q, the Long.MIN_VALUE key), applied by the k_aggregate workgroup owning the key's bucket.
+  // counting-sort rank.  The rest (rare: per-element fires, slices beyond the tile's RT_Q, the
+  // Long.MIN_VALUE key, bucket 0) take the bucket's direct or fire bin group, which the k_aggregate
+  // workgroup owning the bucket applies.
   int64_t m_ref = INT64_MIN;
   {
     const uint64_t lm = __ballot(route_mask != 0);
@@ -768,31 +771,25 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     int32_t q = -1;
     if (wave_uniform) q = routable ? q_ref : -1;
     else if (routable) q = tile_slice(lset, tt[k]);
-    if (q >= 0) {
+    if (routable && q < 0) direct_mask |= 1u << k;   // the tile's slice set is full
+    const bool direct = (direct_mask >> k) & 1u;
+    if (q >= 0 || direct) {
+      // routed and direct records carry the directory hash (a bijection of the key; EMPTY_H is the
+      // Long.MIN_VALUE key's, which lives in bucket 0)
+      const bool kmin = kk[k] == EMPTY_KEY;
       const uint64_t hk = fmix64((uint64_t)kk[k]);
-      bin[k] = q * s.nb + (int32_t)((hk & s.dir_mask) >> s.kb_bits);
+      const int32_t bkt = kmin ? 0 : (int32_t)((hk & s.dir_mask) >> s.kb_bits);
+      const int32_t g = q >= 0 ? q : RT_Q + (int32_t)((fire_mask >> k) & 1u);
+      bin[k] = g * s.nb + bkt;
       rank[k] = atomicAdd(&cnt[bin[k]], 1);
-      kk[k] = (int64_t)hk;   // routed records carry the directory hash (a bijection of the key)
-    } else if (routable) {
-      direct_mask |= 1u << k;   // the tile's slice set is full
+      kk[k] = (int64_t)hk;
     }
   }
   if (__any(late_pairs != 0)) {
     for (int off = 32; off > 0; off >>= 1) late_pairs += __shfl_xor(late_pairs, off);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late_pairs);
   }
-  if (__any(direct_mask != 0)) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int64_t i = base + 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
-      const bool direct = (direct_mask >> k) & 1u;
-      const unsigned long long dpos = wave_append(r.dcount, direct);
-      if (direct) {
-        if ((int64_t)dpos < r.dcap) r.dlist[dpos] = ((unsigned long long)i << 1) | ((fire_mask >> k) & 1u);
-        else set_error(s.err, FW_ERR_CAPACITY);
-      }
-    }
-  }
+  if (direct_mask != 0) *any_direct = 1;
   __syncthreads();   // every wave's slice claims are in lset, every staging read is done
   if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
   FW_STAMP(r, 0, 2);
@@ -815,7 +812,8 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     const int32_t pos = k * NT + (int)threadIdx.x;
     if (pos < total) r.kv[base + pos] = st_kv[pos];
   }
-  if (FIRST) {
+  // the record indices: first arrival (FIRST), and the batch index of every direct record
+  if (FIRST || *any_direct) {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const int32_t pos = 2 * (j * NT + (int)threadIdx.x);
@@ -894,7 +892,8 @@ __device__ __forceinline__ void acc_add(const AggLds& L, bool cmpto, bool by_las
 // LDS bytes k_aggregate needs for buckets of 2^kb_bits slots and ntiles tiles
 __host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_t ntiles, bool by) {
   return (size_t)8 * ((size_t)1 << kb_bits) + ((size_t)(1 << kb_bits) + 65) * (8 * nacc + (by ? 4 : 0)) +
-         ((((size_t)(1 << kb_bits) + 65) + 3) & ~(size_t)3) * 4 + (size_t)12 * RT_Q * ntiles + 8 * (size_t)ntiles + 4 +
+         ((((size_t)(1 << kb_bits) + 65) + 3) & ~(size_t)3) * 4 + (size_t)(8 * RT_Q + 4 * RT_GROUPS) * ntiles +
+         8 * (size_t)ntiles + 4 +
          4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8;
 }
 
@@ -907,7 +906,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   // 128-B lines at their boundaries; with both readers on one XCD the second read hits that XCD's L2
   const int bkt = (s.nb % 8 == 0 && !(r.dbg & 32)) ? (int)(blockIdx.x % 8) * (s.nb / 8) + (int)(blockIdx.x / 8)
                                                     : (int)blockIdx.x;
-  const int nbq = RT_Q * s.nb;
+  const int nbq = RT_GROUPS * s.nb;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
   const int KA = KB + 65;                               // accumulators: KB slots, one dummy per lane, the MIN key
@@ -922,8 +921,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   uint32_t* lfirst = (uint32_t*)(lcnt + ((AGG & FW_AGG_COUNT) ? KA : 0));  // [KA] earliest record (batch index)
   uint32_t* lord = lfirst + ((KA + 3) & ~3);            // [KA] maxBy/minBy: the extremal record (batch index)
   int64_t* lhdr = (int64_t*)(lord + (BY ? ((KA + 3) & ~3) : 0)); // [ntiles][RT_Q] the tiles' routed slices
-  uint32_t* lseg = (uint32_t*)(lhdr + (int64_t)r.ntiles * RT_Q);   // [ntiles][RT_Q] this bucket's segment start | end << 16
-  int32_t* sst = (int32_t*)(lseg + (int64_t)r.ntiles * RT_Q);     // [ntiles] segment start within the tile
+  uint32_t* lseg = (uint32_t*)(lhdr + (int64_t)r.ntiles * RT_Q);   // [ntiles][RT_GROUPS] this bucket's segment start | end << 16
+  int32_t* sst = (int32_t*)(lseg + (int64_t)r.ntiles * RT_GROUPS); // [ntiles] segment start within the tile
   int32_t* off = sst + r.ntiles;                        // [ntiles + 1] segment lengths, then their exclusive prefix
   int32_t* step_tile = off + r.ntiles + 1;              // [AG_CHS] tile holding the first record of each step
   int32_t* awtot = step_tile + AG_CHS;                  // [16] scan scratch
@@ -937,17 +936,18 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   for (int t = threadIdx.x; t < r.ntiles; t += NT) {
     const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
     int64_t h[RT_Q];
-    uint32_t sg[RT_Q];
+    uint32_t sg[RT_GROUPS];
 #pragma unroll
-    for (int q = 0; q < RT_Q; ++q) {
-      h[q] = r.hdr[(int64_t)t * RT_Q + q];
+    for (int q = 0; q < RT_Q; ++q) h[q] = r.hdr[(int64_t)t * RT_Q + q];
+#pragma unroll
+    for (int q = 0; q < RT_GROUPS; ++q)
       sg[q] = (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16);
-    }
 #pragma unroll
-    for (int q = 0; q < RT_Q; ++q) { lhdr[t * RT_Q + q] = h[q]; lseg[t * RT_Q + q] = sg[q]; }
+    for (int q = 0; q < RT_Q; ++q) lhdr[t * RT_Q + q] = h[q];
+#pragma unroll
+    for (int q = 0; q < RT_GROUPS; ++q) lseg[t * RT_GROUPS + q] = sg[q];
   }
   for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
-  const int64_t nd = min((int64_t)*r.dcount, r.dcap);
   // claimed early (slice_slot is idempotent): the slot of tile 0's first routed slice, nearly always the
   // batch's only one
   int64_t m_pre = FREE_TAG;
@@ -967,9 +967,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   const AggLds L{lsum, lmin, lmax, lcnt, lfirst, lord};
   const bool cmpto = s.cmpto != 0, by_last = s.by_last != 0;
   if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
-  // no memset between batches: batch j's counter was zeroed by k_aggregate of batch j - DC_RING/2, whose
-  // counter is no longer read and whose successor k_route starts only after this kernel (event order)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *r.dcount_reset = 0;
   __syncthreads();
   FW_STAMP(r, SB, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -984,25 +981,34 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) break;
       }
     }
-    if (g == RT_GS) set_error(s.err, FW_ERR_CAPACITY);   // more distinct slices in one batch than RT_GS
+    if (g == RT_GS) cap_error(s, 6);   // more distinct slices in one batch than RT_GS
   };
-  // direct-list records of this bucket: per-element fires join the late list (k_late_* apply them after
-  // this kernel, in arrival order); the others are added in the round of their slice below
-  auto direct_mine = [&](int64_t key) {
-    return key == EMPTY_KEY ? bkt == 0 : (int)((fmix64((uint64_t)key) & s.dir_mask) >> s.kb_bits) == bkt;
-  };
-  for (int64_t x = threadIdx.x; x < nd; x += NT) {
-    const unsigned long long ent = r.dlist[x];
-    const int64_t i = (int64_t)(ent >> 1);
-    const int64_t key = b.key[i];
-    if (!direct_mine(key)) continue;
-    const int64_t m = record_windows(s, b.ts[i], b.wm).m;
-    if (!(ent & 1ull)) { gsl_insert(m); continue; }
+  // this bucket's direct-group records (one tile per thread): per-element fires join the late list
+  // (k_late_* apply them after this kernel, in arrival order); the others are added in the round of
+  // their slice below.  A direct record carries its directory hash (EMPTY_H: the Long.MIN_VALUE key) and
+  // its index in the tile, i.e. its batch index
+  for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+    const uint32_t sd = lseg[t * RT_GROUPS + RT_Q], sf = lseg[t * RT_GROUPS + RT_Q + 1];
+    for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) {
+      const int64_t i = (int64_t)t * RT_TILE + r.idx[(int64_t)t * RT_TILE + x];
+      gsl_insert(record_windows(s, b.ts[i], b.wm).m);
+    }
     if (b.late_key == nullptr) continue;
-    const int32_t p = slice_slot(s, m);
-    const int64_t kid = dir_lookup(s, key);
-    if (p < 0 || kid < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
-    late_append(s, b, p, kid, m, i);
+    for (uint32_t x = sf & 0xFFFFu; x < (sf >> 16); ++x) {
+      const int64_t pos = (int64_t)t * RT_TILE + x;
+      const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
+      const uint64_t h = (uint64_t)r.kv[pos].x;
+      const int64_t m = record_windows(s, b.ts[i], b.wm).m;
+      const int32_t p = slice_slot(s, m);
+      int64_t kid = s.D;
+      if (h == EMPTY_H) (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
+      else {
+        const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h);
+        kid = x2 < 0 ? -1 : dbase + x2;
+      }
+      if (p < 0 || kid < 0) { cap_error(s, 7); continue; }
+      late_append(s, b, p, kid, m, i);
+    }
   }
   // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same
   // set).  A lane whose slice equals its left neighbour's leaves the insert to it, so a wave of an
@@ -1047,7 +1053,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       const bool miss2 = miss && !found2;
       if (__any(miss2) && miss2) {
         const int32_t x = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h);
-        if (x < 0) { set_error(s.err, FW_ERR_CAPACITY); act = false; }
+        if (x < 0) { cap_error(s, 8); act = false; }
         else kl = (uint32_t)x;
       }
     }
@@ -1063,13 +1069,13 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     if (threadIdx.x == 0) lclaim = (pre_p >= 0 && m == m_pre) ? pre_p : slice_slot(s, m);
     __syncthreads();
     const int32_t p = lclaim;
-    if (p < 0) { if (threadIdx.x == 0) set_error(s.err, FW_ERR_CAPACITY); continue; }   // slice pool exhausted
+    if (p < 0) { if (threadIdx.x == 0) cap_error(s, 9); continue; }   // slice pool exhausted
     for (int t = threadIdx.x; t < r.ntiles; t += NT) {
       int32_t a0 = 0, a1 = 0;
 #pragma unroll
       for (int q = 0; q < RT_Q; ++q) {
         if (lhdr[t * RT_Q + q] == m) {
-          const uint32_t sg = lseg[t * RT_Q + q];
+          const uint32_t sg = lseg[t * RT_GROUPS + q];
           a0 = (int32_t)(sg & 0xFFFFu);
           a1 = (int32_t)(sg >> 16);
         }
@@ -1145,23 +1151,24 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       }
       __syncthreads();   // the next chunk rewrites step_tile
     }
-    // this bucket's direct records of slice m (rare): the same accumulators, ordered by batch index
-    if (nd > 0) {
-      for (int64_t x = threadIdx.x; x < nd; x += NT) {
-        const unsigned long long ent = r.dlist[x];
-        if (ent & 1ull) continue;
-        const int64_t i = (int64_t)(ent >> 1);
-        const int64_t key = b.key[i];
-        if (!direct_mine(key) || record_windows(s, b.ts[i], b.wm).m != m) continue;
+    // this bucket's direct records of slice m (rare; one tile per thread): the same accumulators, their
+    // batch index as the arrival order
+    for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+      const uint32_t sd = lseg[t * RT_GROUPS + RT_Q];
+      for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) {
+        const int64_t pos = (int64_t)t * RT_TILE + x;
+        const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
+        if (record_windows(s, b.ts[i], b.wm).m != m) continue;
+        const longlong2 rec = r.kv[pos];
         uint32_t kl = KMIN;
-        if (key != EMPTY_KEY) {
-          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, fmix64((uint64_t)key));
-          if (x2 < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
-          kl = (uint32_t)x2;
+        if ((uint64_t)rec.x == EMPTY_H) {
+          (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
         } else {
-          (void)dir_lookup(s, key);   // marks the Long.MIN_VALUE key's column in use
+          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, (uint64_t)rec.x);
+          if (x2 < 0) { cap_error(s, 10); continue; }
+          kl = (uint32_t)x2;
         }
-        acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, b.val[i], (uint32_t)i);
+        acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, rec.y, (uint32_t)i);
       }
     }
     __syncthreads();
@@ -1300,7 +1307,7 @@ __device__ __forceinline__ LateAcc pane_load(const Spec& s, int64_t idx) {
 
 __device__ __forceinline__ void emit_record(const Spec& s, unsigned long long pos, int64_t key, int64_t f1, int64_t ts,
                                             const LateAcc& a) {
-  if ((int64_t)pos >= s.o.capacity) { set_error(s.err, FW_ERR_CAPACITY); return; }
+  if ((int64_t)pos >= s.o.capacity) { cap_error(s, 11); return; }
   s.o.key[pos] = key;
   if (s.o.f1) s.o.f1[pos] = f1;
   s.o.ts[pos] = ts;
@@ -1487,7 +1494,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       if (!owner) continue;
       const int32_t t = atomicAdd(&n_tasks, 1);
       if (t < WM_MAXT) task_n[t] = n;
-      else set_error(s.err, FW_ERR_CAPACITY);
+      else cap_error(s, 12);
     }
     const int64_t ct = cleanup_time(jsub(jadd(window_start_n(s, n_hi), s.size), 1), s.lateness);
     if (ct <= wm_new) purge_now = true;
@@ -1578,7 +1585,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       s.o.mark_pos[mc] = (int64_t)(cnt < (unsigned long long)s.o.capacity ? cnt : (unsigned long long)s.o.capacity);
       *s.o.mark_count = mc + 1;
     } else {
-      set_error(s.err, FW_ERR_CAPACITY);
+      cap_error(s, 13);
     }
   }
 }
@@ -1591,7 +1598,7 @@ __global__ void k_mark_only(Spec s, int64_t wm) {
     s.o.mark_pos[mc] = (int64_t)(cnt < (unsigned long long)s.o.capacity ? cnt : (unsigned long long)s.o.capacity);
     *s.o.mark_count = mc + 1;
   } else {
-    set_error(s.err, FW_ERR_CAPACITY);
+    cap_error(s, 14);
   }
 }
 
@@ -1610,7 +1617,7 @@ __global__ void k_restore(Spec s, const int64_t* ent, int64_t n) {
     const int64_t* x = ent + j * FW_SNAP_ENTRY_WORDS;
     const int64_t kid = dir_lookup(s, x[1]);
     const int32_t p = slice_slot(s, x[0]);
-    if (kid < 0 || p < 0) { set_error(s.err, FW_ERR_CAPACITY); continue; }
+    if (kid < 0 || p < 0) { cap_error(s, 15); continue; }
     const int64_t idx = (int64_t)p * s.stride + kid;
     if (s.c.sum) s.c.sum[idx] = x[2];
     if (s.c.mn) s.c.mn[idx] = x[3];
@@ -1836,9 +1843,8 @@ struct fw_engine {
   unsigned int* wm_done = nullptr;   // k_watermark's workgroup completion counter
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
-  RouteBuf rb{};                            // fields shared by both parities (dbg, stamps, dcap)
+  RouteBuf rb{};                            // fields shared by both parities (dbg, stamps)
   RouteBuf rbs[2] = {};                     // routed-batch buffers, one set per batch parity
-  unsigned long long* dcounts = nullptr;    // direct-list lengths, one per parity
   int64_t batches = 0;
   int32_t max_tiles = 0;
   size_t route_lds = 0, agg_lds = 0;
@@ -1905,8 +1911,6 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   }
   RouteBuf r = e->rbs[par];
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
-  r.dcount = e->dcounts + (e->batches % DC_RING);
-  r.dcount_reset = e->dcounts + ((e->batches + DC_RING / 2) % DC_RING);
   // at least 81 KiB of LDS: one k_aggregate workgroup per CU (the dispatcher would otherwise pair two
   // of the nb = CU-count workgroups on one CU and leave another idle)
   const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, (size_t)e->agg_min_lds);
@@ -2111,16 +2115,13 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
       e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
-      e->rb.dcap = c.max_batch;
-      e->dcounts = e->alloc<unsigned long long>(DC_RING);
       for (int q = 0; q < 2; ++q) {
         RouteBuf& r = e->rbs[q];
         r = e->rb;
         r.kv = e->alloc<longlong2>(cap);
         r.idx = e->alloc<uint16_t>(cap);
-        r.seg = e->alloc<uint16_t>((size_t)(RT_Q * s.nb + 1) * max_tiles);
+        r.seg = e->alloc<uint16_t>((size_t)(RT_GROUPS * s.nb + 1) * max_tiles);
         r.hdr = e->alloc<int64_t>((size_t)max_tiles * RT_Q);
-        r.dlist = e->alloc<unsigned long long>((size_t)c.max_batch);
       }
       e->route_lds = RT_LDS;
       const char* ml = getenv("FW_AGG_MIN_LDS_KB");
@@ -2185,9 +2186,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
   if (e->fire_count) HIPCHK(e, hipMemsetAsync(e->fire_count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(e->wm_done, 0, 4, e->stream));
-  if (e->routed) {
-    HIPCHK(e, hipMemsetAsync(e->dcounts, 0, 8 * DC_RING, e->stream));
-  }
   if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
