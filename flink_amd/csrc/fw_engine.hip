@@ -26,6 +26,9 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <array>
+#include <map>
+#include <set>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -34,6 +37,7 @@
 
 #include "../../include/flink_window.h"
 #include "java_semantics.h"
+#include "flink_kg_format.h"
 
 namespace fw {
 
@@ -208,6 +212,10 @@ __device__ __noinline__ int32_t slice_slot_at(int64_t* slice_tag, int32_t P, int
   return -1;
 }
 __device__ __forceinline__ int32_t slice_slot(const Spec& s, int64_t m) { return slice_slot_at(s.slice_tag, s.P, m); }
+
+// the identity of the sum: 0, or -0.0 for doubles (x + -0.0 == x for every x, -0.0 included; +0.0 would
+// turn a pane whose only values are -0.0 into +0.0, where the reference keeps its first value as is)
+__host__ __device__ __forceinline__ int64_t sum_identity(int32_t vt) { return vt == FW_VALUE_F64 ? INT64_MIN : 0; }
 
 // orderable codes of a value for the min / max columns: int64 values as they are; doubles in Math.min /
 // Math.max order, or Double.compareTo order for ComparableAggregator (.min/.max with FW_AGGF_COMPARABLE,
@@ -517,6 +525,7 @@ constexpr int RT_THREADS = RT_TILE / 8;      // eight records per thread
 constexpr int RT_Q = 2;                 // slices per tile routed through LDS (more go to the direct list)
 constexpr int RT_GS = 64;               // distinct slices per batch (k_aggregate rounds)
 constexpr int RT_MAXNB = 256;           // directory buckets the route table holds
+constexpr int FLAG_RING = 16;           // direct-record flags, one per batch in flight
 constexpr int RT_GROUPS = RT_Q + 2;     // bin groups per bucket: RT_Q routed slices, then the direct records
                                         // (any other slice, the Long.MIN_VALUE key) and the per-element fires
 constexpr int AG_THREADS = 1024;
@@ -532,6 +541,8 @@ struct RouteBuf {
   uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
   uint16_t* seg;         // [ntiles][RT_GROUPS * nb + 1] start of each bin's segment in the tile; [last] = count
   int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
+  unsigned int* dflag;   // set by a tile with direct-group records (a ring of FLAG_RING words, one per batch)
+  unsigned int* dflag_reset;   // the word of batch j + FLAG_RING/2: zeroed by k_aggregate of batch j
   long long* stamps;     // diagnostics (FW_DEBUG_AGG & 16): per-workgroup phase timestamps, 8 per workgroup
   int32_t ntiles;
   int32_t dbg;
@@ -791,6 +802,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   }
   if (direct_mask != 0) *any_direct = 1;
   __syncthreads();   // every wave's slice claims are in lset, every staging read is done
+  if (threadIdx.x == 0 && *any_direct) atomicOr(r.dflag, 1u);
   if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
   FW_STAMP(r, 0, 2);
   block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
@@ -889,6 +901,49 @@ __device__ __forceinline__ void acc_add(const AggLds& L, bool cmpto, bool by_las
   atomicMin(&L.first[kl], oi);   // earliest record of the batch: the first arrival, and the "touched" mark
 }
 
+// Hot keys (Zipf): when 8 or more lanes of a wave carry the slot of the wave's first active lane, they are
+// reduced in registers (butterfly over the wave) and the leader makes one LDS update for all of them —
+// the same-address LDS atomics of a hot key would otherwise serialise 64 ways.  Returns whether this
+// lane still has its own update to make.  (Double sums change association: the tolerance path.)
+template <int VT, int AGG>
+__device__ __forceinline__ bool hot_combine(const AggLds& L, bool cmpto, bool act, uint32_t kl, int64_t v, uint32_t oi,
+                                            int lane) {
+  const uint64_t am = __ballot(act);
+  if (am == 0) return act;
+  const int leader = __ffsll((long long)am) - 1;
+  const uint32_t lk = __shfl(kl, leader);
+  const bool same = act && kl == lk;
+  const uint64_t sm = __ballot(same);
+  if (__popcll(sm) < 8) return act;   // wave-uniform
+  int64_t sv = same ? v : sum_identity(VT);
+  int64_t mn = same ? min_code(VT, cmpto, v) : INT64_MAX;
+  int64_t mx = same ? max_code(VT, cmpto, v) : INT64_MIN;
+  uint32_t fo = same ? oi : NO_FIRST;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    if (AGG & FW_AGG_SUM) {
+      const int64_t y = __shfl_xor(sv, o);
+      if (VT == FW_VALUE_I64) sv = jadd(sv, y);
+      else sv = __double_as_longlong(__longlong_as_double(sv) + __longlong_as_double(y));
+    }
+    if (AGG & FW_AGG_MIN) { const int64_t y = __shfl_xor(mn, o); mn = y < mn ? y : mn; }
+    if (AGG & FW_AGG_MAX) { const int64_t y = __shfl_xor(mx, o); mx = y > mx ? y : mx; }
+    const uint32_t y = __shfl_xor(fo, o);
+    fo = y < fo ? y : fo;
+  }
+  if (lane == leader) {
+    if (AGG & FW_AGG_SUM) {
+      if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&L.sum[lk], (unsigned long long)sv);
+      else unsafeAtomicAdd((double*)&L.sum[lk], __longlong_as_double(sv));
+    }
+    if (AGG & FW_AGG_MIN) atomicMin((long long*)&L.mn[lk], (long long)mn);
+    if (AGG & FW_AGG_MAX) atomicMax((long long*)&L.mx[lk], (long long)mx);
+    if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&L.cnt[lk], (unsigned long long)__popcll(sm));
+    atomicMin(&L.first[lk], fo);
+  }
+  return act && !same;
+}
+
 // LDS bytes k_aggregate needs for buckets of 2^kb_bits slots and ntiles tiles
 __host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_t ntiles, bool by) {
   return (size_t)8 * ((size_t)1 << kb_bits) + ((size_t)(1 << kb_bits) + 65) * (8 * nacc + (by ? 4 : 0)) +
@@ -931,6 +986,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   const int64_t dbase = (int64_t)bkt * KB;
   const int64_t SB = (int64_t)8 << 16;
   FW_STAMP(r, SB, 0);
+  // does any tile hold direct-group records (the batch's flag; no: skip all direct work)
+  const bool has_direct = __builtin_amdgcn_readfirstlane(*r.dflag) != 0;
   // every tile's header and this bucket's segment bounds in each of its bin groups, plus the bucket's
   // directory slice, into LDS: all loads independent, one round trip
   for (int t = threadIdx.x; t < r.ntiles; t += NT) {
@@ -941,7 +998,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     for (int q = 0; q < RT_Q; ++q) h[q] = r.hdr[(int64_t)t * RT_Q + q];
 #pragma unroll
     for (int q = 0; q < RT_GROUPS; ++q)
-      sg[q] = (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16);
+      sg[q] = q < RT_Q || has_direct ? (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16) : 0u;
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q) lhdr[t * RT_Q + q] = h[q];
 #pragma unroll
@@ -957,7 +1014,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     if (m_pre != FREE_TAG) pre_p = slice_slot(s, m_pre);
   }
   for (int x = threadIdx.x; x < KA; x += NT) {
-    lsum[x] = 0;
+    lsum[x] = sum_identity(VT);
     if (HAS_MIN) lmin[x] = INT64_MAX;
     if (HAS_MAX) lmax[x] = INT64_MIN;
     if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
@@ -987,7 +1044,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   // (k_late_* apply them after this kernel, in arrival order); the others are added in the round of
   // their slice below.  A direct record carries its directory hash (EMPTY_H: the Long.MIN_VALUE key) and
   // its index in the tile, i.e. its batch index
-  for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+  // no memset between batches: batch j's flag was zeroed by k_aggregate of batch j - FLAG_RING/2, whose
+  // flag is no longer read and whose successor k_route starts only after this kernel (event order)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *r.dflag_reset = 0u;
+  for (int t = threadIdx.x; has_direct && t < r.ntiles; t += NT) {
     const uint32_t sd = lseg[t * RT_GROUPS + RT_Q], sf = lseg[t * RT_GROUPS + RT_Q + 1];
     for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) {
       const int64_t i = (int64_t)t * RT_TILE + r.idx[(int64_t)t * RT_TILE + x];
@@ -1128,6 +1188,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         for (int u = 0; u < UR; ++u) {
           bool act = ra[u];
           uint32_t kl = probe(act, (uint64_t)rv[u].x);
+          if (!BY) act = hot_combine<VT, AGG>(L, cmpto, act, kl, rv[u].y, ri[u], lane);
           kl = act ? kl : (uint32_t)KB + (uint32_t)lane;   // inactive lanes update a private dummy slot
           acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, rv[u].y, ri[u]);
         }
@@ -1153,7 +1214,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     }
     // this bucket's direct records of slice m (rare; one tile per thread): the same accumulators, their
     // batch index as the arrival order
-    for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+    for (int t = threadIdx.x; has_direct && t < r.ntiles; t += NT) {
       const uint32_t sd = lseg[t * RT_GROUPS + RT_Q];
       for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) {
         const int64_t pos = (int64_t)t * RT_TILE + x;
@@ -1213,7 +1274,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         s.c.present[idx] = 1;
       }
       // cleared for the next round (untouched entries still are; the per-lane dummies are never read)
-      lsum[xl] = 0;
+      lsum[xl] = sum_identity(VT);
       if (HAS_MIN) lmin[xl] = INT64_MAX;
       if (HAS_MAX) lmax[xl] = INT64_MIN;
       if (AGG & FW_AGG_COUNT) lcnt[xl] = 0;
@@ -1377,7 +1438,7 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
     // FIRE_AND_PURGE after the last element: pane cleared (AbstractHeapState.clear).  (Sliding: the slice
     // also feeds windows that have not fired; a purged window's later per-element fires emit the record
     // alone, k_fire_emit)
-    if (s.c.sum) s.c.sum[idx] = 0;
+    if (s.c.sum) s.c.sum[idx] = sum_identity(s.vt);
     if (s.c.mn) s.c.mn[idx] = INT64_MAX;
     if (s.c.mx) s.c.mx[idx] = INT64_MIN;
     if (s.c.cnt) s.c.cnt[idx] = 0;
@@ -1560,7 +1621,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     const int64_t pbase = (int64_t)purge[q] * s.stride;
     for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < s.stride; kid += gstride) {
       const int64_t idx = pbase + kid;
-      if (s.c.sum) s.c.sum[idx] = 0;
+      if (s.c.sum) s.c.sum[idx] = sum_identity(s.vt);
       if (s.c.mn) s.c.mn[idx] = INT64_MAX;
       if (s.c.mx) s.c.mx[idx] = INT64_MIN;
       if (s.c.cnt) s.c.cnt[idx] = 0;
@@ -1793,6 +1854,13 @@ struct fw_engine {
   // fw_snapshot_kg: entries of every key group, built once per engine state (state_epoch)
   int64_t state_epoch = 0, snap_epoch = -1;
   std::vector<std::vector<int64_t>> snap_kg;
+  std::vector<uint8_t> snap_has_key;   // per key group: a key of it is in the directory (it held window state)
+  bool snap_any_key = false;
+  std::vector<uint8_t> kg_touched;     // per key group: restored with present = 1 (fw_restore_kg_flink)
+  int64_t restore_ord = -((int64_t)1 << 62);   // arrival ordinals of restored panes, in blob order
+  // fw_restore_kg_flink: each restored timer's position in the timer sections (restoreTimersForKeyGroup adds
+  // them to the set in that order, so later snapshots list them in it within a hash bucket)
+  std::map<std::array<int64_t, 4>, int64_t> restored_timer_rank;
   int64_t records_in = 0;
   int64_t pushes = 0;                 // non-empty pushes (ev_consumed ring position)
   int grid = 0;
@@ -1845,6 +1913,7 @@ struct fw_engine {
   bool routed = false;
   RouteBuf rb{};                            // fields shared by both parities (dbg, stamps)
   RouteBuf rbs[2] = {};                     // routed-batch buffers, one set per batch parity
+  unsigned int* dflags = nullptr;           // direct-record flags, a ring of FLAG_RING
   int64_t batches = 0;
   int32_t max_tiles = 0;
   size_t route_lds = 0, agg_lds = 0;
@@ -1911,6 +1980,8 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   }
   RouteBuf r = e->rbs[par];
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
+  r.dflag = e->dflags + (e->batches % FLAG_RING);
+  r.dflag_reset = e->dflags + ((e->batches + FLAG_RING / 2) % FLAG_RING);
   // at least 81 KiB of LDS: one k_aggregate workgroup per CU (the dispatcher would otherwise pair two
   // of the nb = CU-count workgroups on one CU and leave another idle)
   const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, (size_t)e->agg_min_lds);
@@ -2115,6 +2186,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
       e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
+      e->dflags = e->alloc<unsigned int>(FLAG_RING);
       for (int q = 0; q < 2; ++q) {
         RouteBuf& r = e->rbs[q];
         r = e->rb;
@@ -2172,7 +2244,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   // initial state
   launch_fill(e, s.dir_keys, EMPTY_KEY, s.D);
   launch_fill(e, s.slice_tag, FREE_TAG, P);
-  launch_fill(e, s.c.sum, 0, (int64_t)cells);
+  launch_fill(e, s.c.sum, sum_identity(s.vt), (int64_t)cells);
   launch_fill(e, s.c.mn, INT64_MAX, (int64_t)cells);
   launch_fill(e, s.c.mx, INT64_MIN, (int64_t)cells);
   launch_fill(e, s.c.cnt, 0, (int64_t)cells);
@@ -2187,6 +2259,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->fire_count) HIPCHK(e, hipMemsetAsync(e->fire_count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(e->wm_done, 0, 4, e->stream));
   if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
+  if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
   *out = e;
@@ -2545,6 +2618,10 @@ static int build_snapshot(fw_engine* e) {
     if (keys[k] != fw::EMPTY_KEY) kid_kg[k] = host_key_group(s, keys[k]);
   if (min_used) kid_kg[s.D] = host_key_group(s, fw::EMPTY_KEY);
   e->snap_kg.assign((size_t)mp, {});
+  e->snap_has_key.assign((size_t)mp, 0);
+  e->snap_any_key = false;
+  for (size_t k = 0; k < kid_kg.size(); ++k)
+    if (kid_kg[k] >= 0) { e->snap_has_key[(size_t)kid_kg[k]] = 1; e->snap_any_key = true; }
   const size_t st = (size_t)s.stride;
   std::vector<int64_t> sum(st), mn, mx, cnt, first, f1v;
   std::vector<uint8_t> present;
@@ -2604,6 +2681,8 @@ int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* le
   return FW_OK;
 }
 
+static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t n);
+
 int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   if (!e || !buf) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
@@ -2627,9 +2706,14 @@ int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   for (int64_t j = 0; j < n; ++j)
     if (host_key_group(e->s, ent[j * FW_SNAP_ENTRY_WORDS + 1]) != kg)
       return reject(e, FW_ERR_KEY_GROUP, "snapshot entry key outside its key group");
+  return restore_entries(e, h[4], ent, n);
+}
+
+// load n validated snapshot entries (FW_SNAP_ENTRY_WORDS each) and set the watermark
+static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t n) {
   HIPCHK(e, hipSetDevice(e->dev));
   e->restored = true;
-  e->cur_wm = h[4];
+  e->cur_wm = wm;
   e->state_epoch++;
   if (n == 0) return FW_OK;
   int64_t* d = nullptr;
@@ -2645,6 +2729,350 @@ int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   HIPCHK(e, r);
   HIPCHK(e, r2);
   return check_device_error(e);
+}
+
+// ------------------------------------------------------------------------------------------------
+// checkpoint state in the reference's key-group layout (flink_kg_format.h; flink_window.h)
+// ------------------------------------------------------------------------------------------------
+
+// one (window, key) entry of a key group's state table, engine encodings (double bits, min/max codes)
+struct KgPane {
+  int64_t start, end, key;
+  int64_t sum, mn, mx, cnt;
+  int64_t first;    // first-arrival ordinal (0 when the config does not track first arrival)
+  int64_t f1;
+};
+
+static int check_state_layout(fw_engine* e, const fw_state_layout* L) {
+  if (!L || L->n_fields < 0 || L->n_fields > FW_SF_MAX_FIELDS)
+    return reject(e, FW_ERR_INVALID_ARG, "bad state layout");
+  int seen[FW_SF_VALUE + 1] = {0};
+  for (int i = 0; i < L->n_fields; ++i) {
+    const int f = L->field[i];
+    if (f < FW_SF_KEY || f > FW_SF_VALUE) return reject(e, FW_ERR_INVALID_ARG, "bad state layout field");
+    seen[f]++;
+  }
+  const fw_config& c = e->cfg;
+  const bool by = e->s.by;
+  const int want[FW_SF_VALUE + 1] = {0, -1, e->s.first ? 1 : 0, !by && (c.agg_mask & FW_AGG_SUM) ? 1 : 0,
+                                     !by && (c.agg_mask & FW_AGG_MIN) ? 1 : 0, !by && (c.agg_mask & FW_AGG_MAX) ? 1 : 0,
+                                     !by && (c.agg_mask & FW_AGG_COUNT) ? 1 : 0, by ? 1 : 0};
+  if (seen[FW_SF_KEY] > 1) return reject(e, FW_ERR_INVALID_ARG, "state layout names the key twice");
+  for (int f = FW_SF_F1; f <= FW_SF_VALUE; ++f)
+    if (seen[f] != want[f])
+      return reject(e, FW_ERR_INVALID_ARG, "state layout must name each computed aggregate (and f1 iff "
+                                           "keep_first_f1) exactly once");
+  return FW_OK;
+}
+
+static int64_t host_window_start(const fw_config& c, int64_t n) {
+  return fw::jadd(c.offset, (int64_t)((uint64_t)n * (uint64_t)(c.assigner == FW_TUMBLING ? c.size : c.slide)));
+}
+
+// the pane value of field f, written as the field's Java type
+static void put_field(const fw_engine* e, fwkg::BeOut& o, int f, const KgPane& p) {
+  const bool f64 = e->s.vt == FW_VALUE_F64;
+  auto val = [&](int64_t bits) { if (f64) { double d; memcpy(&d, &bits, 8); o.f64(d); } else o.i64(bits); };
+  auto code = [&](int64_t c) { if (f64) o.f64(fw::f64_from_code(c)); else o.i64(c); };
+  switch (f) {
+    case FW_SF_KEY: o.i64(p.key); break;
+    case FW_SF_F1: o.i64(p.f1); break;
+    case FW_SF_SUM: val(p.sum); break;
+    case FW_SF_MIN: code(p.mn); break;
+    case FW_SF_MAX: code(p.mx); break;
+    case FW_SF_COUNT: o.i64(p.cnt); break;
+    case FW_SF_VALUE: code(e->cfg.agg_mask == FW_AGG_MAXBY ? p.mx : p.mn); break;
+  }
+}
+
+// The panes of key group kg as the reference holds them: one per (window, key).  Tumbling: a slice is a
+// window.  Sliding: every window still in its lifetime (cleanup time > watermark) that a slice of the key
+// overlaps, combined from its slices in slice order (double sums: the slice-sum order, not arrival order)
+static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
+  const fw_config& c = e->cfg;
+  const fw::Spec& s = e->s;
+  const std::vector<int64_t>& v = e->snap_kg[(size_t)kg];
+  const size_t n = v.size() / FW_SNAP_ENTRY_WORDS;
+  const bool tumbling = c.assigner == FW_TUMBLING;
+  auto pane_of = [&](const int64_t* x, int64_t start) {
+    KgPane p;
+    p.start = start;
+    p.end = fw::jadd(start, c.size);
+    p.key = x[1];
+    p.sum = x[2]; p.mn = x[3]; p.mx = x[4];
+    p.cnt = x[5];               // maxBy/minBy: the extremal record's ordinal
+    p.first = s.first ? x[6] : 0;
+    p.f1 = x[7];
+    return p;
+  };
+  out.clear();
+  if (tumbling) {
+    for (size_t j = 0; j < n; ++j) {
+      const int64_t* x = &v[j * FW_SNAP_ENTRY_WORDS];
+      KgPane p = pane_of(x, host_window_start(c, x[0]));
+      if (fw::cleanup_time(fw::jsub(p.end, 1), c.allowed_lateness) > e->cur_wm) out.push_back(p);
+    }
+    return;
+  }
+  std::vector<size_t> ord(n);
+  for (size_t j = 0; j < n; ++j) ord[j] = j;
+  std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+    const int64_t* x = &v[a * FW_SNAP_ENTRY_WORDS];
+    const int64_t* y = &v[b * FW_SNAP_ENTRY_WORDS];
+    return x[1] != y[1] ? x[1] < y[1] : x[0] < y[0];
+  });
+  std::map<std::pair<int64_t, int64_t>, KgPane> win;   // (window number, key)
+  const bool f64 = s.vt == FW_VALUE_F64;
+  for (size_t j : ord) {
+    const int64_t* x = &v[j * FW_SNAP_ENTRY_WORDS];
+    const int64_t m = x[0];
+    for (int64_t w = fw::floor_div(m - s.K, s.R) + 1; w <= fw::floor_div(m, s.R); ++w) {
+      const int64_t start = host_window_start(c, w);
+      if (fw::cleanup_time(fw::jsub(fw::jadd(start, c.size), 1), c.allowed_lateness) <= e->cur_wm) continue;
+      KgPane b = pane_of(x, start);
+      auto it = win.find({w, b.key});
+      if (it == win.end()) { win.emplace(std::make_pair(w, b.key), b); continue; }
+      KgPane& a = it->second;
+      if (s.by) {   // the extremal record; a tie keeps the earlier one (maxBy/minBy(first = false): the later)
+        const bool maxby = c.agg_mask == FW_AGG_MAXBY;
+        const int64_t ca = maxby ? a.mx : a.mn, cb = maxby ? b.mx : b.mn;
+        const bool better = maxby ? cb > ca : cb < ca;
+        const bool tie_later = (c.agg_flags & FW_AGGF_BY_LAST) != 0;
+        if (better || (cb == ca && (tie_later ? b.cnt > a.cnt : b.cnt < a.cnt))) {
+          a.mx = b.mx; a.mn = b.mn; a.cnt = b.cnt; a.f1 = b.f1;
+        }
+        a.first = std::min(a.first, b.first);
+        continue;
+      }
+      if (f64) {
+        double da, db;
+        memcpy(&da, &a.sum, 8); memcpy(&db, &b.sum, 8);
+        da += db;
+        memcpy(&a.sum, &da, 8);
+      } else {
+        a.sum = fw::jadd(a.sum, b.sum);
+      }
+      a.mn = std::min(a.mn, b.mn);
+      a.mx = std::max(a.mx, b.mx);
+      a.cnt = fw::jadd(a.cnt, b.cnt);
+      if (s.first && b.first < a.first) { a.first = b.first; a.f1 = b.f1; }
+    }
+  }
+  for (auto& kv : win) out.push_back(kv.second);
+}
+
+int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, void* state, int64_t state_cap,
+                         int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
+  if (!e || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
+  if (e->sticky) return e->sticky;
+  if (kg < e->s.kg_start || kg > e->s.kg_end)
+    return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
+  if (e->used_key_hash) return reject(e, FW_ERR_UNSUPPORTED, "snapshot needs Long keys (a push carried Java key hashes)");
+  int rc = check_state_layout(e, layout);
+  if (rc) return rc;
+  const fw_config& c = e->cfg;
+  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0)
+    return reject(e, FW_ERR_UNSUPPORTED, "PurgingTrigger with allowed lateness: purged panes keep timers the "
+                                         "engine does not hold");
+  HIPCHK(e, hipSetDevice(e->dev));
+  rc = build_snapshot(e);
+  if (rc) return rc;
+  std::vector<KgPane> panes;
+  kg_panes(e, kg, panes);
+  const bool first = e->s.first;
+  bool any_state = e->snap_any_key;
+  for (uint8_t t : e->kg_touched) any_state = any_state || t;
+  fwkg::BeOut st, tm;
+  if (any_state) {
+    const bool present = !panes.empty() || e->snap_has_key[(size_t)kg] ||
+                         (!e->kg_touched.empty() && e->kg_touched[(size_t)(kg - e->s.kg_start)]);
+    st.i32(kg);
+    st.i16(0);
+    st.u8(present ? 1 : 0);
+    if (present) {
+      // namespaces: HashMap<TimeWindow, HashMap<K, S>>, created by the first arrival into the window
+      std::map<std::pair<int64_t, int64_t>, std::vector<size_t>> ns;
+      for (size_t i = 0; i < panes.size(); ++i) ns[{panes[i].start, panes[i].end}].push_back(i);
+      std::vector<std::pair<std::pair<int64_t, int64_t>, std::vector<size_t>>> nsv(ns.begin(), ns.end());
+      std::vector<int64_t> ns_first(nsv.size(), INT64_MAX);
+      for (size_t w = 0; w < nsv.size(); ++w)
+        for (size_t i : nsv[w].second) ns_first[w] = std::min(ns_first[w], panes[i].first);
+      std::vector<size_t> wo(nsv.size());
+      for (size_t w = 0; w < wo.size(); ++w) wo[w] = w;
+      fwkg::hashmap_order(
+          wo, [&](size_t w) { return fwkg::window_hash(nsv[w].first.first, nsv[w].first.second); },
+          [&](size_t a, size_t b) {
+            return first && ns_first[a] != ns_first[b] ? ns_first[a] < ns_first[b] : nsv[a].first < nsv[b].first;
+          });
+      st.i32((int32_t)nsv.size());
+      for (size_t w : wo) {
+        st.i64(nsv[w].first.first);
+        st.i64(nsv[w].first.second);
+        std::vector<size_t>& ent = nsv[w].second;
+        fwkg::hashmap_order(
+            ent, [&](size_t i) { return fw::long_hash_code(panes[i].key); },
+            [&](size_t a, size_t b) {
+              return first && panes[a].first != panes[b].first ? panes[a].first < panes[b].first : panes[a].key < panes[b].key;
+            });
+        st.i32((int32_t)ent.size());
+        for (size_t i : ent) {
+          st.i64(panes[i].key);
+          for (int f = 0; f < layout->n_fields; ++f) put_field(e, st, layout->field[f], panes[i]);
+        }
+      }
+    }
+  }
+  // timers: per pane the trigger timer at maxTimestamp while it has not fired, and the cleanup timer (the
+  // same timer when the lateness is 0), registered in that order by the pane's first arrival
+  // (WindowOperator.java:314-330; EventTimeTrigger.onElement :37-45); a record's sliding windows register
+  // theirs latest window first (SlidingEventTimeWindows.assignWindows :64-77)
+  // (restored timers: added at restore, before any later one, in the order of the restored sections)
+  struct Tm { int64_t key, start, end, ts, first; int kind; int64_t rank; };
+  std::vector<Tm> tv;
+  for (const KgPane& p : panes) {
+    const int64_t max_ts = fw::jsub(p.end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+    if (max_ts > e->cur_wm) tv.push_back({p.key, p.start, p.end, max_ts, p.first, 0, INT64_MAX});
+    if (ct != max_ts || max_ts <= e->cur_wm) tv.push_back({p.key, p.start, p.end, ct, p.first, 1, INT64_MAX});
+  }
+  if (!e->restored_timer_rank.empty())
+    for (Tm& t : tv) {
+      auto it = e->restored_timer_rank.find({t.key, t.start, t.end, t.ts});
+      if (it != e->restored_timer_rank.end()) t.rank = it->second;
+    }
+  std::vector<size_t> to(tv.size());
+  for (size_t i = 0; i < to.size(); ++i) to[i] = i;
+  fwkg::hashmap_order(
+      to, [&](size_t i) { return fwkg::timer_hash(tv[i].ts, tv[i].key, tv[i].start, tv[i].end); },
+      [&](size_t a, size_t b) {
+        const Tm &x = tv[a], &y = tv[b];
+        if (x.rank != y.rank) return x.rank < y.rank;
+        if (first && x.first != y.first) return x.first < y.first;
+        if (!first && x.key != y.key) return x.key < y.key;
+        if (x.start != y.start) return x.start > y.start;
+        return x.kind < y.kind;
+      });
+  tm.i32((int32_t)tv.size());
+  for (size_t i : to) {
+    tm.i64(tv[i].key);
+    tm.i64(tv[i].start);
+    tm.i64(tv[i].end);
+    tm.i64(tv[i].ts);
+  }
+  tm.i32(0);
+  *state_len = (int64_t)st.b.size();
+  *timers_len = (int64_t)tm.b.size();
+  if (!state && !timers) return FW_OK;
+  if (!state || !timers || state_cap < *state_len || timers_cap < *timers_len)
+    return reject(e, FW_ERR_CAPACITY, "snapshot buffer too small");
+  if (!st.b.empty()) memcpy(state, st.b.data(), st.b.size());
+  memcpy(timers, tm.b.data(), tm.b.size());
+  return FW_OK;
+}
+
+int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
+                        const void* state, int64_t state_len, const void* timers, int64_t timers_len) {
+  if (!e || (!state && state_len) || !timers || state_len < 0) return FW_ERR_INVALID_ARG;
+  if (e->sticky) return e->sticky;
+  if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
+  if (kg < e->s.kg_start || kg > e->s.kg_end)
+    return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
+  int rc = check_state_layout(e, layout);
+  if (rc) return rc;
+  const fw_config& c = e->cfg;
+  const fw::Spec& s = e->s;
+  if (c.assigner != FW_TUMBLING)
+    return reject(e, FW_ERR_UNSUPPORTED, "window-level state restores into tumbling windows only (sliding: "
+                                         "fw_restore_kg's slice blob)");
+  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0)
+    return reject(e, FW_ERR_UNSUPPORTED, "PurgingTrigger with allowed lateness");
+  if (e->restored && watermark != e->cur_wm)
+    return reject(e, FW_ERR_INVALID_ARG, "key groups restored at different watermarks");
+  const bool f64 = s.vt == FW_VALUE_F64;
+  std::vector<KgPane> panes;
+  std::vector<int64_t> slice_of;
+  bool present = false;
+  if (state_len > 0) {
+    fwkg::BeIn in(state, state_len);
+    if (in.i32() != kg) return reject(e, FW_ERR_INVALID_ARG, "state section of another key group");
+    if (in.i16() != 0) return reject(e, FW_ERR_UNSUPPORTED, "keyed state other than window-contents");
+    present = in.u8() != 0;
+    const int32_t nns = present ? in.i32() : 0;
+    if (nns < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
+    std::set<std::pair<int64_t, int64_t>> seen;
+    for (int32_t w = 0; w < nns && in.ok; ++w) {
+      const int64_t start = in.i64(), end = in.i64();
+      const int64_t m = fw::floor_div(fw::jsub(start, c.offset), c.size);
+      if (in.ok && (end != fw::jadd(start, c.size) || host_window_start(c, m) != start ||
+                    fw::window_start_with_offset(start, c.offset, c.size) != start))
+        return reject(e, FW_ERR_INVALID_ARG, "namespace is not a window of this assigner");
+      const int32_t ne = in.i32();
+      if (ne < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
+      for (int32_t j = 0; j < ne && in.ok; ++j) {
+        KgPane p{start, end, in.i64(), 0, INT64_MAX, INT64_MIN, 0, 0, 0};
+        for (int f = 0; f < layout->n_fields; ++f) {
+          const int64_t x = in.i64();
+          double d;
+          memcpy(&d, &x, 8);
+          switch (layout->field[f]) {
+            case FW_SF_KEY:
+              if (in.ok && x != p.key) return reject(e, FW_ERR_UNSUPPORTED, "state key field differs from the key");
+              break;
+            case FW_SF_F1: p.f1 = x; break;
+            case FW_SF_SUM: p.sum = x; break;
+            case FW_SF_MIN: p.mn = f64 ? (s.cmpto ? fw::f64_cmp_code(d) : fw::f64_min_code(d)) : x; break;
+            case FW_SF_MAX: p.mx = f64 ? (s.cmpto ? fw::f64_cmp_code(d) : fw::f64_max_code(d)) : x; break;
+            case FW_SF_COUNT: p.cnt = x; break;
+            case FW_SF_VALUE: p.mn = p.mx = f64 ? fw::f64_cmp_code(d) : x; break;
+          }
+        }
+        if (!in.ok) break;
+        if (host_key_group(s, p.key) != kg) return reject(e, FW_ERR_KEY_GROUP, "state entry key outside its key group");
+        if (!seen.insert({m, p.key}).second) return reject(e, FW_ERR_INVALID_ARG, "duplicate (window, key) entry");
+        panes.push_back(p);
+        slice_of.push_back(m);
+      }
+    }
+    if (!in.done()) return reject(e, FW_ERR_INVALID_ARG, "state section truncated or with trailing bytes");
+  }
+  // timers: exactly the ones the panes imply at `watermark` (the engine's timers are implicit)
+  std::vector<std::array<int64_t, 4>> got, want, got_in_order;
+  {
+    fwkg::BeIn in(timers, timers_len);
+    const int32_t nt = in.i32();
+    if (nt < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt timer section");
+    for (int32_t i = 0; i < nt && in.ok; ++i) {
+      const int64_t key = in.i64(), start = in.i64(), end = in.i64(), ts = in.i64();
+      got.push_back({key, start, end, ts});
+    }
+    got_in_order = got;
+    const int32_t np = in.i32();
+    if (!in.done()) return reject(e, FW_ERR_INVALID_ARG, "timer section truncated or with trailing bytes");
+    if (np != 0) return reject(e, FW_ERR_UNSUPPORTED, "processing-time timers");
+  }
+  for (const KgPane& p : panes) {
+    const int64_t max_ts = fw::jsub(p.end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+    if (ct <= watermark) return reject(e, FW_ERR_UNSUPPORTED, "pane past its cleanup time at the restore watermark");
+    if (max_ts > watermark) want.push_back({p.key, p.start, p.end, max_ts});
+    if (ct != max_ts) want.push_back({p.key, p.start, p.end, ct});
+  }
+  std::sort(got.begin(), got.end());
+  std::sort(want.begin(), want.end());
+  if (got != want)
+    return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark "
+                                         "(pass the checkpoint's watermark when panes have fired but are kept)");
+  // arrival ordinals in blob order: restored panes precede every later record, and keep the blob's
+  // (HashMap iteration) order as their insertion order, as readStateTableForKeyGroup's puts do
+  std::vector<int64_t> ent(panes.size() * FW_SNAP_ENTRY_WORDS);
+  for (size_t i = 0; i < panes.size(); ++i) {
+    const KgPane& p = panes[i];
+    const int64_t ord = e->restore_ord++;
+    const int64_t w[FW_SNAP_ENTRY_WORDS] = {slice_of[i], p.key, p.sum, p.mn, p.mx, s.by ? ord : p.cnt, ord, p.f1};
+    memcpy(&ent[i * FW_SNAP_ENTRY_WORDS], w, sizeof(w));
+  }
+  for (const auto& t : got_in_order) e->restored_timer_rank[t] = (int64_t)e->restored_timer_rank.size();
+  if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(s.kg_end - s.kg_start + 1), 0);
+  if (present) e->kg_touched[(size_t)(kg - s.kg_start)] = 1;
+  return restore_entries(e, watermark, ent.data(), (int64_t)panes.size());
 }
 
 int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,

@@ -328,6 +328,30 @@ class WindowEngine:
         buf = np.frombuffer(blob, dtype=np.int64).copy()
         self._check(self._fn("restore_kg")(self.h, kg, _ptr(buf), len(blob)))
 
+    def snapshot_kg_flink(self, kg, layout):
+        """Key group kg in the reference's checkpoint layout (fw_snapshot_kg_flink): (state, timers) bytes —
+        the managed keyed-state section at KeyGroupRangeOffsets[kg] (HeapKeyedStateBackend.java:196-248) and
+        the body of HeapInternalTimerService.snapshotTimersForKeyGroup (:285-310).  `layout` names the state
+        tuple's fields in order: "key", "f1", "sum", "min", "max", "count", "value" (maxBy/minBy)."""
+        L = state_layout(layout)
+        ns, nt = ctypes.c_int64(), ctypes.c_int64()
+        fn = self._fn("snapshot_kg_flink")
+        self._check(fn(self.h, kg, ctypes.byref(L), None, 0, ctypes.byref(ns), None, 0, ctypes.byref(nt)))
+        st = ctypes.create_string_buffer(max(ns.value, 1))
+        tm = ctypes.create_string_buffer(max(nt.value, 1))
+        self._check(fn(self.h, kg, ctypes.byref(L), st, ns.value, ctypes.byref(ns), tm, nt.value, ctypes.byref(nt)))
+        return st.raw[:ns.value], tm.raw[:nt.value]
+
+    def restore_kg_flink(self, kg, layout, state, timers, watermark=-(1 << 63)):
+        """Load a key group written in the reference's layout before the first push (fw_restore_kg_flink;
+        readStateTableForKeyGroup + restoreTimersForKeyGroup).  The default watermark is the reference's:
+        its timer service restarts at Long.MIN_VALUE."""
+        L = state_layout(layout)
+        sb = ctypes.create_string_buffer(bytes(state), max(len(state), 1))
+        tb = ctypes.create_string_buffer(bytes(timers), max(len(timers), 1))
+        self._check(self._fn("restore_kg_flink")(self.h, kg, ctypes.byref(L), watermark, sb, len(state), tb,
+                                                 len(timers)))
+
     def stats(self):
         st = _abi.FwStats()
         self._check(self._fn("get_stats")(self.h, ctypes.byref(st)))
@@ -343,6 +367,22 @@ class WindowEngine:
             self.close()
         except Exception:
             pass
+
+
+STATE_FIELDS = {"key": _abi.FW_SF_KEY, "f1": _abi.FW_SF_F1, "sum": _abi.FW_SF_SUM, "min": _abi.FW_SF_MIN,
+                "max": _abi.FW_SF_MAX, "count": _abi.FW_SF_COUNT, "value": _abi.FW_SF_VALUE}
+
+
+def state_layout(fields):
+    """fw_state_layout of a state tuple given as field names in tuple order, e.g. ("key", "f1", "sum") for
+    the Tuple3(key, f1, sum) of Tuple3.of(a.f0, a.f1, a.f2 + b.f2)."""
+    if len(fields) > _abi.FW_SF_MAX_FIELDS:
+        raise ValueError("state tuple has too many fields")
+    L = _abi.FwStateLayout()
+    L.n_fields = len(fields)
+    for i, f in enumerate(fields):
+        L.field[i] = STATE_FIELDS[f]
+    return L
 
 
 def make_config(assigner, reduce_function, trigger=None, allowed_lateness=0, max_parallelism=DEFAULT_MAX_PARALLELISM,

@@ -192,6 +192,56 @@ void        fw_destroy(fw_engine* e);
 int         fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* len);
 int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len);
 
+/* ---- checkpoint state per key group in the reference's own byte layout ----
+ * fw_snapshot_kg_flink <- the per-key-group part of HeapKeyedStateBackend.snapshot (HeapKeyedStateBackend.java
+ *                         :196-212, writeStateTableForKeyGroup :217-248) and of
+ *                         HeapInternalTimerService.snapshotTimersForKeyGroup (:285-310)
+ * fw_restore_kg_flink  <- HeapKeyedStateBackend.restorePartitionedState / readStateTableForKeyGroup (:251-349)
+ *                         + HeapInternalTimerService.restoreTimersForKeyGroup (:319-345)
+ * Two big-endian byte sections per key group, exactly as the JVM writes them:
+ *   state   the bytes at KeyGroupRangeOffsets[kg] of the managed keyed-state stream:
+ *             int kg | short 0 (id of "window-contents", the operator's only keyed state) | byte present |
+ *             [int numNamespaces | (long start | long end | int n | (long key | state tuple) * n) * numNamespaces]
+ *           present = the key group ever held window state (StateTable.get(kg) != null).
+ *   timers  the body of snapshotTimersForKeyGroup after its two InstantiationUtil.serializeObject records:
+ *             int n | (long key | long start | long end | long timestamp) * n | int 0 (processing-time timers)
+ *           The caller writes the raw keyed-state prologue around it (AbstractStreamOperator.snapshotState
+ *           :367-391: int 1, writeUTF("window-timers"), the Java-serialized key and namespace serializers):
+ *           JVM object serialization stays on the JVM side.
+ * The state tuple is the ReduceFunction's value type: layout->field[0..n_fields) in tuple order, each an
+ * 8-byte LongSerializer / DoubleSerializer field (TupleSerializer.serialize :120-129).  The layout must
+ * name every aggregate the config computes (FW_SF_VALUE for maxBy/minBy), FW_SF_F1 iff keep_first_f1,
+ * FW_SF_KEY at most once.  Namespaces, entries and timers come in java.util.HashMap iteration order for
+ * tables sized by their current size (when a JVM table iterates differently).
+ * A buffer argument NULL (or too small: FW_ERR_CAPACITY) stores the required lengths only.
+ * *state_len == 0: no keyed state at all yet (no record accepted, nothing restored), for which
+ * HeapKeyedStateBackend.snapshot writes no stream (:169-171).
+ * Restore: before the first push; tumbling windows only (sliding state restores from fw_snapshot_kg's
+ * slice blob); not with PurgingTrigger and allowed lateness > 0 (its purged panes keep cleanup timers).
+ * `watermark` is the engine's watermark after restore: the reference restarts its timer service at
+ * Long.MIN_VALUE (currentWatermark is not checkpointed) — pass INT64_MIN for exactly that.  The engine's
+ * timers are implicit (a pane's trigger timer is pending iff its window's maxTimestamp > watermark, its
+ * cleanup timer iff the pane exists), so the blob's timers must be exactly the ones its panes imply at
+ * `watermark` (FW_ERR_UNSUPPORTED otherwise: e.g. fired-but-kept panes, allowed lateness > 0, need the
+ * checkpoint's watermark).  Every restored key group must use the same `watermark`. */
+#define FW_SF_KEY    1   /* the key (the tuple's key field, e.g. f0)                          */
+#define FW_SF_F1     2   /* the pass-through field of the first arrival (maxBy/minBy: of the extremal record) */
+#define FW_SF_SUM    3
+#define FW_SF_MIN    4
+#define FW_SF_MAX    5
+#define FW_SF_COUNT  6   /* long                                                              */
+#define FW_SF_VALUE  7   /* maxBy/minBy: the extremal record's value field                    */
+#define FW_SF_MAX_FIELDS 8
+typedef struct {
+  int32_t n_fields;
+  int32_t field[FW_SF_MAX_FIELDS];
+} fw_state_layout;
+int         fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, void* state,
+                                 int64_t state_cap, int64_t* state_len, void* timers, int64_t timers_cap,
+                                 int64_t* timers_len);
+int         fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
+                                const void* state, int64_t state_len, const void* timers, int64_t timers_len);
+
 /* Key-group routing for the multi-GPU keyBy exchange (enqueued on the caller stream when fw_set_stream set one)
  * (KeyGroupStreamPartitioner.selectChannels, SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65;
  *  KeyGroupRangeAssignment.assignKeyToParallelOperator, KeyGroupRangeAssignment.java:40-42,105-107).

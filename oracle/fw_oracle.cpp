@@ -24,6 +24,10 @@
 //   timer service               SJ/api/operators/HeapInternalTimerService.java:211-236,264-278
 //   InternalTimer               SJ/api/operators/InternalTimer.java:59-86
 //   processWatermark            SJ/api/operators/AbstractStreamOperator.java:803-808
+//   checkpoint, per key group   RT/state/heap/HeapKeyedStateBackend.java:196-248 (writeStateTableForKeyGroup),
+//                               :251-349 (readStateTableForKeyGroup); HeapInternalTimerService.java:285-345;
+//                               TimeWindow.Serializer TimeWindow.java:141-158; InternalTimer.TimerSerializer
+//                               InternalTimer.java:145-157; JDK HashMap/HashSet iteration order (see below)
 //   reduce functions            SJ/api/functions/aggregation/SumAggregator.java:64-72, SumFunction.java:60-77,
 //                               JDK Math.min/Math.max (double), Long arithmetic (wrapping),
 //                               ComparableAggregator.java:66-90 + Comparator.java:45-105 (min/max/minBy/maxBy
@@ -35,6 +39,7 @@
 // C API (fwo_*) mirrors include/flink_window.h so tests can drive oracle and engine identically.
 #include "../include/flink_window.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -102,6 +107,7 @@ int64_t getWindowStartWithOffset(int64_t timestamp, int64_t offset, int64_t wind
 
 // ---------------- accumulator = the reduced record ----------------
 struct Acc {
+  int64_t seq;   // when this (namespace, key) entry was put into its HashMap (iteration order), not state
   int64_t key;
   int64_t f1;
   int64_t sum_i, min_i, max_i, count;
@@ -200,6 +206,14 @@ struct Operator {
   std::vector<std::unordered_map<TimeWindow, std::unordered_map<int64_t, Acc>, TimeWindowHash>> state;
   // event-time timers: set gives both the HashSet dedupe and the PriorityQueue order
   std::set<InternalTimer> timers;
+  // insertion order of the JVM's hash tables (checkpoint iteration order): per key group when each
+  // namespace was put into the namespace map, when each timer was added to the timer set; whether the
+  // key group's namespace map exists at all (StateTable.get(kg) != null)
+  int64_t seqCounter = 0;
+  std::vector<std::unordered_map<TimeWindow, int64_t, TimeWindowHash>> nsSeq;
+  std::vector<uint8_t> kgCreated;
+  std::map<InternalTimer, int64_t> timerSeq;
+  bool anyState = false;   // HeapKeyedStateBackend.stateTables non-empty (created by the first state access)
   // current key context
   int64_t curKey = 0;
   int32_t curKeyGroup = 0;
@@ -213,6 +227,8 @@ struct Operator {
 
   explicit Operator(const fw_config& c) : cfg(c) {
     state.resize((size_t)(cfg.kg_end - cfg.kg_start + 1));
+    nsSeq.resize(state.size());
+    kgCreated.assign(state.size(), 0);
   }
 
   // ---- WindowAssigner.assignWindows ----
@@ -254,10 +270,23 @@ struct Operator {
   int stateAdd(const TimeWindow& ns, const Acc& value) {  // HeapReducingState.add :84-122
     auto* m = nsMap();
     if (!m) { err = "Unexpected key group index. This indicates a bug."; return FW_ERR_KEY_GROUP; }  // StateTable.set :59-63
-    auto& keyed = (*m)[ns];
+    const size_t kgi = (size_t)(curKeyGroup - cfg.kg_start);
+    kgCreated[kgi] = 1;
+    anyState = true;
+    auto nit = m->find(ns);
+    if (nit == m->end()) {
+      nit = m->emplace(ns, std::unordered_map<int64_t, Acc>()).first;
+      nsSeq[kgi][ns] = value.seq;
+    }
+    auto& keyed = nit->second;
     auto it = keyed.find(curKey);
-    if (it == keyed.end()) keyed.emplace(curKey, value);
-    else it->second = reduceFn(cfg, it->second, value);
+    if (it == keyed.end()) {
+      keyed.emplace(curKey, value);
+    } else {
+      const int64_t sq = it->second.seq;   // HashMap.put of an existing key keeps its place
+      it->second = reduceFn(cfg, it->second, value);
+      it->second.seq = sq;
+    }
     return FW_OK;
   }
   const Acc* stateGet(const TimeWindow& ns) {  // HeapReducingState.get :72-82
@@ -275,12 +304,20 @@ struct Operator {
     if (nit == m->end()) return;
     if (nit->second.erase(curKey) == 0) return;
     if (!nit->second.empty()) return;
+    nsSeq[(size_t)(curKeyGroup - cfg.kg_start)].erase(ns);
     m->erase(nit);
   }
 
   // ---- timer service ----
-  void registerEventTimeTimer(const TimeWindow& ns, int64_t time) { timers.insert({time, curKey, ns}); }  // :211-218
-  void deleteEventTimeTimer(const TimeWindow& ns, int64_t time) { timers.erase({time, curKey, ns}); }    // :229-236
+  void registerEventTimeTimer(const TimeWindow& ns, int64_t time) {  // :211-218
+    const InternalTimer t{time, curKey, ns};
+    if (timers.insert(t).second) timerSeq[t] = ++seqCounter;
+  }
+  void deleteEventTimeTimer(const TimeWindow& ns, int64_t time) {  // :229-236
+    const InternalTimer t{time, curKey, ns};
+    timers.erase(t);
+    timerSeq.erase(t);
+  }
 
   // ---- trigger ----
   TriggerResult triggerOnElement(const TimeWindow& w) {  // EventTimeTrigger.java:37-45
@@ -327,6 +364,7 @@ struct Operator {
     value.sum_i = value.min_i = value.max_i = vi;
     value.sum_d = value.min_d = value.max_d = vd;
     value.count = 1;
+    value.seq = ++seqCounter;
     for (const TimeWindow& window : elementWindows) {  // :302-333
       if (isLate(window)) { stats.records_late++; continue; }
       rc = stateAdd(window, value);
@@ -363,6 +401,7 @@ struct Operator {
     while (!timers.empty() && timers.begin()->timestamp <= time) {
       InternalTimer timer = *timers.begin();
       timers.erase(timers.begin());
+      timerSeq.erase(timer);
       curKeyGroup = computeKeyGroupForKeyHash(keyHashOf(timer.key), cfg.max_parallelism);
       onEventTime(timer);
     }
@@ -377,6 +416,203 @@ struct Operator {
     return it == explicitHash.end() ? longHashCode(key) : it->second;
   }
 };
+
+
+// ---------------- checkpoint of one key group, in the reference's byte layout ----------------
+// DataOutputStream big-endian primitives (writeByte/Short/Int/Long, writeDouble = doubleToLongBits)
+struct JavaOut {
+  std::vector<uint8_t> b;
+  void writeByte(int v) { b.push_back((uint8_t)v); }
+  void writeShort(int v) { writeByte((v >> 8) & 0xff); writeByte(v & 0xff); }
+  void writeInt(int32_t v) { for (int s = 24; s >= 0; s -= 8) writeByte((int)(((uint32_t)v >> s) & 0xff)); }
+  void writeLong(int64_t v) { for (int s = 56; s >= 0; s -= 8) writeByte((int)(((uint64_t)v >> s) & 0xff)); }
+  void writeDouble(double d) {
+    int64_t bits;
+    if (d != d) bits = 0x7ff8000000000000ll;   // Double.doubleToLongBits: the canonical NaN
+    else std::memcpy(&bits, &d, 8);
+    writeLong(bits);
+  }
+};
+struct JavaIn {
+  const uint8_t* p;
+  int64_t n, pos = 0;
+  bool eof = false;
+  uint64_t read(int k) {
+    if (pos + k > n) { eof = true; pos = n; return 0; }
+    uint64_t v = 0;
+    for (int i = 0; i < k; ++i) v = (v << 8) | p[pos + i];
+    pos += k;
+    return v;
+  }
+  int readByte() { return (int)(int8_t)read(1); }
+  int readShort() { return (int)(int16_t)read(2); }
+  int32_t readInt() { return (int32_t)read(4); }
+  int64_t readLong() { return (int64_t)read(8); }
+};
+
+// java.util.HashMap iteration: bucket (h ^ h >>> 16) & (capacity - 1) in index order, each bucket's chain
+// in insertion order.  Capacity: 16, doubled on a put that makes size > 0.75 capacity.  The JVM table
+// never shrinks; this restatement sizes it by the current entry count (parity unpinned where a table
+// once held more entries — no JVM here to run the reference).
+int32_t hmHash(int32_t h) { return h ^ ushr32(h, 16); }
+uint32_t hmCapacity(size_t n) {
+  uint32_t cap = 16;
+  while ((double)n > cap * 0.75) cap <<= 1;
+  return cap;
+}
+template <class T>
+void hmOrder(std::vector<T>& v, int32_t (*hashOf)(const T&), int64_t (*seqOf)(const T&)) {
+  const uint32_t mask = hmCapacity(v.size()) - 1;
+  std::sort(v.begin(), v.end(), [&](const T& a, const T& b) {
+    const uint32_t ia = (uint32_t)hmHash(hashOf(a)) & mask, ib = (uint32_t)hmHash(hashOf(b)) & mask;
+    return ia != ib ? ia < ib : seqOf(a) < seqOf(b);
+  });
+}
+int32_t timeWindowHashCode(const TimeWindow& w) {  // TimeWindow.hashCode :79-83
+  return jint_add(jint_mul(longHashCode(w.start), 31), longHashCode(w.end));
+}
+int32_t timerHashCode(const InternalTimer& t) {    // InternalTimer.hashCode :81-86
+  int32_t r = longHashCode(t.timestamp);
+  r = jint_add(jint_mul(r, 31), longHashCode(t.key));
+  return jint_add(jint_mul(r, 31), timeWindowHashCode(t.ns));
+}
+
+// the state tuple's fields (the ReduceFunction's value type) from / into the accumulator
+void writeField(const fw_config& c, JavaOut& o, int f, const Acc& a) {
+  const bool d = c.value_type == FW_VALUE_F64;
+  switch (f) {
+    case FW_SF_KEY: o.writeLong(a.key); break;
+    case FW_SF_F1: o.writeLong(a.f1); break;
+    case FW_SF_SUM: if (d) o.writeDouble(a.sum_d); else o.writeLong(a.sum_i); break;
+    case FW_SF_MIN: if (d) o.writeDouble(a.min_d); else o.writeLong(a.min_i); break;
+    case FW_SF_MAX: case FW_SF_VALUE: if (d) o.writeDouble(a.max_d); else o.writeLong(a.max_i); break;
+    case FW_SF_COUNT: o.writeLong(a.count); break;
+  }
+}
+void readField(const fw_config& c, JavaIn& in, int f, Acc& a) {
+  const int64_t x = in.readLong();
+  double d;
+  std::memcpy(&d, &x, 8);
+  switch (f) {
+    case FW_SF_KEY: a.key = x; break;
+    case FW_SF_F1: a.f1 = x; break;
+    case FW_SF_SUM: a.sum_i = x; a.sum_d = d; break;
+    case FW_SF_MIN: a.min_i = x; a.min_d = d; break;
+    case FW_SF_MAX: a.max_i = x; a.max_d = d; break;
+    case FW_SF_COUNT: a.count = x; break;
+    case FW_SF_VALUE: a.sum_i = a.min_i = a.max_i = x; a.sum_d = a.min_d = a.max_d = d; break;
+  }
+  (void)c;
+}
+
+struct NsRef { TimeWindow w; int64_t seq; const std::unordered_map<int64_t, Acc>* entries; };
+struct EntRef { int64_t key; const Acc* acc; };
+struct TimerRef { InternalTimer t; int64_t seq; };
+int32_t nsHash(const NsRef& r) { return timeWindowHashCode(r.w); }
+int64_t nsSeqOf(const NsRef& r) { return r.seq; }
+int32_t entHash(const EntRef& r) { return longHashCode(r.key); }
+int64_t entSeqOf(const EntRef& r) { return r.acc->seq; }
+int32_t tmHash(const TimerRef& r) { return timerHashCode(r.t); }
+int64_t tmSeqOf(const TimerRef& r) { return r.seq; }
+
+// HeapKeyedStateBackend.snapshot's key-group section (:196-212) + writeStateTableForKeyGroup (:217-248), and
+// HeapInternalTimerService.snapshotTimersForKeyGroup (:285-310) after its serializer records
+void snapshotKeyGroup(const Operator& op, int32_t kg, const fw_state_layout& L, JavaOut& st, JavaOut& tm) {
+  const size_t kgi = (size_t)(kg - op.cfg.kg_start);
+  if (op.anyState) {
+    st.writeInt(kg);
+    st.writeShort(0);   // kVStateToId of "window-contents", the only state table
+    if (!op.kgCreated[kgi]) {
+      st.writeByte(0);
+    } else {
+      st.writeByte(1);
+      const auto& nsMap = op.state[kgi];
+      std::vector<NsRef> ns;
+      for (const auto& kv : nsMap) ns.push_back({kv.first, op.nsSeq[kgi].at(kv.first), &kv.second});
+      hmOrder(ns, nsHash, nsSeqOf);
+      st.writeInt((int32_t)ns.size());
+      for (const NsRef& n : ns) {
+        st.writeLong(n.w.start);   // TimeWindow.Serializer.serialize :141-144
+        st.writeLong(n.w.end);
+        std::vector<EntRef> ent;
+        for (const auto& kv : *n.entries) ent.push_back({kv.first, &kv.second});
+        hmOrder(ent, entHash, entSeqOf);
+        st.writeInt((int32_t)ent.size());
+        for (const EntRef& x : ent) {
+          st.writeLong(x.key);     // LongSerializer (Tuple1<Long>: TupleSerializer over it, the same 8 bytes)
+          for (int f = 0; f < L.n_fields; ++f) writeField(op.cfg, st, L.field[f], *x.acc);
+        }
+      }
+    }
+  }
+  std::vector<TimerRef> ts;
+  for (const auto& kv : op.timerSeq)
+    if (computeKeyGroupForKeyHash(op.keyHashOf(kv.first.key), op.cfg.max_parallelism) == kg) ts.push_back({kv.first, kv.second});
+  hmOrder(ts, tmHash, tmSeqOf);
+  tm.writeInt((int32_t)ts.size());
+  for (const TimerRef& t : ts) {   // TimerSerializer.serialize: key, namespace, timestamp
+    tm.writeLong(t.t.key);
+    tm.writeLong(t.t.ns.start);
+    tm.writeLong(t.t.ns.end);
+    tm.writeLong(t.t.timestamp);
+  }
+  tm.writeInt(0);   // processing-time timers
+}
+
+// readStateTableForKeyGroup (:318-349) + restoreTimersForKeyGroup (:319-345); the timer service restarts at
+// `wm` (the reference: Long.MIN_VALUE, its initial currentWatermark)
+int restoreKeyGroup(Operator& op, int32_t kg, const fw_state_layout& L, int64_t wm, const uint8_t* st, int64_t sn,
+                    const uint8_t* tb, int64_t tn) {
+  if (kg < op.cfg.kg_start || kg > op.cfg.kg_end) {
+    op.err = "Key Group " + std::to_string(kg) + " does not belong to the local range.";
+    return FW_ERR_INVALID_ARG;
+  }
+  const size_t kgi = (size_t)(kg - op.cfg.kg_start);
+  if (sn > 0) {
+    JavaIn in{st, sn};
+    const int32_t written = in.readInt();
+    const int stateId = in.readShort();
+    const int present = in.readByte();
+    if (written != kg || stateId != 0) { op.err = "bad key-group section"; return FW_ERR_INVALID_ARG; }
+    if (present) {
+      op.kgCreated[kgi] = 1;
+      op.anyState = true;
+      auto& nsMap = op.state[kgi];
+      const int32_t numNamespaces = in.readInt();
+      for (int32_t k = 0; k < numNamespaces && !in.eof; ++k) {
+        TimeWindow w;
+        w.start = in.readLong();
+        w.end = in.readLong();
+        auto& entries = nsMap[w];
+        op.nsSeq[kgi][w] = ++op.seqCounter;
+        const int32_t numEntries = in.readInt();
+        for (int32_t l = 0; l < numEntries && !in.eof; ++l) {
+          Acc a{};
+          a.key = in.readLong();
+          const int64_t mapKey = a.key;
+          for (int f = 0; f < L.n_fields; ++f) readField(op.cfg, in, L.field[f], a);
+          a.seq = ++op.seqCounter;
+          entries[mapKey] = a;
+        }
+      }
+    }
+    if (in.eof || in.pos != sn) { op.err = "state section truncated or with trailing bytes"; return FW_ERR_INVALID_ARG; }
+  }
+  JavaIn in{tb, tn};
+  const int32_t n = in.readInt();
+  for (int32_t i = 0; i < n && !in.eof; ++i) {
+    InternalTimer t;
+    t.key = in.readLong();
+    t.ns.start = in.readLong();
+    t.ns.end = in.readLong();
+    t.timestamp = in.readLong();
+    if (op.timers.insert(t).second) op.timerSeq[t] = ++op.seqCounter;
+  }
+  const int32_t np = in.readInt();
+  if (in.eof || in.pos != tn || np != 0) { op.err = "bad timer section"; return FW_ERR_INVALID_ARG; }
+  op.currentWatermark = wm;
+  return FW_OK;
+}
 
 }  // namespace
 
@@ -459,6 +695,28 @@ int fwo_get_stats(fw_engine* e, fw_stats* st) {
   st->keys_resident = (int64_t)keys;
   st->ingest_form = 0;
   return FW_OK;
+}
+
+int fwo_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, void* state, int64_t state_cap,
+                          int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
+  if (!e || !layout || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
+  if (kg < e->op.cfg.kg_start || kg > e->op.cfg.kg_end) return FW_ERR_INVALID_ARG;
+  JavaOut st, tm;
+  snapshotKeyGroup(e->op, kg, *layout, st, tm);
+  *state_len = (int64_t)st.b.size();
+  *timers_len = (int64_t)tm.b.size();
+  if (!state && !timers) return FW_OK;
+  if (!state || !timers || state_cap < *state_len || timers_cap < *timers_len) return FW_ERR_CAPACITY;
+  if (!st.b.empty()) std::memcpy(state, st.b.data(), st.b.size());
+  std::memcpy(timers, tm.b.data(), tm.b.size());
+  return FW_OK;
+}
+
+int fwo_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark, const void* state,
+                         int64_t state_len, const void* timers, int64_t timers_len) {
+  if (!e || !layout || !timers) return FW_ERR_INVALID_ARG;
+  return restoreKeyGroup(e->op, kg, *layout, watermark, (const uint8_t*)state, state_len, (const uint8_t*)timers,
+                         timers_len);
 }
 
 const char* fwo_last_error(const fw_engine* e) { return e ? e->op.err.c_str() : "null engine"; }

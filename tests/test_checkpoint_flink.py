@@ -1,0 +1,308 @@
+"""Checkpoint sections in the reference's own key-group byte layout (fw_snapshot_kg_flink /
+fw_restore_kg_flink):
+
+  state   HeapKeyedStateBackend.snapshot's section at KeyGroupRangeOffsets[kg] + writeStateTableForKeyGroup
+          (RT/state/heap/HeapKeyedStateBackend.java:196-248)
+  timers  HeapInternalTimerService.snapshotTimersForKeyGroup after its serializer records (:285-310)
+
+tests/golden/checkpoint_flink.json holds, per scenario, a seeded stream, the checkpoint position and the
+expected bytes of every key group, encoded by tests/golden/make_checkpoint_fixture.py — a plain-Python
+model of the heap backend written from the layout's definition, independent of the oracle and of the
+engine.  Parity is pinned by that hand-built fixture (no JVM here to run the reference).
+
+CPU: the oracle's restatement reproduces the fixture bytes, and restoring them reproduces them again.
+GPU: the HIP engine writes the same bytes; a restore of the fixture into the engine continues exactly as
+the oracle restored from the same bytes; engine and oracle agree byte for byte on larger streams.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from harness import epochs_of
+
+FIX = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "checkpoint_flink.json")))
+SCEN = {s["name"]: s for s in FIX["scenarios"]}
+LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
+
+
+def _cfg(sc, kg=None, mode=0):
+    from flink_amd.windowing import ReduceFunction, SlidingEventTimeWindows, TumblingEventTimeWindows, make_config
+    c = sc["config"]
+    if c["assigner"] == "tumbling":
+        assigner = TumblingEventTimeWindows.of(c["size"], c["offset"])
+    else:
+        assigner = SlidingEventTimeWindows.of(c["size"], c["slide"], c["offset"])
+    kw = dict(max_parallelism=c["mp"], key_capacity=1 << 10, max_batch=1 << 12, out_capacity=1 << 16)
+    if kg is not None:
+        kw["key_group_range"] = kg
+    if mode:
+        kw["ingest_mode"] = mode
+    return make_config(assigner, ReduceFunction(tuple(c["aggs"]), c["value_type"], True), None, c["lateness"], **kw)
+
+
+def _columns(sc, lo, hi):
+    r = np.array(sc["records"][lo:hi], dtype=np.int64).reshape(-1, 4)
+    vals = r[:, 3].copy()
+    if sc["config"]["value_type"] == "f64":
+        vals = vals.view(np.float64)
+    return r[:, 0].copy(), r[:, 1].copy(), r[:, 2].copy(), vals
+
+
+def _drive(eng, sc, lo, hi, final=False):
+    """Push records [lo, hi) and the watermarks between them, in order; collect after each watermark."""
+    out, pos = [], lo
+    marks = [(i, w) for i, w in sc["watermarks"] if lo < i <= hi]
+    if final:
+        marks.append((hi, LONG_MAX))
+    for i, wm in marks:
+        if i > pos:
+            k, f1, ts, v = _columns(sc, pos, i)
+            eng.push(k, ts, v, f1=f1)
+            pos = i
+        eng.advance_watermark(wm)
+        out.append(eng.collect())
+    if pos < hi:
+        k, f1, ts, v = _columns(sc, pos, hi)
+        eng.push(k, ts, v, f1=f1)
+        out.append(eng.collect())
+    return out
+
+
+def _expected(sc):
+    return {int(kg): (bytes.fromhex(s), bytes.fromhex(t)) for kg, (s, t) in sc["kgs"].items()}
+
+
+def _snapshot_all(eng, sc):
+    return {kg: eng.snapshot_kg_flink(kg, sc["layout"]) for kg in range(sc["config"]["mp"])}
+
+
+def _restore_wm(sc):
+    return sc["checkpoint_wm"] if sc["restore_wm"] == "checkpoint" else LONG_MIN
+
+
+def _diff(got, want):
+    for kg in sorted(want):
+        for part, g, w in (("state", got[kg][0], want[kg][0]), ("timers", got[kg][1], want[kg][1])):
+            if g != w:
+                at = next((i for i in range(min(len(g), len(w))) if g[i] != w[i]), min(len(g), len(w)))
+                return f"kg {kg} {part}: {len(g)} vs {len(w)} bytes, first difference at byte {at}"
+    return None
+
+
+@pytest.mark.parametrize("name", list(SCEN))
+def test_fixture_is_well_formed(name):
+    """Every present key group's state section parses to the layout; timers section length matches."""
+    sc = SCEN[name]
+    nf = len(sc["layout"])
+    for kg, (st, tm) in _expected(sc).items():
+        k, sid, present = struct.unpack(">ihb", st[:7])
+        assert (k, sid) == (kg, 0)
+        pos = 7
+        if present:
+            (nns,) = struct.unpack(">i", st[pos:pos + 4])
+            pos += 4
+            for _ in range(nns):
+                start, end, n = struct.unpack(">qqi", st[pos:pos + 20])
+                assert end - start == sc["config"]["size"]
+                pos += 20 + n * 8 * (1 + nf)
+        assert pos == len(st)
+        (nt,) = struct.unpack(">i", tm[:4])
+        assert len(tm) == 8 + 32 * nt
+
+
+@pytest.mark.parametrize("name", list(SCEN))
+def test_oracle_writes_fixture_bytes(name):
+    from oracle.oracle import OracleEngine
+    sc = SCEN[name]
+    eo = OracleEngine(_cfg(sc))
+    _drive(eo, sc, 0, sc["cut"])
+    got = _snapshot_all(eo, sc)
+    eo.close()
+    assert _diff(got, _expected(sc)) is None, _diff(got, _expected(sc))
+
+
+@pytest.mark.parametrize("name", list(SCEN))
+def test_oracle_restore_round_trip(name):
+    """readStateTableForKeyGroup / restoreTimersForKeyGroup put in blob order: a snapshot right after the
+    restore writes the same bytes."""
+    from oracle.oracle import OracleEngine
+    sc = SCEN[name]
+    want = _expected(sc)
+    eo = OracleEngine(_cfg(sc))
+    for kg, (st, tm) in want.items():
+        eo.restore_kg_flink(kg, sc["layout"], st, tm, _restore_wm(sc))
+    got = _snapshot_all(eo, sc)
+    eo.close()
+    assert _diff(got, want) is None, _diff(got, want)
+
+
+# ---------------------------------------------------------------------------------------------- GPU
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("name", list(SCEN))
+def test_engine_writes_fixture_bytes(name, mode):
+    from flink_amd.windowing import WindowEngine
+    sc = SCEN[name]
+    eg = WindowEngine(_cfg(sc, mode=mode))
+    _drive(eg, sc, 0, sc["cut"])
+    got = _snapshot_all(eg, sc)
+    eg.close()
+    assert _diff(got, _expected(sc)) is None, _diff(got, _expected(sc))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("name", [n for n, s in SCEN.items() if s["restore_wm"] is not None])
+def test_engine_restore_continues_like_oracle(name, mode):
+    """Restore the fixture's key groups (into two subtasks, each its KeyGroupRangeAssignment share), run the
+    rest of the stream and a final MAX_WATERMARK: the same output as the oracle restored from the same
+    bytes at the same watermark; a snapshot right after the restore writes the fixture bytes back."""
+    from flink_amd.keygroups import compute_key_group_range_for_operator_index, operator_index_np
+    from flink_amd.windowing import WindowEngine
+    from oracle.oracle import OracleEngine
+    sc = SCEN[name]
+    mp, want, wm = sc["config"]["mp"], _expected(sc), _restore_wm(sc)
+    eo = OracleEngine(_cfg(sc))
+    for kg, (st, tm) in want.items():
+        eo.restore_kg_flink(kg, sc["layout"], st, tm, wm)
+    ro = _drive(eo, sc, sc["cut"], len(sc["records"]), final=True)
+    eo.close()
+    fields = [f"{a}_{sc['config']['value_type']}" if a != "count" else "count" for a in sc["config"]["aggs"]]
+    engines = []
+    for i in range(2):
+        lo, hi = compute_key_group_range_for_operator_index(mp, 2, i)
+        e = WindowEngine(_cfg(sc, kg=(lo, hi), mode=mode))
+        for kg in range(lo, hi + 1):
+            e.restore_kg_flink(kg, sc["layout"], *want[kg], watermark=wm)
+        back = {kg: e.snapshot_kg_flink(kg, sc["layout"]) for kg in range(lo, hi + 1)}
+        assert _diff(back, {kg: want[kg] for kg in range(lo, hi + 1)}) is None
+        engines.append((e, i))
+    # split the rest of the stream by operator index, as keyBy would
+    k_all = np.array([r[0] for r in sc["records"]], np.int64)
+    dest = operator_index_np(k_all, mp, 2)
+    per = []
+    for e, i in engines:
+        sub = dict(sc)
+        sub["records"] = [r if d == i else None for r, d in zip(sc["records"], dest)]
+        per.append(_drive_sparse(e, sub, sc["cut"], len(sc["records"])))
+        e.close()
+    got = _merge([epochs_of(r, fields, True) for r in per])
+    exp = _canon(epochs_of(ro, fields, True))
+    assert got == exp
+
+
+def _drive_sparse(eng, sc, lo, hi):
+    """_drive over a record list in which other subtasks' records are None."""
+    out, pos = [], lo
+    marks = [(i, w) for i, w in sc["watermarks"] if lo < i <= hi] + [(hi, LONG_MAX)]
+
+    def push(a, b):
+        rows = [r for r in sc["records"][a:b] if r is not None]
+        if rows:
+            r = np.array(rows, dtype=np.int64)
+            v = r[:, 3].copy()
+            if sc["config"]["value_type"] == "f64":
+                v = v.view(np.float64)
+            eng.push(r[:, 0].copy(), r[:, 2].copy(), v, f1=r[:, 1].copy())
+    for i, wm in marks:
+        push(pos, i)
+        pos = i
+        eng.advance_watermark(wm)
+        out.append(eng.collect())
+    return out
+
+
+def _canon(ep):
+    """Epochs with doubles as their doubleToLongBits (NaN, -0.0 compare exactly), records sorted."""
+    def tok(x):
+        if isinstance(x, float):
+            return ("d", b"nan" if x != x else struct.pack(">d", x))
+        return x
+    return [(w, sorted((tuple(tok(x) for x in r) for r in recs), key=repr)) for w, recs in ep]
+
+
+def _merge(per_engine):
+    per_engine = [_canon(p) for p in per_engine]
+    merged = per_engine[0]
+    for other in per_engine[1:]:
+        assert [w for w, _ in merged] == [w for w, _ in other]
+        merged = [(w, sorted(a + b, key=repr)) for (w, a), (_, b) in zip(merged, other)]
+    return merged
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", ["tumbling_lateness", "sliding", "tumbling_purging"])
+def test_engine_matches_oracle_bytes_random(window):
+    """Zipf keys, out-of-order timestamps, 128 key groups: every key group's sections byte-identical."""
+    from flink_amd.windowing import (ReduceFunction, SlidingEventTimeWindows, TumblingEventTimeWindows,
+                                     WindowEngine, make_config)
+    from harness import drive, gen_stream
+    from oracle.oracle import OracleEngine
+    keys, ts, vals = gen_stream(60_000, 3000, rate=1 << 14, zipf=1.1, ooo=300)
+    kw = dict(max_parallelism=128, key_capacity=1 << 13, max_batch=1 << 14, out_capacity=1 << 20)
+    if window == "sliding":
+        cfg = make_config(SlidingEventTimeWindows.of(3000, 1000), ReduceFunction(("sum", "count"), "i64", True),
+                          None, 0, **kw)
+        layout = ("key", "f1", "sum", "count")
+    elif window == "tumbling_purging":
+        from flink_amd.windowing import EventTimeTrigger, PurgingTrigger
+        cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "max"), "i64", True),
+                          PurgingTrigger.of(EventTimeTrigger.create()), 0, **kw)
+        layout = ("f1", "key", "max", "sum")
+    else:
+        cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "min", "count"), "i64", True),
+                          None, 400, **kw)
+        layout = ("key", "f1", "sum", "min", "count")
+    f1 = np.arange(len(keys), dtype=np.int64) * 3 + 1
+    n = len(keys) * 2 // 3
+    res = []
+    for factory in (WindowEngine, OracleEngine):
+        e = factory(cfg)
+        drive(e, keys[:n], ts[:n], vals[:n], 4096, 120, None, f1=f1[:n])
+        res.append({kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)})
+        e.close()
+    assert sum(len(s) for s, _ in res[1].values()) > 128 * 8
+    assert _diff(res[0], res[1]) is None, _diff(res[0], res[1])
+
+
+@pytest.mark.gpu
+def test_restore_rejections():
+    from flink_amd import _abi
+    from flink_amd.windowing import WindowEngine
+    sc = SCEN["tumbling_lateness_i64"]
+    want = _expected(sc)
+    kg = max(want, key=lambda k: len(want[k][0]))
+    st, tm = want[kg]
+    e = WindowEngine(_cfg(sc))
+    # fired-but-kept panes have no trigger timer: not what the panes imply at Long.MIN_VALUE
+    with pytest.raises(_abi.FwError) as ei:
+        e.restore_kg_flink(kg, sc["layout"], st, tm)
+    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+    with pytest.raises(_abi.FwError) as ei:
+        e.restore_kg_flink(kg, sc["layout"], st[:-3], tm, sc["checkpoint_wm"])
+    assert ei.value.code == _abi.FW_ERR_INVALID_ARG
+    with pytest.raises(_abi.FwError) as ei:
+        e.restore_kg_flink(kg, ("key", "sum"), st, tm, sc["checkpoint_wm"])    # f1 is tracked: layout must name it
+    assert ei.value.code == _abi.FW_ERR_INVALID_ARG
+    with pytest.raises(_abi.FwError) as ei:
+        e.restore_kg_flink((kg + 1) % 8, sc["layout"], st, tm, sc["checkpoint_wm"])   # another key group's section
+    assert ei.value.code == _abi.FW_ERR_INVALID_ARG
+    e.restore_kg_flink(kg, sc["layout"], st, tm, sc["checkpoint_wm"])
+    with pytest.raises(_abi.FwError):
+        e.restore_kg_flink((kg + 1) % 8, sc["layout"], *want[(kg + 1) % 8], sc["checkpoint_wm"] + 1)
+    e.close()
+    sl = SCEN["sliding_i64"]
+    e = WindowEngine(_cfg(sl))
+    with pytest.raises(_abi.FwError) as ei:
+        e.restore_kg_flink(0, sl["layout"], *_expected(sl)[0])
+    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+    e.close()
+    # no record accepted yet: no keyed state at all (HeapKeyedStateBackend.snapshot writes no stream)
+    e = WindowEngine(_cfg(sc))
+    st0, tm0 = e.snapshot_kg_flink(0, sc["layout"])
+    assert st0 == b"" and tm0 == bytes(8)
+    e.close()

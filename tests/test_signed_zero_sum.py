@@ -1,0 +1,93 @@
+"""Double sums keep the sign of zero as the reference does: a pane's state starts as its first value
+(HeapReducingState.add stores value2 as is when the key has no state, HeapReducingState.java:103-116) and
+then adds (SumFunction.DoubleSum, SumFunction.java:68-77), so a pane of only -0.0 sums to -0.0 and any
++0.0 makes it +0.0.  The engine's accumulators start from -0.0, the identity of IEEE addition.
+
+Known answers worked by hand; the oracle is checked on CPU, the HIP engine on the GPU (both ingest forms,
+tumbling / sliding / per-element late fires).
+"""
+import math
+import struct
+
+import numpy as np
+import pytest
+
+LONG_MAX = (1 << 63) - 1
+
+# key -> values (all in one window); expected sum bits
+CASES = {1: ([-0.0], -0.0), 2: ([-0.0, -0.0, -0.0], -0.0), 3: ([-0.0, 0.0], 0.0), 4: ([0.0, -0.0], 0.0),
+         5: ([1.5, -1.5], 0.0), 6: ([-1.5, 1.5, -0.0], 0.0)}
+
+
+def _stream():
+    keys, vals = [], []
+    for k, (vs, _) in CASES.items():
+        keys += [k] * len(vs)
+        vals += vs
+    n = len(keys)
+    return np.array(keys, np.int64), np.arange(n, dtype=np.int64) * 10 + 100, np.array(vals, np.float64)
+
+
+def _bits(x):
+    return struct.pack(">d", x)
+
+
+def _cfg(window, mode):
+    from flink_amd.windowing import ReduceFunction, SlidingEventTimeWindows, TumblingEventTimeWindows, make_config
+    assigner = SlidingEventTimeWindows.of(2000, 1000) if window == "sliding" else TumblingEventTimeWindows.of(1000)
+    kw = dict(key_capacity=1 << 10, max_batch=1 << 10, out_capacity=1 << 12)
+    if mode:
+        kw["ingest_mode"] = mode
+    return make_config(assigner, ReduceFunction(("sum",), "f64", True), None, 5000 if window == "late" else 0, **kw)
+
+
+def _run(factory, window, mode):
+    keys, ts, vals = _stream()
+    e = factory(_cfg(window, mode))
+    if window == "late":
+        # the window fires empty of these keys first (a bootstrap record of another key), then each record
+        # arrives late within the allowed lateness: one per-element fire per record
+        e.push(np.array([99], np.int64), np.array([0], np.int64), np.array([1.0]))
+        e.advance_watermark(1500)
+        e.collect()
+    e.push(keys, ts, vals)
+    e.advance_watermark(LONG_MAX)
+    r = e.collect()
+    e.close()
+    got = {}
+    for k, s in zip(r["key"], r["sum_f64"]):
+        if int(k) != 99:
+            got.setdefault(int(k), []).append(_bits(float(s)))
+    return got
+
+
+def _check(got, window):
+    for k, (vs, want) in CASES.items():
+        if window == "late":
+            # one per-element fire per record: the pane's contents after it, starting from the first value
+            acc, exp = None, []
+            for v in vs:
+                acc = v if acc is None else acc + v
+                exp.append(_bits(acc))
+            assert sorted(got[k]) == sorted(exp), (k, got[k])
+            assert exp[-1] == _bits(want)
+        else:
+            assert set(got[k]) == {_bits(want)}, (k, window, got[k])
+
+
+@pytest.mark.parametrize("window", ["tumbling", "sliding", "late"])
+def test_signed_zero_sums_oracle(window):
+    from oracle.oracle import OracleEngine
+    _check(_run(OracleEngine, window, 0), window)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("window", ["tumbling", "sliding", "late"])
+def test_signed_zero_sums_hip(window, mode):
+    from flink_amd.windowing import WindowEngine
+    _check(_run(WindowEngine, window, mode), window)
+
+
+def test_cases_are_signed():
+    assert math.copysign(1.0, CASES[1][1]) < 0 and math.copysign(1.0, CASES[3][1]) > 0

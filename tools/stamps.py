@@ -5,8 +5,9 @@ import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flink_amd.synth import stream
 from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, WindowEngine, make_config
-cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", True), key_capacity=1 << 16,
-                  max_batch=1 << 22, out_capacity=1 << 21, ingest_mode=2)
+C4 = os.environ.get("STAMP_CFG") == "c4"   # Zipf(1.2) keys, 300 ms out of order, lag 50, lateness 100 (bench c4)
+cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "count") if C4 else ("sum",), "i64", True),
+                  None, 100 if C4 else 0, key_capacity=1 << 16, max_batch=1 << 22, out_capacity=1 << 22, ingest_mode=2)
 e = WindowEngine(cfg)
 B = 1 << 22
 buf = np.zeros(16 << 16, dtype=np.int64)
@@ -27,7 +28,8 @@ def phases(a, nblk, npts):
             print("      main by blockIdx//32:", [round(m[i*32:(i+1)*32].mean()) for i in range(8)])
     return (a[:, 0] - t0).mean() * 10, d.mean(axis=0), (a[:, npts - 1].max() - t0) * 10
 for j in range(6):
-    k, t, v = stream(j * B, B, 1 << 16, 1 << 24, 1_700_000_000_000, device="cuda")
+    k, t, v = stream(j * B, B, 1 << 16, 1 << 25 if C4 else 1 << 24, 1_700_000_000_000, device="cuda",
+                     zipf=1.2 if C4 else None, ooo=300 if C4 else 0)
     torch.cuda.synchronize()
     e.push(k, t, v)
     e.sync()
@@ -36,5 +38,5 @@ for j in range(6):
     print(f"batch {j} route: start-skew {sk:.0f} ns, load {d[0]:.0f} phaseB {d[1]:.0f} scan {d[2]:.0f} write {d[3]:.0f} | span {span:.0f} ns")
     sk, d, span = phases(buf[8 << 16:], 256, 5)
     print(f"        aggregate: start-skew {sk:.0f} ns, ldir {d[0]:.0f} segtab {d[1]:.0f} main {d[2]:.0f} fold {d[3]:.0f} | span {span:.0f} ns")
-    e.advance_watermark(int(t[-1].item()) - 1)
+    e.advance_watermark(int(t.max().item()) - (50 if C4 else 1))
     e.collect()
