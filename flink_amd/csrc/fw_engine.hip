@@ -39,6 +39,19 @@
 #include "java_semantics.h"
 #include "flink_kg_format.h"
 
+#ifndef FW_NO_HOSTLOAD
+#define FW_NO_HOSTLOAD 0
+#endif
+#ifndef FW_NO_GSLSORT
+#define FW_NO_GSLSORT 0
+#endif
+#ifndef FW_AGG_PRECHECK
+#define FW_AGG_PRECHECK 0
+#endif
+#ifndef FW_AGG_UR
+#define FW_AGG_UR 2   // k_aggregate: wave steps whose loads are in flight together (two sets: 2 x UR)
+#endif
+
 namespace fw {
 
 constexpr int64_t FREE_TAG = INT64_MIN;
@@ -46,7 +59,7 @@ constexpr int64_t EMPTY_KEY = INT64_MIN;
 constexpr int MAX_K = 64;          // max slices per window
 constexpr int BLOCK = 256;
 
-enum Stat { ST_LATE = 0, ST_FIRED = 1, ST_LATE_FIRES = 2, ST_NSTATS = 8 };
+enum Stat { ST_LATE = 0, ST_FIRED = 1, ST_LATE_FIRES = 2, ST_SHARES = 3, ST_NSTATS = 8 };   // ST_SHARES: helper shares run
 
 // ------------------------------------------------------------------------------------------------
 // device views
@@ -532,6 +545,8 @@ constexpr int AG_THREADS = 1024;
 constexpr int AG_WIN = 8;               // k_aggregate: directory slots probed without a branch
 constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
 constexpr int AG_MAXPER = 17;           // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
+constexpr int AG_SPLIT_MAX = 16;        // k_aggregate: shares a hot bucket is split into, at most
+constexpr uint32_t AG_SPLIT_MIN = 16384; // ... and routed records per share, at least
 constexpr int RT_MAX_KB_BITS = 12;      // directory slots per bucket that k_aggregate holds in LDS
 constexpr int IDX_BITS = FW_RT_TILE_LOG; // record index within a tile
 constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
@@ -541,6 +556,16 @@ struct RouteBuf {
   uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
   uint16_t* seg;         // [ntiles][RT_GROUPS * nb + 1] start of each bin's segment in the tile; [last] = count
   int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
+  // hot buckets split over helper workgroups (k_aggregate): per-bucket routed records of the previous /
+  // this / a retired batch (ring), the serialised-fold flags, the helpers launched, the batch tag
+  unsigned int* bload_prev;
+  unsigned int* bload_cur;
+  unsigned int* bload_zero;
+  unsigned int* fold_flag;        // [RT_MAXNB][RT_GS] (tag << 5) | shares folded
+  unsigned int* bload_host;       // host-mapped [RT_MAXNB]: each owner's estimate of its bucket's routed records
+  int32_t helpers;
+  uint32_t tag;
+  int64_t* dm;           // [tiles x RT_TILE] slice number of each direct-group record (at its routed position)
   unsigned int* dflag;   // set by a tile with direct-group records (a ring of FLAG_RING words, one per batch)
   unsigned int* dflag_reset;   // the word of batch j + FLAG_RING/2: zeroed by k_aggregate of batch j
   long long* stamps;     // diagnostics (FW_DEBUG_AGG & 16): per-workgroup phase timestamps, 8 per workgroup
@@ -774,6 +799,8 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   const bool wave_uniform = __all(same);
   int32_t bin[PER];       // routed bin, or -1
   int32_t rank[PER];
+  // (tt[k] keeps the slice number of a direct record for the store below: k_aggregate reads it from
+  // r.dm instead of re-running the window assignment)
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     bin[k] = -1;
@@ -813,6 +840,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     if (bin[k] >= 0) {
       const int32_t pos = cnt[bin[k]] + rank[k];
       st_kv[pos] = make_longlong2(kk[k], vv[k]);
+      if ((direct_mask >> k) & 1u) r.dm[base + pos] = tt[k];
       st_idx[pos] = (uint16_t)(2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1));
     }
   }
@@ -895,10 +923,19 @@ __device__ __forceinline__ void acc_add(const AggLds& L, bool cmpto, bool by_las
     if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&L.sum[kl], (unsigned long long)v);
     else unsafeAtomicAdd((double*)&L.sum[kl], __longlong_as_double(v));
   }
+#if FW_AGG_PRECHECK
+  // min / max / first only ever decrease (increase): a plain LDS read that already beats this record
+  // proves it changes nothing, and the atomic is skipped
+  if (AGG & FW_AGG_MIN) { const int64_t c = min_code(VT, cmpto, v); if (c < L.mn[kl]) atomicMin((long long*)&L.mn[kl], (long long)c); }
+  if (AGG & FW_AGG_MAX) { const int64_t c = max_code(VT, cmpto, v); if (c > L.mx[kl]) atomicMax((long long*)&L.mx[kl], (long long)c); }
+  if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&L.cnt[kl], 1ull);
+  if (oi < L.first[kl]) atomicMin(&L.first[kl], oi);   // earliest record of the batch: first arrival + "touched"
+#else
   if (AGG & FW_AGG_MIN) atomicMin((long long*)&L.mn[kl], (long long)min_code(VT, cmpto, v));
   if (AGG & FW_AGG_MAX) atomicMax((long long*)&L.mx[kl], (long long)max_code(VT, cmpto, v));
   if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&L.cnt[kl], 1ull);
   atomicMin(&L.first[kl], oi);   // earliest record of the batch: the first arrival, and the "touched" mark
+#endif
 }
 
 // Hot keys (Zipf): when 8 or more lanes of a wave carry the slot of the wave's first active lane, they are
@@ -949,18 +986,22 @@ __host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_
   return (size_t)8 * ((size_t)1 << kb_bits) + ((size_t)(1 << kb_bits) + 65) * (8 * nacc + (by ? 4 : 0)) +
          ((((size_t)(1 << kb_bits) + 65) + 3) & ~(size_t)3) * 4 + (size_t)(8 * RT_Q + 4 * RT_GROUPS) * ntiles +
          8 * (size_t)ntiles + 4 +
-         4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8;
+         4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8 + 4 * (size_t)(RT_MAXNB + 4);
 }
 
-template <int VT, int AGG, bool FIRST>
+// SKEW: the variant for skewed key distributions (the host launches it when the posted bucket loads ask
+// for helpers): hot buckets split over helper workgroups, and the in-wave hot-key combine.  The uniform
+// variant carries neither (registers: the 1024-thread workgroup has 128 VGPRs per lane)
+template <int VT, int AGG, bool FIRST, bool SKEW>
 __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, RouteBuf r, const int64_t* f1col) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = AG_THREADS;
   // XCD-aware bucket order: workgroups are dealt to the 8 XCDs round-robin, so XCD x runs the
   // contiguous bucket range [x * nb/8, (x + 1) * nb/8).  Neighbouring buckets' segments share the
   // 128-B lines at their boundaries; with both readers on one XCD the second read hits that XCD's L2
-  const int bkt = (s.nb % 8 == 0 && !(r.dbg & 32)) ? (int)(blockIdx.x % 8) * (s.nb / 8) + (int)(blockIdx.x / 8)
-                                                    : (int)blockIdx.x;
+  const int owner_bkt = blockIdx.x >= (unsigned)s.nb ? -1
+                        : (s.nb % 8 == 0 && !(r.dbg & 32)) ? (int)(blockIdx.x % 8) * (s.nb / 8) + (int)(blockIdx.x / 8)
+                                                          : (int)blockIdx.x;
   const int nbq = RT_GROUPS * s.nb;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
@@ -983,9 +1024,52 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   int32_t* awtot = step_tile + AG_CHS;                  // [16] scan scratch
   int64_t* gsl = (int64_t*)(((uintptr_t)(awtot + 16) + 7) & ~(uintptr_t)7);   // [RT_GS] the batch's slices
   int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
-  const int64_t dbase = (int64_t)bkt * KB;
+  int32_t* plan = (int32_t*)(gsl + RT_GS) + 2;          // [RT_MAXNB + 1] helper prefix; then bucket, share, shares
   const int64_t SB = (int64_t)8 << 16;
   FW_STAMP(r, SB, 0);
+  // Hot buckets (skewed keys) are split over helper workgroups launched after the nb owners: bucket b
+  // with L_b routed records last batch gets S_b = clamp(ceil(L_b / chunk), 1, AG_SPLIT_MAX) shares, share
+  // s taking tiles [s T / S_b, (s + 1) T / S_b) (tiles are in arrival order, so share order is arrival
+  // order).  Every workgroup derives the same plan from the same loads; helpers are assigned to shares in
+  // bucket order, so a share's predecessor always has the lower block index (dispatched earlier).  The
+  // shares of a bucket fold one after another (fold_flag), share 0 first: the fold stays a plain
+  // read-modify-write, first arrival included.
+  int bkt = owner_bkt, share = 0, nshare = 1;
+  if (SKEW && r.helpers > 0) {   // uniform
+    uint32_t tot = 0;
+    for (int x = threadIdx.x; x < s.nb; x += NT) tot += r.bload_prev[x];
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    if ((threadIdx.x & 63) == 0) awtot[threadIdx.x >> 6] = (int32_t)tot;
+    __syncthreads();
+    uint32_t all = 0;
+    for (int w = 0; w < NT / 64; ++w) all += (uint32_t)awtot[w];
+    // (FW_DEBUG_AGG & 64: a share of 256 records, so that tests split buckets at small sizes)
+    const uint32_t chunk = max((r.dbg & 64) ? 256u : AG_SPLIT_MIN, 2u * (all / (uint32_t)s.nb + 1u));
+    for (int x = threadIdx.x; x < s.nb; x += NT) {
+      const uint32_t sh = min((r.bload_prev[x] + chunk - 1) / chunk, (uint32_t)AG_SPLIT_MAX);
+      plan[x] = sh > 1 ? (int32_t)sh - 1 : 0;    // helpers bucket x asks for
+    }
+    if (threadIdx.x == 0) plan[s.nb] = 0;
+    __syncthreads();
+    block_scan_excl<NT, AG_MAXPER>(plan, s.nb + 1, awtot);   // plan[x] = first helper of bucket x; plan[nb] = total
+    const int32_t h = owner_bkt < 0 ? (int32_t)blockIdx.x - s.nb : -1;
+    if (threadIdx.x == 0) plan[RT_MAXNB + 1] = owner_bkt < 0 ? -1 : owner_bkt;
+    __syncthreads();
+    for (int x = threadIdx.x; x < s.nb; x += NT) {
+      const int32_t lo = plan[x], n = max(min(plan[x + 1], r.helpers) - lo, 0);   // helpers bucket x gets
+      if (h >= lo && h < lo + n) { plan[RT_MAXNB + 1] = x; plan[RT_MAXNB + 2] = h - lo + 1; plan[RT_MAXNB + 3] = 1 + n; }
+      if (x == owner_bkt) { plan[RT_MAXNB + 2] = 0; plan[RT_MAXNB + 3] = 1 + n; }
+    }
+    __syncthreads();
+    bkt = plan[RT_MAXNB + 1];
+    if (bkt < 0) return;   // uniform: a helper no bucket needs
+    share = plan[RT_MAXNB + 2];
+    nshare = plan[RT_MAXNB + 3];
+    __syncthreads();   // plan[] is reused below only after every thread has read it
+  }
+  const int t_lo = SKEW ? (int)((int64_t)share * r.ntiles / nshare) : 0;
+  const int t_hi = SKEW ? (int)((int64_t)(share + 1) * r.ntiles / nshare) : r.ntiles;
+  const int64_t dbase = (int64_t)bkt * KB;
   // does any tile hold direct-group records (the batch's flag; no: skip all direct work)
   const bool has_direct = __builtin_amdgcn_readfirstlane(*r.dflag) != 0;
   // every tile's header and this bucket's segment bounds in each of its bin groups, plus the bucket's
@@ -1049,16 +1133,13 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   if (blockIdx.x == 0 && threadIdx.x == 0) *r.dflag_reset = 0u;
   for (int t = threadIdx.x; has_direct && t < r.ntiles; t += NT) {
     const uint32_t sd = lseg[t * RT_GROUPS + RT_Q], sf = lseg[t * RT_GROUPS + RT_Q + 1];
-    for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) {
-      const int64_t i = (int64_t)t * RT_TILE + r.idx[(int64_t)t * RT_TILE + x];
-      gsl_insert(record_windows(s, b.ts[i], b.wm).m);
-    }
-    if (b.late_key == nullptr) continue;
+    for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) gsl_insert(r.dm[(int64_t)t * RT_TILE + x]);
+    if (b.late_key == nullptr || t < t_lo || t >= t_hi) continue;
     for (uint32_t x = sf & 0xFFFFu; x < (sf >> 16); ++x) {
       const int64_t pos = (int64_t)t * RT_TILE + x;
       const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
       const uint64_t h = (uint64_t)r.kv[pos].x;
-      const int64_t m = record_windows(s, b.ts[i], b.wm).m;
+      const int64_t m = r.dm[pos];
       const int32_t p = slice_slot(s, m);
       int64_t kid = s.D;
       if (h == EMPTY_H) (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
@@ -1081,6 +1162,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       const bool dup = lane != 0 && left == m;
       if (m != FREE_TAG && !dup) gsl_insert(m);
     }
+  }
+  __syncthreads();
+  if (SKEW && threadIdx.x == 0) {   // ascending: every share of a bucket takes the slices in the same rounds
+    for (int i = 1; i < RT_GS && gsl[i] != FREE_TAG; ++i)
+      for (int j = i; j > 0 && gsl[j - 1] > gsl[j]; --j) { const int64_t t = gsl[j]; gsl[j] = gsl[j - 1]; gsl[j - 1] = t; }
   }
   __syncthreads();
 
@@ -1120,6 +1206,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     return kl;
   };
 
+  int32_t routed = 0;   // this share's routed records (thread 0's copy is used)
   for (int g = 0; g < RT_GS; ++g) {
     const int64_t m = gsl[g];
     if (m == FREE_TAG) break;                            // uniform
@@ -1134,7 +1221,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       int32_t a0 = 0, a1 = 0;
 #pragma unroll
       for (int q = 0; q < RT_Q; ++q) {
-        if (lhdr[t * RT_Q + q] == m) {
+        if (lhdr[t * RT_Q + q] == m && t >= t_lo && t < t_hi) {
           const uint32_t sg = lseg[t * RT_GROUPS + q];
           a0 = (int32_t)(sg & 0xFFFFu);
           a1 = (int32_t)(sg >> 16);
@@ -1147,13 +1234,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     __syncthreads();
     block_scan_excl<NT, AG_MAXPER>(off, r.ntiles + 1, awtot);   // off[ntiles] = the bucket's records of slice m
     const int32_t R = off[r.ntiles];
+    routed += R;
     FW_STAMP(r, SB, 2 + 3 * min(g, 1));
     // dense assignment: the bucket's records of slice m, concatenated over the tiles in order (record
     // rr lies in the tile t with off[t] <= rr < off[t + 1]), are taken 64 at a time, one per lane, in
     // wave steps; the tile of each step's first record is tabulated per chunk of AG_CHS steps, a lane
     // walks forward from it (a step spans ~4 segments at 256 buckets), and every load of a wave's UR
     // steps is issued before any of them is processed
-    constexpr int UR = 2;
+    constexpr int UR = FW_AGG_UR;
     constexpr int NPASS = BY ? 2 : 1;
     for (int pass = 0; pass < NPASS; ++pass) {
     for (int32_t cb = 0; cb < R; cb += AG_CHS * 64) {   // uniform
@@ -1188,7 +1276,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         for (int u = 0; u < UR; ++u) {
           bool act = ra[u];
           uint32_t kl = probe(act, (uint64_t)rv[u].x);
-          if (!BY) act = hot_combine<VT, AGG>(L, cmpto, act, kl, rv[u].y, ri[u], lane);
+          if (SKEW && !BY) act = hot_combine<VT, AGG>(L, cmpto, act, kl, rv[u].y, ri[u], lane);
           kl = act ? kl : (uint32_t)KB + (uint32_t)lane;   // inactive lanes update a private dummy slot
           acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, rv[u].y, ri[u]);
         }
@@ -1214,12 +1302,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     }
     // this bucket's direct records of slice m (rare; one tile per thread): the same accumulators, their
     // batch index as the arrival order
-    for (int t = threadIdx.x; has_direct && t < r.ntiles; t += NT) {
+    for (int t = t_lo + (int)threadIdx.x; has_direct && t < t_hi; t += NT) {
       const uint32_t sd = lseg[t * RT_GROUPS + RT_Q];
       for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) {
         const int64_t pos = (int64_t)t * RT_TILE + x;
+        if (r.dm[pos] != m) continue;
         const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
-        if (record_windows(s, b.ts[i], b.wm).m != m) continue;
         const longlong2 rec = r.kv[pos];
         uint32_t kl = KMIN;
         if ((uint64_t)rec.x == EMPTY_H) {
@@ -1235,7 +1323,21 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     __syncthreads();
     }   // passes
     FW_STAMP(r, SB, 3 + 3 * min(g, 1));
-    // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes this batch
+    unsigned int* flag = r.fold_flag + (int64_t)bkt * RT_GS + g;
+    if (SKEW && share > 0) {   // uniform: wait for the previous share's fold of this slice
+      if (threadIdx.x == 0) {
+        const unsigned want = (r.tag << 5) | (unsigned)share;
+        int64_t spins = 0;
+        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
+          __builtin_amdgcn_s_sleep(8);
+          if (++spins > ((int64_t)1 << 21)) { cap_error(s, 14); break; }   // never hang: report and go on
+        }
+      }
+      __syncthreads();
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    }
+    // fold into the dense columns: this workgroup (this share, in share order) is the only writer of
+    // (p, bucket) panes while it folds
     for (int x = threadIdx.x; x <= KB; x += NT) {
       if (x == KB && bkt != 0) continue;
       const uint32_t xl = x < KB ? (uint32_t)x : KMIN;
@@ -1280,8 +1382,27 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       if (AGG & FW_AGG_COUNT) lcnt[xl] = 0;
       lfirst[xl] = NO_FIRST;
     }
+    if (SKEW && share + 1 < nshare) __threadfence();   // this share's fold visible before the next one's starts
     __syncthreads();
+    if (SKEW && share + 1 < nshare && threadIdx.x == 0)
+      __hip_atomic_store(flag, (r.tag << 5) | (unsigned)(share + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     FW_STAMP(r, SB, 4 + 3 * min(g, 1));
+  }
+  // this batch's routed records of the bucket (the next batch's split plan); the owner clears the ring
+  // entry of the batch after next
+  if (threadIdx.x == 0 && r.bload_cur) {
+    atomicAdd(&r.bload_cur[bkt], (unsigned)routed);
+    if (share == 0) {
+      r.bload_zero[bkt] = 0u;
+      // for the host's sizing of the next launches: the bucket's load, extrapolated from this share
+#if !FW_NO_HOSTLOAD
+      if (r.bload_host)
+        __hip_atomic_store(&r.bload_host[bkt], (unsigned)routed * (unsigned)nshare, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+    } else {
+      atomicAdd(&s.stats[ST_SHARES], 1ull);
+    }
   }
 }
 
@@ -1914,6 +2035,10 @@ struct fw_engine {
   RouteBuf rb{};                            // fields shared by both parities (dbg, stamps)
   RouteBuf rbs[2] = {};                     // routed-batch buffers, one set per batch parity
   unsigned int* dflags = nullptr;           // direct-record flags, a ring of FLAG_RING
+  unsigned int* bload = nullptr;            // [4][RT_MAXNB] routed records per bucket and batch (k_aggregate split plan)
+  unsigned int* fold_flag = nullptr;        // [RT_MAXNB][RT_GS]
+  unsigned int* bload_host = nullptr;       // host-mapped [RT_MAXNB], written by k_aggregate's owners
+  int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
   int64_t batches = 0;
   int32_t max_tiles = 0;
   size_t route_lds = 0, agg_lds = 0;
@@ -1945,6 +2070,7 @@ struct fw_engine {
     for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
+    if (bload_host) (void)hipHostFree(bload_host);
   }
 };
 
@@ -1975,13 +2101,36 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   static bool attr_set = false;
   if (!attr_set) {   // the largest any engine may ask for
     (void)hipFuncSetAttribute((const void*)k_route<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;   // both kernels use dynamic LDS only, so the whole 160 KiB is grantable
   }
   RouteBuf r = e->rbs[par];
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
   r.dflag = e->dflags + (e->batches % FLAG_RING);
   r.dflag_reset = e->dflags + ((e->batches + FLAG_RING / 2) % FLAG_RING);
+  // helpers for hot buckets: as many as the same plan asks for on the loads the owners posted (read
+  // without a sync: a batch or two stale at most; each launch's device plan caps itself at the helpers
+  // it got)
+  int wanted = 0;
+  if (e->bload_host && e->agg_helpers_max > 0) {
+    uint64_t all = 0;
+    for (int x = 0; x < e->s.nb; ++x) all += __atomic_load_n(&e->bload_host[x], __ATOMIC_RELAXED);
+    const uint32_t cmin = (e->rb.dbg & 64) ? 256u : AG_SPLIT_MIN;
+    const uint64_t chunk = std::max<uint64_t>(cmin, 2 * (all / (uint64_t)e->s.nb + 1));
+    for (int x = 0; x < e->s.nb; ++x) {
+      const uint64_t sh = std::min<uint64_t>((__atomic_load_n(&e->bload_host[x], __ATOMIC_RELAXED) + chunk - 1) / chunk,
+                                             AG_SPLIT_MAX);
+      wanted += sh > 1 ? (int)sh - 1 : 0;
+    }
+  }
+  r.helpers = std::min(e->agg_helpers_max, wanted);
+  r.bload_prev = e->bload + ((e->batches + 3) % 4) * RT_MAXNB;
+  r.bload_cur = e->bload + (e->batches % 4) * RT_MAXNB;
+  r.bload_zero = e->bload + ((e->batches + 2) % 4) * RT_MAXNB;
+  r.fold_flag = e->fold_flag;
+  r.bload_host = e->bload_host;
+  r.tag = (uint32_t)((e->batches + 1) & 0x7FFFFFF);
   // at least 81 KiB of LDS: one k_aggregate workgroup per CU (the dispatcher would otherwise pair two
   // of the nb = CU-count workgroups on one CU and leave another idle)
   const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, (size_t)e->agg_min_lds);
@@ -1992,8 +2141,12 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   (void)hipEventRecord(e->ev_route[par], rs);
   (void)hipStreamWaitEvent(e->stream, e->ev_route[par], 0);
   e->phase_begin(FW_PHASE_AGGREGATE);
-  hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b, r,
-                     f1col);
+  if (r.helpers > 0)
+    hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, true>), dim3(e->s.nb + r.helpers), dim3(AG_THREADS), agg_lds, e->stream,
+                       e->s, b, r, f1col);
+  else
+    hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b,
+                       r, f1col);
   e->phase_end(b.n);
   (void)hipEventRecord(e->ev_agg[par], e->stream);
 }
@@ -2187,6 +2340,12 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       e->rb.dbg = dbg ? atoi(dbg) : 0;
       e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
       e->dflags = e->alloc<unsigned int>(FLAG_RING);
+      e->bload = e->alloc<unsigned int>(4 * RT_MAXNB);
+      e->fold_flag = e->alloc<unsigned int>((size_t)RT_MAXNB * RT_GS);
+      if (hipHostMalloc((void**)&e->bload_host, 4 * RT_MAXNB, hipHostMallocMapped) != hipSuccess) e->bload_host = nullptr;
+      if (e->bload_host) memset(e->bload_host, 0, 4 * RT_MAXNB);
+      const char* hv = getenv("FW_AGG_HELPERS");
+      if (hv) e->agg_helpers_max = std::max(0, std::min(atoi(hv), (int)RT_MAXNB));
       for (int q = 0; q < 2; ++q) {
         RouteBuf& r = e->rbs[q];
         r = e->rb;
@@ -2194,6 +2353,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
         r.idx = e->alloc<uint16_t>(cap);
         r.seg = e->alloc<uint16_t>((size_t)(RT_GROUPS * s.nb + 1) * max_tiles);
         r.hdr = e->alloc<int64_t>((size_t)max_tiles * RT_Q);
+        r.dm = e->alloc<int64_t>(cap);
       }
       e->route_lds = RT_LDS;
       const char* ml = getenv("FW_AGG_MIN_LDS_KB");
@@ -2260,6 +2420,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(e->wm_done, 0, 4, e->stream));
   if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
   if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
+  if (e->bload) HIPCHK(e, hipMemsetAsync(e->bload, 0, 4 * 4 * RT_MAXNB, e->stream));
+  if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)RT_MAXNB * RT_GS, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
   *out = e;

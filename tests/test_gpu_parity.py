@@ -167,6 +167,47 @@ def test_zipf_out_of_order_lateness(hip, oracle_engine, mode):
     assert sg["records_late"] == so["records_late"] and so["records_late"] > 0
 
 
+@pytest.mark.parametrize("case", ["sum_count_lateness", "f64_min_max", "max_by", "purging"])
+def test_hot_buckets_split_over_helpers(hip, oracle_engine, monkeypatch, case):
+    """Zipf(1.3) keys concentrate the records in a few directory buckets; with FW_DEBUG_AGG & 64 a share
+    is 256 records, so from the second batch on the hot buckets are split over helper workgroups that
+    fold one after another (k_aggregate).  Bit-exact against the oracle (double sums: tolerance)."""
+    import ctypes
+    from flink_amd.windowing import EventTimeTrigger, PurgingTrigger, ReduceFunction, TumblingEventTimeWindows
+    from flink_amd.windowing import Aggregations, make_config
+    monkeypatch.setenv("FW_DEBUG_AGG", "64")
+    vt = "f64" if case == "f64_min_max" else "i64"
+    keys, ts, vals = gen_stream(120_000, 1 << 12, rate=1 << 15, zipf=1.3, ooo=150, value_type=vt)
+    kw = dict(key_capacity=1 << 14, max_batch=1 << 14, out_capacity=1 << 20, ingest_mode=2)
+    asg = TumblingEventTimeWindows.of(1000)
+    rel, lag = 0.0, 1
+    if case == "sum_count_lateness":
+        cfg = make_config(asg, ReduceFunction(("sum", "count"), vt, True), None, 100, **kw)
+        fields, lag = ["sum_i64", "count"], 50
+    elif case == "f64_min_max":
+        cfg = make_config(asg, ReduceFunction(("sum", "min", "max"), vt, True), None, 0, **kw)
+        fields, rel = ["sum_f64", "min_f64", "max_f64"], 1e-9
+    elif case == "max_by":
+        cfg = make_config(asg, Aggregations.maxBy(vt), None, 0, **kw)
+        fields = ["max_i64"]
+    else:
+        cfg = make_config(asg, ReduceFunction(("sum", "max"), vt, True), PurgingTrigger.of(EventTimeTrigger.create()),
+                          0, **kw)
+        fields = ["sum_i64", "max_i64"]
+    eg = hip(cfg)
+    eo = oracle_engine(cfg)
+    f1 = np.arange(len(keys), dtype=np.int64) * 5 + 2
+    rg = drive(eg, keys, ts, vals, 1 << 14, lag, LONG_MAX, f1=f1)
+    ro = drive(eo, keys, ts, vals, 1 << 14, lag, LONG_MAX, f1=f1)
+    dbg = np.zeros(8, np.int64)
+    eg.lib.fw_debug_counters(eg.h, dbg.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    eg.close()
+    eo.close()
+    assert dbg[3] > 0, "no bucket was split"
+    assert dbg[7] == 0, f"capacity error at site {dbg[7]}"
+    _compare(epochs_of(rg, fields, True), epochs_of(ro, fields, True), fields, rel)
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_purging_trigger_lateness(hip, oracle_engine, mode):
     from flink_amd.windowing import EventTimeTrigger, PurgingTrigger, TumblingEventTimeWindows

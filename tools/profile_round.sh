@@ -6,6 +6,8 @@ REPO="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$REPO"
 ARGS=${PROF_ARGS:-"--steps 16 --warmup 4 --prof-steps 0 --cpu-sample 0 --no-check"}
 export TMPDIR=/tmp
+rm -rf gpurun_out/prof_trace gpurun_out/prof_fetch gpurun_out/prof_write
+md5sum flink_amd/lib/libflink_window.so | cut -d' ' -f1 > gpurun_out/prof_md5.txt
 timeout -k 10 ${T_PROF:-300} rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/prof_trace" -o run -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 gpurun_out/prof_trace.log
 [ $rc -ne 0 ] && exit $rc

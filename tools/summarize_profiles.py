@@ -33,6 +33,9 @@ def main(tag):
         shutil.copy(src, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
     lib = os.path.join(ROOT, "flink_amd", "lib", "libflink_window.so")
     md5 = hashlib.md5(open(lib, "rb").read()).hexdigest()
+    ran = open(os.path.join(OUT, "prof_md5.txt")).read().strip()
+    if ran != md5:
+        sys.exit(f"gpurun_out/prof_* was measured on library {ran}, not the in-tree {md5}: re-run the profile")
     res = {"library_md5": md5, "units": "KB per dispatch as reported by rocprofv3", "kernels": {}}
     f = os.path.join(OUT, "prof_fetch", "run_counter_collection.csv")
     w = os.path.join(OUT, "prof_write", "run_counter_collection.csv")
