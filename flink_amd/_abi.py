@@ -75,7 +75,7 @@ class FwProfile(ctypes.Structure):
 
 class FwStats(ctypes.Structure):
     _fields_ = [("records_in", _i64), ("records_late", _i64), ("panes_fired", _i64), ("late_fires", _i64),
-                ("keys_resident", _i64), ("slices_live", _i64), ("ingest_form", _i64)]
+                ("keys_resident", _i64), ("slices_live", _i64), ("ingest_form", _i64), ("compactions", _i64)]
 
 
 def declare(lib, prefix="fw"):

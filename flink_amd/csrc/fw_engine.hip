@@ -59,7 +59,8 @@ constexpr int64_t EMPTY_KEY = INT64_MIN;
 constexpr int MAX_K = 64;          // max slices per window
 constexpr int BLOCK = 256;
 
-enum Stat { ST_LATE = 0, ST_FIRED = 1, ST_LATE_FIRES = 2, ST_SHARES = 3, ST_NSTATS = 8 };   // ST_SHARES: helper shares run
+// ST_SHARES: helper shares run; ST_DIR_KEYS: keys in the directory buckets (inserts since the last compaction + the keys it kept)
+enum Stat { ST_LATE = 0, ST_FIRED = 1, ST_LATE_FIRES = 2, ST_SHARES = 3, ST_DIR_KEYS = 4, ST_NSTATS = 8 };
 
 // ------------------------------------------------------------------------------------------------
 // device views
@@ -117,6 +118,7 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   OutLog o;
   int32_t* err;
   unsigned long long* stats;
+  unsigned int* dir_keys_host;   // host-mapped copy of stats[ST_DIR_KEYS], posted at each firing watermark
 };
 
 __device__ __forceinline__ void set_error(int32_t* err, int32_t code) { atomicCAS(err, 0, code); }
@@ -170,7 +172,8 @@ __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
 // stale) load can only under-report, which the CAS then corrects; a key found EMPTY at slot j cannot
 // sit at a later slot.
 __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
-                                                         int32_t kb_bits, int64_t D, int64_t key) {
+                                                         int32_t kb_bits, int64_t D, int64_t key,
+                                                         unsigned long long* inserted) {
   if (key == EMPTY_KEY) {
     if (dir_min_used[0] == 0) dir_min_used[0] = 1;
     return D;
@@ -186,6 +189,7 @@ __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int3
     if (cur == EMPTY_KEY) {
       const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[h], (unsigned long long)EMPTY_KEY,
                                                 (unsigned long long)key);
+      if ((int64_t)prev == EMPTY_KEY) atomicAdd(inserted, 1ull);
       if ((int64_t)prev == EMPTY_KEY || (int64_t)prev == key) return (int64_t)h;
     }
     off = (off + 1) & kbm;
@@ -193,16 +197,17 @@ __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int3
   return -1;
 }
 __device__ __noinline__ int64_t dir_find_or_insert_call(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
-                                                        int32_t kb_bits, int64_t D, int64_t key) {
-  return dir_find_or_insert_at(dir_keys, dir_min_used, dir_mask, kb_bits, D, key);
+                                                        int32_t kb_bits, int64_t D, int64_t key,
+                                                        unsigned long long* inserted) {
+  return dir_find_or_insert_at(dir_keys, dir_min_used, dir_mask, kb_bits, D, key, inserted);
 }
 // inline: the direct form's per-record lookup
 __device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key) {
-  return dir_find_or_insert_at(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key);
+  return dir_find_or_insert_at(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key, s.stats + ST_DIR_KEYS);
 }
 // out of line: the rare lookups of the partitioned form (new keys, direct-list records) and restore
 __device__ __forceinline__ int64_t dir_lookup(const Spec& s, int64_t key) {
-  return dir_find_or_insert_call(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key);
+  return dir_find_or_insert_call(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key, s.stats + ST_DIR_KEYS);
 }
 
 // slice number m -> slot p, claiming a FREE slot.  Returns -1 when slot p holds another live slice.
@@ -873,7 +878,8 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, Rout
 // the bucket's LDS directory-hash table: slot of h, inserting its key (fmix64_inv(h)) into the global
 // directory if absent (the same linear probe sequence as dir_find_or_insert).  Out of line: taken by a
 // wave only when a lane misses the probed windows.
-__device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h) {
+__device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h,
+                                                 unsigned long long* inserted) {
   uint32_t x = (uint32_t)h & kbm;
   for (uint32_t probe = 0; probe <= kbm; ++probe) {
     const uint64_t cur = lh[x];
@@ -882,6 +888,7 @@ __device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys
       const int64_t key = (int64_t)fmix64_inv(h);
       const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[x], (unsigned long long)EMPTY_KEY,
                                                 (unsigned long long)key);
+      if ((int64_t)prev == EMPTY_KEY) atomicAdd(inserted, 1ull);
       const uint64_t now = (int64_t)prev == EMPTY_KEY ? h : fmix64(prev);
       lh[x] = now;   // only globally confirmed keys enter the cache
       if (now == h) return (int32_t)x;
@@ -1144,7 +1151,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       int64_t kid = s.D;
       if (h == EMPTY_H) (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
       else {
-        const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h);
+        const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
         kid = x2 < 0 ? -1 : dbase + x2;
       }
       if (p < 0 || kid < 0) { cap_error(s, 7); continue; }
@@ -1198,7 +1205,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       }
       const bool miss2 = miss && !found2;
       if (__any(miss2) && miss2) {
-        const int32_t x = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h);
+        const int32_t x = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
         if (x < 0) { cap_error(s, 8); act = false; }
         else kl = (uint32_t)x;
       }
@@ -1313,7 +1320,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         if ((uint64_t)rec.x == EMPTY_H) {
           (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
         } else {
-          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, (uint64_t)rec.x);
+          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, (uint64_t)rec.x, s.stats + ST_DIR_KEYS);
           if (x2 < 0) { cap_error(s, 10); continue; }
           kl = (uint32_t)x2;
         }
@@ -1330,7 +1337,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         int64_t spins = 0;
         while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
           __builtin_amdgcn_s_sleep(8);
-          if (++spins > ((int64_t)1 << 21)) { cap_error(s, 14); break; }   // never hang: report and go on
+          if (++spins > ((int64_t)1 << 21)) { cap_error(s, 16); break; }   // never hang: report and go on
         }
       }
       __syncthreads();
@@ -1445,10 +1452,13 @@ struct LateCombine {
   }
 };
 
+// (emit_n > 0: also reserves the emit kernel's emit_n output slots at once, *out_base = the first —
+// one device atomic instead of one per wave of emitters on the shared output cursor)
 __global__ void k_late_prepare(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
                                const int64_t* val, unsigned long long* seg, LateAcc* acc, int64_t* headpos,
-                               const int64_t* f1col, int64_t ord_base) {
+                               const int64_t* f1col, int64_t ord_base, int64_t emit_n, unsigned long long* out_base) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0 && emit_n > 0) *out_base = atomicAdd(s.o.count, (unsigned long long)emit_n);
   if (j >= nl) return;
   unsigned long long k = sorted_key[j];
   int64_t i = (int64_t)(k & ((1ull << idx_bits) - 1));
@@ -1510,11 +1520,11 @@ __device__ __forceinline__ int64_t slot_max_ts(const Spec& s, int32_t p) {
 // emit one result per late record: state(base) (+) prefix
 __global__ void k_late_emit(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
                             const unsigned long long* seg, const LateAcc* acc, const LateAcc* scanned,
-                            const int64_t* f1col, int64_t ord_base, const int64_t* headpos) {
+                            const int64_t* f1col, int64_t ord_base, const int64_t* headpos,
+                            const unsigned long long* out_base) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool act = j < nl;
-  unsigned long long pos = wave_append(s.o.count, act);
-  if (!act) return;
+  if (j >= nl) return;
+  const unsigned long long pos = *out_base + (unsigned long long)j;   // one result per late record, in place
   unsigned long long pane = seg[j];
   int64_t idx = (int64_t)pane;
   int32_t p = (int32_t)(pane / (unsigned long long)s.stride);
@@ -1588,11 +1598,11 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
 // watermark fire and by every per-element fire since (FIRE_AND_PURGE), so the result is the record alone.
 __global__ void k_fire_emit(Spec s, const unsigned long long* sorted_key, int64_t nf, int32_t idx_bits,
                             const unsigned long long* seg, const LateAcc* acc, const LateAcc* scanned,
-                            const int64_t* f1col, const int64_t* tscol, int64_t wm, const int64_t* headpos) {
+                            const int64_t* f1col, const int64_t* tscol, int64_t wm, const int64_t* headpos,
+                            const unsigned long long* out_base) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool act = j < nf;
-  const unsigned long long pos = wave_append(s.o.count, act);
-  if (!act) return;
+  if (j >= nf) return;
+  const unsigned long long pos = *out_base + (unsigned long long)j;   // one result per fire element, in place
   const unsigned long long wpane = seg[j];
   const int32_t wp = (int32_t)(wpane / (unsigned long long)s.stride);
   const int64_t kid = (int64_t)(wpane % (unsigned long long)s.stride);
@@ -1769,7 +1779,98 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     } else {
       cap_error(s, 13);
     }
+    // the directory's key count, for the host's compaction trigger (fw_advance_watermark)
+    if (s.dir_keys_host)
+      __hip_atomic_store(s.dir_keys_host, (unsigned)s.stats[ST_DIR_KEYS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// key directory compaction (unbounded key spaces).  The reference keeps no entry for a key once its
+// last pane is cleared (AbstractHeapState.clear, AbstractHeapState.java:90-119, removes the key from the
+// namespace's map and the namespace when empty): here a key leaves the directory once no live slice
+// holds a pane of it.  One workgroup per directory bucket (probing never leaves a bucket): the bucket's
+// live keys are re-inserted into a fresh linear-probe layout in LDS and their pane columns moved in every
+// live slice; the evicted keys' key groups are remembered (their state tables stay "present" for a
+// checkpoint, HeapKeyedStateBackend.java:228-233).  Launched after a firing watermark when the directory
+// is more than half full; buckets of <= 4096 slots (LDS).
+// ------------------------------------------------------------------------------------------------
+constexpr int CP_THREADS = 1024;
+__host__ __device__ constexpr size_t compact_lds_bytes(int kb_bits, int P) {
+  return (size_t)(1 << kb_bits) * (8 + 8 + 8 + 2) + 8 * (size_t)P + 64;
+}
+
+__global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* kg_evicted) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int KB = 1 << s.kb_bits;
+  const uint32_t kbm = (uint32_t)KB - 1;
+  int64_t* okey = (int64_t*)smem;                 // [KB] the bucket's keys before
+  int64_t* nkey = okey + KB;                      // [KB] after
+  int64_t* tmp = nkey + KB;                       // [KB] one column of one slice
+  int64_t* tags = tmp + KB;                       // [P] slice tags
+  int16_t* inv = (int16_t*)(tags + s.P);          // [KB] new slot -> old slot (-1: empty)
+  const int64_t dbase = (int64_t)blockIdx.x * KB;
+  for (int p = threadIdx.x; p < s.P; p += CP_THREADS) tags[p] = s.slice_tag[p];
+  for (int x = threadIdx.x; x < KB; x += CP_THREADS) {
+    okey[x] = s.dir_keys[dbase + x];
+    nkey[x] = EMPTY_KEY;
+    inv[x] = -1;
+  }
+  __syncthreads();
+  unsigned long long kept = 0;
+  for (int x = threadIdx.x; x < KB; x += CP_THREADS) {
+    const int64_t key = okey[x];
+    if (key == EMPTY_KEY) continue;
+    bool live = false;
+    for (int p = 0; p < s.P && !live; ++p)
+      if (tags[p] != FREE_TAG) live = pane_present(s, (int64_t)p * s.stride + dbase + x);
+    if (!live) {
+      kg_evicted[key_group_for_hash(long_hash_code(key), s.mp)] = 1;
+      continue;
+    }
+    // re-insert: the same probe sequence as dir_find_or_insert, in the fresh LDS layout
+    uint32_t y = (uint32_t)fmix64((uint64_t)key) & kbm;
+    for (;;) {
+      const unsigned long long prev =
+          atomicCAS((unsigned long long*)&nkey[y], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+      if ((int64_t)prev == EMPTY_KEY) break;
+      y = (y + 1) & kbm;
+    }
+    inv[y] = (int16_t)x;
+    ++kept;
+  }
+  for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o);
+  if ((threadIdx.x & 63) == 0 && kept) atomicAdd(&s.stats[ST_DIR_KEYS], kept);
+  __syncthreads();
+  // move the live slices' columns of this bucket: new slot y takes old slot inv[y]
+  auto move = [&](int64_t* col, int64_t ident) {
+    for (int p = 0; p < s.P; ++p) {   // uniform
+      if (tags[p] == FREE_TAG) continue;
+      int64_t* c = col + (int64_t)p * s.stride + dbase;
+      for (int x = threadIdx.x; x < KB; x += CP_THREADS) tmp[x] = c[x];
+      __syncthreads();
+      for (int y = threadIdx.x; y < KB; y += CP_THREADS) c[y] = inv[y] >= 0 ? tmp[inv[y]] : ident;
+      __syncthreads();
+    }
+  };
+  if (s.c.sum) move(s.c.sum, sum_identity(s.vt));
+  if (s.c.mn) move(s.c.mn, INT64_MAX);
+  if (s.c.mx) move(s.c.mx, INT64_MIN);
+  if (s.c.cnt) move(s.c.cnt, 0);
+  if (s.first) {
+    move(s.c.first, INT64_MAX);
+    move(s.c.f1v, 0);
+  } else {
+    for (int p = 0; p < s.P; ++p) {
+      if (tags[p] == FREE_TAG) continue;
+      unsigned char* c = s.c.present + (int64_t)p * s.stride + dbase;
+      for (int x = threadIdx.x; x < KB; x += CP_THREADS) tmp[x] = c[x];
+      __syncthreads();
+      for (int y = threadIdx.x; y < KB; y += CP_THREADS) c[y] = inv[y] >= 0 ? (unsigned char)tmp[inv[y]] : 0;
+      __syncthreads();
+    }
+  }
+  for (int y = threadIdx.x; y < KB; y += CP_THREADS) s.dir_keys[dbase + y] = nkey[y];
 }
 
 __global__ void k_mark_only(Spec s, int64_t wm) {
@@ -1991,6 +2092,7 @@ struct fw_engine {
   int32_t* stg_hash[2] = {};
   // late path
   unsigned long long *late_key = nullptr, *late_key_sorted = nullptr, *late_count = nullptr, *seg = nullptr;
+  unsigned long long* out_base = nullptr;   // first output slot reserved for a per-element emit kernel
   unsigned long long *fire_key = nullptr, *fire_count = nullptr;   // sliding: per-element fire elements
   int64_t fire_cap = 0;
   unsigned long long *late_idx_in = nullptr, *late_idx_out = nullptr;
@@ -2038,6 +2140,13 @@ struct fw_engine {
   unsigned int* bload = nullptr;            // [4][RT_MAXNB] routed records per bucket and batch (k_aggregate split plan)
   unsigned int* fold_flag = nullptr;        // [RT_MAXNB][RT_GS]
   unsigned int* bload_host = nullptr;       // host-mapped [RT_MAXNB], written by k_aggregate's owners
+  // key directory compaction
+  unsigned char* kg_evicted = nullptr;      // [max_parallelism] a key of the key group was evicted
+  unsigned int* dir_keys_host = nullptr;    // host-mapped: keys in the directory at the last firing watermark
+  bool compact_ok = false;
+  size_t compact_lds = 0;
+  double compact_fill = 0.5;                // FW_COMPACT_FILL
+  int64_t compactions = 0;
   int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
   int64_t batches = 0;
   int32_t max_tiles = 0;
@@ -2071,6 +2180,7 @@ struct fw_engine {
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
     if (bload_host) (void)hipHostFree(bload_host);
+    if (dir_keys_host) (void)hipHostFree(dir_keys_host);
   }
 };
 
@@ -2311,6 +2421,19 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   o.mark_count = e->alloc<unsigned long long>(1);
   s.err = e->alloc<int32_t>(1);
   s.stats = e->alloc<unsigned long long>(ST_NSTATS);
+  // key directory compaction (k_compact): buckets that fit LDS
+  e->kg_evicted = e->alloc<unsigned char>((size_t)c.max_parallelism);
+  e->compact_lds = compact_lds_bytes(s.kb_bits, s.P);
+  e->compact_ok = s.kb_bits <= 12 && e->compact_lds <= 160 * 1024;
+  if (e->compact_ok) {
+    if (hipHostMalloc((void**)&e->dir_keys_host, 4, hipHostMallocMapped) != hipSuccess) e->dir_keys_host = nullptr;
+    if (e->dir_keys_host) *e->dir_keys_host = 0;
+    s.dir_keys_host = e->dir_keys_host;
+    (void)hipFuncSetAttribute((const void*)k_compact, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    const char* cf = getenv("FW_COMPACT_FILL");   // percent of the directory's slots (0: never compact)
+    if (cf && atoi(cf) <= 0) e->compact_ok = false;
+    else if (cf) e->compact_fill = std::min(atoi(cf), 95) / 100.0;
+  }
 
   for (int q = 0; q < 2; ++q) {
     e->stg_key[q] = e->alloc<int64_t>((size_t)c.max_batch);
@@ -2384,6 +2507,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->late_key = e->alloc<unsigned long long>((size_t)c.max_batch);
     e->late_key_sorted = e->alloc<unsigned long long>(nb);
     e->late_count = e->alloc<unsigned long long>(1);
+    e->out_base = e->alloc<unsigned long long>(1);
     e->seg = e->alloc<unsigned long long>(nb);
     e->late_acc = e->alloc<LateAcc>(nb);
     e->late_scan = e->alloc<LateAcc>(nb);
@@ -2415,6 +2539,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipMemsetAsync(o.mark_count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(s.err, 0, 4, e->stream));
   HIPCHK(e, hipMemsetAsync(s.stats, 0, 8 * ST_NSTATS, e->stream));
+  HIPCHK(e, hipMemsetAsync(e->kg_evicted, 0, (size_t)c.max_parallelism, e->stream));
   HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
   if (e->fire_count) HIPCHK(e, hipMemsetAsync(e->fire_count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(e->wm_done, 0, 4, e->stream));
@@ -2527,12 +2652,14 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     const bool sliding = e->cfg.assigner == FW_SLIDING;
     if (nl > 0 || nf > 0) e->phase_begin(FW_PHASE_LATE);
     // sort by (pane, arrival), per-pane inclusive scan of the records' accumulators in arrival order
-    auto sorted_scan = [&](unsigned long long* keys, unsigned long long n) -> int {
+    // keys are (pane << idx_bits) | batch index, pane < P * stride: only their low bits are sorted
+    const int key_bits = std::min(64, e->idx_bits + bits_for((uint64_t)e->s.P * (uint64_t)e->s.stride));
+    auto sorted_scan = [&](unsigned long long* keys, unsigned long long n, int64_t emit_n) -> int {
       size_t tb = e->temp_bytes;
-      HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, keys, e->late_key_sorted, (size_t)n, 0, 64, e->stream));
+      HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, keys, e->late_key_sorted, (size_t)n, 0, key_bits, e->stream));
       const int blocks = (int)((n + BLOCK - 1) / BLOCK);
       hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)n,
-                         e->idx_bits, dv, e->seg, e->late_acc, e->headpos, df1, e->ordinal);
+                         e->idx_bits, dv, e->seg, e->late_acc, e->headpos, df1, e->ordinal, emit_n, e->out_base);
       tb = e->temp_bytes;
       HIPCHK(e, rocprim::inclusive_scan(e->temp, tb, e->headpos, e->headpos_scan, (size_t)n,
                                         rocprim::maximum<int64_t>(), e->stream));
@@ -2542,19 +2669,19 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
       return FW_OK;
     };
     if (nf > 0) {   // sliding: the fires first, against the slices before this batch's late records
-      if (int rc = sorted_scan(e->fire_key, nf)) return rc;
+      if (int rc = sorted_scan(e->fire_key, nf, (int64_t)nf)) return rc;
       hipLaunchKernelGGL(k_fire_emit, dim3((unsigned)((nf + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, e->stream, e->s,
                          e->late_key_sorted, (int64_t)nf, e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, dts,
-                         e->cur_wm, e->headpos_scan);
+                         e->cur_wm, e->headpos_scan, e->out_base);
       e->late_fires_host += (int64_t)nf;
       HIPCHK(e, hipMemsetAsync(e->fire_count, 0, 8, e->stream));
     }
     if (nl > 0) {
-      if (int rc = sorted_scan(e->late_key, nl)) return rc;
+      if (int rc = sorted_scan(e->late_key, nl, sliding ? 0 : (int64_t)nl)) return rc;
       const int blocks = (int)((nl + BLOCK - 1) / BLOCK);
       if (!sliding) {
         hipLaunchKernelGGL(k_late_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
-                           e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, e->ordinal, e->headpos_scan);
+                           e->idx_bits, e->seg, e->late_acc, e->late_scan, df1, e->ordinal, e->headpos_scan, e->out_base);
         e->late_fires_host += (int64_t)nl;
       }
       hipLaunchKernelGGL(k_late_commit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)nl,
@@ -2596,6 +2723,18 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   e->phase_end(e->s.stride);
   HIPCHK(e, hipGetLastError());
   e->cur_wm = wm;
+  // evict dead keys once the directory is more than compact_fill full (the count posted by an earlier
+  // firing watermark: read without a sync)
+  if (e->compact_ok && e->dir_keys_host &&
+      (double)__atomic_load_n(e->dir_keys_host, __ATOMIC_RELAXED) > e->compact_fill * (double)e->s.D) {
+    HIPCHK(e, hipMemsetAsync(e->s.stats + ST_DIR_KEYS, 0, 8, e->stream));
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)(e->s.D >> e->s.kb_bits)), dim3(CP_THREADS), e->compact_lds, e->stream,
+                       e->s, e->kg_evicted);
+    HIPCHK(e, hipGetLastError());
+    __atomic_store_n(e->dir_keys_host, 0u, __ATOMIC_RELAXED);
+    e->compactions++;
+    e->state_epoch++;
+  }
   return FW_OK;
 }
 
@@ -2677,8 +2816,9 @@ int fw_get_stats(fw_engine* e, fw_stats* st) {
   int64_t live = 0;
   for (int64_t t : tags) live += t != FREE_TAG;
   st->slices_live = live;
-  st->keys_resident = -1;
+  st->keys_resident = (int64_t)d[ST_DIR_KEYS];   // the Long.MIN_VALUE key's own column not counted
   st->ingest_form = e->routed ? 2 : 1;
+  st->compactions = e->compactions;
   return FW_OK;
 }
 
@@ -2784,6 +2924,11 @@ static int build_snapshot(fw_engine* e) {
   e->snap_any_key = false;
   for (size_t k = 0; k < kid_kg.size(); ++k)
     if (kid_kg[k] >= 0) { e->snap_has_key[(size_t)kid_kg[k]] = 1; e->snap_any_key = true; }
+  if (e->kg_evicted) {   // key groups whose keys were all evicted still had state (StateTable.get(kg) != null)
+    std::vector<uint8_t> ev((size_t)mp);
+    HIPCHK(e, hipMemcpy(ev.data(), e->kg_evicted, (size_t)mp, hipMemcpyDeviceToHost));
+    for (int32_t k = 0; k < mp; ++k) if (ev[(size_t)k]) { e->snap_has_key[(size_t)k] = 1; e->snap_any_key = true; }
+  }
   const size_t st = (size_t)s.stride;
   std::vector<int64_t> sum(st), mn, mx, cnt, first, f1v;
   std::vector<uint8_t> present;

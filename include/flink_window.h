@@ -150,6 +150,7 @@ typedef struct {
   int64_t keys_resident;     /* distinct keys in the key directory            */
   int64_t slices_live;       /* pane slices resident                          */
   int64_t ingest_form;       /* 1 = direct atomics, 2 = partitioned + LDS     */
+  int64_t compactions;       /* key-directory compactions (dead keys evicted) */
 } fw_stats;
 
 int         fw_create(const fw_config* cfg, fw_engine** out);
