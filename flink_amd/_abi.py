@@ -40,10 +40,11 @@ FW_MEM_DEVICE = 1
 EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sync", "fw_collect",
                     "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
                     "fw_get_profile", "fw_debug_counters", "fw_debug_stamps", "fw_set_stream", "fw_stream_wait_input",
-                    "fw_version", "fw_snapshot_kg", "fw_restore_kg", "fw_snapshot_kg_flink", "fw_restore_kg_flink")
+                    "fw_version", "fw_snapshot_kg", "fw_restore_kg", "fw_snapshot_kg_flink", "fw_restore_kg_flink", "fw_decode")
 FW_SNAP_MAGIC, FW_SNAP_HEADER_WORDS, FW_SNAP_ENTRY_WORDS = 0x31474b5746574b, 12, 8
 # state tuple fields of the Flink-layout checkpoint (fw_state_layout)
 FW_SF_KEY, FW_SF_F1, FW_SF_SUM, FW_SF_MIN, FW_SF_MAX, FW_SF_COUNT, FW_SF_VALUE, FW_SF_MAX_FIELDS = 1, 2, 3, 4, 5, 6, 7, 8
+FW_FT_LONG, FW_FT_DOUBLE, FW_FT_INT = 0, 1, 2
 FW_PHASE_INGEST, FW_PHASE_FIXUP, FW_PHASE_LATE, FW_PHASE_FIRE, FW_PHASE_AGGREGATE, FW_NPHASES = 0, 1, 2, 3, 4, 5
 
 _i32, _i64, _p = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
@@ -67,6 +68,15 @@ class FwOut(ctypes.Structure):
 
 class FwStateLayout(ctypes.Structure):
     _fields_ = [("n_fields", _i32), ("field", _i32 * FW_SF_MAX_FIELDS)]
+
+
+class FwTupleSchema(ctypes.Structure):
+    _fields_ = [("n_fields", _i32), ("field_type", _i32 * 8), ("key_field", _i32), ("f1_field", _i32),
+                ("value_field", _i32)]
+
+
+class FwDecodeCounts(ctypes.Structure):
+    _fields_ = [("n_records", _i64), ("n_watermarks", _i64), ("n_latency_markers", _i64), ("consumed", _i64)]
 
 
 class FwProfile(ctypes.Structure):
@@ -101,6 +111,8 @@ def declare(lib, prefix="fw"):
         "restore_kg": (_i32, [_p, _i32, _p, _i64]),
         "snapshot_kg_flink": (_i32, [_p, _i32, P(FwStateLayout), _p, _i64, P(_i64), _p, _i64, P(_i64)]),
         "restore_kg_flink": (_i32, [_p, _i32, P(FwStateLayout), _i64, _p, _i64, _p, _i64]),
+        "decode": (_i32, [_p, P(FwTupleSchema), _p, _i64, _i32, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64,
+                          P(FwDecodeCounts)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}", None)

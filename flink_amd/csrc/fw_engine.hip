@@ -2147,6 +2147,9 @@ struct fw_engine {
   size_t compact_lds = 0;
   double compact_fill = 0.5;                // FW_COMPACT_FILL
   int64_t compactions = 0;
+  // fw_decode scratch (grow-only)
+  void *dec_table = nullptr, *dec_small = nullptr, *dec_bytes = nullptr;
+  size_t dec_table_cap = 0, dec_small_cap = 0, dec_bytes_cap = 0;
   int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
   int64_t batches = 0;
   int32_t max_tiles = 0;
@@ -2181,6 +2184,7 @@ struct fw_engine {
     for (void* p : allocs) (void)hipFree(p);
     if (bload_host) (void)hipHostFree(bload_host);
     if (dir_keys_host) (void)hipHostFree(dir_keys_host);
+    for (void* p : {dec_table, dec_small, dec_bytes}) if (p) (void)hipFree(p);
   }
 };
 
@@ -3409,3 +3413,5 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
 }
 
 }  // extern "C"
+
+#include "fw_decode.hip"

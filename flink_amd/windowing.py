@@ -352,6 +352,60 @@ class WindowEngine:
         self._check(self._fn("restore_kg_flink")(self.h, kg, ctypes.byref(L), watermark, sb, len(state), tb,
                                                  len(timers)))
 
+    def decode(self, data, fields, key=0, value=None, f1=None, record_cap=None, marker_cap=1 << 16, device=False):
+        """Decode Flink network-buffer bytes (fw_decode: length-prefixed StreamElementSerializer elements over a
+        TupleSerializer tuple) into record columns, watermarks and latency markers in stream order.
+
+        data: bytes / numpy uint8 (host) or a torch uint8 tensor on the GPU; fields: the tuple's field types
+        ("long", "double", "int"); key / value / f1: field indices (f1 None: the record timestamp).  Returns a
+        dict of numpy arrays (device=True: torch tensors on the engine's GPU, ready for push) and the counts;
+        "consumed" < len(data) when the bytes end inside an element."""
+        types = {"long": _abi.FW_FT_LONG, "double": _abi.FW_FT_DOUBLE, "int": _abi.FW_FT_INT}
+        sc = _abi.FwTupleSchema()
+        sc.n_fields = len(fields)
+        for i, f in enumerate(fields):
+            sc.field_type[i] = types[f]
+        sc.key_field, sc.value_field = key, len(fields) - 1 if value is None else value
+        sc.f1_field = -1 if f1 is None else f1
+        int_key = fields[key] == "int"
+        on_gpu = self.prefix == "fw"
+        dev_in = on_gpu and hasattr(data, "is_cuda") and data.is_cuda
+        if not dev_in:
+            data = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data
+        nbytes = int(data.numel() if dev_in else data.size)
+        cap = record_cap or max(1, nbytes // 9)
+        if on_gpu:
+            import torch
+            dev = torch.device("cuda", self.cfg.device)
+            mk = lambda n, dt=torch.int64: torch.empty(max(n, 1), dtype=dt, device=dev)
+            ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+        else:
+            mk = lambda n, dt=np.int64: np.empty(max(n, 1), dtype=np.int32 if dt is not np.int64 else np.int64)
+            ptr = lambda t: ctypes.c_void_p(t.ctypes.data)
+        i32 = torch.int32 if on_gpu else np.int32
+        cols = dict(key=mk(cap), f1=mk(cap), ts=mk(cap), value=mk(cap), wm=mk(marker_cap), wm_pos=mk(marker_cap),
+                    lm=mk(2 * marker_cap), lm_pos=mk(marker_cap))
+        cols["key_hash"] = mk(cap, i32) if int_key else None
+        cnt = _abi.FwDecodeCounts()
+        src = ctypes.c_void_p(data.data_ptr()) if dev_in else ctypes.c_void_p(data.ctypes.data)
+        self._check(self._fn("decode")(self.h, ctypes.byref(sc), src, nbytes,
+                                       _abi.FW_MEM_DEVICE if dev_in else _abi.FW_MEM_HOST,
+                                       ptr(cols["key"]), ptr(cols["key_hash"]) if int_key else None, ptr(cols["f1"]),
+                                       ptr(cols["ts"]), ptr(cols["value"]), cap, ptr(cols["wm"]),
+                                       ptr(cols["wm_pos"]), ptr(cols["lm"]), ptr(cols["lm_pos"]), marker_cap,
+                                       ctypes.byref(cnt)))
+        n, nw, nl = cnt.n_records, cnt.n_watermarks, cnt.n_latency_markers
+        out = {"n_records": n, "n_watermarks": nw, "n_latency_markers": nl, "consumed": cnt.consumed}
+        for k in ("key", "key_hash", "f1", "ts", "value"):
+            out[k] = None if cols[k] is None else cols[k][:n]
+        out["wm"], out["wm_pos"] = cols["wm"][:nw], cols["wm_pos"][:nw]
+        out["lm"], out["lm_pos"] = cols["lm"][:2 * nl].reshape(-1, 2), cols["lm_pos"][:nl]
+        if fields[sc.value_field] == "double":
+            out["value"] = out["value"].view(torch.float64 if on_gpu else np.float64)
+        if on_gpu and not device:
+            out = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in out.items()}
+        return out
+
     def stats(self):
         st = _abi.FwStats()
         self._check(self._fn("get_stats")(self.h, ctypes.byref(st)))

@@ -243,6 +243,44 @@ int         fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout
 int         fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
                                 const void* state, int64_t state_len, const void* timers, int64_t timers_len);
 
+/* ---- ingest from Flink's wire format ----
+ * fw_decode <- the receiving side of a channel: SpillingAdaptiveSpanningRecordDeserializer reassembling
+ *              length-prefixed records from network buffers (written by SpanningRecordSerializer.addRecord,
+ *              flink-runtime/.../io/network/api/serialization/SpanningRecordSerializer.java:69-92: int32 BE
+ *              length, then the bytes) + StreamElementSerializer.deserialize
+ *              (SJ/runtime/streamrecord/StreamElementSerializer.java:155-198: tag byte 0 record with
+ *              timestamp (int64 BE follows), 1 record without, 2 watermark (int64), 3 latency marker
+ *              (int64, int32, int32)) + TupleSerializer.deserialize (flink-core/.../typeutils/runtime/
+ *              TupleSerializer.java:120-139: the fields in order, LongSerializer / DoubleSerializer /
+ *              IntSerializer big-endian), as StreamInputProcessor.processInput drives them (:127-177).
+ * `bytes` is the concatenation of the buffers' contents (nbytes, FW_MEM_HOST or FW_MEM_DEVICE) starting at
+ * an element boundary; an element cut by the end stays for the next call (*consumed < nbytes: pass the
+ * rest again in front of the next buffers).  Records are decoded, on the GPU, into device columns ready
+ * for fw_push_batch(FW_MEM_DEVICE): key, key_hash (an int key's Integer.hashCode; NULL for long keys),
+ * f1 (the schema's f1 field, or the timestamp), ts (Long.MIN_VALUE for a record without timestamp) and
+ * value (long or double bits).  Watermarks and latency markers come back in stream order with their
+ * position: the number of records before them (device arrays).  A malformed stream (no element chain
+ * through the bytes) fails with FW_ERR_INVALID_ARG. */
+#define FW_FT_LONG    0   /* LongSerializer: 8 bytes                              */
+#define FW_FT_DOUBLE  1   /* DoubleSerializer: 8 bytes (the value field only)     */
+#define FW_FT_INT     2   /* IntSerializer: 4 bytes (key or f1; sign-extended)    */
+#define FW_DECODE_MAX_FIELDS 8
+typedef struct {
+  int32_t n_fields;                        /* the tuple's arity                            */
+  int32_t field_type[FW_DECODE_MAX_FIELDS];
+  int32_t key_field;                       /* index of the key field                        */
+  int32_t f1_field;                        /* index of the pass-through field, -1: the ts   */
+  int32_t value_field;                     /* index of the reduced field                    */
+} fw_tuple_schema;
+typedef struct {
+  int64_t n_records, n_watermarks, n_latency_markers;
+  int64_t consumed;                        /* bytes of whole elements decoded               */
+} fw_decode_counts;
+int         fw_decode(fw_engine* e, const fw_tuple_schema* schema, const void* bytes, int64_t nbytes, int32_t mem,
+                      int64_t* key, int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap,
+                      int64_t* wm, int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap,
+                      fw_decode_counts* out);
+
 /* Key-group routing for the multi-GPU keyBy exchange (enqueued on the caller stream when fw_set_stream set one)
  * (KeyGroupStreamPartitioner.selectChannels, SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65;
  *  KeyGroupRangeAssignment.assignKeyToParallelOperator, KeyGroupRangeAssignment.java:40-42,105-107).

@@ -24,6 +24,10 @@
 //   timer service               SJ/api/operators/HeapInternalTimerService.java:211-236,264-278
 //   InternalTimer               SJ/api/operators/InternalTimer.java:59-86
 //   processWatermark            SJ/api/operators/AbstractStreamOperator.java:803-808
+//   wire format (decode)        SpanningRecordSerializer.java:69-92 (int32 BE length prefix; the receiver
+//                               reads a length, then that many bytes), StreamElementSerializer.deserialize
+//                               SJ/runtime/streamrecord/StreamElementSerializer.java:183-198, TupleSerializer
+//                               .deserialize flink-core/.../typeutils/runtime/TupleSerializer.java:132-139
 //   checkpoint, per key group   RT/state/heap/HeapKeyedStateBackend.java:196-248 (writeStateTableForKeyGroup),
 //                               :251-349 (readStateTableForKeyGroup); HeapInternalTimerService.java:285-345;
 //                               TimeWindow.Serializer TimeWindow.java:141-158; InternalTimer.TimerSerializer
@@ -717,6 +721,68 @@ int fwo_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   if (!e || !layout || !timers) return FW_ERR_INVALID_ARG;
   return restoreKeyGroup(e->op, kg, *layout, watermark, (const uint8_t*)state, state_len, (const uint8_t*)timers,
                          timers_len);
+}
+
+// the receiving side of one channel, element after element: length, tag, then the element's fields
+// (DataInputDeserializer reads big-endian).  Outputs are host arrays here.
+int fwo_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_t nbytes, int32_t mem, int64_t* key,
+               int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap, int64_t* wm,
+               int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap, fw_decode_counts* out) {
+  (void)e; (void)mem;
+  std::memset(out, 0, sizeof(*out));
+  std::vector<int> off(sc->n_fields + 1, 0);
+  for (int i = 0; i < sc->n_fields; ++i) off[i + 1] = off[i] + (sc->field_type[i] == FW_FT_INT ? 4 : 8);
+  const int tupleBytes = off[sc->n_fields];
+  JavaIn in{(const uint8_t*)bytes, nbytes};
+  int64_t nr = 0, nw = 0, nl = 0;
+  auto field = [&](const uint8_t* t, int i) -> int64_t {
+    JavaIn f{t + off[i], 8};
+    return sc->field_type[i] == FW_FT_INT ? (int64_t)f.readInt() : f.readLong();
+  };
+  while (in.pos + 4 <= nbytes) {
+    const int64_t at = in.pos;
+    const int32_t len = in.readInt();
+    if (len < 1 || at + 4 + len > nbytes) { in.pos = at; break; }   // the rest spans into the next buffer
+    const uint8_t* el = (const uint8_t*)bytes + at + 4;
+    const int tag = (int)(int8_t)el[0];
+    if (tag == 0 || tag == 1) {   // StreamRecord with / without timestamp
+      if (len != (tag == 0 ? 9 : 1) + tupleBytes) return FW_ERR_INVALID_ARG;
+      if (nr >= record_cap) return FW_ERR_CAPACITY;
+      JavaIn r{el + 1, 8};
+      const int64_t t = tag == 0 ? r.readLong() : INT64_MIN;
+      const uint8_t* tuple = el + (tag == 0 ? 9 : 1);
+      key[nr] = field(tuple, sc->key_field);
+      if (key_hash) key_hash[nr] = (int32_t)key[nr];   // Integer.hashCode
+      ts[nr] = t;
+      f1[nr] = sc->f1_field < 0 ? t : field(tuple, sc->f1_field);
+      ((int64_t*)value)[nr] = field(tuple, sc->value_field);   // long, or the double's bits
+      ++nr;
+    } else if (tag == 2) {        // Watermark
+      if (len != 9) return FW_ERR_INVALID_ARG;
+      if (nw >= marker_cap) return FW_ERR_CAPACITY;
+      JavaIn r{el + 1, 8};
+      wm[nw] = r.readLong();
+      wm_pos[nw] = nr;
+      ++nw;
+    } else if (tag == 3) {        // LatencyMarker(markedTime, vertexId, subtaskIndex)
+      if (len != 17) return FW_ERR_INVALID_ARG;
+      if (nl >= marker_cap) return FW_ERR_CAPACITY;
+      JavaIn r{el + 1, 16};
+      lm[2 * nl] = r.readLong();
+      const uint32_t v = (uint32_t)r.readInt(), sidx = (uint32_t)r.readInt();
+      lm[2 * nl + 1] = (int64_t)(((uint64_t)v << 32) | sidx);
+      lm_pos[nl] = nr;
+      ++nl;
+    } else {
+      return FW_ERR_INVALID_ARG;  // "Corrupt stream, found tag: " (StreamElementSerializer.java:196)
+    }
+    in.pos = at + 4 + len;
+  }
+  out->n_records = nr;
+  out->n_watermarks = nw;
+  out->n_latency_markers = nl;
+  out->consumed = in.pos;
+  return FW_OK;
 }
 
 const char* fwo_last_error(const fw_engine* e) { return e ? e->op.err.c_str() : "null engine"; }
