@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--prof-steps", type=int, default=8,
                     help="steps after the timed region run with per-kernel device-time events (roofline); "
                          "timed events serialise kernels, so the timed region runs without them")
+    ap.add_argument("--decode-steps", type=int, default=4,
+                    help="wire-format decode leg (fw_decode of the batch as Flink network bytes; 0 = skip)")
     ap.add_argument("--h2d-steps", type=int, default=8,
                     help="steps after the timed region pushed from pinned host columns (PCIe-inclusive rate; 0 = skip)")
     return ap.parse_args()
@@ -259,6 +261,29 @@ def main():
                        "the same kernels; PCIe-inclusive, never the headline value"}
         collected.append(eng.collect())
 
+    # wire-format ingest: the batch as Flink network bytes (length-prefixed StreamElementSerializer records of
+    # Tuple3<Long key, Long f1, Long value> with timestamps), resident in HBM, decoded by fw_decode
+    dec = None
+    if args.decode_steps > 0 and exch is None and vt == "i64":
+        k, t, v = cols[0]
+        n = k.numel()
+        be = lambda x: x.view(torch.uint8).view(n, 8).flip(1)
+        head = torch.tensor([0, 0, 0, 33, 0], dtype=torch.uint8, device=dev).expand(n, 5)   # length 33, tag 0
+        wire = torch.cat([head, be(t), be(k), be(t), be(v)], dim=1).reshape(-1).contiguous()
+        out = eng.decode(wire, ["long", "long", "long"], key=0, f1=1, value=2, record_cap=n, device=True)
+        ok = out["n_records"] == n and bool(torch.equal(out["key"], k)) and bool(torch.equal(out["value"], v))
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for _ in range(args.decode_steps):
+            eng.decode(wire, ["long", "long", "long"], key=0, f1=1, value=2, record_cap=n, device=True)
+        torch.cuda.synchronize()
+        dtd = (time.perf_counter() - t2) / args.decode_steps
+        dec = {"value": n / dtd, "unit": "records/s", "GB_s_in": wire.numel() / dtd / 1e9, "bytes_per_record": 37,
+               "check": "ok" if ok else "MISMATCH",
+               "note": "fw_decode of one batch as Flink wire bytes in HBM (host-synchronous call incl. its count "
+                       "readback); the window kernels not included"}
+        del wire, out
+
     if world > 1:
         import torch.distributed as dist
         t_all = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -362,6 +387,8 @@ def main():
     }
     if h2d is not None:
         line["h2d_ingest"] = h2d
+    if dec is not None:
+        line["wire_decode"] = dec
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         line["cpu_baseline"] = cpu_baseline(cfg, C, args.cpu_sample)
     if rank == 0:

@@ -8,8 +8,10 @@ Mirrors the reference's hash edge between source and window operator:
             the receiver keeps one watermark per input channel, raised only when a larger one arrives, and
             forwards min over channels only when that minimum increases  SJ/runtime/io/StreamInputProcessor.java:147-161
 MI355X form: the HIP partition kernel (fw_partition_by_operator) counting-sorts a batch by destination
-in HBM; one all-to-all of per-destination counts, per-column all-to-alls of the routed records over
-xGMI (RCCL: torch.distributed backend "nccl"), one MIN all-reduce of the channels' watermarks.
+in HBM; one all-to-all of per-destination counts, one MIN all-reduce of the channels' watermarks, and
+the routed records: a rank's own share is pushed straight from the partition buffers (a local channel:
+no copy), the other shares move as one group of point-to-point sends/receives over xGMI (RCCL via
+torch.distributed backend "nccl": one group call for the three columns of every peer).
 
 Every rank is both a source subtask (its own watermark = one input channel of every window subtask)
 and a window subtask.  Because every watermark is broadcast, all window subtasks see the same channel
@@ -67,14 +69,16 @@ class KeyByExchange:
             S = self.depth + 1          # send sets: partition of batch j must not overwrite batch j - depth's
             z = lambda n, dt=torch.int64: torch.empty(n, dtype=dt, device=self.device)
             self.send = [(z(batch), z(batch), z(batch)) for _ in range(S)]
-            self.counts = [torch.zeros(world, dtype=torch.int64, device=self.device) for _ in range(S)]
+            # per send set: [send counts | received counts | aligned watermark] in one device tensor, read
+            # back by one copy
+            self.meta = [torch.zeros(2 * world + 1, dtype=torch.int64, device=self.device) for _ in range(S)]
             self.offsets = [torch.zeros(world, dtype=torch.int64, device=self.device) for _ in range(S)]
-            self.recv_counts = [torch.zeros(world, dtype=torch.int64, device=self.device) for _ in range(S)]
-            self.wm_dev = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(S)]
             self.host = [torch.zeros(2 * world + 1, dtype=torch.int64).pin_memory() for _ in range(S)]
+            self.local_wm_at = [LONG_MIN] * S   # world 1: the aligned watermark is the local one (host-known)
             self.ready = [torch.cuda.Event() for _ in range(S)]
             self.pending = deque()      # (set, batch size) staged, not yet finished
             self.staged = 0
+            self.send_pushed_at = [None] * S   # engine push index that last read each send set (own share)
             # receive column sets: before a set is rewritten, torch's stream waits on the device for the
             # engine to have read it (fw_stream_wait_input), no host synchronisation
             self.RING = 3
@@ -92,7 +96,7 @@ class KeyByExchange:
         P = lambda x: ctypes.c_void_p(x.data_ptr())
         sk, st, sv = self.send[si]
         rc = self.eng.lib.fw_partition_by_operator(self.eng.h, P(k), None, None, P(t), P(v), n, self.mp, self.world,
-                                                   P(sk), None, None, P(st), P(sv), P(self.counts[si]),
+                                                   P(sk), None, None, P(st), P(sv), P(self.meta[si]),
                                                    P(self.offsets[si]))
         if rc != 0:
             raise RuntimeError(f"fw_partition_by_operator failed: {rc}")
@@ -104,19 +108,40 @@ class KeyByExchange:
         idx = torch.from_numpy(order)
         return k[idx], t[idx], v[idx], counts
 
+    def _transfer(self, send, send_splits, recv_splits, recv):
+        """The routed records between the ranks: `send` = (key, ts, value) sorted by destination with
+        send_splits per rank; the other ranks' shares land in `recv` (concatenated in rank order) through one
+        group of point-to-point sends / receives.  Returns this rank's own share: views of `send` (a local
+        channel, never copied).  Used by the GPU path (RCCL) and the CPU path (gloo) alike."""
+        me, w = self.rank, self.world
+        soff = np.concatenate([[0], np.cumsum(send_splits)]).astype(np.int64).tolist()
+        ops, roff = [], 0
+        for p in range(w):
+            if p == me:
+                continue
+            if recv_splits[p]:
+                c = recv_splits[p]
+                ops += [dist.P2POp(dist.irecv, x[roff:roff + c], p) for x in recv]
+                roff += c
+            if send_splits[p]:
+                ops += [dist.P2POp(dist.isend, x[soff[p]:soff[p + 1]], p) for x in send]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):   # one group; on RCCL wait() orders torch's stream after it
+                req.wait()
+        return tuple(x[soff[me]:soff[me + 1]] for x in send)
+
     def exchange(self, k, t, v):
-        """CPU (gloo) path: route a source batch to the key-group owners; returns this rank's received
-        (key, ts, value)."""
+        """CPU (gloo) path: route a source batch to the key-group owners; returns this rank's shares:
+        [(key, ts, value) of its own records, (key, ts, value) received from the others]."""
         assert not self.cuda, "the GPU path is pipelined: use step() / flush()"
         sk, st, sv, counts = self._route_host(k, t, v)
         recv_counts = torch.empty_like(counts)
         dist.all_to_all_single(recv_counts, counts)
         send_splits, recv_splits = torch.stack([counts, recv_counts]).tolist()
-        m = sum(recv_splits)
-        packed = torch.stack([sk, st, sv.view(torch.int64)], dim=1)
-        out = torch.empty((m, 3), dtype=torch.int64)
-        dist.all_to_all_single(out, packed, recv_splits, send_splits)
-        return out[:, 0].contiguous(), out[:, 1].contiguous(), out[:, 2].contiguous().view(v.dtype)
+        m = sum(recv_splits) - recv_splits[self.rank]
+        recv = (torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=v.dtype))
+        own = self._transfer((sk, st, sv.contiguous()), send_splits, recv_splits, recv)
+        return [own, recv]
 
     # ------------------------------------------------------------------ watermarks
     def _raise_local(self, wm_local):
@@ -140,26 +165,33 @@ class KeyByExchange:
     def step(self, k, t, v, wm_local):
         """Source batch (k, t, v) followed by this source's watermark wm_local."""
         if not self.cuda:
-            rk, rt, rv = self.exchange(k, t, v)
-            if rk.numel():
-                self.eng.push(rk.numpy(), rt.numpy(), rv.numpy())
+            for rk, rt, rv in self.exchange(k, t, v):   # both shares between the same watermarks
+                if rk.numel():
+                    self.eng.push(rk.numpy(), rt.numpy(), rv.numpy())
             self._forward(self.align_watermark(wm_local))
             return
+        # finish the oldest batch first: its push then waits (device-side) for the partitions enqueued so far
+        # only, and this batch's partition, enqueued below, overlaps with the engine's kernels of that batch
+        while len(self.pending) >= self.depth:
+            self._finish(*self.pending.popleft())
         si = self.staged % (self.depth + 1)
         self.staged += 1
+        # the engine may still read this send set (the own share pushed from it): wait on the device
+        if self.send_pushed_at[si] is not None:
+            back = self.pushes - 1 - self.send_pushed_at[si]
+            if back < 8:
+                self.eng.wait_input(torch.cuda.current_stream(self.device).cuda_stream, back)
         self._route_cuda(k, t, v, si)
-        dist.all_to_all_single(self.recv_counts[si], self.counts[si])
-        self.wm_dev[si].fill_(self._raise_local(wm_local))
-        dist.all_reduce(self.wm_dev[si], op=dist.ReduceOp.MIN)
-        h = self.host[si]
-        w = self.world
-        h[:w].copy_(self.counts[si], non_blocking=True)
-        h[w:2 * w].copy_(self.recv_counts[si], non_blocking=True)
-        h[2 * w:].copy_(self.wm_dev[si], non_blocking=True)
+        w, meta = self.world, self.meta[si]
+        local = self._raise_local(wm_local)
+        if w > 1:   # (one rank: its counts are its own receive counts, its watermark the aligned one)
+            dist.all_to_all_single(meta[w:2 * w], meta[:w])
+            meta[2 * w:].fill_(local)
+            dist.all_reduce(meta[2 * w:], op=dist.ReduceOp.MIN)
+        self.local_wm_at[si] = local
+        self.host[si].copy_(meta, non_blocking=True)
         self.ready[si].record()
         self.pending.append((si, k.numel()))
-        while len(self.pending) > self.depth:
-            self._finish(*self.pending.popleft())
 
     def flush(self):
         if self.cuda:
@@ -170,8 +202,12 @@ class KeyByExchange:
         self.ready[si].synchronize()   # counts of a batch staged `depth` steps ago: normally long done
         h = self.host[si].tolist()
         w = self.world
-        send_splits, recv_splits, aligned = h[:w], h[w:2 * w], h[2 * w]
-        m = sum(recv_splits)
+        if w > 1:
+            send_splits, recv_splits, aligned = h[:w], h[w:2 * w], h[2 * w]
+        else:
+            send_splits, recv_splits, aligned = h[:1], h[:1], self.local_wm_at[si]
+        me = self.rank
+        m = sum(recv_splits) - recv_splits[me]   # received from the other ranks
         slot = self.finished % self.RING
         self.finished += 1
         cols = self.ring[slot]
@@ -186,13 +222,19 @@ class KeyByExchange:
                 self.eng.wait_input(torch.cuda.current_stream(self.device).cuda_stream, back)
         rk, rt, rv = (x[:m] for x in cols)
         sk, st, sv = self.send[si]
-        for dst, src in ((rk, sk), (rt, st), (rv, sv)):
-            dist.all_to_all_single(dst, src[:n], recv_splits, send_splits)
-        if m:
-            if m > self.eng.cfg.max_batch:
-                raise ValueError(f"received {m} records, above the engine's max_batch {self.eng.cfg.max_batch}: "
+        own = self._transfer((sk[:n], st[:n], sv[:n]), send_splits, recv_splits, (rk, rt, rv))
+        as_value = (lambda x: x.view(torch.float64)) if self.eng.cfg.value_type == 1 else (lambda x: x)
+        for count, cols3, kind in ((send_splits[me], own, "send"), (m, (rk, rt, rv), "recv")):
+            if not count:
+                continue
+            if count > self.eng.cfg.max_batch:
+                raise ValueError(f"received {count} records, above the engine's max_batch {self.eng.cfg.max_batch}: "
                                  "size max_batch for the most skewed key-group range")
-            self.eng.push(rk, rt, rv.view(torch.float64) if self.eng.cfg.value_type == 1 else rv, keep_alive=False)
-            self.pushed_at[slot] = self.pushes
+            a, b, c = cols3
+            self.eng.push(a, b, as_value(c), keep_alive=False)   # both pushes lie between the same watermarks
+            if kind == "send":
+                self.send_pushed_at[si] = self.pushes
+            else:
+                self.pushed_at[slot] = self.pushes
             self.pushes += 1
         self._forward(aligned)
