@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sy
                     "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
                     "fw_get_profile", "fw_debug_counters", "fw_debug_stamps", "fw_set_stream", "fw_stream_wait_input",
                     "fw_version", "fw_snapshot_kg", "fw_restore_kg", "fw_snapshot_kg_flink", "fw_restore_kg_flink", "fw_decode")
-FW_SNAP_MAGIC, FW_SNAP_HEADER_WORDS, FW_SNAP_ENTRY_WORDS = 0x31474b5746574b, 12, 8
+FW_SNAP_MAGIC, FW_SNAP_HEADER_WORDS, FW_SNAP_ENTRY_WORDS = 0x31474b5746574b, 14, 8
 # state tuple fields of the Flink-layout checkpoint (fw_state_layout)
 FW_SF_KEY, FW_SF_F1, FW_SF_SUM, FW_SF_MIN, FW_SF_MAX, FW_SF_COUNT, FW_SF_VALUE, FW_SF_MAX_FIELDS = 1, 2, 3, 4, 5, 6, 7, 8
 FW_FT_LONG, FW_FT_DOUBLE, FW_FT_INT = 0, 1, 2
@@ -136,6 +136,14 @@ def load_library():
     """Load libflink_window.so (no fallback: a missing library is an error)."""
     global _lib
     if _lib is None:
+        # torch bundles its own HIP runtime; it has to initialise before the engine's (the image's ROCm) does,
+        # or torch finds no GPU later in the same process.  The engine itself does not use torch.
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:
+            pass
         _lib = open_library(LIB_PATH)
     return _lib
 

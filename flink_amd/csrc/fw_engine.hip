@@ -2897,9 +2897,10 @@ static int reject(fw_engine* e, int code, const std::string& msg) {
 
 static void snap_header(const fw_engine* e, int32_t kg, int64_t n, int64_t* h) {
   const fw_config& c = e->cfg;
-  const int64_t w[FW_SNAP_HEADER_WORDS] = {FW_SNAP_MAGIC, 1, kg, n, e->cur_wm, c.assigner, c.size,
+  const int64_t w[FW_SNAP_HEADER_WORDS] = {FW_SNAP_MAGIC, 2, kg, n, e->cur_wm, c.assigner, c.size,
                                           c.assigner == FW_SLIDING ? c.slide : c.size, c.offset, c.value_type,
-                                          c.agg_mask, c.keep_first_f1 ? 1 : 0};
+                                          c.agg_mask, c.keep_first_f1 ? 1 : 0, c.allowed_lateness,
+                                          (int64_t)c.trigger | ((int64_t)c.agg_flags << 8)};
   memcpy(h, w, sizeof(w));
 }
 
@@ -3002,7 +3003,7 @@ int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   const int64_t* h = (const int64_t*)buf;
   int64_t ref[FW_SNAP_HEADER_WORDS];
   snap_header(e, kg, h[3], ref);
-  if (h[0] != FW_SNAP_MAGIC || h[1] != 1) return reject(e, FW_ERR_INVALID_ARG, "not a key-group snapshot (magic/version)");
+  if (h[0] != FW_SNAP_MAGIC || h[1] != 2) return reject(e, FW_ERR_INVALID_ARG, "not a key-group snapshot (magic/version)");
   if (h[2] != kg) return reject(e, FW_ERR_INVALID_ARG, "snapshot holds key group " + std::to_string(h[2]));
   for (int w = 5; w < FW_SNAP_HEADER_WORDS; ++w)
     if (h[w] != ref[w]) return reject(e, FW_ERR_INVALID_ARG, "snapshot of a different window/reduce configuration");

@@ -174,8 +174,9 @@ void        fw_destroy(fw_engine* e);
  *                   + HeapInternalTimerService.restoreTimersForKeyGroup :319-345 (AbstractStreamOperator.java:405-425)
  * One blob per key group: FW_SNAP_HEADER_WORDS int64 header words, then n entries of FW_SNAP_ENTRY_WORDS
  * int64 words, native byte order:
- *   header  [0] FW_SNAP_MAGIC  [1] version (1)  [2] key group  [3] n entries  [4] watermark of the snapshot
+ *   header  [0] FW_SNAP_MAGIC  [1] version (2)  [2] key group  [3] n entries  [4] watermark of the snapshot
  *           [5] assigner  [6] size  [7] slide  [8] offset  [9] value_type  [10] agg_mask  [11] keep_first_f1
+ *           [12] allowed_lateness  [13] trigger | agg_flags << 8  (words 5-13 must match the restoring engine)
  *   entry   [0] slice number m (namespace: the window [m*size+offset, +size) for tumbling; the slice
  *               [m*g+offset, +g), g = gcd(size, slide), of which every window is made for sliding)
  *           [1] key  [2] sum  [3] min  [4] max  [5] count (double bits / Math.min-max codes for FW_VALUE_F64)
@@ -188,7 +189,7 @@ void        fw_destroy(fw_engine* e);
  * fw_snapshot_kg with buf == NULL (or cap too small) stores the required size in *len and returns
  * FW_OK (NULL) or FW_ERR_CAPACITY. */
 #define FW_SNAP_MAGIC         0x31474b5746574bLL   /* "KWFWKG1" */
-#define FW_SNAP_HEADER_WORDS  12
+#define FW_SNAP_HEADER_WORDS  14
 #define FW_SNAP_ENTRY_WORDS   8
 int         fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* len);
 int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len);

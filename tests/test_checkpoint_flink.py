@@ -270,6 +270,38 @@ def test_engine_matches_oracle_bytes_random(window):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_restore_at_long_min_keeps_records_late_at_the_checkpoint(mode):
+    """The reference restarts its timer service at Long.MIN_VALUE (HeapInternalTimerService.java:72, not
+    checkpointed): after a restore, records whose windows were already cleaned at the checkpoint are not
+    late until the next watermark — they build fresh panes that the next watermark fires
+    (WindowOperator.java:302-333).  Restored at INT64_MIN, the engine does the same as the oracle restored
+    the same way (pin restore watermark semantics)."""
+    from flink_amd.windowing import WindowEngine
+    from oracle.oracle import OracleEngine
+    sc = SCEN["tumbling_f64_min_max"]
+    want = _expected(sc)
+    cw = sc["checkpoint_wm"]
+    # records 1-3 s behind the checkpoint's watermark (their windows are gone), then the stream's rest
+    late_ts = np.array([cw - 3000, cw - 2500, cw - 1200, cw - 1100], np.int64)
+    late = dict(key=np.array([3, 5, 3, 7], np.int64), ts=late_ts, f1=np.arange(4, dtype=np.int64) + 9000,
+                value=np.array([1.5, -0.0, 2.25, 7.0]))
+    res = []
+    for factory in (WindowEngine, OracleEngine):
+        e = factory(_cfg(sc, mode=mode))
+        for kg, (st, tm) in want.items():
+            e.restore_kg_flink(kg, sc["layout"], st, tm, LONG_MIN)
+        e.push(late["key"], late["ts"], late["value"], f1=late["f1"])
+        out = [e.collect()]
+        out += _drive(e, sc, sc["cut"], len(sc["records"]), final=True)
+        res.append(_canon(epochs_of(out, ["sum_f64", "min_f64", "max_f64", "count"], True)))
+        e.close()
+    assert res[0] == res[1]
+    first_wm = res[1][0]
+    assert any(t < cw for _, t, *_ in first_wm[1]), "the late records fired at the first watermark"
+
+
+@pytest.mark.gpu
 def test_restore_rejections():
     from flink_amd import _abi
     from flink_amd.windowing import WindowEngine

@@ -35,6 +35,11 @@ def oracle_engine():
     return OracleEngine
 
 
+def _abi_words():
+    from flink_amd import _abi
+    return _abi.FW_SNAP_HEADER_WORDS
+
+
 def _cfg(assigner, fields, vt="i64", first=False, lateness=0, trigger=None, mode=0, kg=(0, MP - 1)):
     from flink_amd.windowing import ReduceFunction, make_config
     return make_config(assigner, ReduceFunction(fields, vt, first), trigger, lateness, max_parallelism=MP,
@@ -103,7 +108,7 @@ def _checkpoint_roundtrip(hip, oracle_engine, make_cfg, keys, ts, vals, batch, l
     e0 = hip(make_cfg((0, MP - 1)))
     r0 = _drive([e0], lambda k: np.zeros(len(k), np.int64), keys, ts, vals, range(cb), wms, batch)[0]
     state = {kg: e0.snapshot_kg(kg) for kg in range(MP)}
-    n_entries = sum((len(b) // 8 - 12) // 8 for b in state.values())
+    n_entries = sum((len(b) // 8 - _abi_words()) // 8 for b in state.values())
     assert n_entries > 0
     e0.close()
     # restore into `parallelism` subtasks, each taking its key-group range, and run the rest
@@ -176,7 +181,7 @@ def test_restore_errors(hip):
     e.advance_watermark(300)
     blobs = {kg: e.snapshot_kg(kg) for kg in range(MP)}
     kg = max(blobs, key=lambda k: len(blobs[k]))
-    hdr = np.frombuffer(blobs[kg], np.int64)[:12]
+    hdr = np.frombuffer(blobs[kg], np.int64)[:_abi_words()]
     assert hdr[0] == _abi.FW_SNAP_MAGIC and hdr[2] == kg and hdr[3] > 0 and hdr[4] == 300
     with pytest.raises(_abi.FwError) as ei:
         e.restore_kg(kg, blobs[kg])           # after the first push
@@ -192,6 +197,10 @@ def test_restore_errors(hip):
     with pytest.raises(_abi.FwError):
         sl.restore_kg(kg, blobs[kg])          # different window configuration
     sl.close()
+    lt = hip(_cfg(TumblingEventTimeWindows.of(1000), ("sum",), lateness=200))
+    with pytest.raises(_abi.FwError):
+        lt.restore_kg(kg, blobs[kg])          # different allowed lateness (the implicit timers would differ)
+    lt.close()
     f = hip(_cfg(TumblingEventTimeWindows.of(1000), ("sum",)))
     f.restore_kg(kg, blobs[kg])
     b2 = np.frombuffer(blobs[(kg + 1) % MP], np.int64).copy()

@@ -208,6 +208,21 @@ def test_hot_buckets_split_over_helpers(hip, oracle_engine, monkeypatch, case):
     _compare(epochs_of(rg, fields, True), epochs_of(ro, fields, True), fields, rel)
 
 
+@pytest.mark.parametrize("lateness", [0, 500])
+@pytest.mark.parametrize("mode", MODES)
+def test_first_arrival_with_tiles_spanning_many_slices(hip, oracle_engine, mode, lateness):
+    """Timestamps 1 s out of order over 100 ms windows: every 4096-record route tile holds records of ~10
+    slices, more than its RT_Q routed ones, so most slices reach a bucket both routed and through the
+    bucket's direct group (the first-arrival f1 after a tile's slice set overflows).  Bit-exact
+    incl. f1 against the oracle."""
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys, ts, vals = gen_stream(150_000, 2048, rate=1 << 14, ooo=1000)
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(100), ("sum", "count"), first=True, lateness=lateness,
+                max_open_slices=48)   # ~11 windows open behind the watermark, plus lateness
+    f1 = np.arange(len(keys), dtype=np.int64) * 11 + 5
+    _run_both(hip, oracle_engine, cfg, keys, ts, vals, 1 << 14, 150, ["sum_i64", "count"], first=True, f1=f1)
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_purging_trigger_lateness(hip, oracle_engine, mode):
     from flink_amd.windowing import EventTimeTrigger, PurgingTrigger, TumblingEventTimeWindows
