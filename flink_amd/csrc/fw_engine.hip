@@ -2066,8 +2066,12 @@ struct fw_engine {
   hipEvent_t ev_in = nullptr;         // client work up to a push (input columns ready)
   static constexpr int NCONS = 8;
   hipEvent_t ev_consumed[NCONS] = {};  // per push (ring): every read of that push's input columns done
-  hipEvent_t ev_route[2] = {nullptr, nullptr};   // k_route of the batch with that parity done
-  hipEvent_t ev_agg[2] = {nullptr, nullptr};     // k_aggregate of the batch with that parity done
+  // routed batches rotate over NBUF buffer sets: k_route of batch j waits only for k_aggregate of batch
+  // j - NBUF, long finished, so neither stream waits on the other's latest kernel (a cross-stream wait costs
+  // ~13 us of signal latency on MI355X, measured: profiles/r02_v13_timeline.txt)
+  static constexpr int NBUF = 3;
+  hipEvent_t ev_route[NBUF] = {};     // k_route of the batch using that buffer set done
+  hipEvent_t ev_agg[NBUF] = {};       // k_aggregate of the batch using that buffer set done
   Spec s{};
   int64_t cur_wm = INT64_MIN;
   int64_t ordinal = 0;
@@ -2088,8 +2092,8 @@ struct fw_engine {
   int grid = 0;
   std::vector<void*> allocs;
   // staging for host-memory (and misaligned device) pushes, one set per batch parity
-  int64_t *stg_key[2] = {}, *stg_ts[2] = {}, *stg_val[2] = {}, *stg_f1[2] = {};
-  int32_t* stg_hash[2] = {};
+  int64_t *stg_key[NBUF] = {}, *stg_ts[NBUF] = {}, *stg_val[NBUF] = {}, *stg_f1[NBUF] = {};
+  int32_t* stg_hash[NBUF] = {};
   // late path
   unsigned long long *late_key = nullptr, *late_key_sorted = nullptr, *late_count = nullptr, *seg = nullptr;
   unsigned long long* out_base = nullptr;   // first output slot reserved for a per-element emit kernel
@@ -2135,7 +2139,7 @@ struct fw_engine {
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
   RouteBuf rb{};                            // fields shared by both parities (dbg, stamps)
-  RouteBuf rbs[2] = {};                     // routed-batch buffers, one set per batch parity
+  RouteBuf rbs[NBUF] = {};                  // routed-batch buffers, one set per buffer slot
   unsigned int* dflags = nullptr;           // direct-record flags, a ring of FLAG_RING
   unsigned int* bload = nullptr;            // [4][RT_MAXNB] routed records per bucket and batch (k_aggregate split plan)
   unsigned int* fold_flag = nullptr;        // [RT_MAXNB][RT_GS]
@@ -2161,7 +2165,14 @@ struct fw_engine {
   int64_t* part_block_counts = nullptr;
   int64_t part_blocks_cap = 0;
   // host output copies
-  std::vector<int64_t> h_key, h_f1, h_ts, h_sum, h_mn, h_mx, h_cnt, h_mark_wm, h_mark_pos;
+  std::vector<int64_t> h_key, h_f1, h_ts, h_sum, h_mn, h_mx, h_cnt, h_mark_wm, h_mark_pos, h_dev_pos;
+  // watermark marks since the last collect, in emission order.  A firing watermark's kernel (and a
+  // k_mark_only) writes a device mark; a quiet watermark with no output appended since the previous
+  // device mark launches nothing: its position is that mark's (dev < 0: the start of the log)
+  struct HostMark { int64_t wm; int64_t dev; bool own; };
+  std::vector<HostMark> hmarks;
+  int64_t dev_marks = 0;        // device marks enqueued since the last collect
+  bool out_dirty = false;       // output appended (per-element fires) after the last device mark
   std::vector<double> h_sum_d, h_mn_d, h_mx_d;
   int dev = 0;
 
@@ -2177,7 +2188,8 @@ struct fw_engine {
     if (stream) (void)hipStreamSynchronize(stream);
     if (rstream) (void)hipStreamDestroy(rstream);
     if (stream) (void)hipStreamDestroy(stream);
-    for (hipEvent_t ev : {ev_in, ev_route[0], ev_route[1], ev_agg[0], ev_agg[1]}) if (ev) (void)hipEventDestroy(ev);
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    for (int q = 0; q < NBUF; ++q) for (hipEvent_t ev : {ev_route[q], ev_agg[q]}) if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : ev_consumed) if (ev) (void)hipEventDestroy(ev);
     for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
@@ -2342,7 +2354,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   e->serial = getenv("FW_SERIAL") && atoi(getenv("FW_SERIAL")) != 0;
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < fw_engine::NBUF; ++q) {
     HIPCHK(e, hipEventCreateWithFlags(&e->ev_route[q], hipEventDisableTiming));
     HIPCHK(e, hipEventCreateWithFlags(&e->ev_agg[q], hipEventDisableTiming));
   }
@@ -2439,7 +2451,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     else if (cf) e->compact_fill = std::min(atoi(cf), 95) / 100.0;
   }
 
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < fw_engine::NBUF; ++q) {
     e->stg_key[q] = e->alloc<int64_t>((size_t)c.max_batch);
     e->stg_ts[q] = e->alloc<int64_t>((size_t)c.max_batch);
     e->stg_val[q] = e->alloc<int64_t>((size_t)c.max_batch);
@@ -2473,7 +2485,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       if (e->bload_host) memset(e->bload_host, 0, 4 * RT_MAXNB);
       const char* hv = getenv("FW_AGG_HELPERS");
       if (hv) e->agg_helpers_max = std::max(0, std::min(atoi(hv), (int)RT_MAXNB));
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < fw_engine::NBUF; ++q) {
         RouteBuf& r = e->rbs[q];
         r = e->rb;
         r.kv = e->alloc<longlong2>(cap);
@@ -2588,8 +2600,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (key_hash) e->used_key_hash = true;
   e->state_epoch++;
   // routed form: the batch's copies and k_route run on the route stream, k_aggregate on the engine
-  // stream; buffers of batch parity par are reused only after k_aggregate of batch j-2 finished
-  const int par = (int)(e->batches & 1);
+  // stream; buffer set par is reused only after k_aggregate of batch j - NBUF finished
+  const int par = (int)(e->batches % fw_engine::NBUF);
+  const int half = (int)(e->batches & 1);   // the direct form's new-pane list counters alternate
   hipStream_t in_stream = e->routed && !e->serial ? e->rstream : e->stream;
   if (e->routed) HIPCHK(e, hipStreamWaitEvent(in_stream, e->ev_agg[par], 0));
   if (e->has_client) {   // input columns are produced on the caller's stream
@@ -2627,7 +2640,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.fire_count = e->fire_count;
   b.fire_capacity = e->fire_cap;
   b.new_list = e->new_list;
-  b.new_count = e->new_counts ? e->new_counts + par : nullptr;
+  b.new_count = e->new_counts ? e->new_counts + half : nullptr;
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
   if (e->routed) {
     FW_DISPATCH(launch_routed_t, e, b, df1, par);
@@ -2641,7 +2654,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (e->s.first && !e->routed) {   // the partitioned form sets f1 in k_aggregate
     e->phase_begin(FW_PHASE_FIXUP);
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
-                       e->stream, e->s, e->new_list, e->new_counts + par, e->new_counts + (par ^ 1), df1, e->ordinal, n,
+                       e->stream, e->s, e->new_list, e->new_counts + half, e->new_counts + (half ^ 1), df1, e->ordinal, n,
                        e->cfg.max_batch);
     e->phase_end(n);
   }
@@ -2693,6 +2706,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
       HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
     }
     if (nl > 0 || nf > 0) e->phase_end((int64_t)(nl + nf));
+    if (nf > 0 || (nl > 0 && !sliding)) e->out_dirty = true;
   }
   HIPCHK(e, hipGetLastError());
   // every reader of this push's columns (k_route, k_aggregate's direct records, the f1 fix-up, the late
@@ -2717,8 +2731,14 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   HIPCHK(e, hipSetDevice(e->dev));
   e->state_epoch++;
   if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
-    hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
-    HIPCHK(e, hipGetLastError());
+    if (e->out_dirty) {   // per-element fires appended since the last device mark: the mark needs the count
+      hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
+      HIPCHK(e, hipGetLastError());
+      e->hmarks.push_back({wm, e->dev_marks++, true});
+      e->out_dirty = false;
+    } else {              // no launch: the position of the previous device mark
+      e->hmarks.push_back({wm, e->dev_marks - 1, false});
+    }
     if (wm > e->cur_wm) e->cur_wm = wm;
     return FW_OK;
   }
@@ -2726,6 +2746,8 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   FW_DISPATCH(launch_watermark_t, e, e->cur_wm, wm);
   e->phase_end(e->s.stride);
   HIPCHK(e, hipGetLastError());
+  e->hmarks.push_back({wm, e->dev_marks++, true});
+  e->out_dirty = false;
   e->cur_wm = wm;
   // evict dead keys once the directory is more than compact_fill full (the count posted by an earlier
   // firing watermark: read without a sync)
@@ -2759,17 +2781,38 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
   HIPCHK(e, hipMemcpyAsync(&mc, e->s.o.mark_count, 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if ((int64_t)cnt > e->s.o.capacity) return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded");
+  const OutLog& L = e->s.o;
+  // the marks in emission order: device marks as written, the others at the position of the device mark
+  // before them
+  const int64_t nm = (int64_t)e->hmarks.size();
+  if (nm > L.mark_capacity || (int64_t)mc != e->dev_marks) return fail(e, FW_ERR_CAPACITY, "watermark mark log capacity exceeded");
+  e->h_dev_pos.resize((size_t)std::max<int64_t>(e->dev_marks, 1));
+  if (e->dev_marks > 0)
+    HIPCHK(e, hipMemcpy(e->h_dev_pos.data(), L.mark_pos, 8 * (size_t)e->dev_marks, hipMemcpyDeviceToHost));
+  e->h_mark_wm.resize((size_t)std::max<int64_t>(nm, 1));
+  e->h_mark_pos.resize((size_t)std::max<int64_t>(nm, 1));
+  for (int64_t i = 0; i < nm; ++i) {
+    const auto& m = e->hmarks[(size_t)i];
+    e->h_mark_wm[(size_t)i] = m.wm;
+    e->h_mark_pos[(size_t)i] = m.dev >= 0 ? e->h_dev_pos[(size_t)m.dev] : 0;
+  }
+  e->hmarks.clear();
+  e->dev_marks = 0;
+  e->out_dirty = false;
   const int64_t n = (int64_t)cnt;
   std::memset(o, 0, sizeof(*o));
   o->n = n;
-  o->n_marks = (int64_t)mc;
-  const OutLog& L = e->s.o;
+  o->n_marks = nm;
   const bool f64 = e->s.vt == FW_VALUE_F64;
   if (mem == FW_MEM_DEVICE) {
     o->key = L.key; o->f1 = L.f1; o->ts = L.ts;
     if (f64) { o->sum_f64 = (const double*)L.sum; o->min_f64 = (const double*)L.mn; o->max_f64 = (const double*)L.mx; }
     else { o->sum_i64 = L.sum; o->min_i64 = L.mn; o->max_i64 = L.mx; }
     o->count = L.cnt;
+    if (nm > 0) {   // the merged marks back into the device arrays
+      HIPCHK(e, hipMemcpy(L.mark_wm, e->h_mark_wm.data(), 8 * (size_t)nm, hipMemcpyHostToDevice));
+      HIPCHK(e, hipMemcpy(L.mark_pos, e->h_mark_pos.data(), 8 * (size_t)nm, hipMemcpyHostToDevice));
+    }
     o->mark_wm = L.mark_wm; o->mark_pos = L.mark_pos;
   } else {
     auto cp = [&](std::vector<int64_t>& h, const int64_t* d, int64_t cnt_) -> const int64_t* {
@@ -2787,8 +2830,8 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
     o->count = cp(e->h_cnt, L.cnt, n);
     if (f64) { o->sum_f64 = (const double*)su; o->min_f64 = (const double*)mn; o->max_f64 = (const double*)mx; }
     else { o->sum_i64 = su; o->min_i64 = mn; o->max_i64 = mx; }
-    o->mark_wm = cp(e->h_mark_wm, L.mark_wm, (int64_t)mc);
-    o->mark_pos = cp(e->h_mark_pos, L.mark_pos, (int64_t)mc);
+    o->mark_wm = e->h_mark_wm.data();
+    o->mark_pos = e->h_mark_pos.data();
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   // only the fields the reduce function asked for
