@@ -21,6 +21,7 @@ FW_ERR_DEVICE = 6
 
 FW_TUMBLING = 0
 FW_SLIDING = 1
+FW_SESSION = 2
 FW_TRIGGER_EVENT_TIME = 0
 FW_TRIGGER_PURGING_EVENT_TIME = 1
 FW_AGG_SUM = 1
@@ -31,6 +32,7 @@ FW_AGG_MAXBY = 16
 FW_AGG_MINBY = 32
 FW_AGGF_COMPARABLE = 1
 FW_AGGF_BY_LAST = 2
+FW_AGGF_FOLD = 4
 FW_VALUE_I64 = 0
 FW_VALUE_F64 = 1
 FW_MEM_HOST = 0
@@ -57,13 +59,13 @@ class FwConfig(ctypes.Structure):
                 ("allowed_lateness", _i64), ("value_type", _i32), ("agg_mask", _i32), ("keep_first_f1", _i32),
                 ("max_parallelism", _i32), ("kg_start", _i32), ("kg_end", _i32), ("device", _i32),
                 ("max_open_slices", _i32), ("key_capacity", _i64), ("max_batch", _i64), ("out_capacity", _i64),
-                ("ingest_mode", _i32), ("agg_flags", _i32)]
+                ("ingest_mode", _i32), ("agg_flags", _i32), ("fold_initial", _i64)]
 
 
 class FwOut(ctypes.Structure):
     _fields_ = [("n", _i64), ("key", _pi64), ("f1", _pi64), ("ts", _pi64), ("sum_i64", _pi64), ("min_i64", _pi64),
                 ("max_i64", _pi64), ("count", _pi64), ("sum_f64", _pf64), ("min_f64", _pf64), ("max_f64", _pf64),
-                ("n_marks", _i64), ("mark_wm", _pi64), ("mark_pos", _pi64)]
+                ("n_marks", _i64), ("mark_wm", _pi64), ("mark_pos", _pi64), ("win_start", _pi64)]
 
 
 class FwStateLayout(ctypes.Structure):

@@ -16,7 +16,8 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 ENGINE_SOURCES = ["fw_engine.hip"]
-ENGINE_DEPS = ["java_semantics.h", os.path.join("..", "..", "include", "flink_window.h"), "flink_kg_format.h", "fw_decode.hip"]
+ENGINE_DEPS = ["java_semantics.h", os.path.join("..", "..", "include", "flink_window.h"), "flink_kg_format.h", "fw_decode.hip",
+               "fw_session.hip"]
 
 
 def _stale(target, deps):

@@ -89,6 +89,7 @@ struct OutLog {
   int64_t* mark_pos;
   unsigned long long* mark_count;
   int64_t mark_capacity;
+  int64_t* win_start;   // session windows: window.getStart() of each result
 };
 
 struct Spec {  // window specification + reduce + subtask, passed by value
@@ -103,6 +104,8 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int32_t cmpto;    // min/max of doubles in Double.compareTo order (ComparableAggregator), else Math.min/max
   int32_t by;       // 0, FW_AGG_MAXBY or FW_AGG_MINBY: the extremal record (value, f1) is the result
   int32_t by_last;  // maxBy/minBy tie rule: the later record (first = false)
+  int32_t fold;     // WindowedStream.fold: every result starts from fold_init (applied where results are emitted)
+  int64_t fold_init;
   // directory
   int64_t* dir_keys;
   int32_t* dir_min_used;
@@ -1500,6 +1503,24 @@ __device__ __forceinline__ LateAcc pane_load(const Spec& s, int64_t idx) {
 __device__ __forceinline__ void emit_record(const Spec& s, unsigned long long pos, int64_t key, int64_t f1, int64_t ts,
                                             const LateAcc& a) {
   if ((int64_t)pos >= s.o.capacity) { cap_error(s, 11); return; }
+  if (s.fold) {   // HeapFoldingState: the first record folded into the initial value (every fold here associates)
+    LateAcc f = a;
+    const int64_t x = s.fold_init;
+    if (s.vt == FW_VALUE_I64) f.sum = jadd(x, a.sum);
+    else f.sum = __double_as_longlong(__longlong_as_double(x) + __longlong_as_double(a.sum));
+    const int64_t cn = min_code(s.vt, s.cmpto, x), cx = max_code(s.vt, s.cmpto, x);
+    f.mn = cn < a.mn ? cn : a.mn;
+    f.mx = cx > a.mx ? cx : a.mx;
+    f.cnt = jadd(x, a.cnt);
+    s.o.key[pos] = key;
+    if (s.o.f1) s.o.f1[pos] = f1;
+    s.o.ts[pos] = ts;
+    if (s.o.sum) s.o.sum[pos] = f.sum;
+    if (s.o.mn) s.o.mn[pos] = s.vt == FW_VALUE_I64 ? f.mn : __double_as_longlong(f64_from_code(f.mn));
+    if (s.o.mx) s.o.mx[pos] = s.vt == FW_VALUE_I64 ? f.mx : __double_as_longlong(f64_from_code(f.mx));
+    if (s.o.cnt) s.o.cnt[pos] = f.cnt;
+    return;
+  }
   s.o.key[pos] = key;
   if (s.o.f1) s.o.f1[pos] = f1;
   s.o.ts[pos] = ts;
@@ -2052,6 +2073,21 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+// session windows (fw_session.hip): per key id `sw` window slots, key-major [D + 1][sw]
+constexpr int SESS_SW_DEFAULT = 32, SESS_SW_MAX = 64;   // in-flight session windows per key
+struct SessDev {
+  int64_t gap;
+  int32_t sw;
+  int64_t* start;   // window [start, end)
+  int64_t* end;
+  int64_t* sum;     // accumulator: sum (long / double bits), min / max codes, count
+  int64_t* mn;
+  int64_t* mx;
+  int64_t* cnt;
+  unsigned long long* live;   // [D + 1] slots in flight
+  unsigned long long* trig;   // [D + 1] slots whose trigger timer (at maxTimestamp) is pending
+};
+
 }  // namespace
 
 struct fw_engine {
@@ -2155,6 +2191,13 @@ struct fw_engine {
   void *dec_table = nullptr, *dec_small = nullptr, *dec_bytes = nullptr;
   size_t dec_table_cap = 0, dec_small_cap = 0, dec_bytes_cap = 0;
   int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
+  // session windows (FW_SESSION, fw_session.hip)
+  bool session = false;
+  SessDev sess{};
+  unsigned long long *sess_key = nullptr, *sess_sorted = nullptr;
+  void* sess_temp = nullptr;
+  size_t sess_temp_bytes = 0;
+  int32_t sess_idx_bits = 0, sess_key_bits = 0;
   int64_t batches = 0;
   int32_t max_tiles = 0;
   size_t route_lds = 0, agg_lds = 0;
@@ -2165,7 +2208,7 @@ struct fw_engine {
   int64_t* part_block_counts = nullptr;
   int64_t part_blocks_cap = 0;
   // host output copies
-  std::vector<int64_t> h_key, h_f1, h_ts, h_sum, h_mn, h_mx, h_cnt, h_mark_wm, h_mark_pos, h_dev_pos;
+  std::vector<int64_t> h_key, h_f1, h_ts, h_sum, h_mn, h_mx, h_cnt, h_mark_wm, h_mark_pos, h_dev_pos, h_start;
   // watermark marks since the last collect, in emission order.  A firing watermark's kernel (and a
   // k_mark_only) writes a device mark; a quiet watermark with no output appended since the previous
   // device mark launches nothing: its position is that mark's (dev < 0: the start of the log)
@@ -2201,6 +2244,11 @@ struct fw_engine {
 };
 
 static thread_local std::string g_create_error;
+
+// session windows (fw_session.hip)
+int session_create(fw_engine* e);
+int session_push(fw_engine* e, const fw::BatchIn& b);
+int session_watermark(fw_engine* e, int64_t wm);
 
 static int fail(fw_engine* e, int code, const std::string& msg) {
   if (e) { e->err = msg; if (e->sticky == FW_OK) e->sticky = code; }
@@ -2333,7 +2381,16 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   auto bad = [&](const char* m) { g_create_error = m; delete e; return FW_ERR_INVALID_ARG; };
   auto unsupported = [&](const char* m) { g_create_error = m; delete e; return FW_ERR_UNSUPPORTED; };
   if (c.size <= 0) return bad("window size must be > 0");
-  if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING) return bad("unknown assigner");
+  if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING && c.assigner != FW_SESSION) return bad("unknown assigner");
+  e->session = c.assigner == FW_SESSION;
+  if (e->session && (c.keep_first_f1 || (c.agg_mask & (FW_AGG_MAXBY | FW_AGG_MINBY))))
+    return unsupported("session windows: first-arrival f1 and maxBy / minBy follow HashSet order after a merge "
+                       "(sum / min / max / count only)");
+  if (e->session) {
+    if (c.max_open_slices > SESS_SW_MAX) return bad("session windows: at most 64 in-flight sessions per key (max_open_slices)");
+    e->sess.sw = c.max_open_slices > 0 ? c.max_open_slices : SESS_SW_DEFAULT;
+    c.slide = c.size; c.offset = 0; c.max_open_slices = 1; c.ingest_mode = 1; e->cfg = c;
+  }
   if (c.assigner == FW_SLIDING && c.slide <= 0) return bad("slide must be > 0");
   if (c.allowed_lateness < 0) return bad("allowed lateness must be >= 0");
   if (c.max_parallelism <= 0 || c.max_parallelism > (1 << 15) || c.kg_start < 0 || c.kg_end < c.kg_start ||
@@ -2343,7 +2400,12 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   const bool by = (c.agg_mask & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;
   if ((c.agg_mask & ~63) != 0 || c.agg_mask == 0 || (by && c.agg_mask != FW_AGG_MAXBY && c.agg_mask != FW_AGG_MINBY))
     return bad("bad aggregate mask (maxBy / minBy return the whole record and combine with nothing else)");
-  if ((c.agg_flags & ~(FW_AGGF_COMPARABLE | FW_AGGF_BY_LAST)) != 0) return bad("bad aggregate flags");
+  if ((c.agg_flags & ~(FW_AGGF_COMPARABLE | FW_AGGF_BY_LAST | FW_AGGF_FOLD)) != 0) return bad("bad aggregate flags");
+  if ((c.agg_flags & FW_AGGF_FOLD) && (c.assigner == FW_SESSION))
+    return unsupported("Fold cannot be used with a merging WindowAssigner.");
+  if ((c.agg_flags & FW_AGGF_FOLD) && (c.keep_first_f1 || !(c.agg_mask == FW_AGG_SUM || c.agg_mask == FW_AGG_MIN ||
+                                                              c.agg_mask == FW_AGG_MAX || c.agg_mask == FW_AGG_COUNT)))
+    return unsupported("fold: one aggregate (sum, count, min or max) from the initial value, no first-arrival f1");
   if (by && c.ingest_mode == 1) return unsupported("maxBy / minBy run on the partitioned ingest form (ingest_mode 0 or 2)");
   if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
   if (c.ingest_mode < 0 || c.ingest_mode > 2) return bad("bad ingest mode");
@@ -2384,6 +2446,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.by = by ? c.agg_mask : 0;
   s.by_last = (c.agg_flags & FW_AGGF_BY_LAST) ? 1 : 0;
   s.cmpto = by || (c.agg_flags & FW_AGGF_COMPARABLE) ? 1 : 0;
+  s.fold = (c.agg_flags & FW_AGGF_FOLD) ? 1 : 0;
+  s.fold_init = c.fold_initial;
   s.first = c.keep_first_f1 || by ? 1 : 0;   // maxBy/minBy: the pane's presence and the extremal f1
 
   // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys): short linear-probe sequences
@@ -2440,7 +2504,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   // key directory compaction (k_compact): buckets that fit LDS
   e->kg_evicted = e->alloc<unsigned char>((size_t)c.max_parallelism);
   e->compact_lds = compact_lds_bytes(s.kb_bits, s.P);
-  e->compact_ok = s.kb_bits <= 12 && e->compact_lds <= 160 * 1024;
+  e->compact_ok = s.kb_bits <= 12 && e->compact_lds <= 160 * 1024 && !e->session;
   if (e->compact_ok) {
     if (hipHostMalloc((void**)&e->dir_keys_host, 4, hipHostMallocMapped) != hipSuccess) e->dir_keys_host = nullptr;
     if (e->dir_keys_host) *e->dir_keys_host = 0;
@@ -2470,7 +2534,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
                       c.max_batch <= (1ll << 26);
     if (c.ingest_mode == 2 && !fits)
       return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
-    e->routed = c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by));
+    e->routed = !e->session && (c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by)));
     if (by && !e->routed) return unsupported("maxBy / minBy need the partitioned ingest form (key_capacity <= 256 Ki)");
     if (e->routed) {
       e->max_tiles = max_tiles;
@@ -2541,6 +2605,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->late_count = e->alloc<unsigned long long>(1);
   }
 
+  if (e->session) {
+    if (int rc = session_create(e)) { g_create_error = "session window state allocation failed"; delete e; return rc; }
+  }
   // initial state
   launch_fill(e, s.dir_keys, EMPTY_KEY, s.D);
   launch_fill(e, s.slice_tag, FREE_TAG, P);
@@ -2642,7 +2709,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.new_list = e->new_list;
   b.new_count = e->new_counts ? e->new_counts + half : nullptr;
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
-  if (e->routed) {
+  if (e->session) {
+    if (int rc = session_push(e, b)) return rc;
+  } else if (e->routed) {
     FW_DISPATCH(launch_routed_t, e, b, df1, par);
   } else {
     e->phase_begin(FW_PHASE_INGEST);
@@ -2658,7 +2727,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
                        e->cfg.max_batch);
     e->phase_end(n);
   }
-  if (e->cfg.allowed_lateness > 0) {
+  if (e->cfg.allowed_lateness > 0 && !e->session) {
     // per-element fires: the list lengths on the host size the sorts
     unsigned long long nl = 0, nf = 0;
     HIPCHK(e, hipMemcpyAsync(&nl, e->late_count, 8, hipMemcpyDeviceToHost, e->stream));
@@ -2730,6 +2799,7 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   if (e->sticky) return e->sticky;
   HIPCHK(e, hipSetDevice(e->dev));
   e->state_epoch++;
+  if (e->session) return session_watermark(e, wm);
   if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
     if (e->out_dirty) {   // per-element fires appended since the last device mark: the mark needs the count
       hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
@@ -2814,6 +2884,7 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
       HIPCHK(e, hipMemcpy(L.mark_pos, e->h_mark_pos.data(), 8 * (size_t)nm, hipMemcpyHostToDevice));
     }
     o->mark_wm = L.mark_wm; o->mark_pos = L.mark_pos;
+    o->win_start = L.win_start;
   } else {
     auto cp = [&](std::vector<int64_t>& h, const int64_t* d, int64_t cnt_) -> const int64_t* {
       if (!d) return nullptr;
@@ -2828,6 +2899,7 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
     const int64_t* mn = cp(e->h_mn, L.mn, n);
     const int64_t* mx = cp(e->h_mx, L.mx, n);
     o->count = cp(e->h_cnt, L.cnt, n);
+    o->win_start = cp(e->h_start, L.win_start, n);
     if (f64) { o->sum_f64 = (const double*)su; o->min_f64 = (const double*)mn; o->max_f64 = (const double*)mx; }
     else { o->sum_i64 = su; o->min_i64 = mn; o->max_i64 = mx; }
     o->mark_wm = e->h_mark_wm.data();
@@ -2859,7 +2931,7 @@ int fw_get_stats(fw_engine* e, fw_stats* st) {
   st->records_in = e->records_in;
   st->records_late = (int64_t)d[ST_LATE];
   st->panes_fired = (int64_t)d[ST_FIRED] + e->late_fires_host;
-  st->late_fires = e->late_fires_host;
+  st->late_fires = e->late_fires_host + (int64_t)d[ST_LATE_FIRES];   // (device-counted: session windows)
   int64_t live = 0;
   for (int64_t t : tags) live += t != FREE_TAG;
   st->slices_live = live;
@@ -3018,6 +3090,8 @@ static int build_snapshot(fw_engine* e) {
 
 int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* len) {
   if (!e || !len) return FW_ERR_INVALID_ARG;
+  if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)   // HeapInternalTimerService.restoreTimersForKeyGroup's check
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -3040,6 +3114,8 @@ static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t
 
 int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   if (!e || !buf) return FW_ERR_INVALID_ARG;
+  if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
   if (len < 8 * FW_SNAP_HEADER_WORDS) return reject(e, FW_ERR_INVALID_ARG, "snapshot blob too short");
@@ -3219,6 +3295,8 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
 int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, void* state, int64_t state_cap,
                          int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
   if (!e || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
+  if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -3327,6 +3405,8 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
 int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
                         const void* state, int64_t state_len, const void* timers, int64_t timers_len) {
   if (!e || (!state && state_len) || !timers || state_len < 0) return FW_ERR_INVALID_ARG;
+  if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
   if (kg < e->s.kg_start || kg > e->s.kg_end)
@@ -3459,3 +3539,4 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
 }  // extern "C"
 
 #include "fw_decode.hip"
+#include "fw_session.hip"

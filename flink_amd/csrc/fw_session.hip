@@ -1,0 +1,286 @@
+// fw_session.hip — event-time session windows on the GPU (included by fw_engine.hip).
+//
+// Replaces the merging branch of WindowOperator.processElement (SJ/runtime/operators/windowing/
+// WindowOperator.java:228-301) over MergingWindowSet (MergingWindowSet.java:142-214, TimeWindow.mergeWindows
+// TimeWindow.java:186-230) and its timers (EventTimeTrigger.onMerge :70-74, onEventTime :344-375), for
+// EventTimeSessionWindows.withGap (EventTimeSessionWindows.java:53-56) with a reducing state of
+// sum / min / max / count.
+//
+// Layout in HBM: per key id (the engine's key directory) `sw` window slots (max_open_slices, default 32),
+// key-major ([D + 1][sw]) so one key's windows share cache lines: window start / end and the accumulator
+// (sum, min / max codes, count); per key two bit masks: slots in flight, slots whose trigger timer is
+// pending.
+//
+// A batch (every record of it sees the same watermark): k_sess_prep resolves each record's key id,
+// rocPRIM sorts (key id, arrival index), and k_sess_walk runs one thread per key over that key's records in
+// arrival order — the reference's per-record state machine, exactly: a new window [ts, ts + gap) merges
+// with every in-flight window it intersects (start <= other.end && end >= other.start), the merged window's
+// trigger timer is registered and the merged windows' timers dropped; the late check applies to the
+// resulting window; the record is reduced into it; onElement fires it at once when its maxTimestamp is
+// already behind the watermark (allowed lateness), purging it under PurgingTrigger.  Keys are independent,
+// so keys run in parallel.  Cleanup timers are implicit: every in-flight window has one, at
+// cleanupTime = maxTimestamp + lateness (clamped).
+//
+// Fixed-gap sessions never meet MergingWindowSet's state-window corner (a new window equal to a merged
+// one: merged windows are longer than the gap), so which merged window holds the state does not matter
+// for order-insensitive fields; first-arrival f1, maxBy / minBy and double sums after a merge follow the
+// JDK HashSet iteration order of the merged windows and are not offered (doubles: within the tolerance).
+//
+// A watermark: k_sess_wm, one thread per key: each live window's timers in time order — the trigger timer
+// at maxTimestamp (FIRE; PurgingTrigger: FIRE_AND_PURGE; cleanup when maxTimestamp is also the cleanup
+// time), then the cleanup timer (retire).  Results are appended wave-aggregated.
+
+namespace fw {
+
+__device__ __forceinline__ void sess_emit(const Spec& s, unsigned long long pos, int64_t key, int64_t start, int64_t max_ts,
+                                          const LateAcc& a) {
+  emit_record(s, pos, key, 0, max_ts, a);
+  if ((int64_t)pos < s.o.capacity) s.o.win_start[pos] = start;
+}
+
+__device__ __forceinline__ LateAcc sess_load(const Spec& s, const SessDev& d, int64_t x) {
+  LateAcc a;
+  a.vt = s.vt;
+  a.sum = d.sum ? d.sum[x] : 0;
+  a.mn = d.mn ? d.mn[x] : INT64_MAX;
+  a.mx = d.mx ? d.mx[x] : INT64_MIN;
+  a.cnt = d.cnt ? d.cnt[x] : 0;
+  return a;
+}
+__device__ __forceinline__ void sess_store(const SessDev& d, int64_t x, const LateAcc& a) {
+  if (d.sum) d.sum[x] = a.sum;
+  if (d.mn) d.mn[x] = a.mn;
+  if (d.mx) d.mx[x] = a.mx;
+  if (d.cnt) d.cnt[x] = a.cnt;
+}
+
+// per record: key group check (AbstractKeyedStateBackend.setCurrentKey :167-170), key id, and the sort key
+// (key id << idx_bits) | arrival index (invalid records sort last)
+__global__ __launch_bounds__(BLOCK) void k_sess_prep(Spec s, BatchIn b, unsigned long long* skey, int32_t idx_bits) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t key = b.key[i];
+    const int32_t h = b.key_hash ? b.key_hash[i] : long_hash_code(key);
+    unsigned long long k = ~0ull;
+    const int32_t kg = record_key_group(s, h);
+    if (kg < s.kg_start || kg > s.kg_end) {
+      set_error(s.err, FW_ERR_KEY_GROUP);
+    } else {
+      const int64_t kid = dir_find_or_insert(s, key);
+      if (kid < 0) cap_error(s, 20);
+      else k = ((unsigned long long)kid << idx_bits) | (unsigned long long)i;
+    }
+    skey[i] = k;
+  }
+}
+
+// one thread per key (the head of its run in the sorted keys): the key's records in arrival order
+__global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn b, const unsigned long long* sorted,
+                                                     int64_t n, int32_t idx_bits) {
+  const int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j0 >= n) return;
+  const unsigned long long k0 = sorted[j0];
+  if (k0 == ~0ull) return;
+  const int64_t kid = (int64_t)(k0 >> idx_bits);
+  if (j0 > 0 && (sorted[j0 - 1] >> idx_bits) == (unsigned long long)kid) return;   // not the head of its run
+  const int64_t key = kid_key(s, kid);
+  const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
+  const int64_t wm = b.wm;
+  const int64_t base = kid * d.sw;
+  const int64_t* st = d.start + base;
+  const int64_t* en = d.end + base;
+  uint64_t live = d.live[kid], trig = d.trig[kid];
+  const uint64_t all = d.sw == 64 ? ~0ull : (1ull << d.sw) - 1;
+  LateCombine op;
+  unsigned long long late = 0, fires = 0;
+  for (int64_t j = j0; j < n; ++j) {
+    const unsigned long long kj = sorted[j];
+    if ((kj >> idx_bits) != (unsigned long long)kid) break;
+    const int64_t i = (int64_t)(kj & ((1ull << idx_bits) - 1));
+    const int64_t ts = b.ts[i];
+    const int64_t v = b.val[i];
+    LateAcc a;
+    a.vt = s.vt;
+    a.sum = v;
+    a.mn = min_code(s.vt, s.cmpto, v);
+    a.mx = max_code(s.vt, s.cmpto, v);
+    a.cnt = 1;
+    // MergingWindowSet.addWindow: the new window's connected group of intersecting in-flight windows
+    int64_t cs = ts, ce = jadd(ts, d.gap);
+    uint64_t mask = 0;
+    for (;;) {
+      uint64_t grew = 0;
+      for (uint64_t m = live & ~mask; m; m &= m - 1) {
+        const int q = __ffsll((long long)m) - 1;
+        if (cs <= en[q] && ce >= st[q]) { cs = min(cs, st[q]); ce = max(ce, en[q]); grew |= 1ull << q; }
+      }
+      if (!grew) break;
+      mask |= grew;
+    }
+    int r = -1;          // slot of the resulting window
+    bool fresh = false;
+    if (mask == 0) {
+      fresh = true;
+    } else {
+      r = __ffsll((long long)mask) - 1;
+      const bool contained = __popcll(mask) == 1 && st[r] == cs && en[r] == ce;   // new window inside an existing one
+      if (!contained) {
+        // merge: EventTimeTrigger.onMerge registers the merged window's timer; the merged windows' timers go,
+        // their states fold into one (AbstractKeyedStateBackend.mergePartitionedStates)
+        LateAcc m = sess_load(s, d, base + r);
+        for (uint64_t o = mask & ~(1ull << r); o; o &= o - 1) m = op(m, sess_load(s, d, base + __ffsll((long long)o) - 1));
+        sess_store(d, base + r, m);
+        live &= ~(mask & ~(1ull << r));
+        trig = (trig & ~mask) | (1ull << r);
+        d.start[base + r] = cs;
+        d.end[base + r] = ce;
+      }
+    }
+    const int64_t max_ts = jsub(ce, 1);
+    if (cleanup_time(max_ts, s.lateness) <= wm) {   // isLate(actualWindow): retireWindow, the record dropped
+      ++late;
+      if (r >= 0) { live &= ~(1ull << r); trig &= ~(1ull << r); }
+      continue;
+    }
+    LateAcc cur;
+    if (fresh) {
+      const uint64_t freem = ~live & all;
+      if (freem == 0) { cap_error(s, 21); continue; }   // more in-flight sessions for the key than slots
+      r = __ffsll((long long)freem) - 1;
+      live |= 1ull << r;
+      trig &= ~(1ull << r);
+      d.start[base + r] = cs;
+      d.end[base + r] = ce;
+      cur = a;
+    } else {
+      cur = op(sess_load(s, d, base + r), a);
+    }
+    sess_store(d, base + r, cur);
+    // EventTimeTrigger.onElement on the (possibly merged) window
+    if (max_ts <= wm) {
+      const unsigned long long pos = atomicAdd(s.o.count, 1ull);
+      sess_emit(s, pos, key, cs, max_ts, cur);
+      ++fires;
+      if (purging) { live &= ~(1ull << r); trig &= ~(1ull << r); }   // FIRE_AND_PURGE: cleanup(actualWindow)
+    } else {
+      trig |= 1ull << r;
+    }
+  }
+  d.live[kid] = live;
+  d.trig[kid] = trig;
+  if (late) atomicAdd(&s.stats[ST_LATE], late);
+  if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
+}
+
+// a watermark: every in-flight window's timers up to wm_new, in time order.  One thread per key; lane by lane
+// the it-th window of each key, so the wave's appends stay aggregated
+__global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm_new) {
+  const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
+  const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < s.stride; k0 += gstride) {   // uniform per wave
+    const int64_t kid = k0 + threadIdx.x;
+    uint64_t live = kid < s.stride ? d.live[kid] : 0, trig = kid < s.stride ? d.trig[kid] : 0;
+    const uint64_t live0 = live, trig0 = trig;
+    int nl = __popcll(live);
+    for (int o = 32; o > 0; o >>= 1) nl = max(nl, __shfl_xor(nl, o));
+    uint64_t todo = live;
+    for (int it = 0; it < nl; ++it) {
+      bool fire = false;
+      int q = -1;
+      int64_t start = 0, max_ts = 0;
+      if (todo) {
+        q = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const int64_t x = kid * d.sw + q;
+        start = d.start[x];
+        max_ts = jsub(d.end[x], 1);
+        const int64_t ct = cleanup_time(max_ts, s.lateness);
+        bool retire = false;
+        if (((trig >> q) & 1ull) && max_ts <= wm_new) {   // onEventTime(maxTimestamp): FIRE
+          fire = true;
+          trig &= ~(1ull << q);
+          if (purging || ct == max_ts) retire = true;       // FIRE_AND_PURGE, or isCleanupTime
+        }
+        if (!retire && ct <= wm_new) {                    // onEventTime(cleanupTime): cleanup
+          if (!fire && ct == max_ts) fire = true;         // (one timer at maxTimestamp == cleanupTime)
+          retire = true;
+        }
+        if (retire) { live &= ~(1ull << q); trig &= ~(1ull << q); }
+      }
+      const unsigned long long pos = wave_append(s.o.count, fire);
+      if (fire) sess_emit(s, pos, kid_key(s, kid), start, max_ts, sess_load(s, d, kid * d.sw + q));
+      wave_count(&s.stats[ST_FIRED], fire);
+    }
+    if (live != live0) d.live[kid] = live;
+    if (trig != trig0) d.trig[kid] = trig;
+  }
+}
+
+}  // namespace fw
+
+using namespace fw;
+
+int session_create(fw_engine* e) {
+  const Spec& s = e->s;
+  SessDev& d = e->sess;
+  d.gap = e->cfg.size;
+  const size_t cells = (size_t)d.sw * (size_t)s.stride;
+  d.start = e->alloc<int64_t>(cells);
+  d.end = e->alloc<int64_t>(cells);
+  d.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>(cells) : nullptr;
+  d.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(cells) : nullptr;
+  d.mx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>(cells) : nullptr;
+  d.cnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>(cells) : nullptr;
+  d.live = e->alloc<unsigned long long>((size_t)s.stride);
+  d.trig = e->alloc<unsigned long long>((size_t)s.stride);
+  e->s.o.win_start = e->alloc<int64_t>((size_t)e->cfg.out_capacity);
+  const size_t nb = (size_t)e->cfg.max_batch;
+  e->sess_key = e->alloc<unsigned long long>(nb);
+  e->sess_sorted = e->alloc<unsigned long long>(nb);
+  e->sess_idx_bits = bits_for((uint64_t)e->cfg.max_batch);
+  if (e->sess_idx_bits + bits_for((uint64_t)s.stride) > 63) return FW_ERR_UNSUPPORTED;
+  e->sess_key_bits = e->sess_idx_bits + bits_for((uint64_t)s.stride);
+  size_t tb = 0;
+  (void)rocprim::radix_sort_keys(nullptr, tb, e->sess_key, e->sess_sorted, nb, 0, e->sess_key_bits, e->stream);
+  e->sess_temp_bytes = tb;
+  e->sess_temp = e->alloc<char>(tb);
+  for (void* p : e->allocs) if (!p) return FW_ERR_DEVICE;
+  HIPCHK(e, hipMemsetAsync(d.live, 0, 8 * (size_t)s.stride, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.trig, 0, 8 * (size_t)s.stride, e->stream));
+  return FW_OK;
+}
+
+int session_push(fw_engine* e, const BatchIn& b) {
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((b.n + BLOCK - 1) / BLOCK, e->grid));
+  e->phase_begin(FW_PHASE_INGEST);
+  hipLaunchKernelGGL(k_sess_prep, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b, e->sess_key, e->sess_idx_bits);
+  size_t tb = e->sess_temp_bytes;
+  HIPCHK(e, rocprim::radix_sort_keys(e->sess_temp, tb, e->sess_key, e->sess_sorted, (size_t)b.n, 0, e->sess_key_bits,
+                                     e->stream));
+  hipLaunchKernelGGL(k_sess_walk, dim3((unsigned)((b.n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, e->stream, e->s, e->sess, b,
+                     e->sess_sorted, b.n, e->sess_idx_bits);
+  e->phase_end(b.n);
+  HIPCHK(e, hipGetLastError());
+  if (e->cfg.allowed_lateness > 0) e->out_dirty = true;   // per-element fires may have appended
+  return FW_OK;
+}
+
+int session_watermark(fw_engine* e, int64_t wm) {
+  if (wm > e->cur_wm) {
+    e->phase_begin(FW_PHASE_FIRE);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid));
+    hipLaunchKernelGGL(k_sess_wm, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
+    e->phase_end(e->s.stride);
+    e->cur_wm = wm;
+    hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
+    e->hmarks.push_back({wm, e->dev_marks++, true});
+    e->out_dirty = false;
+  } else if (e->out_dirty) {
+    hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
+    e->hmarks.push_back({wm, e->dev_marks++, true});
+    e->out_dirty = false;
+  } else {
+    e->hmarks.push_back({wm, e->dev_marks - 1, false});
+  }
+  HIPCHK(e, hipGetLastError());
+  return FW_OK;
+}

@@ -64,6 +64,21 @@ class SlidingEventTimeWindows:
     kind = _abi.FW_SLIDING
 
 
+class EventTimeSessionWindows:
+    """EventTimeSessionWindows.withGap(gap) (SJ/api/windowing/assigners/EventTimeSessionWindows.java:53-56,
+    :75-77): each record opens [ts, ts + gap); windows that intersect merge (TimeWindow.mergeWindows
+    :186-230), the merging branch of WindowOperator (:228-301) keeps them per key."""
+
+    def __init__(self, gap):
+        self.size, self.slide, self.offset = gap, 0, 0
+
+    @staticmethod
+    def withGap(gap):
+        return EventTimeSessionWindows(gap)
+
+    kind = _abi.FW_SESSION
+
+
 class EventTimeTrigger:
     code = _abi.FW_TRIGGER_EVENT_TIME
 
@@ -112,6 +127,35 @@ class ReduceFunction:
         self.comparable = comparable
         self.first = first
         self.flags = (_abi.FW_AGGF_COMPARABLE if comparable else 0) | (0 if first else _abi.FW_AGGF_BY_LAST)
+
+    @property
+    def vt(self):
+        return _abi.FW_VALUE_I64 if self.value_type == "i64" else _abi.FW_VALUE_F64
+
+
+class FoldFunction:
+    """WindowedStream.fold(initialValue, foldFunction) (WindowedStream.java:213-242) for the folds the engine
+    computes: "sum" (acc, v) -> acc + v, "count" (acc, v) -> acc + 1, "min" / "max" (acc, v) -> Math.min/max(acc, v),
+    starting from `initial` (HeapFoldingState.add, HeapFoldingState.java:111-118: the first record folds into the
+    descriptor's default value).  The result of a window is the accumulator."""
+    KINDS = {"sum": _abi.FW_AGG_SUM, "count": _abi.FW_AGG_COUNT, "min": _abi.FW_AGG_MIN, "max": _abi.FW_AGG_MAX}
+
+    def __init__(self, kind, initial, value_type="i64"):
+        if kind not in self.KINDS:
+            raise ValueError(f"fold {kind!r}: the GPU path folds sum, count, min or max")
+        self.fields = (kind,)
+        self.mask = self.KINDS[kind]
+        self.value_type = value_type
+        self.keep_first_f1 = False
+        self.by = False
+        self.comparable = False
+        self.first = True
+        self.flags = _abi.FW_AGGF_FOLD
+        self.initial = initial
+        if kind != "count" and value_type == "f64":   # a double accumulator: its bits
+            self.initial_bits = int(np.array([float(initial)], np.float64).view(np.int64)[0])
+        else:
+            self.initial_bits = int(initial)
 
     @property
     def vt(self):
@@ -308,6 +352,8 @@ class WindowEngine:
             else:
                 res[name] = np.ctypeslib.as_array(p, shape=(n,)).copy() if p else None
         nm = o.n_marks
+        res["win_start"] = (np.ctypeslib.as_array(o.win_start, shape=(n,)).copy() if o.win_start
+                            else (np.zeros(0, np.int64) if n == 0 else None))
         res["mark_wm"] = np.ctypeslib.as_array(o.mark_wm, shape=(nm,)).copy() if nm > 0 else np.zeros(0, np.int64)
         res["mark_pos"] = np.ctypeslib.as_array(o.mark_pos, shape=(nm,)).copy() if nm > 0 else np.zeros(0, np.int64)
         if self.prefix != "fw":
@@ -463,6 +509,7 @@ def make_config(assigner, reduce_function, trigger=None, allowed_lateness=0, max
     c.out_capacity = out_capacity
     c.ingest_mode = ingest_mode
     c.agg_flags = getattr(reduce_function, "flags", 0)
+    c.fold_initial = getattr(reduce_function, "initial_bits", 0)
     return c
 
 
@@ -562,7 +609,8 @@ class WindowOperator:
         if self.window_function is None:
             return [StreamRecord(value, ts)]
         out = Collector()
-        window = TimeWindow(ts + 1 - self.assigner.size, ts + 1)
+        start = int(res["win_start"][i]) if res.get("win_start") is not None else ts + 1 - self.assigner.size
+        window = TimeWindow(start, ts + 1)
         apply = getattr(self.window_function, "apply", self.window_function)
         apply(key, window, [value], out)
         return [StreamRecord(x, ts) for x in out.items]

@@ -58,6 +58,13 @@ extern "C" {
 /* ---- window assigner (SJ/api/windowing/assigners) ---- */
 #define FW_TUMBLING 0            /* TumblingEventTimeWindows.of(size[, offset])  (offset already % size)     */
 #define FW_SLIDING  1            /* SlidingEventTimeWindows.of(size, slide[, offset]) (offset already % slide) */
+#define FW_SESSION  2            /* EventTimeSessionWindows.withGap(size): merging windows [ts, ts + size)
+                                    (SJ/api/windowing/assigners/EventTimeSessionWindows.java:53-56), the merging
+                                    branch of WindowOperator.processElement (:228-301) over MergingWindowSet
+                                    (SJ/runtime/operators/windowing/MergingWindowSet.java:142-214).  Reduce
+                                    fields sum/min/max/count; no first-arrival f1 / maxBy / minBy (after a merge
+                                    they follow HashSet iteration order of the merged windows); no checkpoint
+                                    (the merging-window set is keyed list state of its own). */
 
 /* ---- trigger (SJ/api/windowing/triggers) ---- */
 #define FW_TRIGGER_EVENT_TIME          0   /* EventTimeTrigger.create()                    */
@@ -88,6 +95,14 @@ extern "C" {
                                   NaN above +inf, -0.0 < +0.0) instead of Math.min/max (NaN wins); long
                                   values order the same either way.  MAXBY/MINBY always use compareTo. */
 #define FW_AGGF_BY_LAST     2  /* maxBy/minBy(pos, first = false): a tie takes the later record */
+#define FW_AGGF_FOLD        4  /* WindowedStream.fold(initialValue, FoldFunction) (WindowedStream.java:213-242) over
+                                  HeapFoldingState (flink-runtime/.../state/heap/HeapFoldingState.java:84-122: the
+                                  first add folds into the descriptor's default value): the folds
+                                  (acc, v) -> acc + v, acc + 1, Math.min(acc, v), Math.max(acc, v) — one aggregate
+                                  (FW_AGG_SUM, FW_AGG_COUNT, FW_AGG_MIN or FW_AGG_MAX) starting from fold_initial
+                                  (a long, or a double's bits for a double sum / min / max).  Not with session
+                                  windows ("Fold cannot be used with a merging WindowAssigner", :466-467), maxBy /
+                                  minBy or first-arrival f1; no checkpoint layout. */
 
 #define FW_VALUE_I64  0
 #define FW_VALUE_F64  1
@@ -118,6 +133,7 @@ typedef struct {
   int64_t out_capacity;      /* max fired records between two fw_collect calls                  */
   int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate     */
   int32_t agg_flags;         /* OR of FW_AGGF_*                                                 */
+  int64_t fold_initial;      /* FW_AGGF_FOLD: the fold's initial accumulator                    */
 } fw_config;
 
 /* Output between two collects: records and watermark marks.  Records [mark_pos[i-1], mark_pos[i])
@@ -140,6 +156,7 @@ typedef struct {
   int64_t n_marks;
   const int64_t* mark_wm;
   const int64_t* mark_pos;
+  const int64_t* win_start;  /* FW_SESSION: window.getStart() of each result (window.getEnd() = ts + 1); NULL otherwise */
 } fw_out;
 
 typedef struct {

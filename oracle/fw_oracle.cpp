@@ -17,7 +17,13 @@
 //   onEventTime                 WindowOperator.java:336-375; fire :435-438; cleanup :420-428
 //   isLate/cleanupTime          WindowOperator.java:470-472,479-486,511-514,527-530
 //   EventTimeTrigger            SJ/api/windowing/triggers/EventTimeTrigger.java:37-62
-//   PurgingTrigger              SJ/api/windowing/triggers/PurgingTrigger.java:47-53
+//   PurgingTrigger              SJ/api/windowing/triggers/PurgingTrigger.java:47-53,68-76
+//   session windows             SJ/api/windowing/assigners/EventTimeSessionWindows.java:53-56; TimeWindow
+//                               .intersects/cover/mergeWindows TimeWindow.java:96-105,186-230; MergingWindowSet
+//                               .addWindow/getStateWindow/retireWindow MergingWindowSet.java:97-214; the merging
+//                               branch WindowOperator.java:228-301, onEventTime :344-353, cleanup :420-428;
+//                               AbstractKeyedStateBackend.mergePartitionedStates (reducing) :294-314;
+//                               EventTimeTrigger.onMerge :70-74; TriggerResult.merge
 //   HeapReducingState.add       RT/state/heap/HeapReducingState.java:84-122
 //   AbstractHeapState.clear     RT/state/heap/AbstractHeapState.java:90-119
 //   StateTable                  RT/state/heap/StateTable.java:27-77
@@ -32,6 +38,7 @@
 //                               :251-349 (readStateTableForKeyGroup); HeapInternalTimerService.java:285-345;
 //                               TimeWindow.Serializer TimeWindow.java:141-158; InternalTimer.TimerSerializer
 //                               InternalTimer.java:145-157; JDK HashMap/HashSet iteration order (see below)
+//   fold                        RT/state/heap/HeapFoldingState.java:84-122 (first add folds into the default value)
 //   reduce functions            SJ/api/functions/aggregation/SumAggregator.java:64-72, SumFunction.java:60-77,
 //                               JDK Math.min/Math.max (double), Long arithmetic (wrapping),
 //                               ComparableAggregator.java:66-90 + Comparator.java:45-105 (min/max/minBy/maxBy
@@ -84,6 +91,13 @@ int32_t murmurHash(int32_t code) {
 }
 // JDK Long.hashCode(long) = (int)(value ^ (value >>> 32))
 int32_t longHashCode(int64_t v) { return (int32_t)(uint32_t)((uint64_t)v ^ ((uint64_t)v >> 32)); }
+// java.util.HashMap's spread of a key's hashCode and the capacity a HashSet grew to by n adds
+int32_t hmSpread(int32_t h) { return h ^ ushr32(h, 16); }
+uint32_t hmCapacitySet(size_t n) {
+  uint32_t cap = 16;
+  while ((double)n > cap * 0.75) cap <<= 1;
+  return cap;
+}
 // KeyGroupRangeAssignment.computeKeyGroupForKeyHash — :62-64
 int32_t computeKeyGroupForKeyHash(int32_t keyHash, int32_t maxParallelism) {
   return murmurHash(keyHash) % maxParallelism;
@@ -100,6 +114,10 @@ struct TimeWindow {  // TimeWindow.java:41-62
   bool operator==(const TimeWindow& o) const { return start == o.start && end == o.end; }
   bool operator<(const TimeWindow& o) const { return start != o.start ? start < o.start : end < o.end; }
 };
+// TimeWindow.hashCode (TimeWindow.java:79-83): 31 * Long.hashCode(start) + Long.hashCode(end)
+int32_t timeWindowHash(const TimeWindow& w) {
+  return (int32_t)((uint32_t)longHashCode(w.start) * 31u + (uint32_t)longHashCode(w.end));
+}
 struct TimeWindowHash {
   size_t operator()(const TimeWindow& w) const { return std::hash<int64_t>()(w.start) * 31 + std::hash<int64_t>()(w.end); }
 };
@@ -200,6 +218,7 @@ inline bool isPurge(TriggerResult r) { return r == PURGE || r == FIRE_AND_PURGE;
 struct OutRec {
   Acc acc;
   int64_t ts;
+  int64_t start;   // window.getStart() (the window function's view of the window)
 };
 
 struct Operator {
@@ -226,7 +245,10 @@ struct Operator {
   std::vector<int64_t> mark_wm, mark_pos;
   fw_stats stats{};
   // materialised output columns for fwo_collect
-  std::vector<int64_t> c_key, c_f1, c_ts, c_sum_i, c_min_i, c_max_i, c_count;
+  std::vector<int64_t> c_key, c_f1, c_ts, c_sum_i, c_min_i, c_max_i, c_count, c_start;
+  // session windows: per key the in-flight windows -> their state window (MergingWindowSet.windows, a
+  // HashMap<W, W>; ordered here by (start, end), which mergeWindows' stable sort by start makes equivalent)
+  std::unordered_map<int64_t, std::map<TimeWindow, TimeWindow>> mergingWindowsByKey;
   std::vector<double> c_sum_d, c_min_d, c_max_d;
 
   explicit Operator(const fw_config& c) : cfg(c) {
@@ -285,7 +307,24 @@ struct Operator {
     auto& keyed = nit->second;
     auto it = keyed.find(curKey);
     if (it == keyed.end()) {
-      keyed.emplace(curKey, value);
+      if (cfg.agg_flags & FW_AGGF_FOLD) {
+        // HeapFoldingState.add (HeapFoldingState.java:111-118): no value yet -> fold(defaultValue, value); the
+        // folds offered (acc + v, acc + 1, Math.min/max(acc, v)) then continue exactly as reduce(acc, value)
+        Acc init = value;
+        const int64_t x = cfg.fold_initial;
+        double xd;
+        std::memcpy(&xd, &x, 8);
+        init.sum_i = jlong_add(x, value.sum_i);
+        init.min_i = x <= value.min_i ? x : value.min_i;
+        init.max_i = x >= value.max_i ? x : value.max_i;
+        init.sum_d = xd + value.sum_d;
+        init.min_d = javaMin(xd, value.min_d);
+        init.max_d = javaMax(xd, value.max_d);
+        init.count = jlong_add(x, value.count);
+        keyed.emplace(curKey, init);
+      } else {
+        keyed.emplace(curKey, value);
+      }
     } else {
       const int64_t sq = it->second.seq;   // HashMap.put of an existing key keeps its place
       it->second = reduceFn(cfg, it->second, value);
@@ -344,7 +383,7 @@ struct Operator {
 
   // ---- WindowOperator.fire / cleanup / registerCleanupTimer ----
   void fire(const TimeWindow& w, const Acc& contents) {  // :435-438, InternalSingleValueWindowFunction + PassThrough
-    out.push_back({contents, w.maxTimestamp()});
+    out.push_back({contents, w.maxTimestamp(), w.start});
     stats.panes_fired++;
   }
   void cleanup(const TimeWindow& w) {  // :420-428
@@ -353,8 +392,138 @@ struct Operator {
   }
   void registerCleanupTimer(const TimeWindow& w) { registerEventTimeTimer(w, cleanupTime(w)); }  // :479-486
 
+  // ---- session windows: MergingWindowSet.addWindow (MergingWindowSet.java:142-214) with the merge function
+  // of WindowOperator.processElement (:239-263); returns the window the element belongs to ----
+  TimeWindow addWindow(std::map<TimeWindow, TimeWindow>& windows, const TimeWindow& newWindow) {
+    // TimeWindow.mergeWindows (:186-230): sort by start, chain windows that intersect; the callback gets
+    // every group whose HashSet has more than one window
+    std::vector<TimeWindow> sorted;
+    for (const auto& kv : windows) sorted.push_back(kv.first);
+    sorted.push_back(newWindow);
+    std::stable_sort(sorted.begin(), sorted.end(), [](const TimeWindow& a, const TimeWindow& b) { return a.start < b.start; });
+    struct Group { TimeWindow cover; std::vector<TimeWindow> set; };   // set: HashSet, insertion order
+    std::vector<Group> groups;
+    auto intersects = [](const TimeWindow& a, const TimeWindow& b) { return a.start <= b.end && a.end >= b.start; };
+    for (const TimeWindow& c : sorted) {
+      if (!groups.empty() && intersects(groups.back().cover, c)) {
+        Group& g = groups.back();
+        g.cover = {std::min(g.cover.start, c.start), std::max(g.cover.end, c.end)};   // TimeWindow.cover
+        if (std::find(g.set.begin(), g.set.end(), c) == g.set.end()) g.set.push_back(c);
+      } else {
+        groups.push_back({c, {c}});
+      }
+    }
+    TimeWindow resultWindow = newWindow;
+    bool anyMerge = false;
+    for (Group& g : groups) {
+      if (g.set.size() <= 1) continue;
+      anyMerge = true;
+      const TimeWindow mergeResult = g.cover;
+      // HashSet<TimeWindow> iteration order: bucket of the spread hash in the table the adds grew, then
+      // insertion order (java.util.HashMap)
+      const size_t grown = g.set.size();
+      std::vector<TimeWindow> merged = g.set;
+      auto it = std::find(merged.begin(), merged.end(), newWindow);
+      if (it != merged.end()) { merged.erase(it); resultWindow = mergeResult; }
+      {
+        const uint32_t mask = hmCapacitySet(grown) - 1;
+        std::vector<std::pair<TimeWindow, size_t>> order;
+        for (size_t i = 0; i < merged.size(); ++i) order.push_back({merged[i], i});
+        std::stable_sort(order.begin(), order.end(), [&](const auto& a, const auto& b) {
+          const uint32_t ia = (uint32_t)hmSpread(timeWindowHash(a.first)) & mask, ib = (uint32_t)hmSpread(timeWindowHash(b.first)) & mask;
+          return ia != ib ? ia < ib : a.second < b.second;
+        });
+        for (size_t i = 0; i < merged.size(); ++i) merged[i] = order[i].first;
+      }
+      const TimeWindow mergedStateWindow = windows.at(merged.front());
+      std::vector<TimeWindow> mergedStateWindows;
+      for (const TimeWindow& m : merged) {
+        auto f = windows.find(m);
+        if (f != windows.end()) { mergedStateWindows.push_back(f->second); windows.erase(f); }
+      }
+      windows[mergeResult] = mergedStateWindow;
+      {
+        auto f = std::find(mergedStateWindows.begin(), mergedStateWindows.end(), mergedStateWindow);
+        if (f != mergedStateWindows.end()) mergedStateWindows.erase(f);
+      }
+      const bool selfOnly = merged.size() == 1 && merged.front() == mergeResult;
+      if (!selfOnly) {
+        // the merge function: onMerge registers the merged window's timer (EventTimeTrigger.onMerge :70-74;
+        // PurgingTrigger passes CONTINUE through), the merged windows' trigger and cleanup timers go
+        registerEventTimeTimer(mergeResult, mergeResult.maxTimestamp());
+        for (const TimeWindow& m : merged) {
+          triggerClear(m);
+          deleteEventTimeTimer(m, cleanupTime(m));
+        }
+        // AbstractKeyedStateBackend.mergePartitionedStates (:294-314): the sources reduced in list order
+        // and cleared, the result added to the target state window
+        const TimeWindow target = windows.at(mergeResult);
+        bool have = false;
+        Acc result{};
+        for (const TimeWindow& src : mergedStateWindows) {
+          const Acc* sv = stateGet(src);
+          if (!have) { if (sv) { result = *sv; have = true; } }
+          else if (sv) result = reduceFn(cfg, result, *sv);
+          stateClear(src);
+        }
+        if (have) {
+          result.seq = ++seqCounter;
+          stateAdd(target, result);
+        }
+      }
+    }
+    if (resultWindow == newWindow && !anyMerge) windows[resultWindow] = resultWindow;
+    return resultWindow;
+  }
+
+  int processElementMerging(const Acc& value, int64_t ts) {  // WindowOperator.java:228-301
+    const TimeWindow window{ts, jlong_add(ts, cfg.size)};   // EventTimeSessionWindows.assignWindows :53-56
+    auto& windows = mergingWindowsByKey[curKey];
+    const TimeWindow actualWindow = addWindow(windows, window);
+    if (isLate(actualWindow)) {   // :265-269
+      windows.erase(actualWindow);
+      stats.records_late++;
+      return FW_OK;
+    }
+    auto sw = windows.find(actualWindow);
+    if (sw == windows.end()) { err = "Window is not in in-flight window set."; return FW_ERR_INVALID_ARG; }
+    const TimeWindow stateWindow = sw->second;
+    int rc = stateAdd(stateWindow, value);
+    if (rc) return rc;
+    // onElement on the (possibly merged) window, merged with the merge's CONTINUE
+    TriggerResult triggerResult = triggerOnElement(actualWindow);
+    if (isFire(triggerResult)) {
+      const Acc* contents = stateGet(stateWindow);
+      if (contents == nullptr) return FW_OK;
+      Acc copy = *contents;
+      fire(actualWindow, copy);
+      stats.late_fires++;
+    }
+    if (isPurge(triggerResult)) cleanupMerging(actualWindow, stateWindow, windows);
+    else registerCleanupTimer(actualWindow);
+    return FW_OK;
+  }
+  void cleanupMerging(const TimeWindow& w, const TimeWindow& stateWindow, std::map<TimeWindow, TimeWindow>& windows) {
+    stateClear(stateWindow);   // :420-428
+    windows.erase(w);          // MergingWindowSet.retireWindow
+    triggerClear(w);
+  }
+
   // ---- OneInputStreamOperator.processElement ----
   int processElement(int64_t key, int32_t keyHash, int64_t f1, int64_t ts, int64_t vi, double vd) {
+    if (cfg.assigner == FW_SESSION) {   // (EventTimeSessionWindows has no Long.MIN_VALUE check: [ts, ts + gap))
+      curKey = key;
+      curKeyGroup = computeKeyGroupForKeyHash(keyHash, cfg.max_parallelism);
+      stats.records_in++;
+      Acc value{};
+      value.key = key;
+      value.f1 = f1;
+      value.sum_i = value.min_i = value.max_i = vi;
+      value.sum_d = value.min_d = value.max_d = vd;
+      value.count = 1;
+      value.seq = ++seqCounter;
+      return processElementMerging(value, ts);
+    }
     std::vector<TimeWindow> elementWindows;
     int rc = assignWindows(ts, elementWindows);
     if (rc) return rc;
@@ -391,6 +560,20 @@ struct Operator {
   void onEventTime(const InternalTimer& timer) {
     curKey = timer.key;
     const TimeWindow& window = timer.ns;
+    if (cfg.assigner == FW_SESSION) {   // :344-353: the state lives in the window's state window
+      auto kit = mergingWindowsByKey.find(curKey);
+      if (kit == mergingWindowsByKey.end()) return;
+      auto sw = kit->second.find(window);
+      if (sw == kit->second.end()) return;   // already purged: a leftover cleanup timer
+      const TimeWindow stateWindow = sw->second;
+      const Acc* c = stateGet(stateWindow);
+      if (c == nullptr) return;
+      Acc contents = *c;
+      TriggerResult triggerResult = triggerOnEventTime(window, timer.timestamp);
+      if (isFire(triggerResult)) fire(window, contents);
+      if (isPurge(triggerResult) || isCleanupTime(window, timer.timestamp)) cleanupMerging(window, stateWindow, kit->second);
+      return;
+    }
     const Acc* c = stateGet(window);
     if (c == nullptr) return;
     Acc contents = *c;
@@ -629,6 +812,8 @@ extern "C" {
 
 int fwo_create(const fw_config* cfg, fw_engine** out) {
   if (!cfg || !out) return FW_ERR_INVALID_ARG;
+  if (cfg->assigner != FW_TUMBLING && cfg->assigner != FW_SLIDING && cfg->assigner != FW_SESSION) return FW_ERR_INVALID_ARG;
+  if ((cfg->agg_flags & FW_AGGF_FOLD) && cfg->assigner == FW_SESSION) return FW_ERR_UNSUPPORTED;   // WindowedStream.java:466-467
   if (cfg->size <= 0 || (cfg->assigner == FW_SLIDING && cfg->slide <= 0) || cfg->allowed_lateness < 0 ||
       cfg->max_parallelism <= 0 || cfg->kg_start < 0 || cfg->kg_end < cfg->kg_start || cfg->kg_end >= cfg->max_parallelism)
     return FW_ERR_INVALID_ARG;
@@ -663,9 +848,10 @@ int fwo_collect(fw_engine* e, fw_out* o) {
   size_t n = op.out.size();
   op.c_key.resize(n); op.c_f1.resize(n); op.c_ts.resize(n);
   op.c_sum_i.resize(n); op.c_min_i.resize(n); op.c_max_i.resize(n); op.c_count.resize(n);
-  op.c_sum_d.resize(n); op.c_min_d.resize(n); op.c_max_d.resize(n);
+  op.c_sum_d.resize(n); op.c_min_d.resize(n); op.c_max_d.resize(n); op.c_start.resize(n);
   for (size_t i = 0; i < n; ++i) {
     const Acc& a = op.out[i].acc;
+    op.c_start[i] = op.out[i].start;
     op.c_key[i] = a.key; op.c_f1[i] = a.f1; op.c_ts[i] = op.out[i].ts;
     op.c_sum_i[i] = a.sum_i; op.c_min_i[i] = a.min_i; op.c_max_i[i] = a.max_i; op.c_count[i] = a.count;
     op.c_sum_d[i] = a.sum_d; op.c_min_d[i] = a.min_d; op.c_max_d[i] = a.max_d;
@@ -681,6 +867,7 @@ int fwo_collect(fw_engine* e, fw_out* o) {
   o->n_marks = (int64_t)op.mark_wm.size();
   o->mark_wm = op.mark_wm.data();
   o->mark_pos = op.mark_pos.data();
+  o->win_start = op.cfg.assigner == FW_SESSION ? op.c_start.data() : nullptr;
   return FW_OK;
 }
 
@@ -705,6 +892,8 @@ int fwo_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layou
                           int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
   if (!e || !layout || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
   if (kg < e->op.cfg.kg_start || kg > e->op.cfg.kg_end) return FW_ERR_INVALID_ARG;
+  if (e->op.cfg.assigner == FW_SESSION) { e->op.err = "session windows: no checkpoint layout"; return FW_ERR_UNSUPPORTED; }
+  if (e->op.cfg.agg_flags & FW_AGGF_FOLD) { e->op.err = "fold: no checkpoint layout"; return FW_ERR_UNSUPPORTED; }
   JavaOut st, tm;
   snapshotKeyGroup(e->op, kg, *layout, st, tm);
   *state_len = (int64_t)st.b.size();

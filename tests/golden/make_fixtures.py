@@ -237,6 +237,98 @@ FIXTURES.append(closed_form("itcase_tumbling_closed_form",
 FIXTURES.append(closed_form("itcase_sliding_closed_form",
                             "EventTimeWindowCheckpointingITCase.java:416-485,495-686", 1000, 100))
 
+# ---- session windows (EventTimeSessionWindows.withGap, the merging branch of WindowOperator) ----
+# Expected records carry the window: [key, sum, maxTimestamp, window start].  The reference's
+# ReducedSessionWindowFunction / SessionWindowFunction emit Tuple3(key + "-" + sum, window.getStart(),
+# window.getEnd()) timestamped window.maxTimestamp() (WOT:2290-2320), i.e. exactly (key, sum, start, end = ts + 1).
+def sout(key, value, start, end):
+    return [KEYS[key], value, end - 1, start]
+
+
+SESSION_OOO = [rec("key2", 1, 0), rec("key2", 2, 1000), rec("key2", 3, 2500),
+               rec("key1", 1, 10), rec("key1", 2, 1000), rec("key1", 3, 2500),
+               rec("key2", 4, 5501), rec("key2", 5, 6000), rec("key2", 5, 6000), rec("key2", 6, 6050)]
+SESSION_OUT = [{"wm": 12000, "records": [sout("key1", 6, 10, 5500), sout("key2", 6, 0, 5500), sout("key2", 20, 5501, 9050)]},
+               {"wm": 17999, "records": [sout("key2", 30, 15000, 18000)]}]
+
+# WOT:435-501 testReduceSessionWindows (gap 3 s; its mid-stream snapshot/restore keeps the state)
+FIXTURES.append(fixture(
+    "session_reduce", "WindowOperatorTest.java:435-501", cfg("session", 3000),
+    SESSION_OOO + [wm(12000), rec("key2", 10, 15000), rec("key2", 20, 15000), wm(17999)], SESSION_OUT))
+# WOT:362-431 testSessionWindows: the same elements through ListState + SessionWindowFunction, which
+# emits (key-sum, start, end): identical results to the reducing form (list state itself is not on the
+# GPU path; the fixture pins the merging semantics)
+FIXTURES.append(fixture(
+    "session_windows", "WindowOperatorTest.java:362-431", cfg("session", 3000),
+    SESSION_OOO + [wm(12000), rec("key2", 10, 15000), rec("key2", 20, 15000), wm(17999)], SESSION_OUT))
+
+
+def late_session_events(extra):
+    """The common prefix of the testDropDueToLatenessSession* tests (WOT:1395-1417 and its copies)."""
+    return [rec("key2", 1, 1000), wm(1999), rec("key2", 1, 2000), wm(4998),
+            rec("key2", 1, 4500), rec("key2", 1, 8500), wm(7400),
+            rec("key2", 1, 7000), wm(11501),
+            rec("key2", 1, 11600), wm(14600)] + extra
+
+
+LATE_SESSION_PREFIX = [{"wm": 1999, "records": []}, {"wm": 4998, "records": []}, {"wm": 7400, "records": []},
+                       {"wm": 11501, "records": [sout("key2", 5, 1000, 11500)]},
+                       {"wm": 14600, "records": [sout("key2", 1, 11600, 14600)]}]
+
+# WOT:1367-1448 testDropDueToLatenessSessionZeroLatenessPurgingTrigger
+FIXTURES.append(fixture(
+    "session_late_zero_purging", "WindowOperatorTest.java:1367-1448",
+    cfg("session", 3000, lateness=0, trigger="purging"),
+    late_session_events([rec("key2", 1, 10000), rec("key2", 1, 10100), rec("key2", 1, 14500), wm(20000), wm(100000)]),
+    LATE_SESSION_PREFIX + [{"wm": 20000, "records": [sout("key2", 1, 14500, 17500)]}, {"wm": 100000, "records": []}]))
+# WOT:1451-1534 testDropDueToLatenessSessionZeroLateness
+FIXTURES.append(fixture(
+    "session_late_zero", "WindowOperatorTest.java:1451-1534", cfg("session", 3000, lateness=0),
+    late_session_events([rec("key2", 1, 10000), rec("key2", 1, 14500), wm(20000), wm(100000)]),
+    LATE_SESSION_PREFIX + [{"wm": 20000, "records": [sout("key2", 1, 14500, 17500)]}, {"wm": 100000, "records": []}]))
+# WOT:1537-1618 testDropDueToLatenessSessionWithLatenessPurgingTrigger (lateness 10)
+FIXTURES.append(fixture(
+    "session_late_small_purging", "WindowOperatorTest.java:1537-1618",
+    cfg("session", 3000, lateness=10, trigger="purging"),
+    late_session_events([rec("key2", 1, 10000), rec("key2", 1, 14500), wm(20000), wm(100000)]),
+    LATE_SESSION_PREFIX + [{"wm": 20000, "records": [sout("key2", 1, 14500, 17500)]}, {"wm": 100000, "records": []}]))
+# WOT:1621-1714 testDropDueToLatenessSessionWithLateness (lateness 10): 10000 merges into the fired
+# (11600, 14600) session and fires it at once as (10000, 14600), then 14500 extends it
+FIXTURES.append(fixture(
+    "session_late_small", "WindowOperatorTest.java:1621-1714", cfg("session", 3000, lateness=10),
+    late_session_events([rec("key2", 1, 10000), rec("key2", 1, 14500), wm(20000), wm(100000)]),
+    LATE_SESSION_PREFIX + [{"wm": 20000, "records": [sout("key2", 2, 10000, 14600), sout("key2", 3, 10000, 17500)]},
+                           {"wm": 100000, "records": []}]))
+# WOT:1717-1800 testDropDueToLatenessSessionWithHugeLatenessPurgingTrigger (lateness 10000)
+FIXTURES.append(fixture(
+    "session_late_huge_purging", "WindowOperatorTest.java:1717-1800",
+    cfg("session", 3000, lateness=10000, trigger="purging"),
+    late_session_events([rec("key2", 1, 10000), rec("key2", 1, 14500), wm(20000), wm(100000)]),
+    LATE_SESSION_PREFIX + [{"wm": 20000, "records": [sout("key2", 1, 10000, 13000), sout("key2", 1, 14500, 17500)]},
+                           {"wm": 100000, "records": []}]))
+# WOT:1803-1866 testDropDueToLatenessSessionWithHugeLateness (lateness 10000): 10000 bridges the two fired
+# sessions into (1000, 14600), which fires at once; 14500 extends it to (1000, 17500)
+FIXTURES.append(fixture(
+    "session_late_huge", "WindowOperatorTest.java:1803-1866", cfg("session", 3000, lateness=10000),
+    late_session_events([rec("key2", 1, 10000), rec("key2", 1, 14500), wm(20000), wm(100000)]),
+    LATE_SESSION_PREFIX + [{"wm": 20000, "records": [sout("key2", 7, 1000, 14600), sout("key2", 8, 1000, 17500)]},
+                           {"wm": 100000, "records": []}]))
+# WOT:2133-2175 testCleanupTimerWithEmptyReduceStateForSessionWindows (gap 3 s, lateness 10)
+FIXTURES.append(fixture(
+    "session_cleanup_timer", "WindowOperatorTest.java:2133-2175", cfg("session", 3000, lateness=10),
+    [rec("key2", 1, 1000), wm(4998), wm(14600)],
+    [{"wm": 4998, "records": [sout("key2", 1, 1000, 4000)]}, {"wm": 14600, "records": []}]))
+
+# WOT:2034-2089 testCleanupTimerWithEmptyFoldingStateForTumblingWindows: tumbling 2 s, lateness 1, a
+# FoldingStateDescriptor with default (null, 0) and fold (acc, v) -> (v.f0, acc.f1 + v.f1), i.e. a sum from 0
+FOLD_CFG = cfg("tumbling", 2000, lateness=1)
+FOLD_CFG["fold"] = {"kind": "sum", "initial": 0}
+FIXTURES.append(fixture(
+    "fold_cleanup_timer", "WindowOperatorTest.java:2034-2089", FOLD_CFG,
+    [rec("key2", 1, 1000), wm(1599), wm(1999), wm(2000), wm(5000)],
+    [{"wm": 1599, "records": []}, {"wm": 1999, "records": [out("key2", 1, 1999)]}, {"wm": 2000, "records": []},
+     {"wm": 5000, "records": []}]))
+
 # TimeWindowTest.java:30-58 getWindowStartWithOffset known answers: (ts, offset, size, expected)
 WINDOW_START = {
     "source": "flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/TimeWindowTest.java:30-58",

@@ -10,8 +10,8 @@ import os
 import numpy as np
 
 from flink_amd import _abi
-from flink_amd.windowing import (EventTimeTrigger, PurgingTrigger, ReduceFunction, SlidingEventTimeWindows,
-                                 TumblingEventTimeWindows, make_config)
+from flink_amd.windowing import (EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger, ReduceFunction,
+                                 SlidingEventTimeWindows, TumblingEventTimeWindows, make_config)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -25,15 +25,25 @@ WINDOW_FIXTURES = ["sliding_reduce", "tumbling_reduce", "lateness_purging", "cle
                    "drop_late_tumbling", "drop_late_sliding", "cleanup_timer_empty_state", "tumbling_offset",
                    "sliding_offset", "itcase_tumbling_closed_form", "itcase_sliding_closed_form",
                    "sliding_lateness", "sliding_lateness_purging"]
+SESSION_FIXTURES = ["session_reduce", "session_windows", "session_late_zero_purging", "session_late_zero",
+                    "session_late_small_purging", "session_late_small", "session_late_huge_purging",
+                    "session_late_huge", "session_cleanup_timer"]
+FOLD_FIXTURES = ["fold_cleanup_timer"]
 
 
 def fixture_config(c, **kw):
     if c["assigner"] == "tumbling":
         assigner = TumblingEventTimeWindows(c["size"], c["offset"])
+    elif c["assigner"] == "session":
+        assigner = EventTimeSessionWindows.withGap(c["size"])
     else:
         assigner = SlidingEventTimeWindows(c["size"], c["slide"], c["offset"])
     trig = EventTimeTrigger.create() if c["trigger"] == "event_time" else PurgingTrigger.of(EventTimeTrigger.create())
-    red = ReduceFunction(tuple(c["agg"]), c["value_type"], c["keep_first_f1"])
+    if "fold" in c:
+        from flink_amd.windowing import FoldFunction
+        red = FoldFunction(c["fold"]["kind"], c["fold"]["initial"], c["value_type"])
+    else:
+        red = ReduceFunction(tuple(c["agg"]), c["value_type"], c["keep_first_f1"])
     mp = c["max_parallelism"]
     args = dict(max_parallelism=mp, key_capacity=1024, max_batch=1 << 12, out_capacity=1 << 16)
     args.update(kw)
@@ -79,7 +89,11 @@ def replay(fx, engine_factory, **kw):
             res = eng.collect()
             assert len(res["mark_wm"]) == 1 and res["mark_wm"][0] == e[1]
             assert res["mark_pos"][0] == res["n"], "records emitted after the watermark mark"
-            recs = sorted((int(res["key"][i]), int(res["sum_i64"][i]), int(res["ts"][i])) for i in range(res["n"]))
+            if fx["config"]["assigner"] == "session":   # the window's start too (end = ts + 1)
+                recs = sorted((int(res["key"][i]), int(res["sum_i64"][i]), int(res["ts"][i]), int(res["win_start"][i]))
+                              for i in range(res["n"]))
+            else:
+                recs = sorted((int(res["key"][i]), int(res["sum_i64"][i]), int(res["ts"][i])) for i in range(res["n"]))
             epochs.append((e[1], recs))
     eng.close()
     return epochs

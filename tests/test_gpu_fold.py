@@ -1,0 +1,76 @@
+"""WindowedStream.fold(initialValue, FoldFunction) on the HIP engine (FW_AGGF_FOLD): the reference's known answer
+(WindowOperatorTest.testCleanupTimerWithEmptyFoldingStateForTumblingWindows, tests/golden/fold_cleanup_timer.json)
+and parity with the oracle's HeapFoldingState restatement — bit-exact for long folds, relative 1e-9 for a
+double sum (the reference folds record by record from the initial value; the engine adds it once).
+"""
+import numpy as np
+import pytest
+
+from harness import FOLD_FIXTURES, drive, epochs_of, expected_epochs, gen_stream, load_golden, replay
+
+pytestmark = pytest.mark.gpu
+
+LONG_MAX = (1 << 63) - 1
+MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned")]
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from flink_amd import _abi
+    from flink_amd.windowing import WindowEngine
+    _abi.load_library()
+    return WindowEngine
+
+
+@pytest.fixture(scope="module")
+def oracle_engine():
+    from oracle.oracle import OracleEngine
+    return OracleEngine
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("name", FOLD_FIXTURES)
+def test_fold_golden_fixture(hip, name, mode):
+    fx = load_golden(name)
+    assert replay(fx, hip, ingest_mode=mode) == expected_epochs(fx), fx["source"]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("kind,initial,vt,assigner", [
+    ("sum", 123456789, "i64", "tumbling"), ("count", -7, "i64", "tumbling"), ("max", 1 << 62, "i64", "tumbling"),
+    ("min", -5, "i64", "sliding"), ("sum", 1000, "i64", "sliding"), ("sum", 2.5, "f64", "tumbling"),
+    ("min", 0.25, "f64", "sliding")])
+def test_fold_parity(hip, oracle_engine, mode, kind, initial, vt, assigner):
+    from flink_amd.windowing import FoldFunction, SlidingEventTimeWindows, TumblingEventTimeWindows, make_config
+    a = TumblingEventTimeWindows.of(1000) if assigner == "tumbling" else SlidingEventTimeWindows.of(3000, 1000)
+    keys, ts, vals = gen_stream(200000, 2000, rate=20000, ooo=300, value_type=vt)
+    cfg = make_config(a, FoldFunction(kind, initial, vt), None, 200, key_capacity=1 << 12, max_batch=1 << 16,
+                      out_capacity=1 << 20, ingest_mode=mode)
+    col = {"sum": "sum_", "min": "min_", "max": "max_"}.get(kind)
+    field = "count" if kind == "count" else col + vt
+    res = []
+    for f in (hip, oracle_engine):
+        e = f(cfg)
+        res.append(epochs_of(drive(e, keys, ts, vals, 1 << 14, 100, LONG_MAX), [field]))
+        e.close()
+    g, o = res
+    assert len(g) == len(o) and sum(len(r) for _, r in g) > 1000
+    for (wg, rg), (wo, ro) in zip(g, o):
+        assert wg == wo and len(rg) == len(ro)
+        if vt == "f64" and kind == "sum":
+            for x, y in zip(rg, ro):
+                assert x[:2] == y[:2] and abs(x[2] - y[2]) <= 1e-9 * max(1.0, abs(y[2])), (wg, x, y)
+        else:
+            assert rg == ro, wg
+
+
+def test_fold_rejections(hip):
+    from flink_amd import _abi
+    from flink_amd.windowing import EventTimeSessionWindows, FoldFunction, TumblingEventTimeWindows, make_config
+    with pytest.raises(_abi.FwError):   # WindowedStream.java:466-467
+        hip(make_config(EventTimeSessionWindows.withGap(10), FoldFunction("sum", 0)))
+    e = hip(make_config(TumblingEventTimeWindows.of(1000), FoldFunction("sum", 5)))
+    e.push(np.array([1], np.int64), np.array([5], np.int64), np.array([1], np.int64))
+    with pytest.raises(_abi.FwError, match="fold"):
+        e.snapshot_kg(0)
+    e.close()

@@ -9,7 +9,7 @@ step() {   # name limit cmd...
   echo "== $name rc=$rc"; tail -${TAILN:-4} "gpurun_out/$name.log"
   [ $rc -eq 0 ] || exit $rc
 }
-[ -z "$SKIP_TESTS" ] && step pytest_gpu ${T_TEST:-600} python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS}
+[ -z "$SKIP_TESTS" ] && step pytest_gpu ${T_TEST:-600} python -u -m pytest ${TEST_PATHS:-tests} -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS}
 [ -z "$SKIP_SMOKE" ] && step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 [ -z "$SKIP_BENCH" ] && step bench 300 python bench.py ${BENCH_ARGS}
 for c in ${BENCH_CONFIGS}; do step bench_$c 300 python bench.py --config $c --cpu-sample 0; done
