@@ -60,7 +60,8 @@ constexpr int MAX_K = 64;          // max slices per window
 constexpr int BLOCK = 256;
 
 // ST_SHARES: helper shares run; ST_DIR_KEYS: keys in the directory buckets (inserts since the last compaction + the keys it kept)
-enum Stat { ST_LATE = 0, ST_FIRED = 1, ST_LATE_FIRES = 2, ST_SHARES = 3, ST_DIR_KEYS = 4, ST_NSTATS = 8 };
+// ST_QUIRK: records that got the sliding assigner's extra window (negative remainder, window panes below)
+enum Stat { ST_LATE = 0, ST_FIRED = 1, ST_LATE_FIRES = 2, ST_SHARES = 3, ST_DIR_KEYS = 4, ST_QUIRK = 5, ST_NSTATS = 8 };
 
 // ------------------------------------------------------------------------------------------------
 // device views
@@ -118,6 +119,13 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int64_t stride;   // D + 1
   int64_t* slice_tag;
   Cols c;
+  // sliding windows: per-window panes [W][stride] for the one window a record below offset - slide gets
+  // beyond its slice's windows (SlidingEventTimeWindows.assignWindows starting at
+  // getWindowStartWithOffset, whose Java % of a negative numerator lands one slide above the record:
+  // SlidingEventTimeWindows.java:64-77, TimeWindow.java:239-241); wtag[w] = window number held, FREE else
+  Cols wc;
+  int64_t* wtag;
+  int32_t W;
   OutLog o;
   int32_t* err;
   unsigned long long* stats;
@@ -261,7 +269,9 @@ struct RecWin {
   int32_t n_windows;  // windows assigned
   int32_t n_late;     // of which late (dropped)
   int32_t n_fire;     // of which not late but maxTimestamp <= watermark (per-element fire)
-  bool quirk;         // sliding assignment outside the slice-exact regime
+  bool quirk;         // sliding: the record also gets window qn (Java % of a negative numerator)
+  bool q_late, q_fire;  // ... which is late / already fired (per-element fire)
+  int64_t qn;
   int64_t lo, hi;     // the slice's timestamps [lo, hi]: every ts in it gets this same RecWin (lo > hi: none)
 };
 
@@ -272,19 +282,39 @@ template <bool INL>
 __device__ __forceinline__ RecWin record_windows_sliding_body(const SlideSpec& s, int64_t ts, int64_t wm) {
   RecWin r;
   r.quirk = false;
+  r.q_late = false;
+  r.q_fire = false;
+  r.qn = 0;
   r.n_late = 0;
   r.n_fire = 0;
-  int64_t x = jadd(jsub(ts, s.offset), s.g);
-  if (x < 0 || jadd(jsub(ts, s.offset), s.slide) < 0) r.quirk = true;   // Java % of a negative numerator
-  {
+  const int64_t y = jsub(ts, s.offset);
+  const int64_t x = jadd(y, s.g);
+  if (x >= 0) {
     int64_t q, rem;
     if (INL) jdivmod_inl(x, s.g, s.inv_g, q, rem);
     else jdivmod(x, s.g, s.inv_g, q, rem);
     r.m = q - 1;
-    // ts' in [ts - rem, ts - rem + g) shares q; x >= 0 makes the quirk test monotone over that range
+    // ts' in [ts - rem, ts - rem + g) shares q
     r.lo = jsub(ts, rem);
     r.hi = jadd(r.lo, s.g - 1);
-    if (r.quirk || r.hi < r.lo) { r.lo = 1; r.hi = 0; }
+    if (r.hi < r.lo) { r.lo = 1; r.hi = 0; }
+  } else {
+    r.m = floor_div(y, s.g);   // the slice holding ts (below the first slice at or above the offset)
+    r.lo = 1; r.hi = 0;
+  }
+  if (jadd(y, s.slide) < 0) {
+    // getWindowStartWithOffset(ts, offset, slide) = ts - (y + slide) % slide: a negative Java remainder puts
+    // the first window one slide above the floor start — one window more than the slice's (n_hi + 1)
+    r.lo = 1; r.hi = 0;
+    if (y % s.slide != 0) {
+      r.quirk = true;
+      r.qn = floor_div(r.m, s.R) + 1;
+      const int64_t start = jadd(s.offset, (int64_t)((uint64_t)r.qn * (uint64_t)s.slide));
+      const int64_t max_ts = jsub(jadd(start, s.size), 1);
+      const int64_t ct = cleanup_time(max_ts, s.lateness);
+      r.q_late = ct <= wm;
+      r.q_fire = !r.q_late && max_ts <= wm;
+    }
   }
   int64_t n_hi = floor_div(r.m, s.R);
   int64_t n_lo = floor_div(r.m - s.K, s.R) + 1;
@@ -311,6 +341,9 @@ __device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int6
   }
   RecWin r;
   r.quirk = false;
+  r.q_late = false;
+  r.q_fire = false;
+  r.qn = 0;
   r.n_late = 0;
   r.n_fire = 0;
   int64_t x = jadd(jsub(ts, s.offset), s.size);
@@ -391,7 +424,31 @@ struct BatchIn {
   int64_t* new_list;
   unsigned long long* new_count;
   int64_t new_capacity;
+  // sliding: records with the assigner's extra window (entries of QK_WORDS: key, window number, value,
+  // ordinal, f1), applied to the window panes before the next firing watermark (k_quirk_apply)
+  int64_t* quirk;
+  unsigned long long* quirk_count;
+  int64_t quirk_capacity;
+  const int64_t* f1;   // the batch's f1 column (the quirk entries carry their f1; NULL = the timestamp)
 };
+constexpr int QK_WORDS = 5;
+
+// a record's extra sliding window (RecWin.quirk): late -> counted; already fired -> a per-element fire of
+// a window pane (not implemented: FW_ERR_UNSUPPORTED); else listed for k_quirk_apply
+__device__ __forceinline__ void quirk_record(const Spec& s, const BatchIn& b, int64_t key, int64_t i, int64_t qn, bool q_late,
+                                          bool q_fire) {
+  if (q_late) { atomicAdd(&s.stats[ST_LATE], 1ull); return; }
+  if (q_fire || s.by) { set_error(s.err, FW_ERR_UNSUPPORTED); return; }
+  const unsigned long long pos = atomicAdd(b.quirk_count, 1ull);
+  if ((int64_t)pos >= b.quirk_capacity) { cap_error(s, 22); return; }
+  int64_t* q = b.quirk + (int64_t)pos * QK_WORDS;
+  q[0] = key;
+  q[1] = qn;
+  q[2] = b.val[i];
+  q[3] = b.ord_base + i;
+  q[4] = b.f1 ? b.f1[i] : b.ts[i];
+  atomicAdd(&s.stats[ST_QUIRK], 1ull);
+}
 
 __device__ __forceinline__ int64_t window_start_n(const Spec& s, int64_t n) {
   return jadd(s.offset, (int64_t)((uint64_t)n * (uint64_t)(s.assigner == FW_TUMBLING ? s.size : s.slide)));
@@ -444,7 +501,7 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
     w.m = 0; w.n_late = 0; w.n_fire = 0; w.n_windows = 0; w.quirk = false;
     if (ok) {
       w = record_windows(s, ts, b.wm);
-      if (w.quirk && s.assigner == FW_SLIDING) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
+      if (w.quirk) quirk_record(s, b, key, i, w.qn, w.q_late, w.q_fire);
     }
     // late statistics: (record, window) pairs dropped (wave-uniform reduction)
     {
@@ -754,12 +811,9 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
         const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
         const int64_t ts = b.ts[base + t];
         const RecWin w = record_windows<true>(s, ts, b.wm);
-        int32_t f = 0;
-        if (w.quirk && s.assigner == FW_SLIDING) set_error(s.err, FW_ERR_UNSUPPORTED);
-        else {
-          const bool live = (w.n_windows - w.n_late) > 0;
-          f = (live ? 1 : 0) | (live && w.n_fire > 0 ? 2 : 0) | (w.n_late << 2);
-        }
+        if (w.quirk) quirk_record(s, b, kk[k], base + t, w.qn, w.q_late, w.q_fire);
+        const bool live = (w.n_windows - w.n_late) > 0;
+        const int32_t f = (live ? 1 : 0) | (live && w.n_fire > 0 ? 2 : 0) | (w.n_late << 2);
         sm[t] = w.m;
         sf[t] = f;
       }
@@ -1480,24 +1534,33 @@ __global__ void k_late_prepare(Spec s, const unsigned long long* sorted_key, int
   acc[j] = a;
 }
 
-__device__ __forceinline__ bool pane_present(const Spec& s, int64_t idx) {
-  return s.first ? s.c.first[idx] != INT64_MAX : s.c.present[idx] != 0;
+__device__ __forceinline__ bool cols_present(const Spec& s, const Cols& c, int64_t idx) {
+  return s.first ? c.first[idx] != INT64_MAX : c.present[idx] != 0;
 }
+__device__ __forceinline__ bool pane_present(const Spec& s, int64_t idx) { return cols_present(s, s.c, idx); }
 
-__device__ __forceinline__ LateAcc pane_load(const Spec& s, int64_t idx) {
+__device__ __forceinline__ LateAcc cols_load(const Spec& s, const Cols& c, int64_t idx) {
   LateAcc a;
   a.vt = s.vt;
-  a.sum = s.c.sum ? s.c.sum[idx] : 0;
-  a.mn = s.c.mn ? s.c.mn[idx] : INT64_MAX;
-  a.mx = s.c.mx ? s.c.mx[idx] : INT64_MIN;
-  a.cnt = s.c.cnt ? s.c.cnt[idx] : 0;
+  a.sum = c.sum ? c.sum[idx] : 0;
+  a.mn = c.mn ? c.mn[idx] : INT64_MAX;
+  a.mx = c.mx ? c.mx[idx] : INT64_MIN;
+  a.cnt = c.cnt ? c.cnt[idx] : 0;
   if (s.by) {   // the extremal record: ordinal in the count column, its f1 in f1v
     a.by = s.by | (s.by_last ? 1 : 0);
     a.ord = a.cnt;
     a.cnt = 0;
-    a.f1 = s.c.f1v[idx];
+    a.f1 = c.f1v[idx];
   }
   return a;
+}
+__device__ __forceinline__ LateAcc pane_load(const Spec& s, int64_t idx) { return cols_load(s, s.c, idx); }
+
+// slot of window n's window pane (sliding, -1: none)
+__device__ __forceinline__ int32_t wpane_slot(const Spec& s, int64_t n) {
+  if (s.W == 0) return -1;
+  const int32_t w = (int32_t)floor_mod(n, s.W);
+  return s.wtag[w] == n ? w : -1;
 }
 
 __device__ __forceinline__ void emit_record(const Spec& s, unsigned long long pos, int64_t key, int64_t f1, int64_t ts,
@@ -1654,6 +1717,16 @@ __global__ void k_fire_emit(Spec s, const unsigned long long* sorted_key, int64_
       base = any ? op(base, bb) : bb;
       any = true;
     }
+    const int32_t wq = wpane_slot(s, n);   // the window's own pane (records with the assigner's extra window)
+    if (wq >= 0) {
+      const int64_t idx = (int64_t)wq * s.stride + kid;
+      if (cols_present(s, s.wc, idx)) {
+        if (s.first && s.wc.first[idx] < best) { best = s.wc.first[idx]; bf1 = s.wc.f1v[idx]; }
+        const LateAcc bb = cols_load(s, s.wc, idx);
+        base = any ? op(base, bb) : bb;
+        any = true;
+      }
+    }
     out = any ? op(base, scanned[j]) : scanned[j];
     // first arrival: the window's earliest slice record, else the head of this window's late records
     f1 = any ? bf1 : f1col[(int64_t)(sorted_key[headpos[j]] & ((1ull << idx_bits) - 1))];
@@ -1683,11 +1756,12 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   __shared__ int64_t task_n[WM_MAXT];
   __shared__ int32_t purge[WM_MAXP];
   __shared__ int32_t slots[MAX_K];
-  __shared__ int32_t n_tasks, n_purge, last;
+  __shared__ int32_t wpurge[WM_MAXP];
+  __shared__ int32_t n_tasks, n_purge, n_wpurge, wslot_t, last;
   __shared__ int32_t wtot[WM_THREADS / 64];
   __shared__ unsigned long long base;
   __shared__ unsigned long long fired;
-  if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; last = 0; fired = 0; }
+  if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; n_wpurge = 0; last = 0; fired = 0; }
   __syncthreads();
   for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) {
     const int64_t m = s.slice_tag[p];
@@ -1716,8 +1790,28 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       if (q < WM_MAXP) purge[q] = p;
     }
   }
+  // window panes (sliding: the assigner's extra windows): a firing window without any live slice is a task
+  // of its own; a pane whose window's cleanup time passed is purged
+  for (int32_t w = threadIdx.x; w < s.W; w += WM_THREADS) {
+    const int64_t n = s.wtag[w];
+    if (n == FREE_TAG) continue;
+    const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+    if (max_ts > wm_old && max_ts <= wm_new) {
+      bool slice_live = false;
+      for (int64_t mm = n * s.R; mm < n * s.R + s.K && !slice_live; ++mm) slice_live = s.slice_tag[floor_mod(mm, s.P)] == mm;
+      if (!slice_live) {
+        const int32_t t = atomicAdd(&n_tasks, 1);
+        if (t < WM_MAXT) task_n[t] = n;
+        else cap_error(s, 12);
+      }
+    }
+    if (cleanup_time(max_ts, s.lateness) <= wm_new) {
+      const int32_t q = atomicAdd(&n_wpurge, 1);
+      if (q < WM_MAXP) wpurge[q] = w;
+    }
+  }
   __syncthreads();
-  const int32_t nt = min(n_tasks, WM_MAXT), np = min(n_purge, WM_MAXP);
+  const int32_t nt = min(n_tasks, WM_MAXT), np = min(n_purge, WM_MAXP), nwp = min(n_wpurge, WM_MAXP);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t gstride = (int64_t)gridDim.x * WM_THREADS;
   LateCombine op;
@@ -1728,6 +1822,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       const int32_t pp = (int32_t)floor_mod(mm, s.P);
       slots[threadIdx.x] = s.slice_tag[pp] == mm ? pp : -1;
     }
+    if (threadIdx.x == 0) wslot_t = wpane_slot(s, n);
     __syncthreads();
     const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
     for (int64_t k0 = (int64_t)blockIdx.x * WM_THREADS; k0 < s.stride; k0 += gstride) {
@@ -1753,6 +1848,18 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
           const LateAcc b = pane_load(s, idx);
           a = any ? op(a, b) : b;
           any = true;
+        }
+        if (wslot_t >= 0) {   // the window's own pane
+          const int64_t idx = (int64_t)wslot_t * s.stride + kid;
+          if (cols_present(s, s.wc, idx)) {
+            if (FIRST) {
+              const int64_t o = s.wc.first[idx];
+              if (o < best_ord) { best_ord = o; f1 = s.wc.f1v[idx]; }
+            }
+            const LateAcc b = cols_load(s, s.wc, idx);
+            a = any ? op(a, b) : b;
+            any = true;
+          }
         }
       }
       // block-aggregated append: one device atomic per workgroup and chunk
@@ -1780,6 +1887,17 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       if (s.first) s.c.first[idx] = INT64_MAX; else s.c.present[idx] = 0;
     }
   }
+  for (int32_t q = 0; q < nwp; ++q) {
+    const int64_t pbase = (int64_t)wpurge[q] * s.stride;
+    for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < s.stride; kid += gstride) {
+      const int64_t idx = pbase + kid;
+      if (s.wc.sum) s.wc.sum[idx] = sum_identity(s.vt);
+      if (s.wc.mn) s.wc.mn[idx] = INT64_MAX;
+      if (s.wc.mx) s.wc.mx[idx] = INT64_MIN;
+      if (s.wc.cnt) s.wc.cnt[idx] = 0;
+      if (s.first) s.wc.first[idx] = INT64_MAX; else s.wc.present[idx] = 0;
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     if (fired) atomicAdd(&s.stats[ST_FIRED], fired);
@@ -1789,6 +1907,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   if (!last) return;
   // last workgroup: free the purged slots, then record the watermark's position in the log
   for (int32_t q = threadIdx.x; q < np; q += WM_THREADS) s.slice_tag[purge[q]] = FREE_TAG;
+  for (int32_t q = threadIdx.x; q < nwp; q += WM_THREADS) s.wtag[wpurge[q]] = FREE_TAG;
   if (threadIdx.x == 0) {
     *done = 0u;
     const unsigned long long cnt = atomicAdd(s.o.count, 0ull);
@@ -1845,6 +1964,8 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
     bool live = false;
     for (int p = 0; p < s.P && !live; ++p)
       if (tags[p] != FREE_TAG) live = pane_present(s, (int64_t)p * s.stride + dbase + x);
+    for (int w = 0; w < s.W && !live; ++w)   // window panes (sliding extra windows)
+      if (s.wtag[w] != FREE_TAG) live = cols_present(s, s.wc, (int64_t)w * s.stride + dbase + x);
     if (!live) {
       kg_evicted[key_group_for_hash(long_hash_code(key), s.mp)] = 1;
       continue;
@@ -1874,6 +1995,33 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
       __syncthreads();
     }
   };
+  auto wmove = [&](int64_t* col, int64_t ident) {   // the window panes' columns likewise
+    for (int w = 0; w < s.W; ++w) {   // uniform
+      if (s.wtag[w] == FREE_TAG) continue;
+      int64_t* c = col + (int64_t)w * s.stride + dbase;
+      for (int x = threadIdx.x; x < KB; x += CP_THREADS) tmp[x] = c[x];
+      __syncthreads();
+      for (int y = threadIdx.x; y < KB; y += CP_THREADS) c[y] = inv[y] >= 0 ? tmp[inv[y]] : ident;
+      __syncthreads();
+    }
+  };
+  if (s.W > 0) {
+    if (s.wc.sum) wmove(s.wc.sum, sum_identity(s.vt));
+    if (s.wc.mn) wmove(s.wc.mn, INT64_MAX);
+    if (s.wc.mx) wmove(s.wc.mx, INT64_MIN);
+    if (s.wc.cnt) wmove(s.wc.cnt, 0);
+    if (s.first) { wmove(s.wc.first, INT64_MAX); wmove(s.wc.f1v, 0); }
+    else {
+      for (int w = 0; w < s.W; ++w) {
+        if (s.wtag[w] == FREE_TAG) continue;
+        unsigned char* c = s.wc.present + (int64_t)w * s.stride + dbase;
+        for (int x = threadIdx.x; x < KB; x += CP_THREADS) tmp[x] = c[x];
+        __syncthreads();
+        for (int y = threadIdx.x; y < KB; y += CP_THREADS) c[y] = inv[y] >= 0 ? (unsigned char)tmp[inv[y]] : 0;
+        __syncthreads();
+      }
+    }
+  }
   if (s.c.sum) move(s.c.sum, sum_identity(s.vt));
   if (s.c.mn) move(s.c.mn, INT64_MAX);
   if (s.c.mx) move(s.c.mx, INT64_MIN);
@@ -1892,6 +2040,43 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
     }
   }
   for (int y = threadIdx.x; y < KB; y += CP_THREADS) s.dir_keys[dbase + y] = nkey[y];
+}
+
+// the listed extra-window records into their window panes (one workgroup; the list is short): key id, the
+// pane's slot for window qn, device-scope atomics on the window-pane columns, then f1 of each pane's first
+// arrival.  Launched before every firing watermark of a sliding engine, so the panes are complete before
+// their window fires (a record whose extra window had already fired is rejected at ingest).
+__global__ __launch_bounds__(1024) void k_quirk_apply(Spec s, int64_t* list, unsigned long long* count, int64_t cap) {
+  const int64_t n = min((int64_t)*count, cap);
+  for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+    int64_t* q = list + e * QK_WORDS;
+    const int64_t kid = dir_lookup(s, q[0]);
+    const int32_t w = kid < 0 ? -1 : slice_slot_at(s.wtag, s.W, q[1]);
+    if (kid < 0 || w < 0) { cap_error(s, 23); q[0] = -1; continue; }
+    const int64_t idx = (int64_t)w * s.stride + kid;
+    const int64_t v = q[2];
+    if (s.wc.sum) {
+      if (s.vt == FW_VALUE_I64) atomicAdd((unsigned long long*)&s.wc.sum[idx], (unsigned long long)v);
+      else unsafeAtomicAdd((double*)&s.wc.sum[idx], __longlong_as_double(v));
+    }
+    if (s.wc.mn) atomicMin((long long*)&s.wc.mn[idx], (long long)min_code(s.vt, s.cmpto, v));
+    if (s.wc.mx) atomicMax((long long*)&s.wc.mx[idx], (long long)max_code(s.vt, s.cmpto, v));
+    if (s.wc.cnt) atomicAdd((unsigned long long*)&s.wc.cnt[idx], 1ull);
+    if (s.first) atomicMin((long long*)&s.wc.first[idx], (long long)q[3]);
+    else s.wc.present[idx] = 1;
+    q[0] = idx;   // the pane, for the f1 pass
+  }
+  __threadfence();
+  __syncthreads();
+  if (s.first) {
+    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+      const int64_t* q = list + e * QK_WORDS;
+      if (q[0] < 0) continue;
+      if (__hip_atomic_load(&s.wc.first[q[0]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q[3]) s.wc.f1v[q[0]] = q[4];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *count = 0;
 }
 
 __global__ void k_mark_only(Spec s, int64_t wm) {
@@ -2191,6 +2376,10 @@ struct fw_engine {
   void *dec_table = nullptr, *dec_small = nullptr, *dec_bytes = nullptr;
   size_t dec_table_cap = 0, dec_small_cap = 0, dec_bytes_cap = 0;
   int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
+  // sliding: the assigner's extra-window records, one list per routed buffer set (fw_push_batch applies
+  // a batch's list right after its ingest, on the engine stream)
+  int64_t* quirk_list[NBUF] = {};
+  unsigned long long* quirk_count = nullptr;
   // session windows (FW_SESSION, fw_session.hip)
   bool session = false;
   SessDev sess{};
@@ -2322,7 +2511,7 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
     hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b,
                        r, f1col);
   e->phase_end(b.n);
-  (void)hipEventRecord(e->ev_agg[par], e->stream);
+  // (ev_agg[par] is recorded by fw_push_batch once the batch's extra-window list is applied too)
 }
 
 // no window of the assigner has its maxTimestamp or its cleanup time in (old, new]: the advance fires
@@ -2412,7 +2601,18 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipSetDevice(c.device));
   e->dev = c.device;
   HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-  HIPCHK(e, hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking));
+  {
+    // FW_STREAM_PRIO (diagnostics): 1 = route stream high priority, 2 = engine stream high priority
+    const char* sp = getenv("FW_STREAM_PRIO");
+    const int which = sp ? atoi(sp) : 0;
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    HIPCHK(e, hipStreamCreateWithPriority(&e->rstream, hipStreamNonBlocking, which == 1 ? hi : lo));
+    if (which == 2) {
+      HIPCHK(e, hipStreamDestroy(e->stream));
+      HIPCHK(e, hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, hi));
+    }
+  }
   e->serial = getenv("FW_SERIAL") && atoi(getenv("FW_SERIAL")) != 0;
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -2484,6 +2684,19 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     s.c.first = nullptr;
     s.c.f1v = nullptr;
     s.c.present = e->alloc<uint8_t>(cells);
+  }
+  if (c.assigner == FW_SLIDING) {   // window panes for the assigner's extra windows
+    s.W = P;
+    s.wtag = e->alloc<int64_t>((size_t)P);
+    s.wc.sum = s.c.sum ? e->alloc<int64_t>(cells) : nullptr;
+    s.wc.mn = s.c.mn ? e->alloc<int64_t>(cells) : nullptr;
+    s.wc.mx = s.c.mx ? e->alloc<int64_t>(cells) : nullptr;
+    s.wc.cnt = s.c.cnt ? e->alloc<int64_t>(cells) : nullptr;
+    s.wc.first = s.c.first ? e->alloc<int64_t>(cells) : nullptr;
+    s.wc.f1v = s.c.f1v ? e->alloc<int64_t>(cells) : nullptr;
+    s.wc.present = s.c.present ? e->alloc<uint8_t>(cells) : nullptr;
+    for (int q = 0; q < fw_engine::NBUF; ++q) e->quirk_list[q] = e->alloc<int64_t>((size_t)c.max_batch * QK_WORDS);
+    e->quirk_count = e->alloc<unsigned long long>(fw_engine::NBUF);
   }
   OutLog& o = s.o;
   o.capacity = c.out_capacity;
@@ -2617,6 +2830,16 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   launch_fill(e, s.c.cnt, 0, (int64_t)cells);
   launch_fill(e, s.c.first, INT64_MAX, (int64_t)cells);
   if (s.c.present) HIPCHK(e, hipMemsetAsync(s.c.present, 0, cells, e->stream));
+  if (s.W > 0) {
+    launch_fill(e, s.wtag, FREE_TAG, s.W);
+    launch_fill(e, s.wc.sum, sum_identity(s.vt), (int64_t)cells);
+    launch_fill(e, s.wc.mn, INT64_MAX, (int64_t)cells);
+    launch_fill(e, s.wc.mx, INT64_MIN, (int64_t)cells);
+    launch_fill(e, s.wc.cnt, 0, (int64_t)cells);
+    launch_fill(e, s.wc.first, INT64_MAX, (int64_t)cells);
+    if (s.wc.present) HIPCHK(e, hipMemsetAsync(s.wc.present, 0, cells, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->quirk_count, 0, 8 * fw_engine::NBUF, e->stream));
+  }
   HIPCHK(e, hipMemsetAsync(s.dir_min_used, 0, 4, e->stream));
   HIPCHK(e, hipMemsetAsync(o.count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(o.mark_count, 0, 8, e->stream));
@@ -2649,7 +2872,9 @@ static int check_device_error(fw_engine* e) {
         break;
       case FW_ERR_KEY_GROUP: msg = "Unexpected key group index. This indicates a bug."; break;
       case FW_ERR_CAPACITY: msg = "capacity exceeded (key directory, slice pool, per-element fire list or output log)"; break;
-      case FW_ERR_UNSUPPORTED: msg = "sliding-window timestamp below offset - slide: not supported by the slice path"; break;
+      case FW_ERR_UNSUPPORTED: msg = "a record's extra sliding window (timestamp below offset - slide, Java % of a negative "
+                                     "numerator) is already behind the watermark, or maxBy/minBy with such a record: "
+                                     "per-element fire of a window pane not supported"; break;
     }
     return fail(e, derr, msg);
   }
@@ -2706,6 +2931,10 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.fire_key = e->fire_key;
   b.fire_count = e->fire_count;
   b.fire_capacity = e->fire_cap;
+  b.quirk = e->s.W > 0 ? e->quirk_list[par] : nullptr;
+  b.quirk_count = e->s.W > 0 ? e->quirk_count + par : nullptr;
+  b.quirk_capacity = e->s.W > 0 ? e->cfg.max_batch : 0;
+  b.f1 = df1;
   b.new_list = e->new_list;
   b.new_count = e->new_counts ? e->new_counts + half : nullptr;
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
@@ -2718,6 +2947,10 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     FW_DISPATCH(launch_ingest_t, e, b);
     e->phase_end(n);
   }
+  if (e->s.W > 0)   // sliding: this batch's extra-window records into the window panes
+    hipLaunchKernelGGL(k_quirk_apply, dim3(1), dim3(1024), 0, e->stream, e->s, e->quirk_list[par], e->quirk_count + par,
+                       e->cfg.max_batch);
+  if (e->routed) HIPCHK(e, hipEventRecord(e->ev_agg[par], e->stream));
   e->batches++;
   HIPCHK(e, hipGetLastError());
   if (e->s.first && !e->routed) {   // the partitioned form sets f1 in k_aggregate
@@ -3010,6 +3243,14 @@ static int reject(fw_engine* e, int code, const std::string& msg) {
   return code;
 }
 
+// window panes hold state a checkpoint blob does not carry (the sliding assigner's extra windows)
+static bool window_panes_used(fw_engine* e) {
+  if (e->s.W == 0) return false;
+  unsigned long long n = 0;
+  if (hipMemcpy(&n, e->s.stats + ST_QUIRK, 8, hipMemcpyDeviceToHost) != hipSuccess) return true;
+  return n > 0;
+}
+
 static void snap_header(const fw_engine* e, int32_t kg, int64_t n, int64_t* h) {
   const fw_config& c = e->cfg;
   const int64_t w[FW_SNAP_HEADER_WORDS] = {FW_SNAP_MAGIC, 2, kg, n, e->cur_wm, c.assigner, c.size,
@@ -3092,6 +3333,7 @@ int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* le
   if (!e || !len) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
+  if (window_panes_used(e)) return reject(e, FW_ERR_UNSUPPORTED, "sliding windows: records below offset - slide put state in window panes, which no checkpoint layout carries");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)   // HeapInternalTimerService.restoreTimersForKeyGroup's check
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -3297,6 +3539,7 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   if (!e || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
+  if (window_panes_used(e)) return reject(e, FW_ERR_UNSUPPORTED, "sliding windows: records below offset - slide put state in window panes, which no checkpoint layout carries");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");

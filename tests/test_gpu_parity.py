@@ -143,17 +143,35 @@ def test_sliding_lateness_double_uneven(hip, oracle_engine, mode):
     assert so["late_fires"] > 0 and sg["late_fires"] == so["late_fires"]
 
 
-def test_sliding_negative_timestamp_quirk_is_rejected(hip):
-    """Java's % on a negative (ts - offset + slide) makes SlidingEventTimeWindows assign a window that
-    does not contain ts (TimeWindow.java:239-241); the slice path reports it instead of diverging."""
-    from flink_amd import _abi
+def test_sliding_negative_remainder_known_answer(hip, oracle_engine):
+    """SlidingEventTimeWindows.of(3 s, 1 s) and a record at ts = -1500: getWindowStartWithOffset(-1500, 0, 1000)
+    = -1500 - (-500 % 1000) = -1000 (Java % of a negative numerator, TimeWindow.java:239-241), so the
+    assigner's loop (SlidingEventTimeWindows.java:64-77) yields starts -1000, -2000, -3000, -4000: one window
+    more than the three containing the record.  Worked by hand from the Java source."""
     from flink_amd.windowing import SlidingEventTimeWindows
-    e = hip(_cfg(SlidingEventTimeWindows.of(3000, 1000)))
-    e.push(np.array([1], np.int64), np.array([-1500], np.int64), np.array([1], np.int64))
-    with pytest.raises(_abi.FwError) as ei:
-        e.sync()
-    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
-    e.close()
+    want = sorted([(7, 1999, 5), (7, 999, 5), (7, -1, 5), (7, -1001, 5)])   # (key, maxTimestamp, sum)
+    for f in (hip, oracle_engine):
+        for mode in (1, 2):
+            e = f(_cfg(SlidingEventTimeWindows.of(3000, 1000), mode=mode))
+            e.push(np.array([7], np.int64), np.array([-1500], np.int64), np.array([5], np.int64))
+            e.advance_watermark(LONG_MAX)
+            r = e.collect()
+            e.close()
+            assert sorted(zip(r["key"].tolist(), r["ts"].tolist(), r["sum_i64"].tolist())) == want
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("spec,lateness", [((3000, 1000, 0), 0), ((2500, 1000, 300), 0), ((3000, 1000, 0), 1500),
+                                           ((10000, 1000, 0), 0)])
+def test_sliding_negative_timestamps(hip, oracle_engine, mode, spec, lateness):
+    """A stream crossing from negative to positive event time: records below offset - slide get the
+    assigner's extra window (window panes beside the slices), bit-exact incl. first-arrival f1."""
+    from flink_amd.windowing import SlidingEventTimeWindows
+    keys, ts, vals = gen_stream(100_000, 700, rate=1 << 12, ooo=300, t0=-20_000)
+    cfg = _cfgm(mode, SlidingEventTimeWindows.of(*spec), ("sum", "min", "max", "count"), first=True, lateness=lateness)
+    sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 4096, 200, ["sum_i64", "min_i64", "max_i64", "count"],
+                       first=True)
+    assert sg["records_late"] == so["records_late"]
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -77,3 +77,19 @@ def test_oracle_parallel_job_matches_single_subtask():
     tot = sum(r["n"] for r in res)
     cs = int(np.sum(np.concatenate([r["sum_i64"] for r in res]).astype(np.uint64)).astype(np.int64))
     assert tot == n1 and cs == cs1
+
+
+def test_oracle_sliding_negative_remainder_known_answer():
+    """SlidingEventTimeWindows.of(3 s, 1 s), one record at ts = -1500: Java's -500 % 1000 = -500 puts the first
+    window start at -1000 (TimeWindow.java:239-241), so the loop of SlidingEventTimeWindows.java:64-77 assigns
+    four windows (starts -1000 .. -4000), one more than contain the record (worked by hand from the source)."""
+    from flink_amd.windowing import ReduceFunction, SlidingEventTimeWindows, make_config
+    cfg = make_config(SlidingEventTimeWindows.of(3000, 1000), ReduceFunction(("sum",)), key_capacity=1024,
+                      max_batch=1 << 12, out_capacity=1 << 16)
+    e = oracle.OracleEngine(cfg)
+    e.push(np.array([7], np.int64), np.array([-1500], np.int64), np.array([5], np.int64))
+    e.advance_watermark((1 << 63) - 1)
+    r = e.collect()
+    e.close()
+    assert sorted(zip(r["key"].tolist(), r["ts"].tolist(), r["sum_i64"].tolist())) == \
+        [(7, -1001, 5), (7, -1, 5), (7, 999, 5), (7, 1999, 5)]
