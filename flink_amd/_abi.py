@@ -33,6 +33,7 @@ FW_AGG_MINBY = 32
 FW_AGGF_COMPARABLE = 1
 FW_AGGF_BY_LAST = 2
 FW_AGGF_FOLD = 4
+FW_AGG_LIST = 64
 FW_VALUE_I64 = 0
 FW_VALUE_F64 = 1
 FW_MEM_HOST = 0
@@ -59,7 +60,8 @@ class FwConfig(ctypes.Structure):
                 ("allowed_lateness", _i64), ("value_type", _i32), ("agg_mask", _i32), ("keep_first_f1", _i32),
                 ("max_parallelism", _i32), ("kg_start", _i32), ("kg_end", _i32), ("device", _i32),
                 ("max_open_slices", _i32), ("key_capacity", _i64), ("max_batch", _i64), ("out_capacity", _i64),
-                ("ingest_mode", _i32), ("agg_flags", _i32), ("fold_initial", _i64)]
+                ("ingest_mode", _i32), ("agg_flags", _i32), ("fold_initial", _i64),
+                ("list_capacity", _i64)]
 
 
 class FwOut(ctypes.Structure):

@@ -2258,6 +2258,13 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+// list state (fw_list.hip): per pane slice slot a buffer of elements (kid, ordinal, value, f1)
+struct ListDev {
+  int64_t cap;                  // elements per slice slot
+  unsigned long long* cnt;      // [P] elements buffered
+  int64_t* buf;                 // [P][cap][4]
+};
+
 // session windows (fw_session.hip): per key id `sw` window slots, key-major [D + 1][sw]
 constexpr int SESS_SW_DEFAULT = 32, SESS_SW_MAX = 64;   // in-flight session windows per key
 struct SessDev {
@@ -2380,6 +2387,17 @@ struct fw_engine {
   // a batch's list right after its ingest, on the engine stream)
   int64_t* quirk_list[NBUF] = {};
   unsigned long long* quirk_count = nullptr;
+  // list state (FW_AGG_LIST, fw_list.hip)
+  bool list = false;
+  ListDev lst{};
+  int64_t* list_plan = nullptr;            // k_list_plan's output (device), copied to list_plan_h
+  std::vector<int64_t> list_plan_h;
+  unsigned long long *list_k1 = nullptr, *list_k2 = nullptr;   // sort keys (ordinal, then kid)
+  int64_t *list_v1 = nullptr, *list_v2 = nullptr;              // element indices
+  void* list_temp = nullptr;
+  size_t list_temp_bytes = 0;
+  int64_t list_tmp_cap = 0;
+  int64_t list_out = 0;                    // results appended since the last collect
   // session windows (FW_SESSION, fw_session.hip)
   bool session = false;
   SessDev sess{};
@@ -2429,6 +2447,7 @@ struct fw_engine {
     if (bload_host) (void)hipHostFree(bload_host);
     if (dir_keys_host) (void)hipHostFree(dir_keys_host);
     for (void* p : {dec_table, dec_small, dec_bytes}) if (p) (void)hipFree(p);
+    for (void* p : {(void*)list_k1, (void*)list_k2, (void*)list_v1, (void*)list_v2, list_temp}) if (p) (void)hipFree(p);
   }
 };
 
@@ -2438,6 +2457,10 @@ static thread_local std::string g_create_error;
 int session_create(fw_engine* e);
 int session_push(fw_engine* e, const fw::BatchIn& b);
 int session_watermark(fw_engine* e, int64_t wm);
+// list state (fw_list.hip)
+int list_create(fw_engine* e);
+int list_push(fw_engine* e, const fw::BatchIn& b);
+int list_watermark(fw_engine* e, int64_t wm);
 
 static int fail(fw_engine* e, int code, const std::string& msg) {
   if (e) { e->err = msg; if (e->sticky == FW_OK) e->sticky = code; }
@@ -2575,6 +2598,11 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->session && (c.keep_first_f1 || (c.agg_mask & (FW_AGG_MAXBY | FW_AGG_MINBY))))
     return unsupported("session windows: first-arrival f1 and maxBy / minBy follow HashSet order after a merge "
                        "(sum / min / max / count only)");
+  e->list = c.agg_mask == FW_AGG_LIST;
+  if ((c.agg_mask & FW_AGG_LIST) && !e->list) return bad("list state (FW_AGG_LIST) is used alone");
+  if (e->list && (e->session || (c.agg_flags & FW_AGGF_FOLD)))
+    return unsupported("list state: tumbling and sliding windows (merging list state follows HashSet order)");
+  if (e->list) { c.ingest_mode = 1; c.keep_first_f1 = 1; e->cfg = c; }
   if (e->session) {
     if (c.max_open_slices > SESS_SW_MAX) return bad("session windows: at most 64 in-flight sessions per key (max_open_slices)");
     e->sess.sw = c.max_open_slices > 0 ? c.max_open_slices : SESS_SW_DEFAULT;
@@ -2587,7 +2615,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     return bad("bad key-group range");
   if (c.value_type != FW_VALUE_I64 && c.value_type != FW_VALUE_F64) return bad("bad value type");
   const bool by = (c.agg_mask & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;
-  if ((c.agg_mask & ~63) != 0 || c.agg_mask == 0 || (by && c.agg_mask != FW_AGG_MAXBY && c.agg_mask != FW_AGG_MINBY))
+  if ((c.agg_mask & ~127) != 0 || c.agg_mask == 0 || (by && c.agg_mask != FW_AGG_MAXBY && c.agg_mask != FW_AGG_MINBY))
     return bad("bad aggregate mask (maxBy / minBy return the whole record and combine with nothing else)");
   if ((c.agg_flags & ~(FW_AGGF_COMPARABLE | FW_AGGF_BY_LAST | FW_AGGF_FOLD)) != 0) return bad("bad aggregate flags");
   if ((c.agg_flags & FW_AGGF_FOLD) && (c.assigner == FW_SESSION))
@@ -2642,7 +2670,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.kg_start = c.kg_start;
   s.kg_end = c.kg_end;
   s.vt = c.value_type;
-  s.agg = by ? c.agg_mask : (c.agg_mask == FW_AGG_SUM ? FW_AGG_SUM : 15);   // instantiated reduce shapes
+  s.agg = by ? c.agg_mask : (c.agg_mask == FW_AGG_SUM || e->list ? FW_AGG_SUM : 15);   // instantiated reduce shapes
+  // (list state: the sum column carries each element's value, f1 its f1)
   s.by = by ? c.agg_mask : 0;
   s.by_last = (c.agg_flags & FW_AGGF_BY_LAST) ? 1 : 0;
   s.cmpto = by || (c.agg_flags & FW_AGGF_COMPARABLE) ? 1 : 0;
@@ -2821,6 +2850,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->session) {
     if (int rc = session_create(e)) { g_create_error = "session window state allocation failed"; delete e; return rc; }
   }
+  if (e->list) {
+    if (int rc = list_create(e)) { g_create_error = "list state allocation failed"; delete e; return rc; }
+  }
   // initial state
   launch_fill(e, s.dir_keys, EMPTY_KEY, s.D);
   launch_fill(e, s.slice_tag, FREE_TAG, P);
@@ -2940,6 +2972,8 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
   if (e->session) {
     if (int rc = session_push(e, b)) return rc;
+  } else if (e->list) {
+    if (int rc = list_push(e, b)) return rc;
   } else if (e->routed) {
     FW_DISPATCH(launch_routed_t, e, b, df1, par);
   } else {
@@ -2960,7 +2994,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
                        e->cfg.max_batch);
     e->phase_end(n);
   }
-  if (e->cfg.allowed_lateness > 0 && !e->session) {
+  if (e->cfg.allowed_lateness > 0 && !e->session && !e->list) {
     // per-element fires: the list lengths on the host size the sorts
     unsigned long long nl = 0, nf = 0;
     HIPCHK(e, hipMemcpyAsync(&nl, e->late_count, 8, hipMemcpyDeviceToHost, e->stream));
@@ -3033,6 +3067,7 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   HIPCHK(e, hipSetDevice(e->dev));
   e->state_epoch++;
   if (e->session) return session_watermark(e, wm);
+  if (e->list) return list_watermark(e, wm);
   if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
     if (e->out_dirty) {   // per-element fires appended since the last device mark: the mark needs the count
       hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
@@ -3102,6 +3137,7 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
   e->hmarks.clear();
   e->dev_marks = 0;
   e->out_dirty = false;
+  e->list_out = 0;
   const int64_t n = (int64_t)cnt;
   std::memset(o, 0, sizeof(*o));
   o->n = n;
@@ -3140,7 +3176,7 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   // only the fields the reduce function asked for
-  const int32_t um = e->cfg.agg_mask;
+  const int32_t um = e->list ? FW_AGG_SUM : e->cfg.agg_mask;   // list state: the elements' values
   if (!(um & FW_AGG_SUM)) { o->sum_i64 = nullptr; o->sum_f64 = nullptr; }
   if (!(um & (FW_AGG_MIN | FW_AGG_MINBY))) { o->min_i64 = nullptr; o->min_f64 = nullptr; }
   if (!(um & (FW_AGG_MAX | FW_AGG_MAXBY))) { o->max_i64 = nullptr; o->max_f64 = nullptr; }
@@ -3332,6 +3368,7 @@ static int build_snapshot(fw_engine* e) {
 int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* len) {
   if (!e || !len) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (window_panes_used(e)) return reject(e, FW_ERR_UNSUPPORTED, "sliding windows: records below offset - slide put state in window panes, which no checkpoint layout carries");
   if (e->sticky) return e->sticky;
@@ -3357,6 +3394,7 @@ static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t
 int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   if (!e || !buf) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
@@ -3538,6 +3576,7 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
                          int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
   if (!e || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (window_panes_used(e)) return reject(e, FW_ERR_UNSUPPORTED, "sliding windows: records below offset - slide put state in window panes, which no checkpoint layout carries");
   if (e->sticky) return e->sticky;
@@ -3649,6 +3688,7 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
                         const void* state, int64_t state_len, const void* timers, int64_t timers_len) {
   if (!e || (!state && state_len) || !timers || state_len < 0) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
@@ -3783,3 +3823,4 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
 
 #include "fw_decode.hip"
 #include "fw_session.hip"
+#include "fw_list.hip"

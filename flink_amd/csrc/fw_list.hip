@@ -1,0 +1,247 @@
+// fw_list.hip — list window state on the GPU (included by fw_engine.hip).
+//
+// Replaces HeapListState under WindowedStream.apply(WindowFunction) (WindowedStream.java:244-345; the
+// operator's ListStateDescriptor "window-contents"): every element of a window is kept, and a firing
+// window hands the window function all of them (InternalIterableWindowFunction) in arrival order
+// (HeapListState.add appends; its Iterable iterates in insertion order).
+//
+// Layout: the pane slices of the reduce path (a record belongs to exactly one slice however many sliding
+// windows cover it), each with a buffer of elements (kid, arrival ordinal, value, f1).  A firing window
+// gathers its K slices' elements, sorts them by arrival ordinal and then (stably) by key id — rocPRIM
+// radix sorts — and appends one result row per element, grouped by key, to the output log; the host
+// runs the window function over each (key, window) group.  A slice is dropped when its last window's
+// cleanup time passes, like the reduce path's purge.  An element for a window that already fired but is
+// not yet cleaned up (allowed lateness) would re-fire the window with every element so far: not
+// implemented here, reported as FW_ERR_UNSUPPORTED.
+
+namespace fw {
+
+constexpr int LST_WORDS = 4;   // kid, ordinal, value, f1
+// k_list_plan output: [0] windows firing, [1] slots purged, then WM_MAXT (window, elements) pairs, then
+// WM_MAXP purged slots
+constexpr int LPLAN_WORDS = 2 + 2 * WM_MAXT + WM_MAXP;
+
+__global__ __launch_bounds__(BLOCK) void k_list_ingest(Spec s, BatchIn b, ListDev L) {
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < b.n; i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + threadIdx.x;   // uniform loop: every lane takes part in the wave appends
+    bool live = false;
+    int32_t p = -1;
+    int64_t kid = -1, ts = 0;
+    unsigned long long late = 0;
+    if (i < b.n) {
+      const int64_t key = b.key[i];
+      ts = b.ts[i];
+      const int32_t h = b.key_hash ? b.key_hash[i] : long_hash_code(key);
+      bool ok = true;
+      if (ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
+      const int32_t kg = record_key_group(s, h);
+      if (ok && (kg < s.kg_start || kg > s.kg_end)) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
+      if (ok) {
+        const RecWin w = record_windows(s, ts, b.wm);
+        late = (unsigned long long)w.n_late + (w.q_late ? 1ull : 0ull);
+        if (w.n_fire > 0 || (w.quirk && !w.q_late)) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
+        live = ok && (w.n_windows - w.n_late) > 0;
+        if (live) {
+          p = slice_slot(s, w.m);
+          kid = dir_find_or_insert(s, key);
+          if (p < 0 || kid < 0) { cap_error(s, 24); live = false; }
+        }
+      }
+    }
+    if (__any(late != 0)) {
+      for (int o = 32; o > 0; o >>= 1) late += __shfl_xor(late, o);
+      if ((threadIdx.x & 63) == 0 && late) atomicAdd(&s.stats[ST_LATE], late);
+    }
+    // wave-aggregated append when the wave's live records share one slice (an in-order stream)
+    const uint64_t lm = __ballot(live);
+    if (lm == 0) continue;
+    const int leader = __ffsll((long long)lm) - 1;
+    const int32_t p0 = __shfl(p, leader);
+    unsigned long long pos;
+    if (__all(!live || p == p0)) pos = wave_append(&L.cnt[p0], live);
+    else pos = live ? atomicAdd(&L.cnt[p], 1ull) : 0;
+    if (!live) continue;
+    if ((int64_t)pos >= L.cap) { cap_error(s, 25); continue; }
+    int64_t* el = L.buf + ((int64_t)p * L.cap + (int64_t)pos) * LST_WORDS;
+    el[0] = kid;
+    el[1] = b.ord_base + i;
+    el[2] = b.val[i];
+    el[3] = b.f1 ? b.f1[i] : ts;
+  }
+}
+
+// the firing windows (maxTimestamp in (old, new], a live slice) with their element counts, and the slices
+// whose last window's cleanup time passed
+__global__ __launch_bounds__(1024) void k_list_plan(Spec s, ListDev L, int64_t wm_old, int64_t wm_new, int64_t* plan) {
+  __shared__ int32_t nt, np;
+  if (threadIdx.x == 0) { nt = 0; np = 0; }
+  __syncthreads();
+  for (int32_t p = threadIdx.x; p < s.P; p += blockDim.x) {
+    const int64_t m = s.slice_tag[p];
+    if (m == FREE_TAG) continue;
+    const int64_t n_hi = floor_div(m, s.R), n_lo = floor_div(m - s.K, s.R) + 1;
+    for (int64_t n = n_lo; n <= n_hi; ++n) {
+      const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+      if (!(max_ts > wm_old && max_ts <= wm_new)) continue;
+      bool owner = true;   // the first live slice of window n lists it
+      for (int64_t mm = n * s.R; mm < m; ++mm)
+        if (s.slice_tag[floor_mod(mm, s.P)] == mm) { owner = false; break; }
+      if (!owner) continue;
+      int64_t cnt = 0;
+      for (int64_t mm = n * s.R; mm < n * s.R + s.K; ++mm) {
+        const int32_t pp = (int32_t)floor_mod(mm, s.P);
+        if (s.slice_tag[pp] == mm) cnt += (int64_t)min((unsigned long long)L.cap, L.cnt[pp]);
+      }
+      const int32_t t = atomicAdd(&nt, 1);
+      if (t < WM_MAXT) { plan[2 + 2 * t] = n; plan[3 + 2 * t] = cnt; }
+      else cap_error(s, 26);
+    }
+    const int64_t ct = cleanup_time(jsub(jadd(window_start_n(s, n_hi), s.size), 1), s.lateness);
+    if (ct <= wm_new) {
+      const int32_t q = atomicAdd(&np, 1);
+      if (q < WM_MAXP) plan[2 + 2 * WM_MAXT + q] = p;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) { plan[0] = min(nt, WM_MAXT); plan[1] = min(np, WM_MAXP); }
+}
+
+// window n's elements: sort keys (arrival ordinal) and their buffer positions
+__global__ __launch_bounds__(BLOCK) void k_list_gather(Spec s, ListDev L, int64_t n, unsigned long long* key, int64_t* idx) {
+  int64_t off[MAX_K + 1];
+  int32_t slot[MAX_K];
+  off[0] = 0;
+  for (int k = 0; k < s.K; ++k) {
+    const int64_t mm = n * s.R + k;
+    const int32_t pp = (int32_t)floor_mod(mm, s.P);
+    const bool live = s.slice_tag[pp] == mm;
+    slot[k] = pp;
+    off[k + 1] = off[k] + (live ? (int64_t)min((unsigned long long)L.cap, L.cnt[pp]) : 0);
+  }
+  const int64_t total = off[s.K];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int k = 0;
+    while (off[k + 1] <= e) ++k;
+    const int64_t at = ((int64_t)slot[k] * L.cap + (e - off[k])) * LST_WORDS;
+    key[e] = (unsigned long long)L.buf[at + 1] ^ 0x8000000000000000ull;   // ordinal, order-preserving unsigned
+    idx[e] = at;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_list_kid(ListDev L, const int64_t* idx, int64_t N, unsigned long long* key) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += (int64_t)gridDim.x * blockDim.x)
+    key[e] = (unsigned long long)L.buf[idx[e]];
+}
+
+// one result row per element, grouped by key (sorted), at output positions base..base+N
+__global__ __launch_bounds__(BLOCK) void k_list_emit(Spec s, ListDev L, const int64_t* idx, int64_t N, int64_t base,
+                                                     int64_t max_ts) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t* el = L.buf + idx[e];
+    const int64_t pos = base + e;
+    const bool head = e == 0 || L.buf[idx[e - 1]] != el[0];
+    wave_count(&s.stats[ST_FIRED], head);   // one fire per (key, window)
+    if (pos >= s.o.capacity) { cap_error(s, 11); continue; }
+    s.o.key[pos] = kid_key(s, el[0]);
+    s.o.f1[pos] = el[3];
+    s.o.ts[pos] = max_ts;
+    s.o.sum[pos] = el[2];
+  }
+}
+
+// output count; the expired slices' buffers and slots freed
+__global__ void k_list_finish(Spec s, ListDev L, const int64_t* plan, int64_t count) {
+  const int64_t np = plan[1];
+  for (int64_t q = threadIdx.x; q < np; q += blockDim.x) {
+    const int32_t p = (int32_t)plan[2 + 2 * WM_MAXT + q];
+    L.cnt[p] = 0;
+    s.slice_tag[p] = FREE_TAG;
+  }
+  if (threadIdx.x == 0) *s.o.count = (unsigned long long)count;
+}
+
+}  // namespace fw
+
+using namespace fw;
+
+int list_create(fw_engine* e) {
+  const Spec& s = e->s;
+  ListDev& L = e->lst;
+  L.cap = e->cfg.list_capacity > 0 ? e->cfg.list_capacity : 4 * e->cfg.max_batch;
+  L.cnt = e->alloc<unsigned long long>((size_t)s.P);
+  L.buf = e->alloc<int64_t>((size_t)s.P * (size_t)L.cap * LST_WORDS);
+  e->list_plan = e->alloc<int64_t>(LPLAN_WORDS);
+  e->list_plan_h.resize(LPLAN_WORDS);
+  for (void* p : e->allocs) if (!p) return FW_ERR_DEVICE;
+  HIPCHK(e, hipMemsetAsync(L.cnt, 0, 8 * (size_t)s.P, e->stream));
+  return FW_OK;
+}
+
+int list_push(fw_engine* e, const BatchIn& b) {
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((b.n + BLOCK - 1) / BLOCK, e->grid));
+  e->phase_begin(FW_PHASE_INGEST);
+  hipLaunchKernelGGL(k_list_ingest, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b, e->lst);
+  e->phase_end(b.n);
+  HIPCHK(e, hipGetLastError());
+  return FW_OK;
+}
+
+static int list_grow(fw_engine* e, int64_t n) {
+  if (n <= e->list_tmp_cap) return FW_OK;
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (void* p : {(void*)e->list_k1, (void*)e->list_k2, (void*)e->list_v1, (void*)e->list_v2, e->list_temp})
+    if (p) (void)hipFree(p);
+  const int64_t cap = std::max<int64_t>(n, 2 * e->list_tmp_cap);
+  HIPCHK(e, hipMalloc((void**)&e->list_k1, 8 * (size_t)cap));
+  HIPCHK(e, hipMalloc((void**)&e->list_k2, 8 * (size_t)cap));
+  HIPCHK(e, hipMalloc((void**)&e->list_v1, 8 * (size_t)cap));
+  HIPCHK(e, hipMalloc((void**)&e->list_v2, 8 * (size_t)cap));
+  size_t tb = 0;
+  HIPCHK(e, rocprim::radix_sort_pairs(nullptr, tb, e->list_k1, e->list_k2, e->list_v1, e->list_v2, (size_t)cap, 0, 64,
+                                      e->stream));
+  e->list_temp_bytes = tb;
+  HIPCHK(e, hipMalloc(&e->list_temp, tb));
+  e->list_tmp_cap = cap;
+  return FW_OK;
+}
+
+int list_watermark(fw_engine* e, int64_t wm) {
+  if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
+    e->hmarks.push_back({wm, e->dev_marks - 1, false});
+    if (wm > e->cur_wm) e->cur_wm = wm;
+    return FW_OK;
+  }
+  e->phase_begin(FW_PHASE_FIRE);
+  hipLaunchKernelGGL(k_list_plan, dim3(1), dim3(1024), 0, e->stream, e->s, e->lst, e->cur_wm, wm, e->list_plan);
+  HIPCHK(e, hipMemcpyAsync(e->list_plan_h.data(), e->list_plan, 8 * LPLAN_WORDS, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  const int64_t nt = e->list_plan_h[0];
+  const int kid_bits = bits_for((uint64_t)e->s.stride);
+  for (int64_t t = 0; t < nt; ++t) {
+    const int64_t n = e->list_plan_h[2 + 2 * t], N = e->list_plan_h[3 + 2 * t];
+    if (N == 0) continue;
+    if (e->list_out + N > e->cfg.out_capacity) return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded (list state)");
+    if (int rc = list_grow(e, N)) return rc;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((N + BLOCK - 1) / BLOCK, e->grid));
+    hipLaunchKernelGGL(k_list_gather, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, n, e->list_k1, e->list_v1);
+    size_t tb = e->list_temp_bytes;
+    // arrival order, then (stably) grouped by key id
+    HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v1, e->list_v2, (size_t)N, 0, 64,
+                                        e->stream));
+    hipLaunchKernelGGL(k_list_kid, dim3(blocks), dim3(BLOCK), 0, e->stream, e->lst, e->list_v2, N, e->list_k1);
+    tb = e->list_temp_bytes;
+    HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v2, e->list_v1, (size_t)N, 0,
+                                        kid_bits, e->stream));
+    const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)n * (uint64_t)e->s.slide)), e->s.size), 1);
+    hipLaunchKernelGGL(k_list_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, e->list_v1, N, e->list_out, max_ts);
+    e->list_out += N;
+  }
+  hipLaunchKernelGGL(k_list_finish, dim3(1), dim3(1024), 0, e->stream, e->s, e->lst, e->list_plan, e->list_out);
+  hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
+  e->phase_end(e->s.stride);
+  HIPCHK(e, hipGetLastError());
+  e->hmarks.push_back({wm, e->dev_marks++, true});
+  e->out_dirty = false;
+  e->cur_wm = wm;
+  return FW_OK;
+}

@@ -162,6 +162,29 @@ class FoldFunction:
         return _abi.FW_VALUE_I64 if self.value_type == "i64" else _abi.FW_VALUE_F64
 
 
+class ListStateDescriptor:
+    """The window contents of WindowedStream.apply(WindowFunction) (WindowedStream.java:244-345): every element
+    is kept (HeapListState, HeapListState.java:84-112) and the window function sees all of a key's elements of
+    a firing window in arrival order (InternalIterableWindowFunction).  The engine buffers and groups them on
+    the GPU; the window function runs on the host per (key, window) group.  `list_capacity`: elements buffered
+    per pane slice (0: 4 x max_batch)."""
+
+    def __init__(self, value_type="i64", list_capacity=0):
+        self.fields = ()
+        self.mask = _abi.FW_AGG_LIST
+        self.value_type = value_type
+        self.keep_first_f1 = True
+        self.by = False
+        self.comparable = False
+        self.first = True
+        self.flags = 0
+        self.list_capacity = list_capacity
+
+    @property
+    def vt(self):
+        return _abi.FW_VALUE_I64 if self.value_type == "i64" else _abi.FW_VALUE_F64
+
+
 def SumReducer(value_type="i64"):
     return ReduceFunction(("sum",), value_type)
 
@@ -510,6 +533,7 @@ def make_config(assigner, reduce_function, trigger=None, allowed_lateness=0, max
     c.ingest_mode = ingest_mode
     c.agg_flags = getattr(reduce_function, "flags", 0)
     c.fold_initial = getattr(reduce_function, "initial_bits", 0)
+    c.list_capacity = getattr(reduce_function, "list_capacity", 0)
     return c
 
 
@@ -563,6 +587,7 @@ class WindowOperator:
 
     def processElement(self, record):
         v = record.value
+        self._arity = len(v)
         key, h = self._key(v[0])
         if len(v) == 3:
             f1, val = v[1], v[2]
@@ -615,8 +640,40 @@ class WindowOperator:
         apply(key, window, [value], out)
         return [StreamRecord(x, ts) for x in out.items]
 
+    def _list_groups(self, res, lo, hi):
+        """List state: rows lo..hi are elements grouped by (key, window); the window function gets each group
+        (apply(key, TimeWindow, [elements in arrival order], Collector)), or the elements pass through."""
+        out = []
+        i = lo
+        vals = res["sum_i64"] if self.reduce.value_type == "i64" else res["sum_f64"]
+        while i < hi:
+            k, ts = int(res["key"][i]), int(res["ts"][i])
+            j = i
+            while j < hi and int(res["key"][j]) == k and int(res["ts"][j]) == ts:
+                j += 1
+            key = self._key_names.get(k, k) if self._key_names else k
+            elems = [(key, int(res["f1"][x]), vals[x].item()) if getattr(self, "_arity", 2) == 3 else
+                     (key, vals[x].item()) for x in range(i, j)]
+            if self.window_function is None:
+                out.extend(StreamRecord(e, ts) for e in elems)
+            else:
+                col = Collector()
+                apply = getattr(self.window_function, "apply", self.window_function)
+                apply(key, TimeWindow(ts + 1 - self.assigner.size, ts + 1), elems, col)
+                out.extend(StreamRecord(x, ts) for x in col.items)
+            i = j
+        return out
+
     def _drain(self):
         res = self.engine.collect()
+        if isinstance(self.reduce, ListStateDescriptor):
+            pos = 0
+            for wm, mp in zip(res["mark_wm"], res["mark_pos"]):
+                self.output.extend(self._list_groups(res, pos, int(mp)))
+                pos = int(mp)
+                self.output.append(Watermark(int(wm)))
+            self.output.extend(self._list_groups(res, pos, res["n"]))
+            return
         pos = 0
         for wm, mp in zip(res["mark_wm"], res["mark_pos"]):
             while pos < mp:

@@ -89,6 +89,13 @@ extern "C" {
  * and its f1 — ties resolved by FW_AGGF_BY_LAST (first = keep value1, the earlier record).  Used alone. */
 #define FW_AGG_MAXBY  16
 #define FW_AGG_MINBY  32
+/* ListStateDescriptor: WindowedStream.apply(WindowFunction) (WindowedStream.java:244-345) over HeapListState
+ * (flink-runtime/.../state/heap/HeapListState.java): the window's elements are buffered (up to list_capacity per
+ * pane slice) and a firing window returns every element of every key, grouped by key, in arrival order, one
+ * result row per element (value in the sum column, the element's f1, ts = window.maxTimestamp()); the host runs
+ * the window function over each group.  Tumbling / sliding; no session windows; an element arriving for a
+ * window that already fired (allowed lateness) fails with FW_ERR_UNSUPPORTED.  Used alone. */
+#define FW_AGG_LIST   64
 
 /* agg_flags */
 #define FW_AGGF_COMPARABLE  1  /* min/max order doubles by Double.compareTo (ComparableAggregator .min/.max:
@@ -134,6 +141,7 @@ typedef struct {
   int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate     */
   int32_t agg_flags;         /* OR of FW_AGGF_*                                                 */
   int64_t fold_initial;      /* FW_AGGF_FOLD: the fold's initial accumulator                    */
+  int64_t list_capacity;     /* FW_AGG_LIST: elements buffered per pane slice (0 = 4 x max_batch) */
 } fw_config;
 
 /* Output between two collects: records and watermark marks.  Records [mark_pos[i-1], mark_pos[i])

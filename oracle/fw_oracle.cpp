@@ -39,6 +39,8 @@
 //                               TimeWindow.Serializer TimeWindow.java:141-158; InternalTimer.TimerSerializer
 //                               InternalTimer.java:145-157; JDK HashMap/HashSet iteration order (see below)
 //   fold                        RT/state/heap/HeapFoldingState.java:84-122 (first add folds into the default value)
+//   list state                  RT/state/heap/HeapListState.java:84-112 (add appends; get iterates in insertion order),
+//                               InternalIterableWindowFunction (every element to the window function)
 //   reduce functions            SJ/api/functions/aggregation/SumAggregator.java:64-72, SumFunction.java:60-77,
 //                               JDK Math.min/Math.max (double), Long arithmetic (wrapping),
 //                               ComparableAggregator.java:66-90 + Comparator.java:45-105 (min/max/minBy/maxBy
@@ -55,6 +57,7 @@
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <set>
 #include <string>
 #include <thread>
@@ -128,8 +131,10 @@ int64_t getWindowStartWithOffset(int64_t timestamp, int64_t offset, int64_t wind
 }
 
 // ---------------- accumulator = the reduced record ----------------
+struct ListElem { int64_t vi; double vd; int64_t f1; };
 struct Acc {
   int64_t seq;   // when this (namespace, key) entry was put into its HashMap (iteration order), not state
+  std::shared_ptr<std::vector<ListElem>> list;   // FW_AGG_LIST: HeapListState's elements, insertion order
   int64_t key;
   int64_t f1;
   int64_t sum_i, min_i, max_i, count;
@@ -306,6 +311,17 @@ struct Operator {
     }
     auto& keyed = nit->second;
     auto it = keyed.find(curKey);
+    if (cfg.agg_mask == FW_AGG_LIST) {   // HeapListState.add: append (a new list on the first element)
+      if (it == keyed.end()) {
+        Acc a = value;
+        a.list = std::make_shared<std::vector<ListElem>>();
+        a.list->push_back({value.sum_i, value.sum_d, value.f1});
+        keyed.emplace(curKey, a);
+      } else {
+        it->second.list->push_back({value.sum_i, value.sum_d, value.f1});
+      }
+      return FW_OK;
+    }
     if (it == keyed.end()) {
       if (cfg.agg_flags & FW_AGGF_FOLD) {
         // HeapFoldingState.add (HeapFoldingState.java:111-118): no value yet -> fold(defaultValue, value); the
@@ -383,6 +399,18 @@ struct Operator {
 
   // ---- WindowOperator.fire / cleanup / registerCleanupTimer ----
   void fire(const TimeWindow& w, const Acc& contents) {  // :435-438, InternalSingleValueWindowFunction + PassThrough
+    if (cfg.agg_mask == FW_AGG_LIST) {   // InternalIterableWindowFunction: every element, in insertion order
+      for (const ListElem& x : *contents.list) {
+        Acc a{};
+        a.key = contents.key;
+        a.f1 = x.f1;
+        a.sum_i = x.vi;
+        a.sum_d = x.vd;
+        out.push_back({a, w.maxTimestamp(), w.start});
+      }
+      stats.panes_fired++;
+      return;
+    }
     out.push_back({contents, w.maxTimestamp(), w.start});
     stats.panes_fired++;
   }
@@ -814,6 +842,9 @@ int fwo_create(const fw_config* cfg, fw_engine** out) {
   if (!cfg || !out) return FW_ERR_INVALID_ARG;
   if (cfg->assigner != FW_TUMBLING && cfg->assigner != FW_SLIDING && cfg->assigner != FW_SESSION) return FW_ERR_INVALID_ARG;
   if ((cfg->agg_flags & FW_AGGF_FOLD) && cfg->assigner == FW_SESSION) return FW_ERR_UNSUPPORTED;   // WindowedStream.java:466-467
+  if ((cfg->agg_mask & FW_AGG_LIST) && (cfg->agg_mask != FW_AGG_LIST || cfg->assigner == FW_SESSION ||
+                                        (cfg->agg_flags & FW_AGGF_FOLD)))
+    return FW_ERR_UNSUPPORTED;   // list state: alone, tumbling / sliding (the engine's scope)
   if (cfg->size <= 0 || (cfg->assigner == FW_SLIDING && cfg->slide <= 0) || cfg->allowed_lateness < 0 ||
       cfg->max_parallelism <= 0 || cfg->kg_start < 0 || cfg->kg_end < cfg->kg_start || cfg->kg_end >= cfg->max_parallelism)
     return FW_ERR_INVALID_ARG;

@@ -329,6 +329,46 @@ FIXTURES.append(fixture(
     [{"wm": 1599, "records": []}, {"wm": 1999, "records": [out("key2", 1, 1999)]}, {"wm": 2000, "records": []},
      {"wm": 5000, "records": []}]))
 
+# ---- list state: WindowedStream.apply(WindowFunction) over ListStateDescriptor (HeapListState) ----
+# testSlidingEventTimeWindowsApply / testTumblingEventTimeWindowsApply run the reduce tests' elements through
+# list state and RichSumReducer (a window function summing the iterable: WOT:2255-2285), so the expected
+# outputs are the reduce tests' (WOT:92-157, WOT:196-263); the replay applies that window function
+LIST_SLIDING = cfg("sliding", 3000, 1000)
+LIST_SLIDING["list"] = True
+FIXTURES.append(fixture(
+    "list_sliding_apply", "WindowOperatorTest.java:194-226 (elements/expectations :92-157)", LIST_SLIDING,
+    OOO_ELEMENTS + [wm(999), wm(1999), wm(2999), wm(3999), wm(4999), wm(5999), wm(6999), wm(7999)],
+    [{"wm": 999, "records": [out("key1", 3, 999)]},
+     {"wm": 1999, "records": [out("key1", 3, 1999), out("key2", 3, 1999)]},
+     {"wm": 2999, "records": [out("key1", 3, 2999), out("key2", 3, 2999)]},
+     {"wm": 3999, "records": [out("key2", 5, 3999)]},
+     {"wm": 4999, "records": [out("key2", 2, 4999)]},
+     {"wm": 5999, "records": [out("key2", 2, 5999)]},
+     {"wm": 6999, "records": []},
+     {"wm": 7999, "records": []}]))
+LIST_TUMBLING = cfg("tumbling", 3000)
+LIST_TUMBLING["list"] = True
+FIXTURES.append(fixture(
+    "list_tumbling_apply", "WindowOperatorTest.java:326-358 (elements/expectations :196-263)", LIST_TUMBLING,
+    OOO_ELEMENTS + [wm(999), wm(1999), wm(2999), wm(3999), wm(4999), wm(5999), wm(6999), wm(7999)],
+    [{"wm": 999, "records": []},
+     {"wm": 1999, "records": []},
+     {"wm": 2999, "records": [out("key1", 3, 2999), out("key2", 3, 2999)]},
+     {"wm": 3999, "records": []},
+     {"wm": 4999, "records": []},
+     {"wm": 5999, "records": [out("key2", 2, 5999)]},
+     {"wm": 6999, "records": []},
+     {"wm": 7999, "records": []}]))
+# WOT:1942-1975 testCleanupTimerWithEmptyListStateForTumblingWindows (tumbling 2 s, lateness 1, the elements
+# passed through: one element (key2, 1) -> (key2, 1) @1999)
+LIST_CLEANUP = cfg("tumbling", 2000, lateness=1)
+LIST_CLEANUP["list"] = True
+FIXTURES.append(fixture(
+    "list_cleanup_timer", "WindowOperatorTest.java:1942-1976", LIST_CLEANUP,
+    [rec("key2", 1, 1000), wm(1599), wm(1999), wm(2000), wm(5000)],
+    [{"wm": 1599, "records": []}, {"wm": 1999, "records": [out("key2", 1, 1999)]}, {"wm": 2000, "records": []},
+     {"wm": 5000, "records": []}]))
+
 # TimeWindowTest.java:30-58 getWindowStartWithOffset known answers: (ts, offset, size, expected)
 WINDOW_START = {
     "source": "flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/TimeWindowTest.java:30-58",

@@ -29,6 +29,7 @@ SESSION_FIXTURES = ["session_reduce", "session_windows", "session_late_zero_purg
                     "session_late_small_purging", "session_late_small", "session_late_huge_purging",
                     "session_late_huge", "session_cleanup_timer"]
 FOLD_FIXTURES = ["fold_cleanup_timer"]
+LIST_FIXTURES = ["list_sliding_apply", "list_tumbling_apply", "list_cleanup_timer"]
 
 
 def fixture_config(c, **kw):
@@ -39,7 +40,10 @@ def fixture_config(c, **kw):
     else:
         assigner = SlidingEventTimeWindows(c["size"], c["slide"], c["offset"])
     trig = EventTimeTrigger.create() if c["trigger"] == "event_time" else PurgingTrigger.of(EventTimeTrigger.create())
-    if "fold" in c:
+    if c.get("list"):
+        from flink_amd.windowing import ListStateDescriptor
+        red = ListStateDescriptor(c["value_type"])
+    elif "fold" in c:
         from flink_amd.windowing import FoldFunction
         red = FoldFunction(c["fold"]["kind"], c["fold"]["initial"], c["value_type"])
     else:
@@ -89,7 +93,13 @@ def replay(fx, engine_factory, **kw):
             res = eng.collect()
             assert len(res["mark_wm"]) == 1 and res["mark_wm"][0] == e[1]
             assert res["mark_pos"][0] == res["n"], "records emitted after the watermark mark"
-            if fx["config"]["assigner"] == "session":   # the window's start too (end = ts + 1)
+            if fx["config"].get("list"):   # the window function of the reference test: the sum per (key, window)
+                groups = {}
+                for i in range(res["n"]):
+                    g = (int(res["key"][i]), int(res["ts"][i]))
+                    groups[g] = groups.get(g, 0) + int(res["sum_i64"][i])
+                recs = sorted((k, v, t) for (k, t), v in groups.items())
+            elif fx["config"]["assigner"] == "session":   # the window's start too (end = ts + 1)
                 recs = sorted((int(res["key"][i]), int(res["sum_i64"][i]), int(res["ts"][i]), int(res["win_start"][i]))
                               for i in range(res["n"]))
             else:

@@ -7,12 +7,12 @@ import ctypes
 import numpy as np
 import pytest
 
-from harness import FOLD_FIXTURES, SESSION_FIXTURES, WINDOW_FIXTURES, expected_epochs, load_golden, replay
+from harness import FOLD_FIXTURES, LIST_FIXTURES, SESSION_FIXTURES, WINDOW_FIXTURES, expected_epochs, load_golden, replay
 
 oracle = pytest.importorskip("oracle.oracle")
 
 
-@pytest.mark.parametrize("name", WINDOW_FIXTURES + SESSION_FIXTURES + FOLD_FIXTURES)
+@pytest.mark.parametrize("name", WINDOW_FIXTURES + SESSION_FIXTURES + FOLD_FIXTURES + LIST_FIXTURES)
 def test_oracle_window_fixtures(name):
     fx = load_golden(name)
     got = replay(fx, oracle.OracleEngine)
