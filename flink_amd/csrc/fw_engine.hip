@@ -2291,6 +2291,8 @@ struct fw_engine {
   void* client = nullptr;             // producer/consumer stream of the caller (fw_set_stream)
   bool has_client = false;            // set by fw_set_stream; the handle itself may be 0 (the null stream)
   bool serial = false;                // diagnostics (FW_SERIAL=1): k_route on the engine stream too
+  bool no_consumed = false;           // diagnostics (FW_NO_CONSUMED=1): no per-push consumption event
+  bool event_query = true;            // skip stream waits on events already complete (FW_EVENT_QUERY=0: off)
   hipEvent_t ev_in = nullptr;         // client work up to a push (input columns ready)
   static constexpr int NCONS = 8;
   hipEvent_t ev_consumed[NCONS] = {};  // per push (ring): every read of that push's input columns done
@@ -2642,6 +2644,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     }
   }
   e->serial = getenv("FW_SERIAL") && atoi(getenv("FW_SERIAL")) != 0;
+  e->event_query = !(getenv("FW_EVENT_QUERY") && atoi(getenv("FW_EVENT_QUERY")) == 0);
+  e->no_consumed = getenv("FW_NO_CONSUMED") && atoi(getenv("FW_NO_CONSUMED")) != 0;
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (int q = 0; q < fw_engine::NBUF; ++q) {
@@ -2928,10 +2932,18 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   const int par = (int)(e->batches % fw_engine::NBUF);
   const int half = (int)(e->batches & 1);   // the direct form's new-pane list counters alternate
   hipStream_t in_stream = e->routed && !e->serial ? e->rstream : e->stream;
-  if (e->routed) HIPCHK(e, hipStreamWaitEvent(in_stream, e->ev_agg[par], 0));
-  if (e->has_client) {   // input columns are produced on the caller's stream
+  // a wait whose event has already completed is skipped: each one costs the command processor a barrier
+  // packet on the stream (FW_EVENT_QUERY=0 enqueues them all, for A/B)
+  auto wait_on = [&](hipStream_t st, hipEvent_t ev) -> hipError_t {
+    if (e->event_query && hipEventQuery(ev) == hipSuccess) return hipSuccess;
+    return hipStreamWaitEvent(st, ev, 0);
+  };
+  if (e->routed) HIPCHK(e, wait_on(in_stream, e->ev_agg[par]));
+  // input columns are produced on the caller's stream: order the push after it (nothing to order when that
+  // stream has no work pending)
+  if (e->has_client && !(e->event_query && hipStreamQuery((hipStream_t)e->client) == hipSuccess)) {
     HIPCHK(e, hipEventRecord(e->ev_in, (hipStream_t)e->client));
-    HIPCHK(e, hipStreamWaitEvent(in_stream, e->ev_in, 0));
+    HIPCHK(e, wait_on(in_stream, e->ev_in));
   }
   const int64_t *dk = key, *dts = ts, *dv = (const int64_t*)value, *df1 = f1;
   const int32_t* dh = key_hash;
@@ -3047,7 +3059,8 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   HIPCHK(e, hipGetLastError());
   // every reader of this push's columns (k_route, k_aggregate's direct records, the f1 fix-up, the late
   // path) is ordered before this point of the engine stream
-  HIPCHK(e, hipEventRecord(e->ev_consumed[(e->pushes++) % fw_engine::NCONS], e->stream));
+  if (!e->no_consumed) HIPCHK(e, hipEventRecord(e->ev_consumed[e->pushes % fw_engine::NCONS], e->stream));
+  e->pushes++;
   e->ordinal += n;
   e->records_in += n;
   return FW_OK;
