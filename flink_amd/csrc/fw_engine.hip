@@ -2296,6 +2296,11 @@ struct fw_engine {
   hipEvent_t ev_in = nullptr;         // client work up to a push (input columns ready)
   static constexpr int NCONS = 8;
   hipEvent_t ev_consumed[NCONS] = {};  // per push (ring): every read of that push's input columns done
+  int64_t cons_push[NCONS] = {-1, -1, -1, -1, -1, -1, -1, -1};   // the push each ring event was recorded for
+  // consumption events are recorded only once a caller has asked for one (fw_stream_wait_input): each is a
+  // packet the command processor handles between the engine stream's kernels
+  bool track_consumed = false;
+  hipEvent_t ev_now = nullptr;
   // routed batches rotate over NBUF buffer sets: k_route of batch j waits only for k_aggregate of batch
   // j - NBUF, long finished, so neither stream waits on the other's latest kernel (a cross-stream wait costs
   // ~13 us of signal latency on MI355X, measured: profiles/r02_v13_timeline.txt)
@@ -2443,6 +2448,7 @@ struct fw_engine {
     if (ev_in) (void)hipEventDestroy(ev_in);
     for (int q = 0; q < NBUF; ++q) for (hipEvent_t ev : {ev_route[q], ev_agg[q]}) if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : ev_consumed) if (ev) (void)hipEventDestroy(ev);
+    if (ev_now) (void)hipEventDestroy(ev_now);
     for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
@@ -2648,6 +2654,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   e->no_consumed = getenv("FW_NO_CONSUMED") && atoi(getenv("FW_NO_CONSUMED")) != 0;
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCHK(e, hipEventCreateWithFlags(&e->ev_now, hipEventDisableTiming));
   for (int q = 0; q < fw_engine::NBUF; ++q) {
     HIPCHK(e, hipEventCreateWithFlags(&e->ev_route[q], hipEventDisableTiming));
     HIPCHK(e, hipEventCreateWithFlags(&e->ev_agg[q], hipEventDisableTiming));
@@ -3059,7 +3066,10 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   HIPCHK(e, hipGetLastError());
   // every reader of this push's columns (k_route, k_aggregate's direct records, the f1 fix-up, the late
   // path) is ordered before this point of the engine stream
-  if (!e->no_consumed) HIPCHK(e, hipEventRecord(e->ev_consumed[e->pushes % fw_engine::NCONS], e->stream));
+  if (e->track_consumed && !e->no_consumed) {
+    HIPCHK(e, hipEventRecord(e->ev_consumed[e->pushes % fw_engine::NCONS], e->stream));
+    e->cons_push[e->pushes % fw_engine::NCONS] = e->pushes;
+  }
   e->pushes++;
   e->ordinal += n;
   e->records_in += n;
@@ -3070,7 +3080,15 @@ int fw_stream_wait_input(fw_engine* e, void* stream, int32_t back) {
   if (!e || back < 0 || back >= fw_engine::NCONS) return FW_ERR_INVALID_ARG;
   if (back >= e->pushes) return FW_OK;   // no such push
   HIPCHK(e, hipSetDevice(e->dev));
-  HIPCHK(e, hipStreamWaitEvent((hipStream_t)stream, e->ev_consumed[(e->pushes - 1 - back) % fw_engine::NCONS], 0));
+  const int64_t target = e->pushes - 1 - back;
+  const int slot = (int)(target % fw_engine::NCONS);
+  if (e->cons_push[slot] == target) {
+    HIPCHK(e, hipStreamWaitEvent((hipStream_t)stream, e->ev_consumed[slot], 0));
+  } else {   // not tracked yet: wait for everything the engine stream holds now (a later point, never a cycle)
+    HIPCHK(e, hipEventRecord(e->ev_now, e->stream));
+    HIPCHK(e, hipStreamWaitEvent((hipStream_t)stream, e->ev_now, 0));
+  }
+  e->track_consumed = true;
   return FW_OK;
 }
 
