@@ -89,7 +89,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])   # 8: the ranks of one MI355X node
 def test_keyby_exchange_two_ranks(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
