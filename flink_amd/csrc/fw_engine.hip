@@ -607,7 +607,10 @@ constexpr int FLAG_RING = 16;           // direct-record flags, one per batch in
 constexpr int RT_GROUPS = RT_Q + 2;     // bin groups per bucket: RT_Q routed slices, then the direct records
                                         // (any other slice, the Long.MIN_VALUE key) and the per-element fires
 constexpr int AG_THREADS = 1024;
-constexpr int AG_WIN = 8;               // k_aggregate: directory slots probed without a branch
+#ifndef FW_AG_WIN
+#define FW_AG_WIN 8
+#endif
+constexpr int AG_WIN = FW_AG_WIN;       // k_aggregate: directory slots probed without a branch
 constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
 constexpr int AG_MAXPER = 17;           // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
 constexpr int AG_SPLIT_MAX = 16;        // k_aggregate: shares a hot bucket is split into, at most
