@@ -120,7 +120,7 @@ def cpu_baseline(cfg, C, n):
                       f"watermark every {C['batch']} events, final MAX_WATERMARK; {fired} windows fired"}
 
 
-def pmc_traffic():
+def pmc_traffic(config="c1"):
     """HBM bytes per launch of every engine kernel from the committed rocprofv3 PMC summary of THIS
     library build (profiles/*_pmc.json, written by tools/summarize_profiles.py from separate FETCH_SIZE /
     WRITE_SIZE passes): ({kernel name: bytes}, file), or ({}, None) when no summary matches the library's md5."""
@@ -133,7 +133,7 @@ def pmc_traffic():
             d = json.load(open(f))
         except ValueError:
             continue
-        if d.get("library_md5") != md5:
+        if d.get("library_md5") != md5 or d.get("config", "c1") != config:   # this build, this workload
             continue
         return {n: k["hbm_bytes_corrected"] for n, k in d.get("kernels", {}).items()
                 if k.get("hbm_bytes_corrected")}, os.path.basename(f)
@@ -333,7 +333,7 @@ def main():
     ev_gpu = batch
     alg_step = 24.0 * ev_gpu + C["pane_bytes"] * fired_per_step / max(world, 1)
     achieved = alg_step / (ms_step / 1e3) / 1e9
-    pmc, pmc_src = pmc_traffic()
+    pmc, pmc_src = pmc_traffic(args.config)
     kernels = {}
     names = [("k_route", route_ms, 1.0), ("k_aggregate", agg_ms, 1.0)] if form == 2 else [("k_ingest_direct", route_ms, 1.0)]
     names.append(("k_watermark", wm_ms, wm_per_step))

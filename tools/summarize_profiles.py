@@ -36,7 +36,8 @@ def main(tag):
     ran = open(os.path.join(OUT, "prof_md5.txt")).read().strip()
     if ran != md5:
         sys.exit(f"gpurun_out/prof_* was measured on library {ran}, not the in-tree {md5}: re-run the profile")
-    res = {"library_md5": md5, "units": "KB per dispatch as reported by rocprofv3", "kernels": {}}
+    res = {"library_md5": md5, "config": os.environ.get("PROF_CONFIG", "c1"),   # the bench config profiled
+           "units": "KB per dispatch as reported by rocprofv3", "kernels": {}}
     f = os.path.join(OUT, "prof_fetch", "run_counter_collection.csv")
     w = os.path.join(OUT, "prof_write", "run_counter_collection.csv")
     if os.path.exists(f) and os.path.exists(w):
