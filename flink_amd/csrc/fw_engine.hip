@@ -458,8 +458,8 @@ __device__ __forceinline__ int64_t window_start_n(const Spec& s, int64_t n) {
 // .onElement FIRE, EventTimeTrigger.java:38-40; WindowOperator.java:317-325): its slice update joins the
 // commit list (applied in arrival order by k_late_commit); for sliding windows every such window of the
 // record also gets a fire element (tumbling: the slice is the window, the commit list serves as both)
-__device__ void late_append(const Spec& s, const BatchIn& b, int32_t p, int64_t kid, int64_t m, int64_t i) {
-  const unsigned long long pos = atomicAdd(b.late_count, 1ull);
+__device__ void late_append_at(const Spec& s, const BatchIn& b, unsigned long long pos, int32_t p, int64_t kid, int64_t m,
+                               int64_t i) {
   const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
   if ((int64_t)pos < b.late_capacity) b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
   else cap_error(s, 1);
@@ -473,6 +473,9 @@ __device__ void late_append(const Spec& s, const BatchIn& b, int32_t p, int64_t 
     if ((int64_t)fpos < b.fire_capacity) b.fire_key[fpos] = (wpane << b.idx_bits) | (unsigned long long)i;
     else cap_error(s, 2);
   }
+}
+__device__ void late_append(const Spec& s, const BatchIn& b, int32_t p, int64_t kid, int64_t m, int64_t i) {
+  late_append_at(s, b, atomicAdd(b.late_count, 1ull), p, kid, m, i);
 }
 
 template <int VT, int AGG, bool FIRST>
@@ -1202,20 +1205,25 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     const uint32_t sd = lseg[t * RT_GROUPS + RT_Q], sf = lseg[t * RT_GROUPS + RT_Q + 1];
     for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) gsl_insert(r.dm[(int64_t)t * RT_TILE + x]);
     if (b.late_key == nullptr || t < t_lo || t >= t_hi) continue;
-    for (uint32_t x = sf & 0xFFFFu; x < (sf >> 16); ++x) {
+    const uint32_t f_lo = sf & 0xFFFFu, f_hi = sf >> 16;
+    if (f_hi <= f_lo) continue;
+    // the tile's fire records of this bucket take one reservation of the late list (a per-record atomic on
+    // its shared cursor serialised the hot buckets of skewed streams)
+    const unsigned long long lbase = atomicAdd(b.late_count, (unsigned long long)(f_hi - f_lo));
+    for (uint32_t x = f_lo; x < f_hi; ++x) {
       const int64_t pos = (int64_t)t * RT_TILE + x;
       const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
       const uint64_t h = (uint64_t)r.kv[pos].x;
       const int64_t m = r.dm[pos];
-      const int32_t p = slice_slot(s, m);
+      int32_t p = slice_slot(s, m);
       int64_t kid = s.D;
       if (h == EMPTY_H) (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
       else {
         const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
         kid = x2 < 0 ? -1 : dbase + x2;
       }
-      if (p < 0 || kid < 0) { cap_error(s, 7); continue; }
-      late_append(s, b, p, kid, m, i);
+      if (p < 0 || kid < 0) { cap_error(s, 7); p = 0; kid = 0; }   // (a failed batch: a harmless entry keeps the slot)
+      late_append_at(s, b, lbase + (x - f_lo), p, kid, m, i);
     }
   }
   // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same

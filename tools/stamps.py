@@ -36,7 +36,15 @@ for j in range(6):
     e.lib.fw_debug_stamps(e.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), buf.size)
     sk, d, span = phases(buf, B // 4096, 5)
     print(f"batch {j} route: start-skew {sk:.0f} ns, load {d[0]:.0f} phaseB {d[1]:.0f} scan {d[2]:.0f} write {d[3]:.0f} | span {span:.0f} ns")
-    sk, d, span = phases(buf[8 << 16:], 256, 5)
+    nagg = 256
+    if os.environ.get("STAMP_HELPERS"):   # owners + helper shares (blocks past 256 that ran)
+        a = buf[8 << 16:].reshape(-1, 8)
+        nagg = int(np.nonzero(a[:, 0])[0].max()) + 1 if a[:, 0].any() else 256
+        ends = (a[:nagg, 4] - a[:nagg, 0][a[:nagg, 0] > 0].min()) * 10
+        top = np.argsort(ends)[-8:][::-1]
+        print(f"      agg blocks {nagg}; slowest (blockIdx, end ns, main ns):",
+              [(int(b), int(ends[b]), int((a[b, 3] - a[b, 2]) * 10)) for b in top])
+    sk, d, span = phases(buf[8 << 16:], nagg, 5)
     print(f"        aggregate: start-skew {sk:.0f} ns, ldir {d[0]:.0f} segtab {d[1]:.0f} main {d[2]:.0f} fold {d[3]:.0f} | span {span:.0f} ns")
     e.advance_watermark(int(t.max().item()) - (50 if C4 else 1))
     e.collect()
