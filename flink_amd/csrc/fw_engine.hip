@@ -1010,45 +1010,54 @@ __device__ __forceinline__ void acc_add(const AggLds& L, bool cmpto, bool by_las
 
 // Hot keys (Zipf): when 8 or more lanes of a wave carry the slot of the wave's first active lane, they are
 // reduced in registers (butterfly over the wave) and the leader makes one LDS update for all of them —
-// the same-address LDS atomics of a hot key would otherwise serialise 64 ways.  Returns whether this
-// lane still has its own update to make.  (Double sums change association: the tolerance path.)
+// the same-address LDS atomics of a hot key would otherwise serialise up to 64 ways.  A bucket can hold
+// several hot keys (the first lane is not always the hottest), so up to HC_ROUNDS leaders are tried in
+// turn, each over the lanes left.  Returns whether this lane still has its own update to make.  (Double
+// sums change association: the tolerance path.)
+#ifndef FW_HC_ROUNDS
+#define FW_HC_ROUNDS 3
+#endif
 template <int VT, int AGG>
 __device__ __forceinline__ bool hot_combine(const AggLds& L, bool cmpto, bool act, uint32_t kl, int64_t v, uint32_t oi,
                                             int lane) {
-  const uint64_t am = __ballot(act);
-  if (am == 0) return act;
-  const int leader = __ffsll((long long)am) - 1;
-  const uint32_t lk = __shfl(kl, leader);
-  const bool same = act && kl == lk;
-  const uint64_t sm = __ballot(same);
-  if (__popcll(sm) < 8) return act;   // wave-uniform
-  int64_t sv = same ? v : sum_identity(VT);
-  int64_t mn = same ? min_code(VT, cmpto, v) : INT64_MAX;
-  int64_t mx = same ? max_code(VT, cmpto, v) : INT64_MIN;
-  uint32_t fo = same ? oi : NO_FIRST;
+#pragma unroll 1
+  for (int round = 0; round < FW_HC_ROUNDS; ++round) {
+    const uint64_t am = __ballot(act);
+    if (am == 0) return act;
+    const int leader = __ffsll((long long)am) - 1;
+    const uint32_t lk = __shfl(kl, leader);
+    const bool same = act && kl == lk;
+    const uint64_t sm = __ballot(same);
+    if (__popcll(sm) < 8) return act;   // wave-uniform
+    int64_t sv = same ? v : sum_identity(VT);
+    int64_t mn = same ? min_code(VT, cmpto, v) : INT64_MAX;
+    int64_t mx = same ? max_code(VT, cmpto, v) : INT64_MIN;
+    uint32_t fo = same ? oi : NO_FIRST;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    if (AGG & FW_AGG_SUM) {
-      const int64_t y = __shfl_xor(sv, o);
-      if (VT == FW_VALUE_I64) sv = jadd(sv, y);
-      else sv = __double_as_longlong(__longlong_as_double(sv) + __longlong_as_double(y));
+    for (int o = 32; o > 0; o >>= 1) {
+      if (AGG & FW_AGG_SUM) {
+        const int64_t y = __shfl_xor(sv, o);
+        if (VT == FW_VALUE_I64) sv = jadd(sv, y);
+        else sv = __double_as_longlong(__longlong_as_double(sv) + __longlong_as_double(y));
+      }
+      if (AGG & FW_AGG_MIN) { const int64_t y = __shfl_xor(mn, o); mn = y < mn ? y : mn; }
+      if (AGG & FW_AGG_MAX) { const int64_t y = __shfl_xor(mx, o); mx = y > mx ? y : mx; }
+      const uint32_t y = __shfl_xor(fo, o);
+      fo = y < fo ? y : fo;
     }
-    if (AGG & FW_AGG_MIN) { const int64_t y = __shfl_xor(mn, o); mn = y < mn ? y : mn; }
-    if (AGG & FW_AGG_MAX) { const int64_t y = __shfl_xor(mx, o); mx = y > mx ? y : mx; }
-    const uint32_t y = __shfl_xor(fo, o);
-    fo = y < fo ? y : fo;
-  }
-  if (lane == leader) {
-    if (AGG & FW_AGG_SUM) {
-      if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&L.sum[lk], (unsigned long long)sv);
-      else unsafeAtomicAdd((double*)&L.sum[lk], __longlong_as_double(sv));
+    if (lane == leader) {
+      if (AGG & FW_AGG_SUM) {
+        if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&L.sum[lk], (unsigned long long)sv);
+        else unsafeAtomicAdd((double*)&L.sum[lk], __longlong_as_double(sv));
+      }
+      if (AGG & FW_AGG_MIN) atomicMin((long long*)&L.mn[lk], (long long)mn);
+      if (AGG & FW_AGG_MAX) atomicMax((long long*)&L.mx[lk], (long long)mx);
+      if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&L.cnt[lk], (unsigned long long)__popcll(sm));
+      atomicMin(&L.first[lk], fo);
     }
-    if (AGG & FW_AGG_MIN) atomicMin((long long*)&L.mn[lk], (long long)mn);
-    if (AGG & FW_AGG_MAX) atomicMax((long long*)&L.mx[lk], (long long)mx);
-    if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&L.cnt[lk], (unsigned long long)__popcll(sm));
-    atomicMin(&L.first[lk], fo);
+    act = act && !same;
   }
-  return act && !same;
+  return act;
 }
 
 // LDS bytes k_aggregate needs for buckets of 2^kb_bits slots and ntiles tiles
@@ -1399,7 +1408,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     }   // passes
     FW_STAMP(r, SB, 3 + 3 * min(g, 1));
     unsigned int* flag = r.fold_flag + (int64_t)bkt * RT_GS + g;
-    if (SKEW && share > 0) {   // uniform: wait for the previous share's fold of this slice
+    // integer shares of a split bucket fold concurrently with device atomics (sum / count / min / max
+    // are exact in any order, and the first arrival is the least batch index over the shares: the last
+    // share to fold resolves its f1); double sums and maxBy / minBy fold one share after another
+    constexpr bool AFOLD = SKEW && VT == FW_VALUE_I64 && !BY;
+    const bool afold = AFOLD && nshare > 1;   // uniform
+    if (SKEW && share > 0 && !afold) {   // uniform: wait for the previous share's fold of this slice
       if (threadIdx.x == 0) {
         const unsigned want = (r.tag << 5) | (unsigned)share;
         int64_t spins = 0;
@@ -1419,6 +1433,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       const uint32_t lf = lfirst[xl];
       if (lf == NO_FIRST) continue;
       const int64_t idx = (int64_t)p * s.stride + (x < KB ? dbase + x : s.D);
+      if (AFOLD && afold) {
+        if (AGG & FW_AGG_SUM) atomicAdd((unsigned long long*)&s.c.sum[idx], (unsigned long long)lsum[xl]);
+        if (AGG & FW_AGG_MIN) atomicMin((long long*)&s.c.mn[idx], (long long)lmin[xl]);
+        if (AGG & FW_AGG_MAX) atomicMax((long long*)&s.c.mx[idx], (long long)lmax[xl]);
+        if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&s.c.cnt[idx], (unsigned long long)lcnt[xl]);
+        if (FIRST) atomicMin((long long*)&s.c.first[idx], (long long)(ord_base + (int64_t)lf));
+        else s.c.present[idx] = 1;
+      } else {
       if (AGG & FW_AGG_SUM) {
         if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[xl]);
         else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(lsum[xl]));
@@ -1450,6 +1472,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       } else {
         s.c.present[idx] = 1;
       }
+      }   // !afold
       // cleared for the next round (untouched entries still are; the per-lane dummies are never read)
       lsum[xl] = sum_identity(VT);
       if (HAS_MIN) lmin[xl] = INT64_MAX;
@@ -1457,10 +1480,37 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       if (AGG & FW_AGG_COUNT) lcnt[xl] = 0;
       lfirst[xl] = NO_FIRST;
     }
-    if (SKEW && share + 1 < nshare) __threadfence();   // this share's fold visible before the next one's starts
-    __syncthreads();
-    if (SKEW && share + 1 < nshare && threadIdx.x == 0)
-      __hip_atomic_store(flag, (r.tag << 5) | (unsigned)(share + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (AFOLD && afold) {
+      // count this share's fold in; the last one reads the first arrivals back (agent atomics: coherent
+      // across the XCDs' L2s) and stores the f1 of each pane the batch opened
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned old = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nv;
+        do {
+          const unsigned done = (old >> 5) == r.tag ? (old & 31u) : 0u;
+          nv = (r.tag << 5) | (done + 1);
+        } while (!__hip_atomic_compare_exchange_strong(flag, &old, nv, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+        lclaim = (int32_t)(nv & 31u) == nshare ? 1 : 0;
+      }
+      __syncthreads();
+      if (FIRST && lclaim) {   // uniform
+        __threadfence();
+        for (int x = threadIdx.x; x <= KB; x += NT) {
+          if (x == KB && bkt != 0) continue;
+          const int64_t idx = (int64_t)p * s.stride + (x < KB ? dbase + x : s.D);
+          const int64_t f = (int64_t)__hip_atomic_fetch_add((unsigned long long*)&s.c.first[idx], 0ull,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (f >= ord_base && f != INT64_MAX) s.c.f1v[idx] = f1col[f - ord_base];
+        }
+      }
+    } else {
+      if (SKEW && share + 1 < nshare) __threadfence();   // this share's fold visible before the next one's starts
+      __syncthreads();
+      if (SKEW && share + 1 < nshare && threadIdx.x == 0)
+        __hip_atomic_store(flag, (r.tag << 5) | (unsigned)(share + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
     FW_STAMP(r, SB, 4 + 3 * min(g, 1));
   }
   // this batch's routed records of the bucket (the next batch's split plan); the owner clears the ring
@@ -2586,7 +2636,7 @@ static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
         case 1: if (_f) FN<0, 1, true>(e, ##__VA_ARGS__); else FN<0, 1, false>(e, ##__VA_ARGS__); break;   \
         case 16: FN<0, 16, true>(e, ##__VA_ARGS__); break;                                       \
         case 32: FN<0, 32, true>(e, ##__VA_ARGS__); break;                                       \
-        case 15: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
+        case 9: if (_f) FN<0, 9, true>(e, ##__VA_ARGS__); else FN<0, 9, false>(e, ##__VA_ARGS__); break;   \
         default: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
       }                                                                                          \
     } else {                                                                                     \
@@ -2594,6 +2644,7 @@ static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
         case 1: if (_f) FN<1, 1, true>(e, ##__VA_ARGS__); else FN<1, 1, false>(e, ##__VA_ARGS__); break;   \
         case 16: FN<1, 16, true>(e, ##__VA_ARGS__); break;                                       \
         case 32: FN<1, 32, true>(e, ##__VA_ARGS__); break;                                       \
+        case 9: if (_f) FN<1, 9, true>(e, ##__VA_ARGS__); else FN<1, 9, false>(e, ##__VA_ARGS__); break;   \
         default: if (_f) FN<1, 15, true>(e, ##__VA_ARGS__); else FN<1, 15, false>(e, ##__VA_ARGS__); break; \
       }                                                                                          \
     }                                                                                            \
@@ -2692,7 +2743,10 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.kg_start = c.kg_start;
   s.kg_end = c.kg_end;
   s.vt = c.value_type;
-  s.agg = by ? c.agg_mask : (c.agg_mask == FW_AGG_SUM || e->list ? FW_AGG_SUM : 15);   // instantiated reduce shapes
+  s.agg = by ? c.agg_mask
+             : (c.agg_mask == FW_AGG_SUM || e->list) ? FW_AGG_SUM
+             : c.agg_mask == (FW_AGG_SUM | FW_AGG_COUNT) ? c.agg_mask   // the average shape: no min/max columns
+             : 15;   // instantiated reduce shapes
   // (list state: the sum column carries each element's value, f1 its f1)
   s.by = by ? c.agg_mask : 0;
   s.by_last = (c.agg_flags & FW_AGGF_BY_LAST) ? 1 : 0;

@@ -185,11 +185,13 @@ def test_zipf_out_of_order_lateness(hip, oracle_engine, mode):
     assert sg["records_late"] == so["records_late"] and so["records_late"] > 0
 
 
-@pytest.mark.parametrize("case", ["sum_count_lateness", "f64_min_max", "max_by", "purging"])
+@pytest.mark.parametrize("case", ["sum_count_lateness", "f64_min_max", "max_by", "purging", "min_no_first"])
 def test_hot_buckets_split_over_helpers(hip, oracle_engine, monkeypatch, case):
     """Zipf(1.3) keys concentrate the records in a few directory buckets; with FW_DEBUG_AGG & 64 a share
-    is 256 records, so from the second batch on the hot buckets are split over helper workgroups that
-    fold one after another (k_aggregate).  Bit-exact against the oracle (double sums: tolerance)."""
+    is 256 records, so from the second batch on the hot buckets are split over helper workgroups
+    (k_aggregate): integer shares fold concurrently with device atomics, the last one resolving the first
+    arrivals' f1; double sums and maxBy fold one share after another.  Bit-exact against the oracle
+    (double sums: tolerance)."""
     import ctypes
     from flink_amd.windowing import EventTimeTrigger, PurgingTrigger, ReduceFunction, TumblingEventTimeWindows
     from flink_amd.windowing import Aggregations, make_config
@@ -208,6 +210,9 @@ def test_hot_buckets_split_over_helpers(hip, oracle_engine, monkeypatch, case):
     elif case == "max_by":
         cfg = make_config(asg, Aggregations.maxBy(vt), None, 0, **kw)
         fields = ["max_i64"]
+    elif case == "min_no_first":
+        cfg = make_config(asg, ReduceFunction(("min", "count"), vt, False), None, 0, **kw)
+        fields = ["min_i64", "count"]
     else:
         cfg = make_config(asg, ReduceFunction(("sum", "max"), vt, True), PurgingTrigger.of(EventTimeTrigger.create()),
                           0, **kw)
@@ -223,7 +228,8 @@ def test_hot_buckets_split_over_helpers(hip, oracle_engine, monkeypatch, case):
     eo.close()
     assert dbg[3] > 0, "no bucket was split"
     assert dbg[7] == 0, f"capacity error at site {dbg[7]}"
-    _compare(epochs_of(rg, fields, True), epochs_of(ro, fields, True), fields, rel)
+    keep_f1 = case != "min_no_first"
+    _compare(epochs_of(rg, fields, keep_f1), epochs_of(ro, fields, keep_f1), fields, rel)
 
 
 @pytest.mark.parametrize("lateness", [0, 500])
