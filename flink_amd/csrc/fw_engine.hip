@@ -616,7 +616,11 @@ constexpr int AG_THREADS = 1024;
 constexpr int AG_WIN = FW_AG_WIN;       // k_aggregate: directory slots probed without a branch
 constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
 constexpr int AG_MAXPER = 17;           // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
-constexpr int AG_SPLIT_MAX = 16;        // k_aggregate: shares a hot bucket is split into, at most
+constexpr int AG_SPLIT_MAX = 31;        // k_aggregate: shares a hot bucket is split into, at most 
+#ifndef FW_AGG_SPLIT_INT
+#define FW_AGG_SPLIT_INT 31
+#endif
+constexpr int AG_SPLIT_CHAIN = 16;      // ... when its shares fold one after another (double sums, maxBy / minBy)
 constexpr uint32_t AG_SPLIT_MIN = 16384; // ... and routed records per share, at least
 constexpr int RT_MAX_KB_BITS = 12;      // directory slots per bucket that k_aggregate holds in LDS
 constexpr int IDX_BITS = FW_RT_TILE_LOG; // record index within a tile
@@ -633,8 +637,12 @@ struct RouteBuf {
   unsigned int* bload_cur;
   unsigned int* bload_zero;
   unsigned int* fold_flag;        // [RT_MAXNB][RT_GS] (tag << 5) | shares folded
+  unsigned int* fold_cnt;         // [RT_MAXNB][RT_GS] shares folded concurrently (integer variants): this batch's
+  unsigned int* fold_cnt_zero;    // ring entry, and the one of the batch after next that the owners clear
   unsigned int* bload_host;       // host-mapped [RT_MAXNB]: each owner's estimate of its bucket's routed records
   int32_t helpers;
+  int32_t split_max;     // shares per hot bucket, at most (<= AG_SPLIT_MAX)
+  int32_t chunk_pct;     // a share's records: at least this percentage of the mean bucket load
   uint32_t tag;
   int64_t* dm;           // [tiles x RT_TILE] slice number of each direct-group record (at its routed position)
   unsigned int* dflag;   // set by a tile with direct-group records (a ring of FLAG_RING words, one per batch)
@@ -1078,9 +1086,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   // XCD-aware bucket order: workgroups are dealt to the 8 XCDs round-robin, so XCD x runs the
   // contiguous bucket range [x * nb/8, (x + 1) * nb/8).  Neighbouring buckets' segments share the
   // 128-B lines at their boundaries; with both readers on one XCD the second read hits that XCD's L2
-  const int owner_bkt = blockIdx.x >= (unsigned)s.nb ? -1
-                        : (s.nb % 8 == 0 && !(r.dbg & 32)) ? (int)(blockIdx.x % 8) * (s.nb / 8) + (int)(blockIdx.x / 8)
-                                                          : (int)blockIdx.x;
+  // Integer variants fold a split bucket's shares without waiting on each other, so their helpers (the
+  // hot buckets' shares, the longest work items) take the first block indices and start at once instead
+  // of waiting for an owner's CU; vb is the block's index in the owners-then-helpers numbering
+  constexpr bool HELPERS_FIRST = SKEW && VT == FW_VALUE_I64 && !(AGG & (FW_AGG_MAXBY | FW_AGG_MINBY));
+  const int H = HELPERS_FIRST ? r.helpers : 0;
+  const int vb = (int)blockIdx.x < H ? s.nb + (int)blockIdx.x : (int)blockIdx.x - H;
+  const int owner_bkt = vb >= s.nb ? -1
+                        : (s.nb % 8 == 0 && !(r.dbg & 32)) ? (vb % 8) * (s.nb / 8) + vb / 8
+                                                          : vb;
   const int nbq = RT_GROUPS * s.nb;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
@@ -1123,15 +1137,16 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     uint32_t all = 0;
     for (int w = 0; w < NT / 64; ++w) all += (uint32_t)awtot[w];
     // (FW_DEBUG_AGG & 64: a share of 256 records, so that tests split buckets at small sizes)
-    const uint32_t chunk = max((r.dbg & 64) ? 256u : AG_SPLIT_MIN, 2u * (all / (uint32_t)s.nb + 1u));
+    const uint32_t chunk = max((r.dbg & 64) ? 256u : AG_SPLIT_MIN,
+                               (uint32_t)(((uint64_t)(all / (uint32_t)s.nb + 1u) * (uint32_t)r.chunk_pct) / 100u));
     for (int x = threadIdx.x; x < s.nb; x += NT) {
-      const uint32_t sh = min((r.bload_prev[x] + chunk - 1) / chunk, (uint32_t)AG_SPLIT_MAX);
+      const uint32_t sh = min((r.bload_prev[x] + chunk - 1) / chunk, (uint32_t)r.split_max);
       plan[x] = sh > 1 ? (int32_t)sh - 1 : 0;    // helpers bucket x asks for
     }
     if (threadIdx.x == 0) plan[s.nb] = 0;
     __syncthreads();
     block_scan_excl<NT, AG_MAXPER>(plan, s.nb + 1, awtot);   // plan[x] = first helper of bucket x; plan[nb] = total
-    const int32_t h = owner_bkt < 0 ? (int32_t)blockIdx.x - s.nb : -1;
+    const int32_t h = owner_bkt < 0 ? (int32_t)vb - s.nb : -1;
     if (threadIdx.x == 0) plan[RT_MAXNB + 1] = owner_bkt < 0 ? -1 : owner_bkt;
     __syncthreads();
     for (int x = threadIdx.x; x < s.nb; x += NT) {
@@ -1149,6 +1164,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   const int t_lo = SKEW ? (int)((int64_t)share * r.ntiles / nshare) : 0;
   const int t_hi = SKEW ? (int)((int64_t)(share + 1) * r.ntiles / nshare) : r.ntiles;
   const int64_t dbase = (int64_t)bkt * KB;
+  if (share == 0 && r.fold_cnt_zero)
+    for (int g = threadIdx.x; g < RT_GS; g += NT) r.fold_cnt_zero[(int64_t)bkt * RT_GS + g] = 0u;
   // does any tile hold direct-group records (the batch's flag; no: skip all direct work)
   const bool has_direct = __builtin_amdgcn_readfirstlane(*r.dflag) != 0;
   // every tile's header and this bucket's segment bounds in each of its bin groups, plus the bucket's
@@ -1421,9 +1438,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
           __builtin_amdgcn_s_sleep(8);
           if (++spins > ((int64_t)1 << 21)) { cap_error(s, 16); break; }   // never hang: report and go on
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 invalidated once, for the workgroup
       }
       __syncthreads();
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);
     }
     // fold into the dense columns: this workgroup (this share, in share order) is the only writer of
     // (p, bucket) panes while it folds
@@ -1482,21 +1499,18 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     }
     if (AFOLD && afold) {
       // count this share's fold in; the last one reads the first arrivals back (agent atomics: coherent
-      // across the XCDs' L2s) and stores the f1 of each pane the batch opened
-      __threadfence();
+      // across the XCDs' L2s) and stores the f1 of each pane the batch opened.  Atomics on both sides, so
+      // no L2 write-back: each wave waits for its own atomics, then one add counts the share in (a
+      // __threadfence() per thread here wrote back the XCD's whole L2 sixteen times: ~50 us per share)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (threadIdx.x == 0) {
-        unsigned old = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nv;
-        do {
-          const unsigned done = (old >> 5) == r.tag ? (old & 31u) : 0u;
-          nv = (r.tag << 5) | (done + 1);
-        } while (!__hip_atomic_compare_exchange_strong(flag, &old, nv, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT));
-        lclaim = (int32_t)(nv & 31u) == nshare ? 1 : 0;
+      if (threadIdx.x == 0) {   // (one add: a compare-and-swap loop here serialised the shares for ~50 us)
+        const unsigned done = __hip_atomic_fetch_add(r.fold_cnt + (int64_t)bkt * RT_GS + g, 1u, __ATOMIC_ACQ_REL,
+                                                     __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        lclaim = (int32_t)done == nshare ? 1 : 0;
       }
       __syncthreads();
       if (FIRST && lclaim) {   // uniform
-        __threadfence();
         for (int x = threadIdx.x; x <= KB; x += NT) {
           if (x == KB && bkt != 0) continue;
           const int64_t idx = (int64_t)p * s.stride + (x < KB ? dbase + x : s.D);
@@ -1506,10 +1520,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         }
       }
     } else {
-      if (SKEW && share + 1 < nshare) __threadfence();   // this share's fold visible before the next one's starts
+      // this share's fold visible before the next one's starts: every wave's stores complete, then one
+      // release (one L2 write-back) and the flag
+      if (SKEW && share + 1 < nshare) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (SKEW && share + 1 < nshare && threadIdx.x == 0)
+      if (SKEW && share + 1 < nshare && threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_store(flag, (r.tag << 5) | (unsigned)(share + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     FW_STAMP(r, SB, 4 + 3 * min(g, 1));
   }
@@ -2438,7 +2456,7 @@ struct fw_engine {
   RouteBuf rbs[NBUF] = {};                  // routed-batch buffers, one set per buffer slot
   unsigned int* dflags = nullptr;           // direct-record flags, a ring of FLAG_RING
   unsigned int* bload = nullptr;            // [4][RT_MAXNB] routed records per bucket and batch (k_aggregate split plan)
-  unsigned int* fold_flag = nullptr;        // [RT_MAXNB][RT_GS]
+  unsigned int* fold_flag = nullptr;        // [5][RT_MAXNB][RT_GS]: chained-fold flags, concurrent-fold count ring
   unsigned int* bload_host = nullptr;       // host-mapped [RT_MAXNB], written by k_aggregate's owners
   // key directory compaction
   unsigned char* kg_evicted = nullptr;      // [max_parallelism] a key of the key group was evicted
@@ -2451,6 +2469,8 @@ struct fw_engine {
   void *dec_table = nullptr, *dec_small = nullptr, *dec_bytes = nullptr;
   size_t dec_table_cap = 0, dec_small_cap = 0, dec_bytes_cap = 0;
   int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
+  int agg_split = AG_SPLIT_CHAIN;           // shares per hot bucket, at most (FW_AGG_SPLIT)
+  int agg_chunk_pct = 200;                  // records per share: at least this % of the mean load (FW_AGG_CHUNK_PCT)
   // sliding: the assigner's extra-window records, one list per routed buffer set (fw_push_batch applies
   // a batch's list right after its ingest, on the engine stream)
   int64_t* quirk_list[NBUF] = {};
@@ -2572,18 +2592,22 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
     uint64_t all = 0;
     for (int x = 0; x < e->s.nb; ++x) all += __atomic_load_n(&e->bload_host[x], __ATOMIC_RELAXED);
     const uint32_t cmin = (e->rb.dbg & 64) ? 256u : AG_SPLIT_MIN;
-    const uint64_t chunk = std::max<uint64_t>(cmin, 2 * (all / (uint64_t)e->s.nb + 1));
+    const uint64_t chunk = std::max<uint64_t>(cmin, ((all / (uint64_t)e->s.nb + 1) * (uint64_t)e->agg_chunk_pct) / 100);
     for (int x = 0; x < e->s.nb; ++x) {
       const uint64_t sh = std::min<uint64_t>((__atomic_load_n(&e->bload_host[x], __ATOMIC_RELAXED) + chunk - 1) / chunk,
-                                             AG_SPLIT_MAX);
+                                             (uint64_t)e->agg_split);
       wanted += sh > 1 ? (int)sh - 1 : 0;
     }
   }
   r.helpers = std::min(e->agg_helpers_max, wanted);
+  r.split_max = e->agg_split;
+  r.chunk_pct = e->agg_chunk_pct;
   r.bload_prev = e->bload + ((e->batches + 3) % 4) * RT_MAXNB;
   r.bload_cur = e->bload + (e->batches % 4) * RT_MAXNB;
   r.bload_zero = e->bload + ((e->batches + 2) % 4) * RT_MAXNB;
   r.fold_flag = e->fold_flag;
+  r.fold_cnt = e->fold_flag + (size_t)(1 + e->batches % 4) * RT_MAXNB * RT_GS;
+  r.fold_cnt_zero = e->fold_flag + (size_t)(1 + (e->batches + 2) % 4) * RT_MAXNB * RT_GS;
   r.bload_host = e->bload_host;
   r.tag = (uint32_t)((e->batches + 1) & 0x7FFFFFF);
   // at least 81 KiB of LDS: one k_aggregate workgroup per CU (the dispatcher would otherwise pair two
@@ -2862,11 +2886,18 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
       e->dflags = e->alloc<unsigned int>(FLAG_RING);
       e->bload = e->alloc<unsigned int>(4 * RT_MAXNB);
-      e->fold_flag = e->alloc<unsigned int>((size_t)RT_MAXNB * RT_GS);
+      e->fold_flag = e->alloc<unsigned int>((size_t)5 * RT_MAXNB * RT_GS);   // flags, then the 4-entry count ring
       if (hipHostMalloc((void**)&e->bload_host, 4 * RT_MAXNB, hipHostMallocMapped) != hipSuccess) e->bload_host = nullptr;
       if (e->bload_host) memset(e->bload_host, 0, 4 * RT_MAXNB);
       const char* hv = getenv("FW_AGG_HELPERS");
       if (hv) e->agg_helpers_max = std::max(0, std::min(atoi(hv), (int)RT_MAXNB));
+      // integer reduces fold a split bucket's shares concurrently, so they take more of them
+      const bool afold = e->s.vt == FW_VALUE_I64 && !e->s.by;
+      e->agg_split = afold ? FW_AGG_SPLIT_INT : AG_SPLIT_CHAIN;
+      const char* sv = getenv("FW_AGG_SPLIT");
+      if (sv) e->agg_split = std::max(1, std::min(atoi(sv), afold ? AG_SPLIT_MAX : AG_SPLIT_CHAIN));
+      const char* cv = getenv("FW_AGG_CHUNK_PCT");
+      if (cv) e->agg_chunk_pct = std::max(50, std::min(atoi(cv), 1000));
       for (int q = 0; q < fw_engine::NBUF; ++q) {
         RouteBuf& r = e->rbs[q];
         r = e->rb;
@@ -2960,7 +2991,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
   if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
   if (e->bload) HIPCHK(e, hipMemsetAsync(e->bload, 0, 4 * 4 * RT_MAXNB, e->stream));
-  if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)RT_MAXNB * RT_GS, e->stream));
+  if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)5 * RT_MAXNB * RT_GS, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
   *out = e;

@@ -44,6 +44,9 @@ for j in range(6):
         top = np.argsort(ends)[-8:][::-1]
         print(f"      agg blocks {nagg}; slowest (blockIdx, end ns, main ns):",
               [(int(b), int(ends[b]), int((a[b, 3] - a[b, 2]) * 10)) for b in top])
+        t0 = a[:nagg, 0][a[:nagg, 0] > 0].min()
+        for b in top[:4]:   # every stamp of the block, ns from the kernel's first stamp (0 = not reached)
+            print(f"        block {int(b)}:", [int((x - t0) * 10) if x else 0 for x in a[b]])
     sk, d, span = phases(buf[8 << 16:], nagg, 5)
     print(f"        aggregate: start-skew {sk:.0f} ns, ldir {d[0]:.0f} segtab {d[1]:.0f} main {d[2]:.0f} fold {d[3]:.0f} | span {span:.0f} ns")
     e.advance_watermark(int(t.max().item()) - (50 if C4 else 1))
