@@ -1228,28 +1228,44 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   // flag is no longer read and whose successor k_route starts only after this kernel (event order)
   if (blockIdx.x == 0 && threadIdx.x == 0) *r.dflag_reset = 0u;
   for (int t = threadIdx.x; has_direct && t < r.ntiles; t += NT) {
-    const uint32_t sd = lseg[t * RT_GROUPS + RT_Q], sf = lseg[t * RT_GROUPS + RT_Q + 1];
+    const uint32_t sd = lseg[t * RT_GROUPS + RT_Q];
     for (uint32_t x = sd & 0xFFFFu; x < (sd >> 16); ++x) gsl_insert(r.dm[(int64_t)t * RT_TILE + x]);
-    if (b.late_key == nullptr || t < t_lo || t >= t_hi) continue;
-    const uint32_t f_lo = sf & 0xFFFFu, f_hi = sf >> 16;
-    if (f_hi <= f_lo) continue;
-    // the tile's fire records of this bucket take one reservation of the late list (a per-record atomic on
-    // its shared cursor serialised the hot buckets of skewed streams)
-    const unsigned long long lbase = atomicAdd(b.late_count, (unsigned long long)(f_hi - f_lo));
-    for (uint32_t x = f_lo; x < f_hi; ++x) {
-      const int64_t pos = (int64_t)t * RT_TILE + x;
-      const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
-      const uint64_t h = (uint64_t)r.kv[pos].x;
-      const int64_t m = r.dm[pos];
-      int32_t p = slice_slot(s, m);
-      int64_t kid = s.D;
-      if (h == EMPTY_H) (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
-      else {
-        const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
-        kid = x2 < 0 ? -1 : dbase + x2;
+  }
+  // the per-element fire records of this share's tiles, flattened over the workgroup in tile order (after a
+  // window boundary most of a hot key's tile can be fire records: one thread per tile walked them
+  // serially), under one reservation of the late list
+  if (has_direct && b.late_key != nullptr) {   // uniform
+    for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+      const uint32_t sf = lseg[t * RT_GROUPS + RT_Q + 1];
+      const uint32_t f_lo = sf & 0xFFFFu, f_hi = sf >> 16;
+      off[t] = (t >= t_lo && t < t_hi && f_hi > f_lo) ? (int32_t)(f_hi - f_lo) : 0;
+    }
+    if (threadIdx.x == 0) off[r.ntiles] = 0;
+    __syncthreads();
+    block_scan_excl<NT, AG_MAXPER>(off, r.ntiles + 1, awtot);
+    const int32_t nf = off[r.ntiles];
+    if (nf > 0) {   // uniform
+      if (threadIdx.x == 0) lclaim = (int32_t)atomicAdd(b.late_count, (unsigned long long)nf);
+      __syncthreads();
+      const unsigned long long lbase = (uint32_t)lclaim;
+      for (int32_t j = threadIdx.x; j < nf; j += NT) {
+        int t = 0, hi = r.ntiles;   // the last tile t with off[t] <= j holds record j
+        while (hi - t > 1) { const int mid = (t + hi) >> 1; if (off[mid] <= j) t = mid; else hi = mid; }
+        const uint32_t x = (lseg[t * RT_GROUPS + RT_Q + 1] & 0xFFFFu) + (uint32_t)(j - off[t]);
+        const int64_t pos = (int64_t)t * RT_TILE + x;
+        const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
+        const uint64_t h = (uint64_t)r.kv[pos].x;
+        const int64_t m = r.dm[pos];
+        int32_t p = slice_slot(s, m);
+        int64_t kid = s.D;
+        if (h == EMPTY_H) (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
+        else {
+          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
+          kid = x2 < 0 ? -1 : dbase + x2;
+        }
+        if (p < 0 || kid < 0) { cap_error(s, 7); p = 0; kid = 0; }   // (a failed batch: a harmless entry keeps the slot)
+        late_append_at(s, b, lbase + (unsigned long long)j, p, kid, m, i);
       }
-      if (p < 0 || kid < 0) { cap_error(s, 7); p = 0; kid = 0; }   // (a failed batch: a harmless entry keeps the slot)
-      late_append_at(s, b, lbase + (x - f_lo), p, kid, m, i);
     }
   }
   // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same
