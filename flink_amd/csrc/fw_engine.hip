@@ -1635,7 +1635,10 @@ __global__ void k_late_prepare(Spec s, const unsigned long long* sorted_key, int
 // one workgroup; then the records of each tile ahead of its first head take their carry.  A fixed
 // combine tree: double sums are reproducible run to run (replaces a rocPRIM scan-by-key of the 56-B
 // accumulator, ~0.57 ms per 1.6 M records)
-constexpr int LS_T = 256, LS_I = 8, LS_TILE = LS_T * LS_I, LS_CT = 512;
+#ifndef FW_LS_I
+#define FW_LS_I 1
+#endif
+constexpr int LS_T = 256, LS_I = FW_LS_I, LS_TILE = LS_T * LS_I, LS_CT = 512;
 struct SegPart {
   LateAcc v;
   int64_t hp;      // the last segment head at or before this point (-1: none)
@@ -1652,8 +1655,10 @@ __device__ __forceinline__ SegPart seg_join(const SegPart& x, const SegPart& y) 
   r.empty = 0;
   return r;
 }
-__global__ __launch_bounds__(LS_T) void k_segscan_tile(const unsigned long long* seg, const LateAcc* acc, int64_t n,
-                                                        LateAcc* out, int64_t* hp_out, SegPart* tile_agg,
+__global__ __launch_bounds__(LS_T) void k_segscan_tile(const unsigned long long* __restrict__ seg,
+                                                        const LateAcc* __restrict__ acc, int64_t n,
+                                                        LateAcc* __restrict__ out, int64_t* __restrict__ hp_out,
+                                                        SegPart* tile_agg,
                                                         int32_t* tile_first_head) {
   __shared__ __attribute__((aligned(16))) unsigned char sp_raw[LS_T * sizeof(SegPart)];   // (LateAcc has a constructor)
   SegPart* sp = (SegPart*)sp_raw;
