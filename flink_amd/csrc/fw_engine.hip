@@ -2779,6 +2779,22 @@ static bool wm_quiet(const Spec& s, int64_t old_wm, int64_t new_wm) {
   return !crosses(a) && !crosses(a + s.lateness);
 }
 
+// can a record pushed under watermark wm be a per-element fire (a window of it with maxTimestamp <= wm <
+// cleanup time, WindowOperator.java:302-325)?  Window maxTimestamps are a + n d, so only if the latest one
+// at or below wm lies within the allowed lateness of wm.  If not, the push needs no late-record count
+// read-back (a host sync per batch that kept the next k_route from overlapping).  Conservative near the
+// int64 edges.
+static bool fires_possible(const Spec& s, int64_t wm) {
+  const int64_t lim = (int64_t)1 << 61;
+  if (wm <= -lim || wm >= lim || s.lateness >= lim || s.size >= lim || s.offset <= -lim || s.offset >= lim)
+    return true;
+  const __int128 d = s.assigner == FW_TUMBLING ? s.size : s.slide;
+  const __int128 a = (__int128)s.offset + s.size - 1;
+  __int128 r = ((__int128)wm - a) % d;   // wm minus the latest maxTimestamp <= wm
+  if (r < 0) r += d;
+  return r < (__int128)s.lateness;
+}
+
 template <int VT, int AGG, bool FIRST>
 static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + WM_THREADS - 1) / WM_THREADS, e->grid / 8));
@@ -3243,7 +3259,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
                        e->cfg.max_batch);
     e->phase_end(n);
   }
-  if (e->cfg.allowed_lateness > 0 && !e->session && !e->list) {
+  if (e->cfg.allowed_lateness > 0 && !e->session && !e->list && fires_possible(e->s, e->cur_wm)) {
     // per-element fires: the list lengths on the host size the sorts
     unsigned long long nl = 0, nf = 0;
     HIPCHK(e, hipMemcpyAsync(&nl, e->late_count, 8, hipMemcpyDeviceToHost, e->stream));
