@@ -335,7 +335,8 @@ def main():
     achieved = alg_step / (ms_step / 1e3) / 1e9
     pmc, pmc_src = pmc_traffic(args.config)
     kernels = {}
-    names = [("k_route", route_ms, 1.0), ("k_aggregate", agg_ms, 1.0)] if form == 2 else [("k_ingest_direct", route_ms, 1.0)]
+    names = ([("k_route", route_ms, 1.0), ("k_aggregate", agg_ms, 1.0)] if form == 2 else
+             [("k_fused", route_ms, 1.0)] if form == 3 else [("k_ingest_direct", route_ms, 1.0)])
     names.append(("k_watermark", wm_ms, wm_per_step))
     for name, ms, per_step in names:
         tr = traffic_of(pmc, name)

@@ -2454,6 +2454,18 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
 
 }  // namespace fw
 
+#include "fw_fused.hip"
+
+#include <mutex>
+struct fw_engine;
+namespace {
+// fused launches are serialised device-wide: each one needs every CU of the device resident at once, so two
+// engines' launches must not split the CUs between them (fw_fused.hip)
+std::mutex g_fused_mu;
+hipEvent_t g_fused_ev[64] = {};
+const fw_engine* g_fused_owner[64] = {};
+}  // namespace
+
 // ==================================================================================================
 // host side
 // ==================================================================================================
@@ -2587,6 +2599,12 @@ struct fw_engine {
   unsigned int* wm_done = nullptr;   // k_watermark's workgroup completion counter
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
+  // fused ingest (ingest_mode 3, fw_fused.hip)
+  bool fused = false;
+  FusedBuf fb{};
+  size_t fused_lds = 0;
+  int64_t fused_launches = 0;
+  unsigned long long fused_uses[FU_S] = {};
   RouteBuf rb{};                            // fields shared by both parities (dbg, stamps)
   RouteBuf rbs[NBUF] = {};                  // routed-batch buffers, one set per buffer slot
   unsigned int* dflags = nullptr;           // direct-record flags, a ring of FLAG_RING
@@ -2657,6 +2675,10 @@ struct fw_engine {
     return (T*)p;
   }
   ~fw_engine() {
+    {
+      std::lock_guard<std::mutex> lk(g_fused_mu);
+      if (g_fused_owner[dev & 63] == this) g_fused_owner[dev & 63] = nullptr;
+    }
     if (rstream) (void)hipStreamSynchronize(rstream);
     if (stream) (void)hipStreamSynchronize(stream);
     if (rstream) (void)hipStreamDestroy(rstream);
@@ -2765,6 +2787,30 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   // (ev_agg[par] is recorded by fw_push_batch once the batch's extra-window list is applied too)
 }
 
+// fused form (fw_fused.hip): one launch per batch, FU_GRID workgroups, after any other engine's fused launch
+template <int VT, int AGG, bool FIRST>
+static void launch_fused_t(fw_engine* e, const BatchIn& b, const int64_t* f1col) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_fused<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  FusedBuf f = e->fb;
+  const int64_t per_round = (int64_t)FU_GRID * FU_CH;
+  f.rounds = (int32_t)((b.n + per_round - 1) / per_round);
+  f.epoch = e->fused_launches;
+  for (int q = 0; q < FU_S; ++q) f.uses[q] = e->fused_uses[q];
+  std::lock_guard<std::mutex> lk(g_fused_mu);
+  const int d = e->dev & 63;
+  if (!g_fused_ev[d]) (void)hipEventCreateWithFlags(&g_fused_ev[d], hipEventDisableTiming);
+  if (g_fused_owner[d] && g_fused_owner[d] != e && g_fused_ev[d]) (void)hipStreamWaitEvent(e->stream, g_fused_ev[d], 0);
+  hipLaunchKernelGGL((k_fused<VT, AGG, FIRST>), dim3(FU_GRID), dim3(FU_THREADS), e->fused_lds, e->stream, e->s, b, f, f1col);
+  if (g_fused_ev[d]) (void)hipEventRecord(g_fused_ev[d], e->stream);
+  g_fused_owner[d] = e;
+  e->fused_launches++;
+  for (int k = 0; k < f.rounds; ++k) e->fused_uses[k % FU_S]++;
+}
+
 // no window of the assigner has its maxTimestamp or its cleanup time in (old, new]: the advance fires
 // and purges nothing (a live slice's fire and cleanup times lie above the watermark it was created
 // under), only the watermark's mark is due.  Conservative near the int64 edges.
@@ -2825,6 +2871,26 @@ static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
     }                                                                                            \
   } while (0)
 
+// the fused form's instantiated reduce shapes (no maxBy / minBy)
+#define FW_DISPATCH_FUSED(FN, e, ...)                                                            \
+  do {                                                                                           \
+    const Spec& _s = (e)->s;                                                                     \
+    const bool _f = _s.first != 0;                                                               \
+    if (_s.vt == FW_VALUE_I64) {                                                                 \
+      switch (_s.agg) {                                                                          \
+        case 1: if (_f) FN<0, 1, true>(e, ##__VA_ARGS__); else FN<0, 1, false>(e, ##__VA_ARGS__); break;   \
+        case 9: if (_f) FN<0, 9, true>(e, ##__VA_ARGS__); else FN<0, 9, false>(e, ##__VA_ARGS__); break;   \
+        default: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
+      }                                                                                          \
+    } else {                                                                                     \
+      switch (_s.agg) {                                                                          \
+        case 1: if (_f) FN<1, 1, true>(e, ##__VA_ARGS__); else FN<1, 1, false>(e, ##__VA_ARGS__); break;   \
+        case 9: if (_f) FN<1, 9, true>(e, ##__VA_ARGS__); else FN<1, 9, false>(e, ##__VA_ARGS__); break;   \
+        default: if (_f) FN<1, 15, true>(e, ##__VA_ARGS__); else FN<1, 15, false>(e, ##__VA_ARGS__); break; \
+      }                                                                                          \
+    }                                                                                            \
+  } while (0)
+
 extern "C" {
 
 const char* fw_version(void) { return "flink_amd fw 0.1 (gfx950)"; }
@@ -2870,7 +2936,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     return unsupported("fold: one aggregate (sum, count, min or max) from the initial value, no first-arrival f1");
   if (by && c.ingest_mode == 1) return unsupported("maxBy / minBy run on the partitioned ingest form (ingest_mode 0 or 2)");
   if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
-  if (c.ingest_mode < 0 || c.ingest_mode > 2) return bad("bad ingest mode");
+  if (c.ingest_mode < 0 || c.ingest_mode > 3) return bad("bad ingest mode");
   HIPCHK(e, hipSetDevice(c.device));
   e->dev = c.device;
   HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
@@ -2930,12 +2996,30 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.fold_init = c.fold_initial;
   s.first = c.keep_first_f1 || by ? 1 : 0;   // maxBy/minBy: the pane's presence and the extremal f1
 
-  // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys): short linear-probe sequences
-  s.D = next_pow2(std::max<int64_t>((c.key_capacity <= (1 << 20) ? 4 : 2) * c.key_capacity, 64));
+  // fused ingest (ingest_mode 3, fw_fused.hip): reduce / fold of tumbling or sliding windows without allowed
+  // lateness, on a device that holds the whole grid resident (one workgroup per CU), with an owner's range of
+  // the directory (D / 32 slots, D = 2 x key capacity) and its accumulators in LDS.  Auto mode takes it for
+  // batches of >= 64 Ki records (FW_FUSED=0: never)
+  const int nacc_f = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
+  const int64_t d_fused = next_pow2(std::max<int64_t>(2 * c.key_capacity, 2048));
+  const int so_bits_f = bits_for((uint64_t)d_fused) - 1 - 5;
+  {
+    const char* fv = getenv("FW_FUSED");
+    const bool ok = !e->session && !e->list && !by && c.allowed_lateness == 0 && c.max_batch <= (1ll << 26) &&
+                    prop.multiProcessorCount >= FU_GRID && fused_lds_bytes(so_bits_f, nacc_f) <= 160 * 1024;
+    if (c.ingest_mode == 3 && !ok)
+      return unsupported("fused ingest (ingest_mode 3): tumbling or sliding reduce / fold without allowed lateness, "
+                         "key_capacity <= 64 Ki (sum) / 32 Ki (sum, min, max, count), on a 256-CU device");
+    e->fused = ok && (c.ingest_mode == 3 || (c.ingest_mode == 0 && !(fv && atoi(fv) == 0) && c.max_batch >= (1 << 16)));
+  }
+  // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys, and for the fused form): short linear-probe
+  // sequences
+  s.D = e->fused ? d_fused : next_pow2(std::max<int64_t>((c.key_capacity <= (1 << 20) ? 4 : 2) * c.key_capacity, 64));
   s.dir_mask = (uint64_t)s.D - 1;
   {
     int dbits = bits_for((uint64_t)s.D) - 1;                  // D = 2^dbits
     int kb = std::max(std::min(dbits, 9), dbits - 8);          // <= 256 buckets of >= 512 slots
+    if (e->fused) kb = std::min(9, dbits - 5);                 // fused: >= 32 buckets (one owner range is whole buckets)
     s.kb_bits = kb;
     s.nb = (int32_t)(s.D >> kb);
   }
@@ -3027,7 +3111,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
                       c.max_batch <= (1ll << 26);
     if (c.ingest_mode == 2 && !fits)
       return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
-    e->routed = !e->session && (c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by)));
+    e->routed = !e->session && !e->fused && (c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by)));
     if (by && !e->routed) return unsupported("maxBy / minBy need the partitioned ingest form (key_capacity <= 256 Ki)");
     if (e->routed) {
       e->max_tiles = max_tiles;
@@ -3063,6 +3147,24 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       e->agg_min_lds = (ml ? atoi(ml) : 81) * 1024;
       e->agg_lds = agg_need;   // at launch: less the unused tiles, at least agg_min_lds
     }
+  }
+  if (e->fused) {
+    FusedBuf& f = e->fb;
+    f.so_bits = so_bits_f;
+    f.owner_shift = bits_for((uint64_t)s.D) - 1 - 5;
+    f.ring = e->alloc<unsigned char>((size_t)FU_GRID * FU_S * FU_SLOT);
+    f.ctr = e->alloc<unsigned long long>(FU_C_N);
+    f.xcc = e->alloc<int32_t>(FU_GRID);
+    const size_t np = (size_t)FU_GROUPS * (size_t)s.D;   // [32 ranges][8 groups][D / 32 slots]
+    f.psum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>(np) : nullptr;
+    f.pmn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(np) : nullptr;
+    f.pmx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>(np) : nullptr;
+    f.pcnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>(np) : nullptr;
+    f.pfirst = e->alloc<uint32_t>(np);
+    const char* fs = getenv("FW_FUSED_SAFE");
+    f.force_safe = fs && atoi(fs) != 0 ? 1 : 0;
+    // at least 81 KiB: one workgroup per CU, so the 256 of a launch are resident together on 256 CUs
+    e->fused_lds = std::max<size_t>(fused_lds_bytes(so_bits_f, nacc_f), 81 * 1024);
   }
   e->wm_done = e->alloc<unsigned int>(1);
   if (s.first && !e->routed) {
@@ -3141,6 +3243,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
   if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
   if (e->bload) HIPCHK(e, hipMemsetAsync(e->bload, 0, 4 * 4 * RT_MAXNB, e->stream));
+  if (e->fb.ctr) HIPCHK(e, hipMemsetAsync(e->fb.ctr, 0, 8 * FU_C_N, e->stream));
   if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)5 * RT_MAXNB * RT_GS, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
@@ -3208,8 +3311,8 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     if (key_hash) { HIPCHK(e, hipMemcpyAsync(e->stg_hash[par], key_hash, 4 * n, hipMemcpyHostToDevice, in_stream)); dh = e->stg_hash[par]; }
     if (f1) { HIPCHK(e, hipMemcpyAsync(e->stg_f1[par], f1, 8 * n, hipMemcpyHostToDevice, in_stream)); df1 = e->stg_f1[par]; }
   }
-  if (e->routed && mem == FW_MEM_DEVICE) {
-    // k_route streams the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
+  if ((e->routed || e->fused) && mem == FW_MEM_DEVICE) {
+    // k_route / k_fused stream the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
     auto mis = [](const void* ptr, uintptr_t a) { return ((uintptr_t)ptr & (a - 1)) != 0; };
     if (mis(dk, 16)) { HIPCHK(e, hipMemcpyAsync(e->stg_key[par], dk, 8 * n, hipMemcpyDeviceToDevice, in_stream)); dk = e->stg_key[par]; }
     if (mis(dts, 16)) { HIPCHK(e, hipMemcpyAsync(e->stg_ts[par], dts, 8 * n, hipMemcpyDeviceToDevice, in_stream)); dts = e->stg_ts[par]; }
@@ -3233,7 +3336,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.quirk_capacity = e->s.W > 0 ? e->cfg.max_batch : 0;
   b.f1 = df1;
   b.new_list = e->new_list;
-  b.new_count = e->new_counts ? e->new_counts + half : nullptr;
+  b.new_count = e->new_counts ? e->new_counts + (e->fused ? 0 : half) : nullptr;
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
   if (e->session) {
     if (int rc = session_push(e, b)) return rc;
@@ -3241,6 +3344,10 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     if (int rc = list_push(e, b)) return rc;
   } else if (e->routed) {
     FW_DISPATCH(launch_routed_t, e, b, df1, par);
+  } else if (e->fused) {
+    e->phase_begin(FW_PHASE_INGEST);
+    FW_DISPATCH_FUSED(launch_fused_t, e, b, df1);
+    e->phase_end(n);
   } else {
     e->phase_begin(FW_PHASE_INGEST);
     FW_DISPATCH(launch_ingest_t, e, b);
@@ -3252,7 +3359,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (e->routed) HIPCHK(e, hipEventRecord(e->ev_agg[par], e->stream));
   e->batches++;
   HIPCHK(e, hipGetLastError());
-  if (e->s.first && !e->routed) {   // the partitioned form sets f1 in k_aggregate
+  if (e->s.first && !e->routed && !e->fused) {   // the partitioned form sets f1 in k_aggregate, the fused one in k_fused
     e->phase_begin(FW_PHASE_FIXUP);
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
                        e->stream, e->s, e->new_list, e->new_counts + half, e->new_counts + (half ^ 1), df1, e->ordinal, n,
@@ -3482,7 +3589,7 @@ int fw_get_stats(fw_engine* e, fw_stats* st) {
   for (int64_t t : tags) live += t != FREE_TAG;
   st->slices_live = live;
   st->keys_resident = (int64_t)d[ST_DIR_KEYS];   // the Long.MIN_VALUE key's own column not counted
-  st->ingest_form = e->routed ? 2 : 1;
+  st->ingest_form = e->fused ? 3 : e->routed ? 2 : 1;
   st->compactions = e->compactions;
   return FW_OK;
 }

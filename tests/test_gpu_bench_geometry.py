@@ -85,7 +85,18 @@ def test_c1_bench_geometry():
     cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", keep_first_f1=True),
                       max_parallelism=128, key_capacity=1 << 16, max_batch=batch, out_capacity=1 << 20)
     sg, so = _run(cfg, 5, batch, 1 << 16, 1 << 24, 1)
-    assert sg["ingest_form"] == 2   # the partitioned form the bench runs
+    assert sg["ingest_form"] == 3   # the fused form the bench runs
+    assert sg["panes_fired"] == so["panes_fired"] > 0
+
+
+def test_c1_bench_geometry_partitioned():
+    """The same C1 stream through the two-kernel partitioned form (ingest_mode 2)."""
+    from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, make_config
+    batch = 1 << 22
+    cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", keep_first_f1=True),
+                      max_parallelism=128, key_capacity=1 << 16, max_batch=batch, out_capacity=1 << 20, ingest_mode=2)
+    sg, so = _run(cfg, 5, batch, 1 << 16, 1 << 24, 1)
+    assert sg["ingest_form"] == 2
     assert sg["panes_fired"] == so["panes_fired"] > 0
 
 

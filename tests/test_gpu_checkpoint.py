@@ -24,9 +24,9 @@ MP = 128
 @pytest.fixture(scope="module")
 def hip():
     from flink_amd import _abi
-    from flink_amd.windowing import WindowEngine
+    from harness import hip_engine
     _abi.load_library()
-    return WindowEngine
+    return hip_engine
 
 
 @pytest.fixture(scope="module")
@@ -128,7 +128,7 @@ def _checkpoint_roundtrip(hip, oracle_engine, make_cfg, keys, ts, vals, batch, l
     return n_entries
 
 
-MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned")]
+MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned"), pytest.param(3, id="fused")]
 
 
 @pytest.mark.parametrize("mode", MODES)

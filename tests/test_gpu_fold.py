@@ -11,15 +11,15 @@ from harness import FOLD_FIXTURES, drive, epochs_of, expected_epochs, gen_stream
 pytestmark = pytest.mark.gpu
 
 LONG_MAX = (1 << 63) - 1
-MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned")]
+MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned"), pytest.param(3, id="fused")]
 
 
 @pytest.fixture(scope="module")
 def hip():
     from flink_amd import _abi
-    from flink_amd.windowing import WindowEngine
+    from harness import hip_engine
     _abi.load_library()
-    return WindowEngine
+    return hip_engine
 
 
 @pytest.fixture(scope="module")

@@ -17,9 +17,9 @@ LONG_MAX = (1 << 63) - 1
 @pytest.fixture(scope="module")
 def hip():
     from flink_amd import _abi
-    from flink_amd.windowing import WindowEngine
+    from harness import hip_engine
     _abi.load_library()
-    return WindowEngine
+    return hip_engine
 
 
 @pytest.fixture(scope="module")
@@ -28,7 +28,7 @@ def oracle_engine():
     return OracleEngine
 
 
-MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned")]
+MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned"), pytest.param(3, id="fused")]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -151,7 +151,7 @@ def test_sliding_negative_remainder_known_answer(hip, oracle_engine):
     from flink_amd.windowing import SlidingEventTimeWindows
     want = sorted([(7, 1999, 5), (7, 999, 5), (7, -1, 5), (7, -1001, 5)])   # (key, maxTimestamp, sum)
     for f in (hip, oracle_engine):
-        for mode in (1, 2):
+        for mode in (1, 2, 3):
             e = f(_cfg(SlidingEventTimeWindows.of(3000, 1000), mode=mode))
             e.push(np.array([7], np.int64), np.array([-1500], np.int64), np.array([5], np.int64))
             e.advance_watermark(LONG_MAX)

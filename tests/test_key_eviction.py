@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from harness import drive, epochs_of
+from harness import drive, epochs_of, hip_engine
 
 pytestmark = pytest.mark.gpu
 
@@ -33,7 +33,7 @@ def _drifting_stream(n_windows=44, per_window=6000, span=2000, step=500, seed=3)
     return keys, ts, vals
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("window", ["tumbling", "sliding"])
 def test_keys_evicted_over_time(mode, window):
     from flink_amd.windowing import (ReduceFunction, SlidingEventTimeWindows, TumblingEventTimeWindows,
@@ -48,7 +48,7 @@ def test_keys_evicted_over_time(mode, window):
     n = len(keys) - 6000
     res = []
     for factory in (WindowEngine, OracleEngine):
-        e = factory(cfg)
+        e = factory(cfg) if factory is OracleEngine else hip_engine(cfg)
         out = drive(e, keys[:n], ts[:n], vals[:n], 6000, 1, None, f1=f1[:n])
         snap = {kg: e.snapshot_kg_flink(kg, ("key", "f1", "sum", "count")) for kg in range(128)}
         out += drive(e, keys[n:], ts[n:], vals[n:], 6000, 1, LONG_MAX, f1=f1[n:])

@@ -82,11 +82,11 @@ def test_signed_zero_sums_oracle(window):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("window", ["tumbling", "sliding", "late"])
 def test_signed_zero_sums_hip(window, mode):
-    from flink_amd.windowing import WindowEngine
-    _check(_run(WindowEngine, window, mode), window)
+    from harness import hip_engine
+    _check(_run(hip_engine, window, mode), window)
 
 
 def test_cases_are_signed():
