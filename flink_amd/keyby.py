@@ -22,7 +22,14 @@ all-to-all and the watermark all-reduce of batch j and copies counts and waterma
 behind an event; the host then finishes batch j - depth (its counts arrived long ago): record
 all-to-alls, the engine push and the watermark.  No host synchronisation waits on the batch just
 enqueued.  `flush()` finishes the rest.  The same class runs on CPU tensors with the gloo backend for
-the multi-process tests (routing by the numpy restatement in flink_amd.keygroups, no pipelining).
+the multi-process tests (routing by the numpy restatement in flink_amd.keygroups): either unpipelined
+(`exchange()`), or through the very pipelined step()/_finish() code the GPUs run (`pipelined=True`: only
+the partition kernel, the events and the device-side input waits are swapped for their host forms).
+
+Skew: a rank may receive more records than its engine's max_batch (Zipf keys concentrate on a few key
+groups); the received share is then pushed in max_batch pieces, all between the same two watermarks,
+which is exact (a push is any run of records between watermarks, RecordWriter buffers any amount per
+channel, RecordWriter.java:82-85).
 """
 import ctypes
 from collections import deque
@@ -34,6 +41,16 @@ import torch.distributed as dist
 from .keygroups import operator_index_np
 
 LONG_MIN = -(1 << 63)
+
+
+class _HostEvent:
+    """The CPU path's stand-in for a torch.cuda.Event: host work is complete when it returns."""
+
+    def record(self):
+        pass
+
+    def synchronize(self):
+        pass
 
 
 class ChannelWatermarks:
@@ -56,16 +73,25 @@ class ChannelWatermarks:
 
 
 class KeyByExchange:
-    def __init__(self, engine, world, rank, max_parallelism, batch, device, depth=2):
+    # the engine records one consumption event per push in a ring of this many (fw_stream_wait_input)
+    CONSUMED_RING = 8
+
+    def __init__(self, engine, world, rank, max_parallelism, batch, device, depth=2, pipelined=None):
         self.eng = engine
         self.world, self.rank, self.mp = world, rank, max_parallelism
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
+        self.pipelined = self.cuda if pipelined is None else bool(pipelined)
+        assert self.pipelined or not self.cuda, "the GPU path is pipelined"
         self.local_wm = LONG_MIN        # this source's channel watermark, only raised
         self.last_emitted = LONG_MIN    # last watermark forwarded to the window subtask
         self.emitted = []               # the forwarded watermarks, in order (tests)
-        if self.cuda:
-            self.depth = max(1, depth)
+        if self.pipelined:
+            if not 1 <= depth <= 3:
+                # a send set returns every depth + 1 steps, each making up to two pushes: its last reader lies
+                # at most 2 (depth + 1) - 1 pushes back, within the engine's ring of consumption events
+                raise ValueError("KeyByExchange depth must be 1, 2 or 3")
+            self.depth = depth
             S = self.depth + 1          # send sets: partition of batch j must not overwrite batch j - depth's
             z = lambda n, dt=torch.int64: torch.empty(n, dtype=dt, device=self.device)
             self.send = [(z(batch), z(batch), z(batch)) for _ in range(S)]
@@ -73,9 +99,10 @@ class KeyByExchange:
             # back by one copy
             self.meta = [torch.zeros(2 * world + 1, dtype=torch.int64, device=self.device) for _ in range(S)]
             self.offsets = [torch.zeros(world, dtype=torch.int64, device=self.device) for _ in range(S)]
-            self.host = [torch.zeros(2 * world + 1, dtype=torch.int64).pin_memory() for _ in range(S)]
+            host = (lambda x: x.pin_memory()) if self.cuda else (lambda x: x)
+            self.host = [host(torch.zeros(2 * world + 1, dtype=torch.int64)) for _ in range(S)]
             self.local_wm_at = [LONG_MIN] * S   # world 1: the aligned watermark is the local one (host-known)
-            self.ready = [torch.cuda.Event() for _ in range(S)]
+            self.ready = [torch.cuda.Event() if self.cuda else _HostEvent() for _ in range(S)]
             self.pending = deque()      # (set, batch size) staged, not yet finished
             self.staged = 0
             self.send_pushed_at = [None] * S   # engine push index that last read each send set (own share)
@@ -86,7 +113,8 @@ class KeyByExchange:
             self.pushed_at = [None] * self.RING   # engine push index that last read each set
             self.finished = self.pushes = 0
             # the engine enqueues its partition on torch's stream, so the exchange below is ordered after it
-            self.eng.use_stream(torch.cuda.current_stream(self.device).cuda_stream)
+            if self.cuda:
+                self.eng.use_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     # ------------------------------------------------------------------ routing
     def _route_cuda(self, k, t, v, si):
@@ -100,6 +128,47 @@ class KeyByExchange:
                                                    P(self.offsets[si]))
         if rc != 0:
             raise RuntimeError(f"fw_partition_by_operator failed: {rc}")
+
+    def _route_into(self, k, t, v, si):
+        """Partition a source batch into send set si and its send counts (meta[si][:world])."""
+        if self.cuda:
+            self._route_cuda(k, t, v, si)
+            return
+        n = k.numel()
+        if n > self.send[si][0].numel():
+            raise ValueError(f"batch of {n} records exceeds the exchange's batch capacity {self.send[si][0].numel()}")
+        rk, rt, rv, counts = self._route_host(k, t, v)
+        sk, st, sv = self.send[si]
+        sk[:n].copy_(rk)
+        st[:n].copy_(rt)
+        sv[:n].copy_(rv.view(torch.int64) if rv.dtype == torch.float64 else rv)   # value bits, as the kernel writes
+        self.meta[si][:self.world].copy_(counts)
+
+    def _wait_read(self, pushed_at):
+        """Before a send set or receive set is rewritten: the engine has read it (the push made at index
+        pushed_at).  GPU: torch's stream waits on the device; beyond the event ring, or on CPU: a sync."""
+        if pushed_at is None:
+            return
+        back = self.pushes - 1 - pushed_at
+        if self.cuda and back < self.CONSUMED_RING:
+            self.eng.wait_input(torch.cuda.current_stream(self.device).cuda_stream, back)
+        else:
+            self.eng.sync()
+
+    def _push_share(self, cols3, count):
+        """Push `count` records (one channel's share) to the engine in pieces of at most max_batch, all
+        between the same two watermarks; returns the index of the last push that read them."""
+        a, b, c = cols3
+        as_value = (lambda x: x.view(torch.float64)) if self.eng.cfg.value_type == 1 else (lambda x: x)
+        mb = int(self.eng.cfg.max_batch)
+        for s0 in range(0, count, mb):
+            s1 = min(count, s0 + mb)
+            if self.cuda:
+                self.eng.push(a[s0:s1], b[s0:s1], as_value(c[s0:s1]), keep_alive=False)
+            else:
+                self.eng.push(a[s0:s1].numpy(), b[s0:s1].numpy(), as_value(c[s0:s1]).numpy())
+            self.pushes += 1
+        return self.pushes - 1
 
     def _route_host(self, k, t, v):
         dest = operator_index_np(k.numpy(), self.mp, self.world)
@@ -164,7 +233,7 @@ class KeyByExchange:
     # ------------------------------------------------------------------ one step
     def step(self, k, t, v, wm_local):
         """Source batch (k, t, v) followed by this source's watermark wm_local."""
-        if not self.cuda:
+        if not self.pipelined:
             for rk, rt, rv in self.exchange(k, t, v):   # both shares between the same watermarks
                 if rk.numel():
                     self.eng.push(rk.numpy(), rt.numpy(), rv.numpy())
@@ -177,11 +246,8 @@ class KeyByExchange:
         si = self.staged % (self.depth + 1)
         self.staged += 1
         # the engine may still read this send set (the own share pushed from it): wait on the device
-        if self.send_pushed_at[si] is not None:
-            back = self.pushes - 1 - self.send_pushed_at[si]
-            if back < 8:
-                self.eng.wait_input(torch.cuda.current_stream(self.device).cuda_stream, back)
-        self._route_cuda(k, t, v, si)
+        self._wait_read(self.send_pushed_at[si])
+        self._route_into(k, t, v, si)
         w, meta = self.world, self.meta[si]
         local = self._raise_local(wm_local)
         if w > 1:   # (one rank: its counts are its own receive counts, its watermark the aligned one)
@@ -189,12 +255,12 @@ class KeyByExchange:
             meta[2 * w:].fill_(local)
             dist.all_reduce(meta[2 * w:], op=dist.ReduceOp.MIN)
         self.local_wm_at[si] = local
-        self.host[si].copy_(meta, non_blocking=True)
+        self.host[si].copy_(meta, non_blocking=self.cuda)
         self.ready[si].record()
         self.pending.append((si, k.numel()))
 
     def flush(self):
-        if self.cuda:
+        if self.pipelined:
             while self.pending:
                 self._finish(*self.pending.popleft())
 
@@ -216,25 +282,14 @@ class KeyByExchange:
                 self.eng.sync()   # growing: the old set is dropped only once nothing reads it
             cap = max(m, int(1.25 * n))
             cols = self.ring[slot] = [torch.empty(cap, dtype=torch.int64, device=self.device) for _ in range(3)]
-        elif self.pushed_at[slot] is not None:
-            back = self.pushes - 1 - self.pushed_at[slot]
-            if back < 8:
-                self.eng.wait_input(torch.cuda.current_stream(self.device).cuda_stream, back)
+        else:
+            self._wait_read(self.pushed_at[slot])
         rk, rt, rv = (x[:m] for x in cols)
         sk, st, sv = self.send[si]
         own = self._transfer((sk[:n], st[:n], sv[:n]), send_splits, recv_splits, (rk, rt, rv))
-        as_value = (lambda x: x.view(torch.float64)) if self.eng.cfg.value_type == 1 else (lambda x: x)
-        for count, cols3, kind in ((send_splits[me], own, "send"), (m, (rk, rt, rv), "recv")):
-            if not count:
-                continue
-            if count > self.eng.cfg.max_batch:
-                raise ValueError(f"received {count} records, above the engine's max_batch {self.eng.cfg.max_batch}: "
-                                 "size max_batch for the most skewed key-group range")
-            a, b, c = cols3
-            self.eng.push(a, b, as_value(c), keep_alive=False)   # both pushes lie between the same watermarks
-            if kind == "send":
-                self.send_pushed_at[si] = self.pushes
-            else:
-                self.pushed_at[slot] = self.pushes
-            self.pushes += 1
+        # both shares lie between the same watermarks; a share above max_batch (skew) goes in pieces
+        if send_splits[me]:
+            self.send_pushed_at[si] = self._push_share(own, send_splits[me])
+        if m:
+            self.pushed_at[slot] = self._push_share((rk, rt, rv), m)
         self._forward(aligned)

@@ -5,7 +5,10 @@ all-to-all, record all-to-all), aligns the watermark with a MIN all-reduce, and 
 subtask (key-group range of its operator index).  The union of both subtasks' fired results must
 equal one subtask over the whole stream (order-independent fields: int64 sum/count, bit-exact).
 The window subtasks here are oracle engines (no GPU); on GPUs the same class drives the HIP engine
-and the HIP partition kernel over RCCL.
+and the HIP partition kernel over RCCL.  `pipelined` runs the GPUs' own step()/_finish() code (the
+depth-2 software pipeline, count all-to-all and MIN all-reduce in one meta tensor, the receive ring) on
+CPU tensors; the Zipf(1.2) case makes one rank receive several times its engine's max_batch, which the
+exchange pushes in pieces (the hot keys' key groups meet on one operator at p = 8).
 """
 import os
 import socket
@@ -39,14 +42,19 @@ def _local_wm(j, r, t_part):
     return wm
 
 
-def expected_forwarded(world, steps, batch):
+def _stream(j, world, zipf):
+    from flink_amd.synth import stream
+    return stream(j * BATCH * world, BATCH * world, 3000, 1 << 13, zipf=zipf)
+
+
+def expected_forwarded(world, steps, batch, zipf=None):
     """StreamInputProcessor.java:147-161 over the world's source channels, one forward per step at most."""
     from flink_amd.keyby import ChannelWatermarks
     from flink_amd.synth import stream
     valve = ChannelWatermarks(world)
     out = []
     for j in range(steps):
-        _, t, _ = stream(j * batch * world, batch * world, 3000, 1 << 13)
+        _, t, _ = stream(j * batch * world, batch * world, 3000, 1 << 13, zipf=zipf)
         fwd = None
         for r in range(world):
             x = valve.on_watermark(r, _local_wm(j, r, t[r::world]))
@@ -58,7 +66,7 @@ def expected_forwarded(world, steps, batch):
 STEPS, BATCH = 12, 4096
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, pipelined=False, zipf=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -74,39 +82,47 @@ def _worker(rank, world, port, q):
 
     cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "count")), max_parallelism=128,
                       key_group_range=compute_key_group_range_for_operator_index(128, world, rank),
-                      key_capacity=4096, max_batch=1 << 14, out_capacity=1 << 18)
+                      key_capacity=4096, max_batch=BATCH if zipf else 1 << 14, out_capacity=1 << 18)
     eng = OracleEngine(cfg)
-    ex = KeyByExchange(eng, world, rank, 128, 1 << 13, "cpu")
+    ex = KeyByExchange(eng, world, rank, 128, 1 << 13, "cpu", pipelined=pipelined)
     results = []
     for j in range(STEPS):
-        k, t, v = stream(j * BATCH * world, BATCH * world, 3000, 1 << 13)
+        k, t, v = _stream(j, world, zipf)
         k, t, v = k[rank::world].contiguous(), t[rank::world].contiguous(), v[rank::world].contiguous()
         ex.step(k, t, v, _local_wm(j, rank, t))
         results.append(eng.collect())
+    ex.flush()
+    results.append(eng.collect())
     eng.advance_watermark(LONG_MAX)
     results.append(eng.collect())
-    q.put((rank, epochs_of(results, ["sum_i64", "count"]), ex.emitted))
+    pushes = ex.pushes if pipelined else None
+    q.put((rank, epochs_of(results, ["sum_i64", "count"]), ex.emitted, pushes))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])   # 8: the ranks of one MI355X node
-def test_keyby_exchange_two_ranks(world):
+@pytest.mark.parametrize("world,pipelined,zipf", [
+    (2, False, None), (3, False, None), (8, False, None),   # 8: the ranks of one MI355X node
+    (2, True, None), (8, True, None),                      # the GPU path's pipelined step() / _finish()
+    (8, True, 1.2)])                                       # skew: shares above max_batch pushed in pieces
+def test_keyby_exchange_two_ranks(world, pipelined, zipf):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined, zipf)) for r in range(world)]
     for p in procs:
         p.start()
-    got, emitted = {}, {}
+    got, emitted, pushes = {}, {}, {}
     for _ in range(world):
-        rank, ep, em = q.get(timeout=240)
-        got[rank], emitted[rank] = ep, em
+        rank, ep, em, pu = q.get(timeout=240)
+        got[rank], emitted[rank], pushes[rank] = ep, em, pu
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    exp = expected_forwarded(world, STEPS, BATCH)
+    exp = expected_forwarded(world, STEPS, BATCH, zipf)
     if world == 2:
         assert any(e is None for e in exp), "the stream must exercise non-increasing aligned watermarks"
+    if zipf:   # some rank received more than max_batch = BATCH per step: more pushes than 2 per step
+        assert max(pushes.values()) > 2 * STEPS
     forwarded = [e for e in exp if e is not None]
     # every window subtask forwards exactly the valve's watermarks (positions included)
     for r in range(world):
@@ -126,7 +142,7 @@ def test_keyby_exchange_two_ranks(world):
     e = OracleEngine(cfg)
     res = []
     for j in range(STEPS):
-        k, t, v = stream(j * BATCH * world, BATCH * world, 3000, 1 << 13)
+        k, t, v = _stream(j, world, zipf)
         e.push(k.numpy(), t.numpy(), v.numpy())
         if exp[j] is not None:
             e.advance_watermark(exp[j])
