@@ -57,6 +57,11 @@ CONFIGS = {
     "c4": dict(keys=1 << 16, rate=1 << 25, batch=1 << 22, key_cap=1 << 16, window=("tumbling", 1000),
                reduce=(("sum", "count"), "i64"), zipf=1.2, ooo=300, wm_lag=50, lateness=100, pane_bytes=96,
                desc="Zipf(1.2) keys, ts up to 300 ms out of order, watermark lag 50 ms, allowed lateness 100 ms"),
+    # BASELINE configs[4]: the keyBy shuffle over N GPUs, maxParallelism 128, 100 M uniform keys; each rank's
+    # engine holds its key-group range's share of the keys (KeyGroupRangeAssignment.java:78-89)
+    "c5": dict(keys=100_000_000, rate=1 << 27, batch=1 << 22, key_cap=None, window=("tumbling", 1000),
+               reduce=(("sum",), "i64"), zipf=None, ooo=0, wm_lag=1, lateness=0, pane_bytes=96,
+               desc="keyBy shuffle (maxParallelism 128) over 100M uniform keys, tumbling 1s long-sum, f1 = first arrival"),
 }
 
 
@@ -159,6 +164,8 @@ def main():
     from flink_amd.keygroups import compute_key_group_range_for_operator_index
     mp = 128
     kg = compute_key_group_range_for_operator_index(mp, world, rank)
+    if key_cap is None:   # this rank's key groups' share of the key space, with a margin for the hash spread
+        key_cap = int(n_keys * (kg[1] - kg[0] + 1) / mp * 1.05) + 4096
     reduce_fn = ReduceFunction(fields, vt, keep_first_f1=True)
     if C["window"][0] == "tumbling":
         assigner = TumblingEventTimeWindows.of(C["window"][1])
@@ -167,12 +174,13 @@ def main():
         assigner = SlidingEventTimeWindows.of(C["window"][1], C["window"][2])
         windows_per_record = C["window"][1] // C["window"][2]
     windows_in_run = (total_steps * batch * world) // rate + 2
-    out_cap = windows_in_run * windows_per_record * key_cap // max(world, 1) * 2 + 4096
+    per_window = min(key_cap, rate // max(world, 1) * (C["window"][1] // 1000 or 1))   # panes of a rank per window
+    out_cap = windows_in_run * windows_per_record * per_window * 2 + 4096
     if C["lateness"]:
         out_cap += total_steps * batch // 4
     cfg = make_config(assigner, reduce_fn, allowed_lateness=C["lateness"], max_parallelism=mp, key_group_range=kg,
                       device=local, key_capacity=key_cap, max_batch=batch * (2 if world > 1 or args.force_exchange else 1),
-                      out_capacity=int(min(out_cap, 1 << 27)), ingest_mode=args.ingest_mode)
+                      out_capacity=int(min(out_cap, 1 << 29)), ingest_mode=args.ingest_mode)
     eng = WindowEngine(cfg)
 
     # resident synthetic input: rank r is source subtask r; its i-th event is global index i*world + r

@@ -2791,8 +2791,11 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
 template <int VT, int AGG, bool FIRST>
 static void launch_fused_t(fw_engine* e, const BatchIn& b, const int64_t* f1col) {
   static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_fused<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (!attr_set) {   // all of LDS less the kernel's static part (none expected)
+    hipFuncAttributes fa{};
+    const size_t stat = hipFuncGetAttributes(&fa, (const void*)k_fused<VT, AGG, FIRST>) == hipSuccess ? fa.sharedSizeBytes : 0;
+    (void)hipFuncSetAttribute((const void*)k_fused<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(160 * 1024 - stat));
     attr_set = true;
   }
   FusedBuf f = e->fb;
@@ -3287,14 +3290,16 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   // stream; buffer set par is reused only after k_aggregate of batch j - NBUF finished
   const int par = (int)(e->batches % fw_engine::NBUF);
   const int half = (int)(e->batches & 1);   // the direct form's new-pane list counters alternate
-  hipStream_t in_stream = e->routed && !e->serial ? e->rstream : e->stream;
+  // host columns are copied on the route stream (a copy queue beside the engine stream's kernels)
+  hipStream_t in_stream = (e->routed || mem == FW_MEM_HOST) && !e->serial ? e->rstream : e->stream;
   // a wait whose event has already completed is skipped: each one costs the command processor a barrier
   // packet on the stream (FW_EVENT_QUERY=0 enqueues them all, for A/B)
   auto wait_on = [&](hipStream_t st, hipEvent_t ev) -> hipError_t {
     if (e->event_query && hipEventQuery(ev) == hipSuccess) return hipSuccess;
     return hipStreamWaitEvent(st, ev, 0);
   };
-  if (e->routed) HIPCHK(e, wait_on(in_stream, e->ev_agg[par]));
+  // buffer set par (routed buffers, host staging) is rewritten only after the push that used it NBUF pushes ago
+  if (e->routed || mem == FW_MEM_HOST) HIPCHK(e, wait_on(in_stream, e->ev_agg[par]));
   // input columns are produced on the caller's stream: order the push after it (nothing to order when that
   // stream has no work pending)
   if (e->has_client && !(e->event_query && hipStreamQuery((hipStream_t)e->client) == hipSuccess)) {
@@ -3310,6 +3315,12 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     dk = e->stg_key[par]; dts = e->stg_ts[par]; dv = e->stg_val[par];
     if (key_hash) { HIPCHK(e, hipMemcpyAsync(e->stg_hash[par], key_hash, 4 * n, hipMemcpyHostToDevice, in_stream)); dh = e->stg_hash[par]; }
     if (f1) { HIPCHK(e, hipMemcpyAsync(e->stg_f1[par], f1, 8 * n, hipMemcpyHostToDevice, in_stream)); df1 = e->stg_f1[par]; }
+    // the caller may reuse its arrays once fw_push_batch returns (flink_window.h): wait for the copies here
+    // (pinned host memory would otherwise still be read by the DMA engine afterwards); the earlier batches'
+    // kernels keep running on the engine stream meanwhile
+    HIPCHK(e, hipEventRecord(e->ev_route[par], in_stream));
+    HIPCHK(e, hipEventSynchronize(e->ev_route[par]));
+    if (in_stream != e->stream && !e->routed) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_route[par], 0));
   }
   if ((e->routed || e->fused) && mem == FW_MEM_DEVICE) {
     // k_route / k_fused stream the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
@@ -3356,7 +3367,6 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (e->s.W > 0)   // sliding: this batch's extra-window records into the window panes
     hipLaunchKernelGGL(k_quirk_apply, dim3(1), dim3(1024), 0, e->stream, e->s, e->quirk_list[par], e->quirk_count + par,
                        e->cfg.max_batch);
-  if (e->routed) HIPCHK(e, hipEventRecord(e->ev_agg[par], e->stream));
   e->batches++;
   HIPCHK(e, hipGetLastError());
   if (e->s.first && !e->routed && !e->fused) {   // the partitioned form sets f1 in k_aggregate, the fused one in k_fused
@@ -3418,7 +3428,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   }
   HIPCHK(e, hipGetLastError());
   // every reader of this push's columns (k_route, k_aggregate's direct records, the f1 fix-up, the late
-  // path) is ordered before this point of the engine stream
+  // path) is ordered before this point of the engine stream: buffer set par (routed buffers, host staging)
+  // may be rewritten after it
+  HIPCHK(e, hipEventRecord(e->ev_agg[par], e->stream));
   if (e->track_consumed && !e->no_consumed) {
     HIPCHK(e, hipEventRecord(e->ev_consumed[e->pushes % fw_engine::NCONS], e->stream));
     e->cons_push[e->pushes % fw_engine::NCONS] = e->pushes;

@@ -468,7 +468,12 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
       }
     }
     // the primary slice's pane slot: claimed (idempotently) once some slot of this share was touched
-    if (__syncthreads_or(touched)) {   // uniform
+    // (a block-wide OR through LDS: all of this kernel's LDS stays dynamic)
+    if (tid == 0) misc[4] = 0;
+    __syncthreads();
+    if (__any(touched) && lane == 0) misc[4] = 1;
+    __syncthreads();
+    if (misc[4]) {   // uniform
       if (tid == 0) misc[2] = slice_slot(s, m0);
       __syncthreads();
       const int32_t p0 = misc[2];

@@ -138,7 +138,9 @@ typedef struct {
   int64_t key_capacity;      /* distinct keys over the engine lifetime                          */
   int64_t max_batch;         /* max records per fw_push_batch                                   */
   int64_t out_capacity;      /* max fired records between two fw_collect calls                  */
-  int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate     */
+  int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate,    */
+                             /* 3 = fused (one launch per batch, XCD-local hand-off; reduce /  */
+                             /*     fold without allowed lateness, key_capacity <= 64 Ki)     */
   int32_t agg_flags;         /* OR of FW_AGGF_*                                                 */
   int64_t fold_initial;      /* FW_AGGF_FOLD: the fold's initial accumulator                    */
   int64_t list_capacity;     /* FW_AGG_LIST: elements buffered per pane slice (0 = 4 x max_batch) */
@@ -174,13 +176,17 @@ typedef struct {
   int64_t late_fires;        /* per-element fires (allowed lateness > 0)      */
   int64_t keys_resident;     /* distinct keys in the key directory            */
   int64_t slices_live;       /* pane slices resident                          */
-  int64_t ingest_form;       /* 1 = direct atomics, 2 = partitioned + LDS     */
+  int64_t ingest_form;       /* 1 = direct atomics, 2 = partitioned + LDS, 3 = fused */
   int64_t compactions;       /* key-directory compactions (dead keys evicted) */
 } fw_stats;
 
 int         fw_create(const fw_config* cfg, fw_engine** out);
 /* key: record keys (int64).  key_hash: optional Java key.hashCode() per record (NULL = Long.hashCode(key)).
- * f1: optional pass-through field (NULL = ts).  ts: event timestamps.  value: int64 or double per value_type. */
+ * f1: optional pass-through field (NULL = ts).  ts: event timestamps.  value: int64 or double per value_type.
+ * mem = FW_MEM_HOST: the call returns once the columns have been copied to the device, so the caller may
+ * reuse or release its arrays right away (pageable or pinned alike; e.g. ReleasePrimitiveArrayCritical).
+ * mem = FW_MEM_DEVICE: the columns are read asynchronously, after the work enqueued so far on the stream set
+ * with fw_set_stream; keep them unchanged until fw_stream_wait_input / fw_sync / fw_collect says they are read. */
 int         fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,
                           const int64_t* ts, const void* value, int64_t n, int32_t mem);
 int         fw_advance_watermark(fw_engine* e, int64_t wm);

@@ -378,3 +378,39 @@ def test_partition_by_operator_matches_key_group_routing(hip):
     assert np.array_equal(ot.cpu().numpy(), ts[order])
     assert np.array_equal(counts.cpu().numpy(), np.bincount(dest, minlength=8))
     e.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
+def test_host_buffers_reusable_after_push(hip, oracle_engine, mode, pinned):
+    """fw_push_batch(FW_MEM_HOST) returns once the columns are on the device (flink_window.h): the caller
+    overwrites its arrays right after each push (as a JNI caller releasing its critical arrays would) and the
+    results still equal the oracle's on the true stream."""
+    import torch
+    from flink_amd.windowing import TumblingEventTimeWindows
+    keys, ts, vals = gen_stream(200_000, 3000, rate=1 << 15)
+    batch = 1 << 14
+    cfg = _cfgm(mode, TumblingEventTimeWindows.of(1000), ("sum", "count"), first=True)
+    eg = hip(cfg)
+    bufs = [torch.empty(batch, dtype=torch.int64) for _ in range(3)]
+    if pinned:
+        bufs = [b.pin_memory() for b in bufs]
+    out, max_ts = [], -(1 << 63)
+    for s in range(0, len(keys), batch):
+        e = min(len(keys), s + batch)
+        m = e - s
+        for b, src in zip(bufs, (keys, ts, vals)):
+            b[:m].copy_(torch.from_numpy(src[s:e]))
+        eg.push(bufs[0][:m], bufs[1][:m], bufs[2][:m])
+        for b in bufs:
+            b.fill_(-7)   # the caller's arrays reused at once
+        max_ts = max(max_ts, int(ts[s:e].max()))
+        eg.advance_watermark(max_ts - 1)
+        out.append(eg.collect())
+    eg.advance_watermark(LONG_MAX)
+    out.append(eg.collect())
+    eg.close()
+    eo = oracle_engine(cfg)
+    ro = drive(eo, keys, ts, vals, batch, 1, LONG_MAX)
+    eo.close()
+    _compare(epochs_of(out, ["sum_i64", "count"], True), epochs_of(ro, ["sum_i64", "count"], True), None)
