@@ -3001,8 +3001,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
 
   // fused ingest (ingest_mode 3, fw_fused.hip): reduce / fold of tumbling or sliding windows without allowed
   // lateness, on a device that holds the whole grid resident (one workgroup per CU), with an owner's range of
-  // the directory (D / 32 slots, D = 2 x key capacity) and its accumulators in LDS.  Auto mode takes it for
-  // batches of >= 64 Ki records (FW_FUSED=0: never)
+  // the directory (D / 32 slots, D = 2 x key capacity) and its accumulators in LDS.  Only on request
+  // (ingest_mode 3, or FW_FUSED=1 in auto mode): measured at 23 G events/s against the partitioned form's
+  // 56 G on C1 (round-serial phases, tools/fused_stamps.py)
   const int nacc_f = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
   const int64_t d_fused = next_pow2(std::max<int64_t>(2 * c.key_capacity, 2048));
   const int so_bits_f = bits_for((uint64_t)d_fused) - 1 - 5;
@@ -3013,7 +3014,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (c.ingest_mode == 3 && !ok)
       return unsupported("fused ingest (ingest_mode 3): tumbling or sliding reduce / fold without allowed lateness, "
                          "key_capacity <= 64 Ki (sum) / 32 Ki (sum, min, max, count), on a 256-CU device");
-    e->fused = ok && (c.ingest_mode == 3 || (c.ingest_mode == 0 && !(fv && atoi(fv) == 0) && c.max_batch >= (1 << 16)));
+    e->fused = ok && (c.ingest_mode == 3 || (c.ingest_mode == 0 && fv && atoi(fv) != 0 && c.max_batch >= (1 << 16)));
   }
   // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys, and for the fused form): short linear-probe
   // sequences
@@ -3166,6 +3167,10 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     f.pfirst = e->alloc<uint32_t>(np);
     const char* fs = getenv("FW_FUSED_SAFE");
     f.force_safe = fs && atoi(fs) != 0 ? 1 : 0;
+    const char* dbg = getenv("FW_DEBUG_AGG");
+    e->rb.dbg = dbg ? atoi(dbg) : 0;
+    e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
+    f.stamps = e->rb.stamps;
     // at least 81 KiB: one workgroup per CU, so the 256 of a launch are resident together on 256 CUs
     e->fused_lds = std::max<size_t>(fused_lds_bytes(so_bits_f, nacc_f), 81 * 1024);
   }

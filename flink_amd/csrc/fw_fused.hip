@@ -67,7 +67,11 @@ struct FusedBuf {
   int32_t so_bits;              // log2(SO)
   int32_t owner_shift;          // log2(D) - 5: (fmix64(key) & dir_mask) >> owner_shift = owning member
   int32_t force_safe;           // diagnostics (FW_FUSED_SAFE=1): the release/acquire hand-off for every group
+  long long* stamps;            // diagnostics (FW_DEBUG_AGG & 16): per-workgroup realtime stamps, 64 per workgroup
 };
+// stamp i of this workgroup: 0 start, 1 placement known, 2 + 4k + {0 produced, 1 published, 2 round k - 1 arrived,
+// 3 consumed}, 60 partials published, 61 fold range ready, 62 end; 63 = xcc | one_l2 << 8
+#define FU_STAMP(i) do { if (f.stamps && tid == 0 && (i) < 63) f.stamps[(int64_t)w * 64 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 // LDS bytes of k_fused: staging of one chunk, bin counts, the owner's directory copy and accumulators
 __host__ __device__ constexpr size_t fused_lds_bytes(int so_bits, int nacc) {
@@ -129,6 +133,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
     const int64_t tm = b.ts[n >> 1];
     if (tm != INT64_MIN) m0 = uniform64(record_windows(s, tm, b.wm).m);
   }
+  FU_STAMP(0);
   // registration: this workgroup's XCD, published write-through, then counted
   const int my_xcc = fu_xcc_id();
   if (tid == 0) {
@@ -182,6 +187,8 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
   }
   __syncthreads();
   const bool one_l2 = misc[0] != 0;
+  FU_STAMP(1);
+  if (f.stamps && tid == 0) f.stamps[(int64_t)w * 64 + 63] = my_xcc | (one_l2 ? 256 : 0);
   const bool all_kg = s.kg_start == 0 && s.kg_end == s.mp - 1;
   const uint32_t kbm = (1u << s.kb_bits) - 1u;
   unsigned long long late_pairs = 0;
@@ -317,6 +324,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
           st_idx[pos] = (uint16_t)(2 * tid + e);
         }
       }
+      FU_STAMP(2 + 4 * k);
       // the ring slot is free once every owner of the group read its previous use
       const int sl = k % FU_S;
       if (tid == 0) (void)fu_wait(s, f.ctr, FU_C_DONE + g * FU_S + sl, (f.uses[sl] + (unsigned long long)(k / FU_S)) * FU_MEMBERS, broken);
@@ -339,6 +347,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
         }
         __hip_atomic_fetch_add(f.ctr + FU_C_PROD + g * FU_S + sl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      FU_STAMP(3 + 4 * k);
     }
     if (k >= 1) {
       // ---------------- consume round kc = k - 1 ----------------
@@ -351,6 +360,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
+      FU_STAMP(4 + 4 * kc);
       // 32 threads per producer: its segment for this owner, 16-B L1-bypassing loads from the XCD's L2
       const int p = tid >> 5, u = tid & 31;
       const int wp = p * FU_GROUPS + g;
@@ -401,6 +411,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
         if (two) add(r1, i1);
       }
       __syncthreads();
+      FU_STAMP(5 + 4 * kc);
       if (tid == 0) __hip_atomic_fetch_add(f.ctr + FU_C_DONE + g * FU_S + sl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -427,11 +438,13 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  FU_STAMP(60);
   if (tid == 0) {
     __hip_atomic_fetch_add(f.ctr + FU_C_FOLD + me, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     (void)fu_wait(s, f.ctr, FU_C_FOLD + me, (ep + 1) * FU_GROUPS, broken);
   }
   __syncthreads();
+  FU_STAMP(61);
 
   // ---------------- fold: slots [g SH, (g+1) SH) of range me over the 8 groups' partials ----------------
   const int SH = SO / FU_GROUPS;
@@ -523,6 +536,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
       if (tid == 0) __hip_atomic_store(b.new_count, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  FU_STAMP(62);
 }
 
 }  // namespace fw

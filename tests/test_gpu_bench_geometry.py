@@ -8,6 +8,8 @@ sum / count), per watermark epoch (TestHarnessUtil contract, SJT/util/TestHarnes
       order, watermark lag 50 ms, allowed lateness 100 ms: per-element late fires and late drops
   C2  10 M key capacity (the direct ingest form: a directory bucket does not fit LDS), 16 Mi events
       over 10 M keys in batches of 2^22, one window purged and its slot reused
+  C3  64 Ki keys, 2^22-event batches, sliding 10 s / 1 s doubles (sum/min/max/count) over 12 s of event
+      time, checked against the oracle sharded by key-group range over 16 threads
 
 The streams are the bench's synthetic generator (flink_amd.synth), made on the GPU and copied to the
 oracle.  Sizes are the bench's; the oracle needs tens of seconds for the largest (C2).
@@ -85,18 +87,18 @@ def test_c1_bench_geometry():
     cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", keep_first_f1=True),
                       max_parallelism=128, key_capacity=1 << 16, max_batch=batch, out_capacity=1 << 20)
     sg, so = _run(cfg, 5, batch, 1 << 16, 1 << 24, 1)
-    assert sg["ingest_form"] == 3   # the fused form the bench runs
+    assert sg["ingest_form"] == 2   # the partitioned form the bench runs
     assert sg["panes_fired"] == so["panes_fired"] > 0
 
 
-def test_c1_bench_geometry_partitioned():
-    """The same C1 stream through the two-kernel partitioned form (ingest_mode 2)."""
+def test_c1_bench_geometry_fused():
+    """The same C1 stream through the fused form (ingest_mode 3)."""
     from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, make_config
     batch = 1 << 22
     cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", keep_first_f1=True),
-                      max_parallelism=128, key_capacity=1 << 16, max_batch=batch, out_capacity=1 << 20, ingest_mode=2)
+                      max_parallelism=128, key_capacity=1 << 16, max_batch=batch, out_capacity=1 << 20, ingest_mode=3)
     sg, so = _run(cfg, 5, batch, 1 << 16, 1 << 24, 1)
-    assert sg["ingest_form"] == 2
+    assert sg["ingest_form"] == 3
     assert sg["panes_fired"] == so["panes_fired"] > 0
 
 
@@ -110,6 +112,132 @@ def test_c4_zipf_lateness_bench_geometry():
     assert sg["ingest_form"] == 2
     assert so["late_fires"] > 0 and sg["late_fires"] == so["late_fires"]
     assert sg["records_late"] == so["records_late"] > 0
+
+
+class _ShardedOracle:
+    """The oracle as `p` subtasks of one key space (KeyGroupRangeAssignment.java:78-89): each shard holds a
+    key-group range and runs in its own thread (ctypes drops the GIL), so a bench-sized sliding stream
+    (10 panes per record in the reference) checks in seconds.  Keyed state is per key, so the union of
+    the shards' fired records per watermark is the single operator's output."""
+
+    def __init__(self, cfg, p=8):
+        import copy
+        from oracle.oracle import OracleEngine, key_group_range
+        self.mp, self.p = cfg.max_parallelism, p
+        self.engs = []
+        for i in range(p):
+            c = copy.copy(cfg)
+            c.kg_start, c.kg_end = key_group_range(self.mp, p, i)
+            self.engs.append(OracleEngine(c))
+
+    def _each(self, fn):
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(self.p) as ex:
+            return list(ex.map(fn, range(self.p)))
+
+    def push(self, k, t, v):
+        from flink_amd.keygroups import operator_index_np
+        op = operator_index_np(k, self.mp, self.p)
+        order = np.argsort(op, kind="stable")   # arrival order within a shard
+        bounds = np.searchsorted(op[order], np.arange(self.p + 1))
+        parts = [order[bounds[i]:bounds[i + 1]] for i in range(self.p)]
+        self._each(lambda i: self.engs[i].push(k[parts[i]], t[parts[i]], v[parts[i]]) if len(parts[i]) else None)
+
+    def advance_watermark(self, wm):
+        self._each(lambda i: self.engs[i].advance_watermark(wm))
+
+    def collect(self):
+        """One result dict: per watermark mark, the shards' records of that mark concatenated."""
+        outs = self._each(lambda i: self.engs[i].collect())
+        names = [n for n in outs[0] if n not in ("n", "mark_wm", "mark_pos") and outs[0][n] is not None]
+        marks = [int(w) for w in outs[0]["mark_wm"]]
+        assert all([int(w) for w in o["mark_wm"]] == marks for o in outs)
+        cols = {n: [] for n in names}
+        mark_pos, pos = [], 0
+        for m in range(len(marks) + 1):
+            for o in outs:
+                lo = 0 if m == 0 else int(o["mark_pos"][m - 1])
+                hi = int(o["mark_pos"][m]) if m < len(marks) else o["n"]
+                for n in names:
+                    cols[n].append(o[n][lo:hi])
+                pos += hi - lo
+            if m < len(marks):
+                mark_pos.append(pos)
+        res = {n: np.concatenate(cols[n]) for n in names}
+        res.update(n=pos, mark_wm=np.array(marks, np.int64), mark_pos=np.array(mark_pos, np.int64))
+        return res
+
+    def stats(self):
+        st = [e.stats() for e in self.engs]
+        return {k: sum(s[k] for s in st) for k in st[0]}
+
+    def close(self):
+        for e in self.engs:
+            e.close()
+
+
+def test_c3_sliding_doubles_bench_geometry():
+    """C3 at the bench's geometry: 64 Ki keys, 2^22-event batches, sliding 10 s / 1 s windows
+    (SlidingEventTimeWindows.java:64-77), double sum / min / max / count, f1 = first arrival.  The event
+    rate is R = 2^22 per second (the bench's is 2^24) so that 12 batches span 12 s of event time and the
+    last windows fire over all 10 of their slices while the oracle (10 panes per record) stays within a
+    minute; every batch still falls in one slice, as the bench's do.
+    Bar: key, window, f1, count, min and max bit-exact; sums within relative 1e-9 (the engine adds a
+    window's slices, the reference adds each record into each of its 10 panes: a different association)."""
+    from flink_amd.windowing import ReduceFunction, SlidingEventTimeWindows, WindowEngine, make_config
+    batch, n_keys, rate = 1 << 22, 1 << 16, 1 << 22
+    cfg = make_config(SlidingEventTimeWindows.of(10_000, 1000),
+                      ReduceFunction(("sum", "min", "max", "count"), "f64", keep_first_f1=True),
+                      max_parallelism=128, key_capacity=n_keys, max_batch=batch, out_capacity=1 << 22)
+    eg, eo = WindowEngine(cfg), _ShardedOracle(cfg, p=16)
+    full_windows = 0
+    max_ts = -(1 << 63)
+
+    def epochs(res):
+        """Per watermark mark: the fired records sorted by (key, window) as an int64 block (key, ts, f1,
+        count, min / max bits) and the double sums."""
+        out, pos = [], 0
+        for wm, mp in list(zip(res["mark_wm"], res["mark_pos"])) + [(None, res["n"])]:
+            sl = slice(pos, int(mp))
+            pos = int(mp)
+            if wm is None and sl.stop == sl.start:
+                continue
+            ints = np.stack([res["key"][sl], res["ts"][sl], res["f1"][sl], res["count"][sl],
+                             res["min_f64"][sl].view(np.int64), res["max_f64"][sl].view(np.int64)], axis=1)
+            order = np.lexsort((ints[:, 1], ints[:, 0]))
+            out.append((None if wm is None else int(wm), ints[order], res["sum_f64"][sl][order]))
+        return out
+
+    def check(rg, ro):
+        nonlocal full_windows
+        a, b = epochs(rg), epochs(ro)
+        assert [w for w, _, _ in a] == [w for w, _, _ in b]
+        for (w, x, xs), (_, y, ys) in zip(a, b):
+            assert x.shape == y.shape, f"wm {w}: {x.shape[0]} vs {y.shape[0]} records"
+            assert np.array_equal(x[:, :3], y[:, :3]), f"wm {w}: keys / windows / f1 differ"
+            assert np.array_equal(x[:, 3:], y[:, 3:]), f"wm {w}: count / min / max differ"
+            assert np.allclose(xs, ys, rtol=1e-9, atol=0), f"wm {w}: sums beyond relative 1e-9"
+            full_windows += int((x[:, 1] >= T0 + 10_000 - 1).sum())   # windows starting at or after T0
+
+    for j in range(12):
+        k, t, v = _stream(j, batch, n_keys, rate, vt="f64")
+        max_ts = max(max_ts, int(t.max().item()))
+        wm = max_ts - 1
+        eg.push(k, t, v)
+        eg.advance_watermark(wm)
+        rg = eg.collect()
+        eo.push(k.cpu().numpy(), t.cpu().numpy(), v.cpu().numpy())
+        eo.advance_watermark(wm)
+        check(rg, eo.collect())
+    eg.advance_watermark(LONG_MAX)
+    eo.advance_watermark(LONG_MAX)
+    check(eg.collect(), eo.collect())
+    sg, so = eg.stats(), eo.stats()
+    eg.close()
+    eo.close()
+    assert sg["ingest_form"] == 2   # the partitioned form the bench runs
+    assert sg["panes_fired"] == so["panes_fired"] > 0
+    assert full_windows >= n_keys   # at least one window per key fired over 10 live slices
 
 
 def test_c2_ten_million_keys():
