@@ -373,9 +373,9 @@ __device__ __forceinline__ int32_t record_key_group(const Spec& s, int32_t key_h
 // ------------------------------------------------------------------------------------------------
 // ingest, direct form: every (record, slice) update is a device-scope atomic on the dense columns.
 // ------------------------------------------------------------------------------------------------
-template <int VT, int AGG, bool FIRST>
+template <int VT, int AGG, bool FIRST, bool COLS_ONLY = false>
 // returns true for exactly one record of a pane absent before the launch (FIRST: the min-ordinal
-// atomic that found the pane empty)
+// atomic that found the pane empty).  COLS_ONLY: the reduce columns only (no first-arrival / presence)
 __device__ __forceinline__ bool pane_update(const Spec& s, int64_t idx, int64_t vbits, int64_t ord) {
   if (AGG & FW_AGG_SUM) {
     if (VT == FW_VALUE_I64) {
@@ -392,6 +392,7 @@ __device__ __forceinline__ bool pane_update(const Spec& s, int64_t idx, int64_t 
     atomicMax((long long*)&s.c.mx[idx], (long long)max_code(VT, s.cmpto, vbits));
   }
   if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&s.c.cnt[idx], 1ull);
+  if (COLS_ONLY) return false;
   if (FIRST) {
     // first arrival = min ordinal; values only decrease within a kernel, so a stale load that is
     // already below our ordinal proves we are not first
@@ -543,34 +544,42 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
       late_append(s, b, p, kid, w.m, i);
       live = false;
     }
-    bool fresh = false;
     int64_t idx = 0;
     if (live) {
       idx = (int64_t)p * s.stride + kid;
-      fresh = pane_update<VT, AGG, FIRST>(s, idx, v, b.ord_base + i);
-    }
-    if (FIRST) {   // list the panes this batch created: their f1 is taken from the batch after the launch
-      const unsigned long long pos = wave_append(b.new_count, fresh);
-      if (fresh) {
-        if ((int64_t)pos < b.new_capacity) b.new_list[pos] = idx;
-        else cap_error(s, 5);
+      if (FIRST) {
+        (void)pane_update<VT, AGG, false, true>(s, idx, v, 0);   // the reduce columns
+        // first arrival = min ordinal (values only decrease within a kernel, so a stale load already below
+        // this record's ordinal proves it is not first).  The record that creates the pane stores its f1 at
+        // once; a record that lowers an existing ordinal is listed by record index (the slot list[i], no
+        // shared counter) and k_fix_first_f1 stores the f1 of the pane's final first arrival after the launch
+        const int64_t ord = b.ord_base + i;
+        int64_t fi = -1;
+        if (ord < s.c.first[idx]) {
+          const int64_t old = (int64_t)atomicMin((long long*)&s.c.first[idx], (long long)ord);
+          if (old == INT64_MAX) s.c.f1v[idx] = b.f1 ? b.f1[i] : ts;
+          else if (old > ord) fi = idx;
+        }
+        b.new_list[i] = fi;
+      } else {
+        (void)pane_update<VT, AGG, false>(s, idx, v, b.ord_base + i);
       }
+    } else if (FIRST && valid) {
+      b.new_list[i] = -1;
     }
   }
 }
 
-// after the direct ingest: f1 of the panes the batch created (listed by k_ingest_direct), from the
-// batch's column; clears the other batch parity's list counter (used next by the following batch)
-__global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* list, const unsigned long long* count,
-                                                       unsigned long long* count_next, const int64_t* f1col,
-                                                       int64_t ord_base, int64_t n, int64_t cap) {
-  const int64_t nl = min((int64_t)*count, cap);
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nl; j += (int64_t)gridDim.x * blockDim.x) {
+// after the direct ingest: the panes whose first-arrival ordinal a record lowered after another record of
+// the batch created them (list[j] = the pane, or -1): the record that is the pane's first arrival now
+// stores its f1 (one writer per pane, ordered after the creator's store by the launch boundary)
+__global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* list, const int64_t* f1col,
+                                                       int64_t ord_base, int64_t n) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t idx = list[j];
-    const int64_t o = s.c.first[idx] - ord_base;
-    if (o >= 0 && o < n) s.c.f1v[idx] = f1col[o];
+    if (idx < 0) continue;
+    if (s.c.first[idx] == ord_base + j) s.c.f1v[idx] = f1col[j];
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *count_next = 0;
 }
 
 // a wave-uniform 64-bit value moved to scalar registers
@@ -3294,7 +3303,6 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   // routed form: the batch's copies and k_route run on the route stream, k_aggregate on the engine
   // stream; buffer set par is reused only after k_aggregate of batch j - NBUF finished
   const int par = (int)(e->batches % fw_engine::NBUF);
-  const int half = (int)(e->batches & 1);   // the direct form's new-pane list counters alternate
   // host columns are copied on the route stream (a copy queue beside the engine stream's kernels)
   hipStream_t in_stream = (e->routed || mem == FW_MEM_HOST) && !e->serial ? e->rstream : e->stream;
   // a wait whose event has already completed is skipped: each one costs the command processor a barrier
@@ -3352,7 +3360,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.quirk_capacity = e->s.W > 0 ? e->cfg.max_batch : 0;
   b.f1 = df1;
   b.new_list = e->new_list;
-  b.new_count = e->new_counts ? e->new_counts + (e->fused ? 0 : half) : nullptr;
+  b.new_count = e->new_counts;   // (the fused form's appended list; the direct form indexes by record)
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
   if (e->session) {
     if (int rc = session_push(e, b)) return rc;
@@ -3377,8 +3385,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (e->s.first && !e->routed && !e->fused) {   // the partitioned form sets f1 in k_aggregate, the fused one in k_fused
     e->phase_begin(FW_PHASE_FIXUP);
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
-                       e->stream, e->s, e->new_list, e->new_counts + half, e->new_counts + (half ^ 1), df1, e->ordinal, n,
-                       e->cfg.max_batch);
+                       e->stream, e->s, e->new_list, df1, e->ordinal, n);
     e->phase_end(n);
   }
   if (e->cfg.allowed_lateness > 0 && !e->session && !e->list && fires_possible(e->s, e->cur_wm)) {
