@@ -2509,8 +2509,17 @@ struct SessDev {
   int64_t* mn;
   int64_t* mx;
   int64_t* cnt;
+  int64_t* f1;      // first-arrival f1 (keep_first_f1) / the extremal record's f1 (maxBy / minBy), or null
   unsigned long long* live;   // [D + 1] slots in flight
   unsigned long long* trig;   // [D + 1] slots whose trigger timer (at maxTimestamp) is pending
+  // list state (FW_AGG_LIST): per slot the window's elements as a linked list through an element pool, a ring
+  // of pcap entries indexed by arrival ordinal (pord = -1: entry free)
+  int32_t list;
+  int64_t* head;
+  int64_t* tail;
+  int64_t* len;
+  int64_t *pv, *pf1, *pnext, *pord;
+  int64_t pcap;
 };
 
 }  // namespace
@@ -2918,13 +2927,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (c.size <= 0) return bad("window size must be > 0");
   if (c.assigner != FW_TUMBLING && c.assigner != FW_SLIDING && c.assigner != FW_SESSION) return bad("unknown assigner");
   e->session = c.assigner == FW_SESSION;
-  if (e->session && (c.keep_first_f1 || (c.agg_mask & (FW_AGG_MAXBY | FW_AGG_MINBY))))
-    return unsupported("session windows: first-arrival f1 and maxBy / minBy follow HashSet order after a merge "
-                       "(sum / min / max / count only)");
   e->list = c.agg_mask == FW_AGG_LIST;
   if ((c.agg_mask & FW_AGG_LIST) && !e->list) return bad("list state (FW_AGG_LIST) is used alone");
-  if (e->list && (e->session || (c.agg_flags & FW_AGGF_FOLD)))
-    return unsupported("list state: tumbling and sliding windows (merging list state follows HashSet order)");
+  if (e->list && (c.agg_flags & FW_AGGF_FOLD)) return unsupported("list state: no fold");
   if (e->list) { c.ingest_mode = 1; c.keep_first_f1 = 1; e->cfg = c; }
   if (e->session) {
     if (c.max_open_slices > SESS_SW_MAX) return bad("session windows: at most 64 in-flight sessions per key (max_open_slices)");
@@ -2946,7 +2951,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if ((c.agg_flags & FW_AGGF_FOLD) && (c.keep_first_f1 || !(c.agg_mask == FW_AGG_SUM || c.agg_mask == FW_AGG_MIN ||
                                                               c.agg_mask == FW_AGG_MAX || c.agg_mask == FW_AGG_COUNT)))
     return unsupported("fold: one aggregate (sum, count, min or max) from the initial value, no first-arrival f1");
-  if (by && c.ingest_mode == 1) return unsupported("maxBy / minBy run on the partitioned ingest form (ingest_mode 0 or 2)");
+  if (by && c.ingest_mode == 1 && !e->session)
+    return unsupported("maxBy / minBy run on the partitioned ingest form (ingest_mode 0 or 2)");
   if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
   if (c.ingest_mode < 0 || c.ingest_mode > 3) return bad("bad ingest mode");
   HIPCHK(e, hipSetDevice(c.device));
@@ -3125,7 +3131,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (c.ingest_mode == 2 && !fits)
       return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
     e->routed = !e->session && !e->fused && (c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by)));
-    if (by && !e->routed) return unsupported("maxBy / minBy need the partitioned ingest form (key_capacity <= 256 Ki)");
+    if (by && !e->routed && !e->session)
+      return unsupported("maxBy / minBy need the partitioned ingest form (key_capacity <= 256 Ki)");
     if (e->routed) {
       e->max_tiles = max_tiles;
       const size_t cap = (size_t)max_tiles * RT_TILE;
@@ -3226,7 +3233,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->session) {
     if (int rc = session_create(e)) { g_create_error = "session window state allocation failed"; delete e; return rc; }
   }
-  if (e->list) {
+  if (e->list && !e->session) {
     if (int rc = list_create(e)) { g_create_error = "list state allocation failed"; delete e; return rc; }
   }
   // initial state

@@ -3,8 +3,8 @@
 // Replaces the merging branch of WindowOperator.processElement (SJ/runtime/operators/windowing/
 // WindowOperator.java:228-301) over MergingWindowSet (MergingWindowSet.java:142-214, TimeWindow.mergeWindows
 // TimeWindow.java:186-230) and its timers (EventTimeTrigger.onMerge :70-74, onEventTime :344-375), for
-// EventTimeSessionWindows.withGap (EventTimeSessionWindows.java:53-56) with a reducing state of
-// sum / min / max / count.
+// EventTimeSessionWindows.withGap (EventTimeSessionWindows.java:53-56) with a reducing state (sum / min / max /
+// count, first-arrival f1, maxBy / minBy) or a list state (WindowedStream.apply: the window's elements).
 //
 // Layout in HBM: per key id (the engine's key directory) `sw` window slots (max_open_slices, default 32),
 // key-major ([D + 1][sw]) so one key's windows share cache lines: window start / end and the accumulator
@@ -21,20 +21,27 @@
 // so keys run in parallel.  Cleanup timers are implicit: every in-flight window has one, at
 // cleanupTime = maxTimestamp + lateness (clamped).
 //
-// Fixed-gap sessions never meet MergingWindowSet's state-window corner (a new window equal to a merged
-// one: merged windows are longer than the gap), so which merged window holds the state does not matter
-// for order-insensitive fields; first-arrival f1, maxBy / minBy and double sums after a merge follow the
-// JDK HashSet iteration order of the merged windows and are not offered (doubles: within the tolerance).
+// A merge follows MergingWindowSet.addWindow exactly: the merged in-flight windows in the iteration order of
+// the JDK HashSet TimeWindow.mergeWindows put them in (bucket of the spread TimeWindow.hashCode in a table
+// of the capacity the adds grew, then insertion order = start order); the state window is the first one's,
+// the others' states are reduced in that order and the result added to it
+// (AbstractKeyedStateBackend.mergePartitionedStates :294-333).  So first-arrival f1, maxBy / minBy (ties by
+// argument order, ComparableAggregator.java:74-81) and double sums come out as the reference's.  List state
+// keeps each window's elements as a linked list through an element pool (a ring indexed by arrival
+// ordinal, list_capacity entries): a merge concatenates the target's list and the sources' in that order.
+// (Not modelled: HashMap treeification / early resize of a bucket holding 8+ of one group's windows.)
 //
-// A watermark: k_sess_wm, one thread per key: each live window's timers in time order — the trigger timer
-// at maxTimestamp (FIRE; PurgingTrigger: FIRE_AND_PURGE; cleanup when maxTimestamp is also the cleanup
-// time), then the cleanup timer (retire).  Results are appended wave-aggregated.
+// A watermark: k_sess_wm, one thread per key: each live window's timers — the trigger timer at maxTimestamp
+// (FIRE; PurgingTrigger: FIRE_AND_PURGE; cleanup when maxTimestamp is also the cleanup time), then the
+// cleanup timer (retire).  Results are appended wave-aggregated; their order within one watermark's mark is
+// unspecified (the reference's timer queue orders by timestamp, ties between keys in heap order; the
+// operator contract compares a mark's records as a set, TestHarnessUtil.java:80-117).
 
 namespace fw {
 
 __device__ __forceinline__ void sess_emit(const Spec& s, unsigned long long pos, int64_t key, int64_t start, int64_t max_ts,
                                           const LateAcc& a) {
-  emit_record(s, pos, key, 0, max_ts, a);
+  emit_record(s, pos, key, a.f1, max_ts, a);
   if ((int64_t)pos < s.o.capacity) s.o.win_start[pos] = start;
 }
 
@@ -45,6 +52,8 @@ __device__ __forceinline__ LateAcc sess_load(const Spec& s, const SessDev& d, in
   a.mn = d.mn ? d.mn[x] : INT64_MAX;
   a.mx = d.mx ? d.mx[x] : INT64_MIN;
   a.cnt = d.cnt ? d.cnt[x] : 0;
+  a.f1 = d.f1 ? d.f1[x] : 0;
+  a.by = s.by;
   return a;
 }
 __device__ __forceinline__ void sess_store(const SessDev& d, int64_t x, const LateAcc& a) {
@@ -52,6 +61,63 @@ __device__ __forceinline__ void sess_store(const SessDev& d, int64_t x, const La
   if (d.mn) d.mn[x] = a.mn;
   if (d.mx) d.mx[x] = a.mx;
   if (d.cnt) d.cnt[x] = a.cnt;
+  if (d.f1) d.f1[x] = a.f1;
+}
+
+// ReduceFunction.reduce(v1 = a, v2 = b) of the operator's reduce: the aggregates combined, f1 of v1 (the
+// Tuple3.of(a.f0, a.f1, ...) shape); maxBy / minBy the extremal record, a tie to v1 (first) or v2 (last) —
+// by argument order, as ComparableAggregator.reduce decides it (ComparableAggregator.java:74-81)
+__device__ __forceinline__ LateAcc sess_combine(const Spec& s, const LateAcc& a, const LateAcc& b) {
+  if (s.by) {
+    const bool maxby = (s.by & FW_AGG_MAXBY) != 0;
+    const int64_t ca = maxby ? a.mx : a.mn, cb = maxby ? b.mx : b.mn;
+    if (ca == cb) return s.by_last ? b : a;
+    return (maxby ? ca > cb : ca < cb) ? a : b;
+  }
+  LateAcc r = LateCombine()(a, b);
+  r.f1 = a.f1;
+  return r;
+}
+
+// java.util.HashSet<TimeWindow> iteration rank of a window: the bucket of its spread hash (HashMap.hash) in a
+// table of `cap` buckets (TimeWindow.hashCode, TimeWindow.java:79-83)
+__device__ __forceinline__ uint32_t sess_bucket(int64_t start, int64_t end, uint32_t cap) {
+  const int32_t hs = (int32_t)(start ^ (int64_t)((uint64_t)start >> 32));
+  const int32_t he = (int32_t)(end ^ (int64_t)((uint64_t)end >> 32));
+  const uint32_t h = (uint32_t)hs * 31u + (uint32_t)he;
+  return (h ^ (h >> 16)) & (cap - 1u);
+}
+// HashMap capacity after n adds to a default HashSet (16 buckets, load factor 0.75)
+__device__ __forceinline__ uint32_t sess_set_cap(int n) {
+  uint32_t cap = 16;
+  while ((uint32_t)n * 4u > cap * 3u) cap <<= 1;
+  return cap;
+}
+
+// list state: free a window's elements (their pool entries may be reused)
+__device__ __forceinline__ void sess_list_free(const SessDev& d, int64_t x) {
+  for (int64_t e = d.head[x], n = d.len[x]; n > 0 && e >= 0; --n) {
+    const int64_t nx = d.pnext[e];
+    d.pord[e] = -1;
+    e = nx;
+  }
+  d.len[x] = 0;
+}
+// list state: one output row per element of the window, in list order (InternalIterableWindowFunction)
+__device__ __forceinline__ void sess_list_emit(const Spec& s, const SessDev& d, int64_t x, int64_t key, int64_t start,
+                                               int64_t max_ts) {
+  const int64_t n = d.len[x];
+  if (n <= 0) return;
+  unsigned long long pos = atomicAdd(s.o.count, (unsigned long long)n);
+  int64_t e = d.head[x];
+  for (int64_t j = 0; j < n && e >= 0; ++j, ++pos) {
+    LateAcc a;
+    a.vt = s.vt;
+    a.sum = d.pv[e];
+    sess_emit(s, pos, key, start, max_ts, a);
+    if ((int64_t)pos < s.o.capacity && s.o.f1) s.o.f1[pos] = d.pf1[e];
+    e = d.pnext[e];
+  }
 }
 
 // per record: key group check (AbstractKeyedStateBackend.setCurrentKey :167-170), key id, and the sort key
@@ -90,8 +156,14 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   const int64_t* en = d.end + base;
   uint64_t live = d.live[kid], trig = d.trig[kid];
   const uint64_t all = d.sw == 64 ? ~0ull : (1ull << d.sw) - 1;
-  LateCombine op;
   unsigned long long late = 0, fires = 0;
+  // retire a slot: its trigger and cleanup timers gone; list state frees its elements (a reducing state is
+  // overwritten by the slot's next window)
+  auto retire = [&](int q) {
+    live &= ~(1ull << q);
+    trig &= ~(1ull << q);
+    if (d.list) sess_list_free(d, base + q);
+  };
   for (int64_t j = j0; j < n; ++j) {
     const unsigned long long kj = sorted[j];
     if ((kj >> idx_bits) != (unsigned long long)kid) break;
@@ -104,6 +176,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
     a.mn = min_code(s.vt, s.cmpto, v);
     a.mx = max_code(s.vt, s.cmpto, v);
     a.cnt = 1;
+    a.f1 = b.f1 ? b.f1[i] : ts;
+    a.by = s.by;
     // MergingWindowSet.addWindow: the new window's connected group of intersecting in-flight windows
     int64_t cs = ts, ce = jadd(ts, d.gap);
     uint64_t mask = 0;
@@ -124,13 +198,57 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       r = __ffsll((long long)mask) - 1;
       const bool contained = __popcll(mask) == 1 && st[r] == cs && en[r] == ce;   // new window inside an existing one
       if (!contained) {
-        // merge: EventTimeTrigger.onMerge registers the merged window's timer; the merged windows' timers go,
-        // their states fold into one (AbstractKeyedStateBackend.mergePartitionedStates)
-        LateAcc m = sess_load(s, d, base + r);
-        for (uint64_t o = mask & ~(1ull << r); o; o &= o - 1) m = op(m, sess_load(s, d, base + __ffsll((long long)o) - 1));
-        sess_store(d, base + r, m);
-        live &= ~(mask & ~(1ull << r));
-        trig = (trig & ~mask) | (1ull << r);
+        // merge: the group's HashSet holds the merged in-flight windows and the new one (distinct from all of
+        // them here); iterated by (bucket, insertion = start order), the first window's state is the target,
+        // the others' states reduce in that order into one result added to it.  EventTimeTrigger.onMerge
+        // registers the merged window's timer, the merged windows' timers go.
+        const uint32_t cap = sess_set_cap(__popcll(mask) + 1);
+        auto before = [&](int c, uint32_t bc, int q, uint32_t bq) { return q < 0 || bc < bq || (bc == bq && st[c] < st[q]); };
+        int t = -1;
+        uint32_t tb = 0;
+        for (uint64_t m = mask; m; m &= m - 1) {   // the target: least (bucket, start)
+          const int c = __ffsll((long long)m) - 1;
+          const uint32_t bc = sess_bucket(st[c], en[c], cap);
+          if (before(c, bc, t, tb)) { t = c; tb = bc; }
+        }
+        LateAcc res;
+        bool have = false;
+        int64_t lh = -1, lt = -1, ll = 0;
+        if (d.list) { lh = d.head[base + t]; lt = d.tail[base + t]; ll = d.len[base + t]; }
+        for (uint64_t todo = mask & ~(1ull << t); todo;) {   // the sources in iteration order
+          int q = -1;
+          uint32_t bq = 0;
+          for (uint64_t m = todo; m; m &= m - 1) {
+            const int c = __ffsll((long long)m) - 1;
+            const uint32_t bc = sess_bucket(st[c], en[c], cap);
+            if (before(c, bc, q, bq)) { q = c; bq = bc; }
+          }
+          todo &= ~(1ull << q);
+          const int64_t x = base + q;
+          if (d.list) {   // the source's elements appended (mergePartitionedStates, list branch :315-333)
+            if (d.len[x] > 0) {
+              if (ll == 0) lh = d.head[x];
+              else d.pnext[lt] = d.head[x];
+              lt = d.tail[x];
+              ll += d.len[x];
+              d.len[x] = 0;
+            }
+          } else {
+            const LateAcc sv = sess_load(s, d, x);
+            res = have ? sess_combine(s, res, sv) : sv;
+            have = true;
+          }
+        }
+        if (d.list) {
+          d.head[base + t] = lh;
+          d.tail[base + t] = lt;
+          d.len[base + t] = ll;
+        } else if (have) {
+          sess_store(d, base + t, sess_combine(s, sess_load(s, d, base + t), res));   // HeapReducingState.add
+        }
+        live &= ~(mask & ~(1ull << t));
+        trig = (trig & ~mask) | (1ull << t);
+        r = t;
         d.start[base + r] = cs;
         d.end[base + r] = ce;
       }
@@ -138,10 +256,9 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
     const int64_t max_ts = jsub(ce, 1);
     if (cleanup_time(max_ts, s.lateness) <= wm) {   // isLate(actualWindow): retireWindow, the record dropped
       ++late;
-      if (r >= 0) { live &= ~(1ull << r); trig &= ~(1ull << r); }
+      if (r >= 0) retire(r);
       continue;
     }
-    LateAcc cur;
     if (fresh) {
       const uint64_t freem = ~live & all;
       if (freem == 0) { cap_error(s, 21); continue; }   // more in-flight sessions for the key than slots
@@ -150,17 +267,41 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       trig &= ~(1ull << r);
       d.start[base + r] = cs;
       d.end[base + r] = ce;
-      cur = a;
-    } else {
-      cur = op(sess_load(s, d, base + r), a);
+      if (d.list) d.len[base + r] = 0;
     }
-    sess_store(d, base + r, cur);
+    const int64_t x = base + r;
+    LateAcc cur;
+    if (d.list) {
+      // HeapListState.add: the element appended; its pool entry is the ring slot of its arrival ordinal
+      const int64_t ord = b.ord_base + i;
+      const int64_t e = ord % d.pcap;
+      if (d.pord[e] >= 0) {   // that entry still holds a buffered element: list_capacity exceeded
+        cap_error(s, 26);
+        if (fresh) live &= ~(1ull << r);
+        continue;
+      }
+      d.pord[e] = ord;
+      d.pv[e] = v;
+      d.pf1[e] = a.f1;
+      d.pnext[e] = -1;
+      if (d.len[x] == 0) d.head[x] = e;
+      else d.pnext[d.tail[x]] = e;
+      d.tail[x] = e;
+      d.len[x] += 1;
+    } else {
+      cur = fresh ? a : sess_combine(s, sess_load(s, d, x), a);
+      sess_store(d, x, cur);
+    }
     // EventTimeTrigger.onElement on the (possibly merged) window
     if (max_ts <= wm) {
-      const unsigned long long pos = atomicAdd(s.o.count, 1ull);
-      sess_emit(s, pos, key, cs, max_ts, cur);
+      if (d.list) {
+        sess_list_emit(s, d, x, key, cs, max_ts);
+      } else {
+        const unsigned long long pos = atomicAdd(s.o.count, 1ull);
+        sess_emit(s, pos, key, cs, max_ts, cur);
+      }
       ++fires;
-      if (purging) { live &= ~(1ull << r); trig &= ~(1ull << r); }   // FIRE_AND_PURGE: cleanup(actualWindow)
+      if (purging) retire(r);   // FIRE_AND_PURGE: cleanup(actualWindow)
     } else {
       trig |= 1ull << r;
     }
@@ -171,8 +312,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
 }
 
-// a watermark: every in-flight window's timers up to wm_new, in time order.  One thread per key; lane by lane
-// the it-th window of each key, so the wave's appends stay aggregated
+// a watermark: every in-flight window's timers up to wm_new.  One thread per key; lane by lane the it-th window of
+// each key, so the wave's appends stay aggregated (list state: one append per window, its element count)
 __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm_new) {
   const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
   const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
@@ -205,9 +346,15 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
           retire = true;
         }
         if (retire) { live &= ~(1ull << q); trig &= ~(1ull << q); }
+        if (d.list) {   // list state: every element of the window, then (retired) its pool entries freed
+          if (fire) sess_list_emit(s, d, x, kid_key(s, kid), start, max_ts);
+          if (retire) sess_list_free(d, x);
+        }
       }
-      const unsigned long long pos = wave_append(s.o.count, fire);
-      if (fire) sess_emit(s, pos, kid_key(s, kid), start, max_ts, sess_load(s, d, kid * d.sw + q));
+      if (!d.list) {
+        const unsigned long long pos = wave_append(s.o.count, fire);
+        if (fire) sess_emit(s, pos, kid_key(s, kid), start, max_ts, sess_load(s, d, kid * d.sw + q));
+      }
       wave_count(&s.stats[ST_FIRED], fire);
     }
     if (live != live0) d.live[kid] = live;
@@ -230,6 +377,22 @@ int session_create(fw_engine* e) {
   d.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(cells) : nullptr;
   d.mx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>(cells) : nullptr;
   d.cnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>(cells) : nullptr;
+  if (s.by) {   // maxBy / minBy: the extremal value's code in its min / max column
+    d.mn = (s.by & FW_AGG_MINBY) ? e->alloc<int64_t>(cells) : nullptr;
+    d.mx = (s.by & FW_AGG_MAXBY) ? e->alloc<int64_t>(cells) : nullptr;
+  }
+  d.f1 = s.first && !e->list ? e->alloc<int64_t>(cells) : nullptr;
+  d.list = e->list ? 1 : 0;
+  if (e->list) {
+    d.head = e->alloc<int64_t>(cells);
+    d.tail = e->alloc<int64_t>(cells);
+    d.len = e->alloc<int64_t>(cells);
+    d.pcap = e->cfg.list_capacity > 0 ? e->cfg.list_capacity : 4 * e->cfg.max_batch;
+    d.pv = e->alloc<int64_t>((size_t)d.pcap);
+    d.pf1 = e->alloc<int64_t>((size_t)d.pcap);
+    d.pnext = e->alloc<int64_t>((size_t)d.pcap);
+    d.pord = e->alloc<int64_t>((size_t)d.pcap);
+  }
   d.live = e->alloc<unsigned long long>((size_t)s.stride);
   d.trig = e->alloc<unsigned long long>((size_t)s.stride);
   e->s.o.win_start = e->alloc<int64_t>((size_t)e->cfg.out_capacity);
@@ -245,6 +408,10 @@ int session_create(fw_engine* e) {
   e->sess_temp = e->alloc<char>(tb);
   for (void* p : e->allocs) if (!p) return FW_ERR_DEVICE;
   HIPCHK(e, hipMemsetAsync(d.live, 0, 8 * (size_t)s.stride, e->stream));
+  if (d.list) {
+    HIPCHK(e, hipMemsetAsync(d.pord, 0xFF, 8 * (size_t)d.pcap, e->stream));   // every pool entry free (-1)
+    HIPCHK(e, hipMemsetAsync(d.len, 0, 8 * cells, e->stream));
+  }
   HIPCHK(e, hipMemsetAsync(d.trig, 0, 8 * (size_t)s.stride, e->stream));
   return FW_OK;
 }

@@ -659,7 +659,8 @@ class WindowOperator:
             else:
                 col = Collector()
                 apply = getattr(self.window_function, "apply", self.window_function)
-                apply(key, TimeWindow(ts + 1 - self.assigner.size, ts + 1), elems, col)
+                start = int(res["win_start"][i]) if res.get("win_start") is not None else ts + 1 - self.assigner.size
+                apply(key, TimeWindow(start, ts + 1), elems, col)
                 out.extend(StreamRecord(x, ts) for x in col.items)
             i = j
         return out

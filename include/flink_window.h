@@ -62,9 +62,13 @@ extern "C" {
                                     (SJ/api/windowing/assigners/EventTimeSessionWindows.java:53-56), the merging
                                     branch of WindowOperator.processElement (:228-301) over MergingWindowSet
                                     (SJ/runtime/operators/windowing/MergingWindowSet.java:142-214).  Reduce
-                                    fields sum/min/max/count; no first-arrival f1 / maxBy / minBy (after a merge
-                                    they follow HashSet iteration order of the merged windows); no checkpoint
-                                    (the merging-window set is keyed list state of its own). */
+                                    fields, first-arrival f1, maxBy / minBy and list state: a merge takes the
+                                    merged windows in the JDK HashSet iteration order TimeWindow.mergeWindows
+                                    produces (state window = the first one's; the others reduced / their lists
+                                    appended in that order), so f1, ties and double sums match the reference.
+                                    At most 64 in-flight sessions per key (max_open_slices, default 32:
+                                    FW_ERR_CAPACITY beyond).  No checkpoint (the merging-window set is keyed
+                                    list state of its own). */
 
 /* ---- trigger (SJ/api/windowing/triggers) ---- */
 #define FW_TRIGGER_EVENT_TIME          0   /* EventTimeTrigger.create()                    */
@@ -93,8 +97,11 @@ extern "C" {
  * (flink-runtime/.../state/heap/HeapListState.java): the window's elements are buffered (up to list_capacity per
  * pane slice) and a firing window returns every element of every key, grouped by key, in arrival order, one
  * result row per element (value in the sum column, the element's f1, ts = window.maxTimestamp()); the host runs
- * the window function over each group.  Tumbling / sliding; no session windows; an element arriving for a
- * window that already fired (allowed lateness) fails with FW_ERR_UNSUPPORTED.  Used alone. */
+ * the window function over each group.  Tumbling / sliding: an element arriving for a window that already
+ * fired (allowed lateness) fails with FW_ERR_UNSUPPORTED.  Session windows: each window's elements in list
+ * order (a merge appends the sources' lists to the target's, AbstractKeyedStateBackend.mergePartitionedStates
+ * :315-333), a late element's per-element fire re-emits the whole list; list_capacity bounds the elements
+ * buffered at once (a pool indexed by arrival ordinal).  Used alone. */
 #define FW_AGG_LIST   64
 
 /* agg_flags */
@@ -143,7 +150,8 @@ typedef struct {
                              /*     fold without allowed lateness, key_capacity <= 64 Ki)     */
   int32_t agg_flags;         /* OR of FW_AGGF_*                                                 */
   int64_t fold_initial;      /* FW_AGGF_FOLD: the fold's initial accumulator                    */
-  int64_t list_capacity;     /* FW_AGG_LIST: elements buffered per pane slice (0 = 4 x max_batch) */
+  int64_t list_capacity;     /* FW_AGG_LIST: elements buffered per pane slice (session windows: */
+                             /* ... in all, a ring by arrival ordinal); 0 = 4 x max_batch      */
 } fw_config;
 
 /* Output between two collects: records and watermark marks.  Records [mark_pos[i-1], mark_pos[i])

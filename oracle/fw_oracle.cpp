@@ -486,6 +486,26 @@ struct Operator {
         // AbstractKeyedStateBackend.mergePartitionedStates (:294-314): the sources reduced in list order
         // and cleared, the result added to the target state window
         const TimeWindow target = windows.at(mergeResult);
+        if (cfg.agg_mask == FW_AGG_LIST) {
+          // list state (:315-333): the sources' elements concatenated in list order, each source cleared,
+          // then every element added to the target (HeapListState.add appends)
+          std::vector<ListElem> elems;
+          for (const TimeWindow& src : mergedStateWindows) {
+            const Acc* sv = stateGet(src);
+            if (sv && sv->list) elems.insert(elems.end(), sv->list->begin(), sv->list->end());
+            stateClear(src);
+          }
+          for (const ListElem& x : elems) {
+            Acc a{};
+            a.key = curKey;
+            a.sum_i = x.vi;
+            a.sum_d = x.vd;
+            a.f1 = x.f1;
+            a.seq = ++seqCounter;
+            stateAdd(target, a);
+          }
+          continue;
+        }
         bool have = false;
         Acc result{};
         for (const TimeWindow& src : mergedStateWindows) {
@@ -842,9 +862,8 @@ int fwo_create(const fw_config* cfg, fw_engine** out) {
   if (!cfg || !out) return FW_ERR_INVALID_ARG;
   if (cfg->assigner != FW_TUMBLING && cfg->assigner != FW_SLIDING && cfg->assigner != FW_SESSION) return FW_ERR_INVALID_ARG;
   if ((cfg->agg_flags & FW_AGGF_FOLD) && cfg->assigner == FW_SESSION) return FW_ERR_UNSUPPORTED;   // WindowedStream.java:466-467
-  if ((cfg->agg_mask & FW_AGG_LIST) && (cfg->agg_mask != FW_AGG_LIST || cfg->assigner == FW_SESSION ||
-                                        (cfg->agg_flags & FW_AGGF_FOLD)))
-    return FW_ERR_UNSUPPORTED;   // list state: alone, tumbling / sliding (the engine's scope)
+  if ((cfg->agg_mask & FW_AGG_LIST) && (cfg->agg_mask != FW_AGG_LIST || (cfg->agg_flags & FW_AGGF_FOLD)))
+    return FW_ERR_UNSUPPORTED;   // list state: alone
   if (cfg->size <= 0 || (cfg->assigner == FW_SLIDING && cfg->slide <= 0) || cfg->allowed_lateness < 0 ||
       cfg->max_parallelism <= 0 || cfg->kg_start < 0 || cfg->kg_end < cfg->kg_start || cfg->kg_end >= cfg->max_parallelism)
     return FW_ERR_INVALID_ARG;

@@ -255,11 +255,13 @@ SESSION_OUT = [{"wm": 12000, "records": [sout("key1", 6, 10, 5500), sout("key2",
 FIXTURES.append(fixture(
     "session_reduce", "WindowOperatorTest.java:435-501", cfg("session", 3000),
     SESSION_OOO + [wm(12000), rec("key2", 10, 15000), rec("key2", 20, 15000), wm(17999)], SESSION_OUT))
-# WOT:362-431 testSessionWindows: the same elements through ListState + SessionWindowFunction, which
-# emits (key-sum, start, end): identical results to the reducing form (list state itself is not on the
-# GPU path; the fixture pins the merging semantics)
+# WOT:362-431 testSessionWindows: the same elements through ListState (ListStateDescriptor) +
+# SessionWindowFunction, which emits (key-sum, start, end) over the merged window's element list; the replay
+# applies that window function to the list-state rows
+SESSION_LIST = cfg("session", 3000)
+SESSION_LIST["list"] = True
 FIXTURES.append(fixture(
-    "session_windows", "WindowOperatorTest.java:362-431", cfg("session", 3000),
+    "session_windows", "WindowOperatorTest.java:362-431", SESSION_LIST,
     SESSION_OOO + [wm(12000), rec("key2", 10, 15000), rec("key2", 20, 15000), wm(17999)], SESSION_OUT))
 
 

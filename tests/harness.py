@@ -107,11 +107,12 @@ def replay(fx, engine_factory, **kw):
             assert len(res["mark_wm"]) == 1 and res["mark_wm"][0] == e[1]
             assert res["mark_pos"][0] == res["n"], "records emitted after the watermark mark"
             if fx["config"].get("list"):   # the window function of the reference test: the sum per (key, window)
+                session = fx["config"]["assigner"] == "session"
                 groups = {}
                 for i in range(res["n"]):
-                    g = (int(res["key"][i]), int(res["ts"][i]))
+                    g = (int(res["key"][i]), int(res["ts"][i])) + ((int(res["win_start"][i]),) if session else ())
                     groups[g] = groups.get(g, 0) + int(res["sum_i64"][i])
-                recs = sorted((k, v, t) for (k, t), v in groups.items())
+                recs = sorted((g[0], v) + g[1:] for g, v in groups.items())
             elif fx["config"]["assigner"] == "session":   # the window's start too (end = ts + 1)
                 recs = sorted((int(res["key"][i]), int(res["sum_i64"][i]), int(res["ts"][i]), int(res["win_start"][i]))
                               for i in range(res["n"]))

@@ -113,9 +113,7 @@ def test_list_operator_window_function(hip, oracle_engine):
 
 def test_list_rejections(hip):
     from flink_amd import _abi
-    from flink_amd.windowing import EventTimeSessionWindows, ListStateDescriptor, TumblingEventTimeWindows, make_config
-    with pytest.raises(_abi.FwError):
-        hip(make_config(EventTimeSessionWindows.withGap(10), ListStateDescriptor()))
+    from flink_amd.windowing import ListStateDescriptor, TumblingEventTimeWindows, make_config
     e = hip(make_config(TumblingEventTimeWindows.of(1000), ListStateDescriptor(), None, 500, key_capacity=64,
                         max_batch=64, out_capacity=1024))
     e.push(np.array([1], np.int64), np.array([100], np.int64), np.array([1], np.int64))

@@ -105,11 +105,133 @@ def test_session_extreme_timestamps(hip, oracle_engine):
     _both(hip, oracle_engine, cfg, keys, ts, vals, 6, 0, ["sum_i64", "count"])
 
 
+def _red_cfg(gap, red, lateness=0, purging=False, **kw):
+    from flink_amd.windowing import EventTimeSessionWindows, EventTimeTrigger, PurgingTrigger, make_config
+    trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else EventTimeTrigger.create()
+    args = dict(max_parallelism=128, key_capacity=4096, max_batch=1 << 14, out_capacity=1 << 20)
+    args.update(kw)
+    return make_config(EventTimeSessionWindows.withGap(gap), red, trig, lateness, **args)
+
+
+def _merge_heavy_stream(n, n_keys, seed, gap):
+    """Out-of-order records whose sessions keep bridging earlier ones: many merges of 2+ windows (the HashSet
+    order of the merged windows decides the state window, f1 and the reduce order)."""
+    rng = np.random.default_rng(seed)
+    keys = rng.integers(0, n_keys, n).astype(np.int64)
+    base = np.sort(rng.integers(0, max(1, int(n / n_keys * gap * 0.8)), n)).astype(np.int64)   # ~0.8 gap apart per key
+    ts = base - rng.integers(0, 4 * gap, n).astype(np.int64)
+    vals = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    return keys, ts, vals
+
+
+@pytest.mark.parametrize("lateness,purging", [(0, False), (300, False), (300, True)])
+def test_session_first_arrival_f1(hip, oracle_engine, lateness, purging):
+    """Tuple3.of(a.f0, a.f1, a.f2 + b.f2): f1 of the merge target's state (MergingWindowSet.addWindow takes the
+    state window of the first merged window in HashSet order, MergingWindowSet.java:142-214) — bit-exact."""
+    from flink_amd.windowing import ReduceFunction
+    keys, ts, vals = _merge_heavy_stream(30000, 200, 5 + lateness, 40)
+    f1 = np.arange(len(keys), dtype=np.int64) * 7 + 3
+    cfg = _red_cfg(40, ReduceFunction(("sum", "count"), "i64", keep_first_f1=True), lateness, purging)
+    out = []
+    for f in (hip, oracle_engine):
+        e = f(cfg)
+        r = drive(e, keys, ts, vals, 2048, 60, LONG_MAX, f1=f1)
+        out.append((epochs_of(r, ["sum_i64", "count", "win_start"], f1=True), e.stats()))
+        e.close()
+    (g, sg), (o, so) = out
+    assert g == o
+    assert sg["panes_fired"] == so["panes_fired"] > 1000
+
+
+def test_session_double_sums_exact(hip, oracle_engine):
+    """Double sums reduce in the reference's order (sources in HashSet order, then into the target): bit-exact."""
+    from flink_amd.windowing import ReduceFunction
+    keys, ts, _ = _merge_heavy_stream(30000, 150, 9, 50)
+    vals = np.random.default_rng(4).random(len(keys)) * 1e6
+    cfg = _red_cfg(50, ReduceFunction(("sum", "min", "max", "count"), "f64", keep_first_f1=True), 100)
+    out = []
+    for f in (hip, oracle_engine):
+        e = f(cfg)
+        r = drive(e, keys, ts, vals, 2048, 80, LONG_MAX)
+        out.append(epochs_of(r, ["sum_f64", "min_f64", "max_f64", "count", "win_start"], f1=True))
+        e.close()
+    assert out[0] == out[1]
+
+
+@pytest.mark.parametrize("field,first", [("maxBy", True), ("maxBy", False), ("minBy", True), ("minBy", False)])
+def test_session_max_by(hip, oracle_engine, field, first):
+    """maxBy / minBy over merging windows: the extremal record, ties by argument order of the reduce
+    (ComparableAggregator.java:74-81) — values drawn from a small range so ties are common."""
+    from flink_amd.windowing import ReduceFunction
+    keys, ts, _ = _merge_heavy_stream(20000, 100, 13, 40)
+    vals = np.random.default_rng(6).integers(0, 8, len(keys)).astype(np.int64)
+    f1 = np.arange(len(keys), dtype=np.int64)
+    cfg = _red_cfg(40, ReduceFunction((field,), "i64", first=first), 200)
+    col = "max_i64" if field == "maxBy" else "min_i64"
+    out = []
+    for f in (hip, oracle_engine):
+        e = f(cfg)
+        r = drive(e, keys, ts, vals, 2048, 60, LONG_MAX, f1=f1)
+        out.append(epochs_of(r, [col, "win_start"], f1=True))
+        e.close()
+    assert out[0] == out[1]
+
+
+def _list_groups(results):
+    """Per watermark mark: {(key, window maxTimestamp, window start): [(f1, value) in emitted order]} — the
+    element order of a window is its list order (HeapListState), the order between windows unspecified."""
+    ep = []
+    for res in results:
+        pos = 0
+        for wm, mp in list(zip(res["mark_wm"], res["mark_pos"])) + [(None, res["n"])]:
+            groups = {}
+            for j in range(pos, int(mp)):
+                g = (int(res["key"][j]), int(res["ts"][j]), int(res["win_start"][j]))
+                groups.setdefault(g, []).append((int(res["f1"][j]), int(res["sum_i64"][j])))
+            if wm is not None or groups:
+                ep.append((None if wm is None else int(wm), groups))
+            pos = int(mp)
+    return ep
+
+
+@pytest.mark.parametrize("lateness,purging", [(0, False), (200, False), (200, True)])
+def test_session_list_state(hip, oracle_engine, lateness, purging):
+    """WindowedStream.apply over EventTimeSessionWindows (the reference's testSessionWindows shape): each
+    window's elements in list order — a merge appends the sources' lists to the target's in HashSet order
+    (AbstractKeyedStateBackend.mergePartitionedStates :315-333) — grouped per window, bit-exact."""
+    from flink_amd.windowing import ListStateDescriptor
+    keys, ts, vals = _merge_heavy_stream(20000, 150, 21 + lateness, 40)
+    f1 = np.arange(len(keys), dtype=np.int64) + 100
+    cfg = _red_cfg(40, ListStateDescriptor("i64", list_capacity=1 << 16), lateness, purging)
+    out = []
+    for f in (hip, oracle_engine):
+        e = f(cfg)
+        r = drive(e, keys, ts, vals, 2048, 60, LONG_MAX, f1=f1)
+        out.append((_list_groups(r), e.stats()))
+        e.close()
+    (g, sg), (o, so) = out
+    assert len(g) == len(o)
+    for (wg, xg), (wo, xo) in zip(g, o):
+        assert wg == wo and xg == xo, wg
+    assert sg["panes_fired"] == so["panes_fired"] > 500
+    assert sg["records_late"] == so["records_late"]
+
+
+def test_session_list_capacity(hip):
+    """More buffered elements than list_capacity: FW_ERR_CAPACITY, not a wrong answer."""
+    from flink_amd import _abi
+    from flink_amd.windowing import ListStateDescriptor
+    e = hip(_red_cfg(1000, ListStateDescriptor("i64", list_capacity=64)))
+    n = 200   # one key, one long session: every element stays buffered
+    e.push(np.ones(n, np.int64), np.arange(n, dtype=np.int64), np.ones(n, np.int64))
+    with pytest.raises(_abi.FwError) as ei:
+        e.collect()
+    assert ei.value.code == _abi.FW_ERR_CAPACITY
+    e.close()
+
+
 def test_session_rejections(hip):
     from flink_amd import _abi
-    from flink_amd.windowing import (EventTimeSessionWindows, ReduceFunction, make_config)
-    with pytest.raises(_abi.FwError):
-        hip(make_config(EventTimeSessionWindows.withGap(10), ReduceFunction(("sum",), keep_first_f1=True)))
     e = hip(_cfg(10, ("sum",)))
     e.push(np.array([1], np.int64), np.array([5], np.int64), np.array([1], np.int64))
     with pytest.raises(_abi.FwError, match="session"):
