@@ -130,6 +130,11 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int32_t* err;
   unsigned long long* stats;
   unsigned int* dir_keys_host;   // host-mapped copy of stats[ST_DIR_KEYS], posted at each firing watermark
+  // restored tumbling windows whose trigger timers fired before the checkpoint (restore at Long.MIN_VALUE,
+  // fw_restore_kg_flink): disarm[p] marks such a window's slot; a pane fires at its maxTimestamp only if a
+  // record re-armed its timer (armed[p * stride + kid], EventTimeTrigger.onElement :37-45).  Null otherwise
+  uint8_t* disarm;
+  uint8_t* armed;
 };
 
 __device__ __forceinline__ void set_error(int32_t* err, int32_t code) { atomicCAS(err, 0, code); }
@@ -579,6 +584,23 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* l
     const int64_t idx = list[j];
     if (idx < 0) continue;
     if (s.c.first[idx] == ord_base + j) s.c.f1v[idx] = f1col[j];
+  }
+}
+
+// after a batch's ingest, while restored windows are disarmed and ahead of the watermark: each record of such a
+// window re-arms its pane's trigger timer (EventTimeTrigger.onElement registers maxTimestamp while the
+// watermark is below it; the window then fires at its maxTimestamp with everything the pane holds)
+__global__ __launch_bounds__(BLOCK) void k_arm(Spec s, BatchIn b) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ts = b.ts[i];
+    if (ts == INT64_MIN) continue;
+    const int64_t m = floor_div(jsub(ts, s.offset), s.size);   // tumbling: the slice is the window
+    const int32_t p = (int32_t)floor_mod(m, s.P);
+    if (!s.disarm[p] || s.slice_tag[p] != m) continue;
+    const int64_t max_ts = jsub(jadd(window_start_n(s, m), s.size), 1);
+    if (max_ts <= b.wm) continue;
+    const int64_t kid = dir_lookup(s, b.key[i]);
+    if (kid >= 0) s.armed[(int64_t)p * s.stride + kid] = 1;
   }
 }
 
@@ -2046,6 +2068,8 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     if (threadIdx.x == 0) wslot_t = wpane_slot(s, n);
     __syncthreads();
     const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+    // a restored window whose trigger timers fired before the checkpoint: only re-armed panes fire
+    const int32_t p_dis = (s.disarm && s.K == 1 && slots[0] >= 0 && s.disarm[slots[0]]) ? slots[0] : -1;
     for (int64_t k0 = (int64_t)blockIdx.x * WM_THREADS; k0 < s.stride; k0 += gstride) {
       const int64_t kid = k0 + threadIdx.x;
       bool any = false;
@@ -2066,6 +2090,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
             pres = s.c.present[idx] != 0;
           }
           if (!pres) continue;
+          if (p_dis >= 0 && !s.armed[idx]) continue;
           const LateAcc b = pane_load(s, idx);
           a = any ? op(a, b) : b;
           any = true;
@@ -2496,6 +2521,10 @@ struct ListDev {
   int64_t cap;                  // elements per slice slot
   unsigned long long* cnt;      // [P] elements buffered
   int64_t* buf;                 // [P][cap][4]
+  // allowed lateness: the batch's per-element re-fires (kid, window number, arrival ordinal)
+  int64_t* fire;
+  unsigned long long* fcnt;
+  int64_t fcap;
 };
 
 // session windows (fw_session.hip): per key id `sw` window slots, key-major [D + 1][sw]
@@ -2554,6 +2583,10 @@ struct fw_engine {
   int64_t ordinal = 0;
   bool used_key_hash = false;         // a push carried Java key hashes: key groups are not derivable from keys
   bool restored = false;              // fw_restore_kg was called (fixes the watermark of every later restore)
+  // restored tumbling windows (slice numbers) whose trigger timers fired before the checkpoint, still ahead of
+  // the watermark (Spec::disarm / armed); and the restored windows that did carry their trigger timers
+  std::set<int64_t> disarmed, armed_windows;
+  std::set<std::pair<int64_t, int64_t>> snap_unarmed;   // build_snapshot: (slice, key) panes not re-armed
   // fw_snapshot_kg: entries of every key group, built once per engine state (state_epoch)
   int64_t state_epoch = 0, snap_epoch = -1;
   std::vector<std::vector<int64_t>> snap_kg;
@@ -3389,6 +3422,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
                        e->cfg.max_batch);
   e->batches++;
   HIPCHK(e, hipGetLastError());
+  if (!e->disarmed.empty() &&
+      jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)*e->disarmed.rbegin() * (uint64_t)e->s.size)), e->s.size), 1) > e->cur_wm)
+    hipLaunchKernelGGL(k_arm, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0, e->stream, e->s, b);
   if (e->s.first && !e->routed && !e->fused) {   // the partitioned form sets f1 in k_aggregate, the fused one in k_fused
     e->phase_begin(FW_PHASE_FIXUP);
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
@@ -3499,6 +3535,17 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   FW_DISPATCH(launch_watermark_t, e, e->cur_wm, wm);
   e->phase_end(e->s.stride);
   HIPCHK(e, hipGetLastError());
+  // restored disarmed windows whose maxTimestamp the watermark passed: their re-armed panes fired above; the
+  // rest never fires again (cleanup at the cleanup time, as any window)
+  for (auto it = e->disarmed.begin(); it != e->disarmed.end();) {
+    const int64_t m = *it;
+    const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)m * (uint64_t)e->s.size)), e->s.size), 1);
+    if (max_ts > wm) { ++it; continue; }
+    const int32_t p = (int32_t)floor_mod(m, e->s.P);
+    HIPCHK(e, hipMemsetAsync(e->s.disarm + p, 0, 1, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->s.armed + (size_t)p * (size_t)e->s.stride, 0, (size_t)e->s.stride, e->stream));
+    it = e->disarmed.erase(it);
+  }
   e->hmarks.push_back({wm, e->dev_marks++, true});
   e->out_dirty = false;
   e->cur_wm = wm;
@@ -3732,6 +3779,7 @@ static int build_snapshot(fw_engine* e) {
     if (keys[k] != fw::EMPTY_KEY) kid_kg[k] = host_key_group(s, keys[k]);
   if (min_used) kid_kg[s.D] = host_key_group(s, fw::EMPTY_KEY);
   e->snap_kg.assign((size_t)mp, {});
+  e->snap_unarmed.clear();
   e->snap_has_key.assign((size_t)mp, 0);
   e->snap_any_key = false;
   for (size_t k = 0; k < kid_kg.size(); ++k)
@@ -3764,10 +3812,17 @@ static int build_snapshot(fw_engine* e) {
       present.resize(st);
       HIPCHK(e, hipMemcpy(present.data(), s.c.present + off, st, hipMemcpyDeviceToHost));
     }
+    std::vector<uint8_t> armed;
+    const bool dis = e->disarmed.count(m) != 0;
+    if (dis) {
+      armed.resize(st);
+      HIPCHK(e, hipMemcpy(armed.data(), s.armed + off, st, hipMemcpyDeviceToHost));
+    }
     for (size_t k = 0; k < st; ++k) {
       const bool pres = s.first ? first[k] != INT64_MAX : present[k] != 0;
       if (!pres || kid_kg[k] < 0) continue;
       const int64_t key = (int64_t)k == s.D ? fw::EMPTY_KEY : keys[k];
+      if (dis && !armed[k]) e->snap_unarmed.insert({m, key});
       const int64_t ent[FW_SNAP_ENTRY_WORDS] = {
           m, key, sum[k], s.c.mn ? mn[k] : INT64_MAX, s.c.mx ? mx[k] : INT64_MIN,
           s.c.cnt ? (s.by ? cnt[k] - e->ordinal : cnt[k]) : 0,
@@ -3786,6 +3841,9 @@ int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* le
   if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (window_panes_used(e)) return reject(e, FW_ERR_UNSUPPORTED, "sliding windows: records below offset - slide put state in window panes, which no checkpoint layout carries");
+  if (!e->disarmed.empty())
+    return reject(e, FW_ERR_UNSUPPORTED, "restored windows without trigger timers: only the reference layout (explicit "
+                                         "timers, fw_snapshot_kg_flink) carries them");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)   // HeapInternalTimerService.restoreTimersForKeyGroup's check
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -3867,6 +3925,7 @@ struct KgPane {
   int64_t sum, mn, mx, cnt;
   int64_t first;    // first-arrival ordinal (0 when the config does not track first arrival)
   int64_t f1;
+  bool unarmed;     // a restored window's pane whose trigger timer fired before the checkpoint (none pending)
 };
 
 static int check_state_layout(fw_engine* e, const fw_state_layout* L) {
@@ -3929,6 +3988,7 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
     p.cnt = x[5];               // maxBy/minBy: the extremal record's ordinal
     p.first = s.first ? x[6] : 0;
     p.f1 = x[7];
+    p.unarmed = tumbling && e->snap_unarmed.count({x[0], x[1]}) != 0;
     return p;
   };
   out.clear();
@@ -4061,7 +4121,7 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   std::vector<Tm> tv;
   for (const KgPane& p : panes) {
     const int64_t max_ts = fw::jsub(p.end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
-    if (max_ts > e->cur_wm) tv.push_back({p.key, p.start, p.end, max_ts, p.first, 0, INT64_MAX});
+    if (max_ts > e->cur_wm && !p.unarmed) tv.push_back({p.key, p.start, p.end, max_ts, p.first, 0, INT64_MAX});
     if (ct != max_ts || max_ts <= e->cur_wm) tv.push_back({p.key, p.start, p.end, ct, p.first, 1, INT64_MAX});
   }
   if (!e->restored_timer_rank.empty())
@@ -4141,7 +4201,7 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
       const int32_t ne = in.i32();
       if (ne < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
       for (int32_t j = 0; j < ne && in.ok; ++j) {
-        KgPane p{start, end, in.i64(), 0, INT64_MAX, INT64_MIN, 0, 0, 0};
+        KgPane p{start, end, in.i64(), 0, INT64_MAX, INT64_MIN, 0, 0, 0, false};
         for (int f = 0; f < layout->n_fields; ++f) {
           const int64_t x = in.i64();
           double d;
@@ -4182,17 +4242,47 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
     if (!in.done()) return reject(e, FW_ERR_INVALID_ARG, "timer section truncated or with trailing bytes");
     if (np != 0) return reject(e, FW_ERR_UNSUPPORTED, "processing-time timers");
   }
-  for (const KgPane& p : panes) {
+  // a window ahead of `watermark` whose panes carry no trigger timer fired before the checkpoint (the
+  // reference restarts its timer service at Long.MIN_VALUE): it is restored disarmed — it fires again only for
+  // keys a later record re-arms before the watermark passes it.  The panes of one window agree, in every key
+  // group (an aligned checkpoint fired a window's timers for all its keys at one watermark)
+  std::sort(got.begin(), got.end());
+  std::set<int64_t> dis_now, armed_now;
+  for (size_t i = 0; i < panes.size(); ++i) {
+    const KgPane& p = panes[i];
     const int64_t max_ts = fw::jsub(p.end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
     if (ct <= watermark) return reject(e, FW_ERR_UNSUPPORTED, "pane past its cleanup time at the restore watermark");
-    if (max_ts > watermark) want.push_back({p.key, p.start, p.end, max_ts});
+    if (max_ts <= watermark) continue;
+    const bool has = std::binary_search(got.begin(), got.end(), std::array<int64_t, 4>{p.key, p.start, p.end, max_ts});
+    (has ? armed_now : dis_now).insert(slice_of[i]);
+  }
+  for (int64_t m : dis_now)
+    if (armed_now.count(m) || e->armed_windows.count(m) || c.allowed_lateness == 0)
+      return reject(e, FW_ERR_UNSUPPORTED, "a window with and without trigger timers (not an aligned checkpoint)");
+  for (int64_t m : armed_now)
+    if (e->disarmed.count(m)) return reject(e, FW_ERR_UNSUPPORTED, "a window with and without trigger timers (not an aligned checkpoint)");
+  for (size_t i = 0; i < panes.size(); ++i) {
+    const KgPane& p = panes[i];
+    const int64_t max_ts = fw::jsub(p.end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+    if (max_ts > watermark && !dis_now.count(slice_of[i])) want.push_back({p.key, p.start, p.end, max_ts});
     if (ct != max_ts) want.push_back({p.key, p.start, p.end, ct});
   }
-  std::sort(got.begin(), got.end());
   std::sort(want.begin(), want.end());
   if (got != want)
-    return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark "
-                                         "(pass the checkpoint's watermark when panes have fired but are kept)");
+    return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
+  if (!dis_now.empty() && !e->s.disarm) {   // per-slot flags and per-pane re-arm marks, first needed here
+    e->s.disarm = e->alloc<uint8_t>((size_t)s.P);
+    e->s.armed = e->alloc<uint8_t>((size_t)s.P * (size_t)s.stride);
+    if (!e->s.disarm || !e->s.armed) return reject(e, FW_ERR_DEVICE, "out of device memory");
+    HIPCHK(e, hipMemset(e->s.disarm, 0, (size_t)s.P));
+    HIPCHK(e, hipMemset(e->s.armed, 0, (size_t)s.P * (size_t)s.stride));
+  }
+  for (int64_t m : dis_now) {
+    e->disarmed.insert(m);
+    const uint8_t one = 1;
+    HIPCHK(e, hipMemcpy(e->s.disarm + floor_mod(m, s.P), &one, 1, hipMemcpyHostToDevice));
+  }
+  e->armed_windows.insert(armed_now.begin(), armed_now.end());
   // arrival ordinals in blob order: restored panes precede every later record, and keep the blob's
   // (HashMap iteration) order as their insertion order, as readStateTableForKeyGroup's puts do
   std::vector<int64_t> ent(panes.size() * FW_SNAP_ENTRY_WORDS);

@@ -11,8 +11,11 @@
 // radix sorts — and appends one result row per element, grouped by key, to the output log; the host
 // runs the window function over each (key, window) group.  A slice is dropped when its last window's
 // cleanup time passes, like the reduce path's purge.  An element for a window that already fired but is
-// not yet cleaned up (allowed lateness) would re-fire the window with every element so far: not
-// implemented here, reported as FW_ERR_UNSUPPORTED.
+// not yet cleaned up (allowed lateness) is added and re-fires the window for its key with every element so
+// far (EventTimeTrigger.onElement FIRE, WindowOperator.java:302-333): each such (key, window, arrival) is
+// listed at ingest; after the batch the window's elements are gathered and sorted as for a watermark fire,
+// and each listed fire emits its key's elements up to its own arrival.  PurgingTrigger with such fires
+// (the purge would clear one window of slices other windows share) stays FW_ERR_UNSUPPORTED.
 
 namespace fw {
 
@@ -39,12 +42,26 @@ __global__ __launch_bounds__(BLOCK) void k_list_ingest(Spec s, BatchIn b, ListDe
       if (ok) {
         const RecWin w = record_windows(s, ts, b.wm);
         late = (unsigned long long)w.n_late + (w.q_late ? 1ull : 0ull);
-        if (w.n_fire > 0 || (w.quirk && !w.q_late)) { set_error(s.err, FW_ERR_UNSUPPORTED); ok = false; }
+        if ((w.n_fire > 0 && s.trigger == FW_TRIGGER_PURGING_EVENT_TIME) || (w.quirk && !w.q_late)) {
+          set_error(s.err, FW_ERR_UNSUPPORTED);
+          ok = false;
+        }
         live = ok && (w.n_windows - w.n_late) > 0;
         if (live) {
           p = slice_slot(s, w.m);
           kid = dir_find_or_insert(s, key);
           if (p < 0 || kid < 0) { cap_error(s, 24); live = false; }
+        }
+        if (live && w.n_fire > 0) {   // the windows of the record that fired already: one re-fire each
+          for (int64_t n = floor_div(w.m - s.K, s.R) + 1; n <= floor_div(w.m, s.R); ++n) {
+            const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+            if (max_ts > b.wm || cleanup_time(max_ts, s.lateness) <= b.wm) continue;
+            const unsigned long long f = atomicAdd(L.fcnt, 1ull);
+            if ((int64_t)f >= L.fcap) { cap_error(s, 27); continue; }
+            L.fire[3 * f] = kid;
+            L.fire[3 * f + 1] = n;
+            L.fire[3 * f + 2] = b.ord_base + i;
+          }
         }
       }
     }
@@ -149,6 +166,44 @@ __global__ __launch_bounds__(BLOCK) void k_list_emit(Spec s, ListDev L, const in
   }
 }
 
+// per-element re-fires of window n (pairs (kid, arrival ordinal) in arrival order): the element count of
+// each — its key's elements of the window (sorted by key id, then arrival: kids[], pos[]) up to its arrival
+__global__ __launch_bounds__(BLOCK) void k_list_fire_count(ListDev L, const unsigned long long* kids, const int64_t* pos,
+                                                          int64_t N, const int64_t* pairs, int64_t F, int64_t* cnt) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < F; j += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long kid = (unsigned long long)pairs[2 * j];
+    const int64_t ord = pairs[2 * j + 1];
+    int64_t lo = 0, hi = N;   // first element of the key
+    while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (kids[mid] < kid) lo = mid + 1; else hi = mid; }
+    int64_t a = lo, z = N;    // first element of the key after its arrival (ordinals increase within a key)
+    while (a < z) {
+      const int64_t mid = (a + z) >> 1;
+      if (kids[mid] == kid && L.buf[pos[mid] + 1] <= ord) a = mid + 1; else z = mid;
+    }
+    cnt[2 * j] = lo;
+    cnt[2 * j + 1] = a - lo;
+  }
+}
+
+// their rows at base + off[j]: the window's elements of the key, in arrival order (ts = window.maxTimestamp())
+__global__ __launch_bounds__(BLOCK) void k_list_fire_emit(Spec s, ListDev L, const int64_t* pos, const int64_t* cnt,
+                                                         const int64_t* off, int64_t F, int64_t base, int64_t max_ts) {
+  for (int64_t j = blockIdx.x; j < F; j += gridDim.x) {
+    const int64_t lo = cnt[2 * j], c = cnt[2 * j + 1];
+    for (int64_t e = threadIdx.x; e < c; e += blockDim.x) {
+      const int64_t* el = L.buf + pos[lo + e];
+      const int64_t at = base + off[j] + e;
+      if (at >= s.o.capacity) { cap_error(s, 11); continue; }
+      s.o.key[at] = kid_key(s, el[0]);
+      s.o.f1[at] = el[3];
+      s.o.ts[at] = max_ts;
+      s.o.sum[at] = el[2];
+    }
+  }
+}
+
+__global__ void k_list_set_count(Spec s, int64_t count) { *s.o.count = (unsigned long long)count; }
+
 // output count; the expired slices' buffers and slots freed
 __global__ void k_list_finish(Spec s, ListDev L, const int64_t* plan, int64_t count) {
   const int64_t np = plan[1];
@@ -170,12 +225,21 @@ int list_create(fw_engine* e) {
   L.cap = e->cfg.list_capacity > 0 ? e->cfg.list_capacity : 4 * e->cfg.max_batch;
   L.cnt = e->alloc<unsigned long long>((size_t)s.P);
   L.buf = e->alloc<int64_t>((size_t)s.P * (size_t)L.cap * LST_WORDS);
+  if (e->cfg.allowed_lateness > 0) {   // per-element re-fires: (kid, window, arrival) of one batch
+    L.fcap = e->cfg.max_batch;
+    L.fire = e->alloc<int64_t>((size_t)L.fcap * 3);
+    L.fcnt = e->alloc<unsigned long long>(1);
+  }
   e->list_plan = e->alloc<int64_t>(LPLAN_WORDS);
   e->list_plan_h.resize(LPLAN_WORDS);
   for (void* p : e->allocs) if (!p) return FW_ERR_DEVICE;
   HIPCHK(e, hipMemsetAsync(L.cnt, 0, 8 * (size_t)s.P, e->stream));
+  if (L.fcnt) HIPCHK(e, hipMemsetAsync(L.fcnt, 0, 8, e->stream));
   return FW_OK;
 }
+
+static int list_grow(fw_engine* e, int64_t n);
+static int list_sort_window(fw_engine* e, int64_t n, int64_t N);
 
 int list_push(fw_engine* e, const BatchIn& b) {
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((b.n + BLOCK - 1) / BLOCK, e->grid));
@@ -183,6 +247,65 @@ int list_push(fw_engine* e, const BatchIn& b) {
   hipLaunchKernelGGL(k_list_ingest, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b, e->lst);
   e->phase_end(b.n);
   HIPCHK(e, hipGetLastError());
+  if (!e->lst.fcnt || !fires_possible(e->s, e->cur_wm)) return FW_OK;
+  // per-element re-fires (allowed lateness): the batch's list, grouped by window in arrival order
+  unsigned long long F = 0;
+  HIPCHK(e, hipMemcpyAsync(&F, e->lst.fcnt, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  F = std::min<unsigned long long>(F, (unsigned long long)e->lst.fcap);
+  if (F == 0) return FW_OK;
+  std::vector<int64_t> fl(3 * F);
+  HIPCHK(e, hipMemcpy(fl.data(), e->lst.fire, 8 * 3 * F, hipMemcpyDeviceToHost));
+  HIPCHK(e, hipMemsetAsync(e->lst.fcnt, 0, 8, e->stream));
+  std::map<int64_t, std::vector<std::pair<int64_t, int64_t>>> by_win;   // window -> (arrival, kid)
+  for (unsigned long long j = 0; j < F; ++j) by_win[fl[3 * j + 1]].push_back({fl[3 * j + 2], fl[3 * j]});
+  e->phase_begin(FW_PHASE_LATE);
+  for (auto& wv : by_win) {
+    const int64_t n = wv.first;
+    auto& pr = wv.second;
+    std::sort(pr.begin(), pr.end());
+    // the window's elements, sorted by key id then arrival (its count from the live slices' counters)
+    std::vector<unsigned long long> cnts((size_t)e->s.P);
+    std::vector<int64_t> tags((size_t)e->s.P);
+    HIPCHK(e, hipMemcpy(cnts.data(), e->lst.cnt, 8 * (size_t)e->s.P, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(tags.data(), e->s.slice_tag, 8 * (size_t)e->s.P, hipMemcpyDeviceToHost));
+    int64_t N = 0;
+    for (int64_t mm = n * e->s.R; mm < n * e->s.R + e->s.K; ++mm) {
+      const int32_t pp = (int32_t)floor_mod(mm, e->s.P);
+      if (tags[(size_t)pp] == mm) N += (int64_t)std::min<unsigned long long>((unsigned long long)e->lst.cap, cnts[(size_t)pp]);
+    }
+    if (N == 0) continue;
+    if (int rc = list_sort_window(e, n, N)) return rc;   // kids in list_k2, positions in list_v1
+    const int64_t Fn = (int64_t)pr.size();
+    std::vector<int64_t> pairs(2 * (size_t)Fn), cnt(2 * (size_t)Fn), off((size_t)Fn);
+    for (int64_t j = 0; j < Fn; ++j) { pairs[2 * (size_t)j] = pr[(size_t)j].second; pairs[2 * (size_t)j + 1] = pr[(size_t)j].first; }
+    int64_t* dp = nullptr;
+    HIPCHK(e, hipMalloc(&dp, 8 * (size_t)(5 * Fn)));
+    HIPCHK(e, hipMemcpy(dp, pairs.data(), 16 * (size_t)Fn, hipMemcpyHostToDevice));
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((Fn + BLOCK - 1) / BLOCK, e->grid));
+    hipLaunchKernelGGL(k_list_fire_count, dim3(blocks), dim3(BLOCK), 0, e->stream, e->lst, e->list_k2, e->list_v1, N, dp,
+                       Fn, dp + 2 * Fn);
+    HIPCHK(e, hipMemcpyAsync(cnt.data(), dp + 2 * Fn, 16 * (size_t)Fn, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    int64_t tot = 0;
+    for (int64_t j = 0; j < Fn; ++j) { off[(size_t)j] = tot; tot += cnt[2 * (size_t)j + 1]; }
+    if (e->list_out + tot > e->cfg.out_capacity) {
+      (void)hipFree(dp);
+      return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded (list state)");
+    }
+    HIPCHK(e, hipMemcpy(dp + 4 * Fn, off.data(), 8 * (size_t)Fn, hipMemcpyHostToDevice));
+    const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)n * (uint64_t)e->s.slide)), e->s.size), 1);
+    hipLaunchKernelGGL(k_list_fire_emit, dim3((unsigned)std::min<int64_t>(Fn, 4096)), dim3(BLOCK), 0, e->stream, e->s,
+                       e->lst, e->list_v1, dp + 2 * Fn, dp + 4 * Fn, Fn, e->list_out, max_ts);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    (void)hipFree(dp);
+    e->list_out += tot;
+    e->late_fires_host += Fn;
+  }
+  hipLaunchKernelGGL(k_list_set_count, dim3(1), dim3(1), 0, e->stream, e->s, e->list_out);
+  e->phase_end((int64_t)F);
+  HIPCHK(e, hipGetLastError());
+  e->out_dirty = true;
   return FW_OK;
 }
 
@@ -205,9 +328,33 @@ static int list_grow(fw_engine* e, int64_t n) {
   return FW_OK;
 }
 
+// window n's N elements gathered and sorted: arrival order, then (stably) grouped by key id — the sorted key
+// ids in list_k2, the elements' buffer positions in list_v1
+static int list_sort_window(fw_engine* e, int64_t n, int64_t N) {
+  if (int rc = list_grow(e, N)) return rc;
+  const int kid_bits = bits_for((uint64_t)e->s.stride);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((N + BLOCK - 1) / BLOCK, e->grid));
+  hipLaunchKernelGGL(k_list_gather, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, n, e->list_k1, e->list_v1);
+  size_t tb = e->list_temp_bytes;
+  HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v1, e->list_v2, (size_t)N, 0, 64,
+                                      e->stream));
+  hipLaunchKernelGGL(k_list_kid, dim3(blocks), dim3(BLOCK), 0, e->stream, e->lst, e->list_v2, N, e->list_k1);
+  tb = e->list_temp_bytes;
+  HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v2, e->list_v1, (size_t)N, 0,
+                                      kid_bits, e->stream));
+  return FW_OK;
+}
+
 int list_watermark(fw_engine* e, int64_t wm) {
   if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
-    e->hmarks.push_back({wm, e->dev_marks - 1, false});
+    if (e->out_dirty) {   // per-element re-fires appended since the last device mark
+      hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
+      HIPCHK(e, hipGetLastError());
+      e->hmarks.push_back({wm, e->dev_marks++, true});
+      e->out_dirty = false;
+    } else {
+      e->hmarks.push_back({wm, e->dev_marks - 1, false});
+    }
     if (wm > e->cur_wm) e->cur_wm = wm;
     return FW_OK;
   }
@@ -216,22 +363,12 @@ int list_watermark(fw_engine* e, int64_t wm) {
   HIPCHK(e, hipMemcpyAsync(e->list_plan_h.data(), e->list_plan, 8 * LPLAN_WORDS, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   const int64_t nt = e->list_plan_h[0];
-  const int kid_bits = bits_for((uint64_t)e->s.stride);
   for (int64_t t = 0; t < nt; ++t) {
     const int64_t n = e->list_plan_h[2 + 2 * t], N = e->list_plan_h[3 + 2 * t];
     if (N == 0) continue;
     if (e->list_out + N > e->cfg.out_capacity) return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded (list state)");
-    if (int rc = list_grow(e, N)) return rc;
+    if (int rc = list_sort_window(e, n, N)) return rc;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((N + BLOCK - 1) / BLOCK, e->grid));
-    hipLaunchKernelGGL(k_list_gather, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, n, e->list_k1, e->list_v1);
-    size_t tb = e->list_temp_bytes;
-    // arrival order, then (stably) grouped by key id
-    HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v1, e->list_v2, (size_t)N, 0, 64,
-                                        e->stream));
-    hipLaunchKernelGGL(k_list_kid, dim3(blocks), dim3(BLOCK), 0, e->stream, e->lst, e->list_v2, N, e->list_k1);
-    tb = e->list_temp_bytes;
-    HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v2, e->list_v1, (size_t)N, 0,
-                                        kid_bits, e->stream));
     const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)n * (uint64_t)e->s.slide)), e->s.size), 1);
     hipLaunchKernelGGL(k_list_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, e->list_v1, N, e->list_out, max_ts);
     e->list_out += N;

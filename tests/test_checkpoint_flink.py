@@ -302,6 +302,55 @@ def test_restore_at_long_min_keeps_records_late_at_the_checkpoint(mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_restore_at_long_min_with_fired_but_kept_panes(mode):
+    """Allowed lateness 500: at the checkpoint some windows have fired and are kept for their lateness — their
+    panes carry only cleanup timers.  Restored at Long.MIN_VALUE (the reference's timer service restarts there,
+    HeapInternalTimerService.java:72), such a window fires again only for keys a record re-arms before the
+    watermark passes it (EventTimeTrigger.onElement registers maxTimestamp, :37-45), with the restored contents;
+    the other keys' panes wait for their cleanup.  Two subtasks by KeyGroupRangeAssignment, the same output as
+    the oracle restored the same way; a snapshot right after the restore writes the fixture bytes back."""
+    from flink_amd.keygroups import compute_key_group_range_for_operator_index, operator_index_np
+    from flink_amd.windowing import WindowEngine
+    from oracle.oracle import OracleEngine
+    sc = SCEN["tumbling_lateness_i64"]
+    mp, want, cw = sc["config"]["mp"], _expected(sc), sc["checkpoint_wm"]
+    # records for windows that fired before the checkpoint (and some that did not), pushed before any watermark
+    pre_keys = np.array([k for k in range(12)] * 3, np.int64)
+    pre_ts = np.array([cw - 450 + 37 * j for j in range(len(pre_keys))], np.int64)
+    pre_f1 = np.arange(len(pre_keys), dtype=np.int64) + 50_000
+    pre_v = np.arange(len(pre_keys), dtype=np.int64) * 11 + 5
+    eo = OracleEngine(_cfg(sc))
+    for kg, (st, tm) in want.items():
+        eo.restore_kg_flink(kg, sc["layout"], st, tm, LONG_MIN)
+    eo.push(pre_keys, pre_ts, pre_v, f1=pre_f1)
+    ro = [eo.collect()] + _drive(eo, sc, sc["cut"], len(sc["records"]), final=True)
+    eo.close()
+    pre_dest = operator_index_np(pre_keys, mp, 2)
+    dest = operator_index_np(np.array([r[0] for r in sc["records"]], np.int64), mp, 2)
+    per = []
+    for i in range(2):
+        lo, hi = compute_key_group_range_for_operator_index(mp, 2, i)
+        e = WindowEngine(_cfg(sc, kg=(lo, hi), mode=mode))
+        for kg in range(lo, hi + 1):
+            e.restore_kg_flink(kg, sc["layout"], *want[kg], watermark=LONG_MIN)
+        back = {kg: e.snapshot_kg_flink(kg, sc["layout"]) for kg in range(lo, hi + 1)}
+        assert _diff(back, {kg: want[kg] for kg in range(lo, hi + 1)}) is None
+        sel = pre_dest == i
+        e.push(pre_keys[sel], pre_ts[sel], pre_v[sel], f1=pre_f1[sel])
+        sub = dict(sc)
+        sub["records"] = [r if d == i else None for r, d in zip(sc["records"], dest)]
+        per.append([e.collect()] + _drive_sparse(e, sub, sc["cut"], len(sc["records"])))
+        e.close()
+    fields = ["sum_i64"]
+    got = _merge([epochs_of(r, fields, True) for r in per])
+    exp = _canon(epochs_of(ro, fields, True))
+    assert got == exp
+    refired = [r for _, recs in exp for r in recs if r[1] <= cw]
+    assert refired, "a window that fired before the checkpoint fired again after its re-arm"
+
+
+@pytest.mark.gpu
 def test_restore_rejections():
     from flink_amd import _abi
     from flink_amd.windowing import WindowEngine
@@ -310,10 +359,6 @@ def test_restore_rejections():
     kg = max(want, key=lambda k: len(want[k][0]))
     st, tm = want[kg]
     e = WindowEngine(_cfg(sc))
-    # fired-but-kept panes have no trigger timer: not what the panes imply at Long.MIN_VALUE
-    with pytest.raises(_abi.FwError) as ei:
-        e.restore_kg_flink(kg, sc["layout"], st, tm)
-    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
     with pytest.raises(_abi.FwError) as ei:
         e.restore_kg_flink(kg, sc["layout"], st[:-3], tm, sc["checkpoint_wm"])
     assert ei.value.code == _abi.FW_ERR_INVALID_ARG
