@@ -2347,19 +2347,22 @@ __global__ void k_fill_i64(int64_t* p, int64_t v, int64_t n) {
 // into the directory, claims the slice's slot and writes the pane — readStateTableForKeyGroup
 // (HeapKeyedStateBackend.java:318-349) putting (namespace, key) -> state into the state table
 // ------------------------------------------------------------------------------------------------
-__global__ void k_restore(Spec s, const int64_t* ent, int64_t n) {
+// wpane = 0: entries of slices (x[0] = slice number); 1: sliding windows' own panes (x[0] = window number, the
+// reference layout's per-window state restored as it is)
+__global__ void k_restore(Spec s, const int64_t* ent, int64_t n, int32_t wpane) {
+  const Cols& c = wpane ? s.wc : s.c;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t* x = ent + j * FW_SNAP_ENTRY_WORDS;
     const int64_t kid = dir_lookup(s, x[1]);
-    const int32_t p = slice_slot(s, x[0]);
+    const int32_t p = wpane ? slice_slot_at(s.wtag, s.W, x[0]) : slice_slot(s, x[0]);
     if (kid < 0 || p < 0) { cap_error(s, 15); continue; }
     const int64_t idx = (int64_t)p * s.stride + kid;
-    if (s.c.sum) s.c.sum[idx] = x[2];
-    if (s.c.mn) s.c.mn[idx] = x[3];
-    if (s.c.mx) s.c.mx[idx] = x[4];
-    if (s.c.cnt) s.c.cnt[idx] = x[5];
-    if (s.first) { s.c.first[idx] = x[6]; s.c.f1v[idx] = x[7]; }
-    else s.c.present[idx] = 1;
+    if (c.sum) c.sum[idx] = x[2];
+    if (c.mn) c.mn[idx] = x[3];
+    if (c.mx) c.mx[idx] = x[4];
+    if (c.cnt) c.cnt[idx] = x[5];
+    if (s.first) { c.first[idx] = x[6]; c.f1v[idx] = x[7]; }
+    else c.present[idx] = 1;
   }
 }
 
@@ -2590,6 +2593,7 @@ struct fw_engine {
   // fw_snapshot_kg: entries of every key group, built once per engine state (state_epoch)
   int64_t state_epoch = 0, snap_epoch = -1;
   std::vector<std::vector<int64_t>> snap_kg;
+  std::vector<std::vector<int64_t>> snap_wkg;   // sliding: the windows' own panes (entry word 0 = window number)
   std::vector<uint8_t> snap_has_key;   // per key group: a key of it is in the directory (it held window state)
   bool snap_any_key = false;
   std::vector<uint8_t> kg_touched;     // per key group: restored with present = 1 (fw_restore_kg_flink)
@@ -3779,6 +3783,7 @@ static int build_snapshot(fw_engine* e) {
     if (keys[k] != fw::EMPTY_KEY) kid_kg[k] = host_key_group(s, keys[k]);
   if (min_used) kid_kg[s.D] = host_key_group(s, fw::EMPTY_KEY);
   e->snap_kg.assign((size_t)mp, {});
+  e->snap_wkg.assign((size_t)mp, {});
   e->snap_unarmed.clear();
   e->snap_has_key.assign((size_t)mp, 0);
   e->snap_any_key = false;
@@ -3831,6 +3836,43 @@ static int build_snapshot(fw_engine* e) {
       v.insert(v.end(), ent, ent + FW_SNAP_ENTRY_WORDS);
     }
   }
+  // sliding: the windows' own panes (restored window state, records below offset - slide)
+  if (s.W > 0) {
+    std::vector<int64_t> wtags((size_t)s.W);
+    HIPCHK(e, hipMemcpy(wtags.data(), s.wtag, 8 * (size_t)s.W, hipMemcpyDeviceToHost));
+    for (int32_t w = 0; w < s.W; ++w) {
+      const int64_t n = wtags[(size_t)w];
+      if (n == fw::FREE_TAG) continue;
+      const size_t off = (size_t)w * st;
+      auto get = [&](std::vector<int64_t>& v, const int64_t* col) -> hipError_t {
+        if (!col) return hipSuccess;
+        v.resize(st);
+        return hipMemcpy(v.data(), col + off, 8 * st, hipMemcpyDeviceToHost);
+      };
+      HIPCHK(e, get(sum, s.wc.sum));
+      HIPCHK(e, get(mn, s.wc.mn));
+      HIPCHK(e, get(mx, s.wc.mx));
+      HIPCHK(e, get(cnt, s.wc.cnt));
+      if (s.first) {
+        HIPCHK(e, get(first, s.wc.first));
+        HIPCHK(e, get(f1v, s.wc.f1v));
+      } else {
+        present.resize(st);
+        HIPCHK(e, hipMemcpy(present.data(), s.wc.present + off, st, hipMemcpyDeviceToHost));
+      }
+      for (size_t k = 0; k < st; ++k) {
+        const bool pres = s.first ? first[k] != INT64_MAX : present[k] != 0;
+        if (!pres || kid_kg[k] < 0) continue;
+        const int64_t key = (int64_t)k == s.D ? fw::EMPTY_KEY : keys[k];
+        const int64_t ent[FW_SNAP_ENTRY_WORDS] = {
+            n, key, sum[k], s.wc.mn ? mn[k] : INT64_MAX, s.wc.mx ? mx[k] : INT64_MIN,
+            s.wc.cnt ? (s.by ? cnt[k] - e->ordinal : cnt[k]) : 0,
+            s.first ? first[k] - e->ordinal : -1, s.first ? f1v[k] : 0};
+        auto& v = e->snap_wkg[(size_t)kid_kg[k]];
+        v.insert(v.end(), ent, ent + FW_SNAP_ENTRY_WORDS);
+      }
+    }
+  }
   e->snap_epoch = e->state_epoch;
   return FW_OK;
 }
@@ -3862,7 +3904,7 @@ int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* le
   return FW_OK;
 }
 
-static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t n);
+static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t n, int32_t wpane = 0);
 
 int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   if (!e || !buf) return FW_ERR_INVALID_ARG;
@@ -3894,7 +3936,7 @@ int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
 }
 
 // load n validated snapshot entries (FW_SNAP_ENTRY_WORDS each) and set the watermark
-static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t n) {
+static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t n, int32_t wpane) {
   HIPCHK(e, hipSetDevice(e->dev));
   e->restored = true;
   e->cur_wm = wm;
@@ -3905,7 +3947,7 @@ static int restore_entries(fw_engine* e, int64_t wm, const int64_t* ent, int64_t
   hipError_t r = hipMemcpyAsync(d, ent, 8 * (size_t)n * FW_SNAP_ENTRY_WORDS, hipMemcpyHostToDevice, e->stream);
   if (r == hipSuccess) {
     const int blocks = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, 1024);
-    hipLaunchKernelGGL(fw::k_restore, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, d, n);
+    hipLaunchKernelGGL(fw::k_restore, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, d, n, wpane);
     r = hipGetLastError();
   }
   const hipError_t r2 = hipStreamSynchronize(e->stream);
@@ -3988,7 +4030,7 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
     p.cnt = x[5];               // maxBy/minBy: the extremal record's ordinal
     p.first = s.first ? x[6] : 0;
     p.f1 = x[7];
-    p.unarmed = tumbling && e->snap_unarmed.count({x[0], x[1]}) != 0;
+    p.unarmed = e->snap_unarmed.count({x[0], x[1]}) != 0 && tumbling;
     return p;
   };
   out.clear();
@@ -4009,10 +4051,17 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
   });
   std::map<std::pair<int64_t, int64_t>, KgPane> win;   // (window number, key)
   const bool f64 = s.vt == FW_VALUE_F64;
-  for (size_t j : ord) {
-    const int64_t* x = &v[j * FW_SNAP_ENTRY_WORDS];
+  // the windows' own panes first (restored window state: the earlier arrivals), then each slice into every
+  // window it makes up
+  const std::vector<int64_t>& wv = e->snap_wkg[(size_t)kg];
+  std::vector<std::pair<int64_t, const int64_t*>> items;   // (window number or -1 for a slice, entry)
+  for (size_t j = 0; j < wv.size() / FW_SNAP_ENTRY_WORDS; ++j) items.push_back({1, &wv[j * FW_SNAP_ENTRY_WORDS]});
+  for (size_t j : ord) items.push_back({0, &v[j * FW_SNAP_ENTRY_WORDS]});
+  for (const auto& item : items) {
+    const int64_t* x = item.second;
     const int64_t m = x[0];
-    for (int64_t w = fw::floor_div(m - s.K, s.R) + 1; w <= fw::floor_div(m, s.R); ++w) {
+    const int64_t w_lo = item.first ? m : fw::floor_div(m - s.K, s.R) + 1, w_hi = item.first ? m : fw::floor_div(m, s.R);
+    for (int64_t w = w_lo; w <= w_hi; ++w) {
       const int64_t start = host_window_start(c, w);
       if (fw::cleanup_time(fw::jsub(fw::jadd(start, c.size), 1), c.allowed_lateness) <= e->cur_wm) continue;
       KgPane b = pane_of(x, start);
@@ -4053,7 +4102,6 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
   if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
   if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
-  if (window_panes_used(e)) return reject(e, FW_ERR_UNSUPPORTED, "sliding windows: records below offset - slide put state in window panes, which no checkpoint layout carries");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -4173,9 +4221,10 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   if (rc) return rc;
   const fw_config& c = e->cfg;
   const fw::Spec& s = e->s;
-  if (c.assigner != FW_TUMBLING)
-    return reject(e, FW_ERR_UNSUPPORTED, "window-level state restores into tumbling windows only (sliding: "
-                                         "fw_restore_kg's slice blob)");
+  const bool sliding = c.assigner == FW_SLIDING;
+  if (sliding && c.allowed_lateness > 0)
+    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows with allowed lateness: window-level state restores into "
+                                         "tumbling windows, or sliding without lateness");
   if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0)
     return reject(e, FW_ERR_UNSUPPORTED, "PurgingTrigger with allowed lateness");
   if (e->restored && watermark != e->cur_wm)
@@ -4194,9 +4243,11 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
     std::set<std::pair<int64_t, int64_t>> seen;
     for (int32_t w = 0; w < nns && in.ok; ++w) {
       const int64_t start = in.i64(), end = in.i64();
-      const int64_t m = fw::floor_div(fw::jsub(start, c.offset), c.size);
+      // tumbling: the window's slice; sliding: the window number (its own pane holds the window's state)
+      const int64_t step = sliding ? c.slide : c.size;
+      const int64_t m = fw::floor_div(fw::jsub(start, c.offset), step);
       if (in.ok && (end != fw::jadd(start, c.size) || host_window_start(c, m) != start ||
-                    fw::window_start_with_offset(start, c.offset, c.size) != start))
+                    fw::window_start_with_offset(start, c.offset, step) != start))
         return reject(e, FW_ERR_INVALID_ARG, "namespace is not a window of this assigner");
       const int32_t ne = in.i32();
       if (ne < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
@@ -4295,7 +4346,7 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   for (const auto& t : got_in_order) e->restored_timer_rank[t] = (int64_t)e->restored_timer_rank.size();
   if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(s.kg_end - s.kg_start + 1), 0);
   if (present) e->kg_touched[(size_t)(kg - s.kg_start)] = 1;
-  return restore_entries(e, watermark, ent.data(), (int64_t)panes.size());
+  return restore_entries(e, watermark, ent.data(), (int64_t)panes.size(), sliding ? 1 : 0);
 }
 
 int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,

@@ -257,14 +257,18 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * A buffer argument NULL (or too small: FW_ERR_CAPACITY) stores the required lengths only.
  * *state_len == 0: no keyed state at all yet (no record accepted, nothing restored), for which
  * HeapKeyedStateBackend.snapshot writes no stream (:169-171).
- * Restore: before the first push; tumbling windows only (sliding state restores from fw_snapshot_kg's
- * slice blob); not with PurgingTrigger and allowed lateness > 0 (its purged panes keep cleanup timers).
+ * Restore: before the first push.  Tumbling windows restore into their slices; sliding windows (without
+ * allowed lateness) into each window's own pane (later records go to slices; a window fires its slices
+ * and its pane).  Not with PurgingTrigger and allowed lateness > 0 (its purged panes keep cleanup timers).
  * `watermark` is the engine's watermark after restore: the reference restarts its timer service at
  * Long.MIN_VALUE (currentWatermark is not checkpointed) — pass INT64_MIN for exactly that.  The engine's
  * timers are implicit (a pane's trigger timer is pending iff its window's maxTimestamp > watermark, its
- * cleanup timer iff the pane exists), so the blob's timers must be exactly the ones its panes imply at
- * `watermark` (FW_ERR_UNSUPPORTED otherwise: e.g. fired-but-kept panes, allowed lateness > 0, need the
- * checkpoint's watermark).  Every restored key group must use the same `watermark`. */
+ * cleanup timer iff the pane exists), so the blob's timers must be the ones its panes imply at `watermark`,
+ * with one exception the reference's own checkpoints produce: a tumbling window ahead of `watermark` whose
+ * panes carry no trigger timer (it fired before the checkpoint and is kept for its allowed lateness) is
+ * restored disarmed — it fires again only for keys whose records re-arm it before the watermark passes its
+ * maxTimestamp (EventTimeTrigger.onElement), otherwise it waits for its cleanup time.  Every restored key
+ * group must use the same `watermark`. */
 #define FW_SF_KEY    1   /* the key (the tuple's key field, e.g. f0)                          */
 #define FW_SF_F1     2   /* the pass-through field of the first arrival (maxBy/minBy: of the extremal record) */
 #define FW_SF_SUM    3

@@ -161,11 +161,23 @@ def test_engine_restore_continues_like_oracle(name, mode):
     """Restore the fixture's key groups (into two subtasks, each its KeyGroupRangeAssignment share), run the
     rest of the stream and a final MAX_WATERMARK: the same output as the oracle restored from the same
     bytes at the same watermark; a snapshot right after the restore writes the fixture bytes back."""
+    _restore_and_continue(SCEN[name], _restore_wm(SCEN[name]), mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_sliding_restore_into_window_panes(mode):
+    """Sliding windows in the reference layout hold one state per window (namespace = TimeWindow); the engine
+    restores each into that window's own pane (records after the restore go to slices, and a window fires
+    slices + pane) — restored at Long.MIN_VALUE, as the reference restarts its timers."""
+    _restore_and_continue(SCEN["sliding_i64"], LONG_MIN, mode)
+
+
+def _restore_and_continue(sc, wm, mode):
     from flink_amd.keygroups import compute_key_group_range_for_operator_index, operator_index_np
     from flink_amd.windowing import WindowEngine
     from oracle.oracle import OracleEngine
-    sc = SCEN[name]
-    mp, want, wm = sc["config"]["mp"], _expected(sc), _restore_wm(sc)
+    mp, want = sc["config"]["mp"], _expected(sc)
     eo = OracleEngine(_cfg(sc))
     for kg, (st, tm) in want.items():
         eo.restore_kg_flink(kg, sc["layout"], st, tm, wm)
@@ -372,7 +384,8 @@ def test_restore_rejections():
     with pytest.raises(_abi.FwError):
         e.restore_kg_flink((kg + 1) % 8, sc["layout"], *want[(kg + 1) % 8], sc["checkpoint_wm"] + 1)
     e.close()
-    sl = SCEN["sliding_i64"]
+    sl = dict(SCEN["sliding_i64"])
+    sl["config"] = dict(sl["config"], lateness=100)   # sliding + allowed lateness: no window-level restore
     e = WindowEngine(_cfg(sl))
     with pytest.raises(_abi.FwError) as ei:
         e.restore_kg_flink(0, sl["layout"], *_expected(sl)[0])
