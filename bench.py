@@ -159,7 +159,7 @@ def main():
     C = CONFIGS[args.config]
     n_keys, rate, batch, key_cap = C["keys"], C["rate"], C["batch"], C["key_cap"]
     fields, vt = C["reduce"]
-    total_steps = args.warmup + args.steps + args.prof_steps + args.h2d_steps
+    total_steps = args.warmup + args.steps + args.prof_steps + args.h2d_steps + args.decode_steps + 2
 
     from flink_amd.keygroups import compute_key_group_range_for_operator_index
     mp = 128
@@ -291,6 +291,29 @@ def main():
                "note": "fw_decode of one batch as Flink wire bytes in HBM (host-synchronous call incl. its count "
                        "readback); the window kernels not included"}
         del wire, out
+        # the drop-in path end to end: wire bytes in HBM -> fw_decode -> fw_push_batch of the decoded columns ->
+        # the watermark, per step (fresh batches after everything above, so their windows are live)
+        jd = args.warmup + args.steps + args.prof_steps + args.h2d_steps + 2
+        wires = []
+        for j in range(jd, jd + args.decode_steps):
+            k, t, v = stream(j * batch, batch, n_keys, rate, T0, device=dev, value_type=vt, zipf=C["zipf"], ooo=C["ooo"])
+            wires.append(torch.cat([head, be(t), be(k), be(t), be(v)], dim=1).reshape(-1).contiguous())
+        eng.sync()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        for q, w in enumerate(wires):
+            o = eng.decode(w, ["long", "long", "long"], key=0, f1=1, value=2, record_cap=n, device=True)
+            m = o["n_records"]
+            eng.push(o["key"][:m], o["ts"][:m], o["value"][:m], f1=o["f1"][:m])
+            eng.advance_watermark(wm_of(jd + q))
+        eng.sync()
+        torch.cuda.synchronize()
+        dtw = (time.perf_counter() - t3) / args.decode_steps
+        dec["decode_window"] = {"value": n / dtw, "unit": "events/s", "GB_s_in": wires[0].numel() / dtw / 1e9,
+                                "note": "wire bytes in HBM -> fw_decode -> fw_push_batch -> fw_advance_watermark per "
+                                        "batch (the drop-in path from network buffers), host-synchronous decode"}
+        collected.append(eng.collect())
+        del wires
 
     if world > 1:
         import torch.distributed as dist

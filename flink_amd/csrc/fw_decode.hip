@@ -9,21 +9,31 @@
 // TupleSerializer.serialize's fields in order (flink-core/.../typeutils/runtime/TupleSerializer.java:120-129).
 //
 // Finding element boundaries is the sequential part of the receiver (one length after another,
-// SpillingAdaptiveSpanningRecordDeserializer).  Here the bytes are cut into 4 KiB chunks; every chunk
-// follows the length chain from each offset an element could start at (elements are shorter than
+// SpillingAdaptiveSpanningRecordDeserializer).  Here the bytes are cut into 512-byte chunks; for every chunk
+// one lane follows the length chain from each offset an element could start at (elements are shorter than
 // DEC_MAXE bytes), validating every step against the lengths and tags the schema allows.  Chains from
 // different offsets merge within a few elements and the ones off the boundaries die at a bad length or
 // tag, so the surviving chains of a chunk nearly always leave it at one offset: the next chunk's entry,
 // known without the chunks before.  The rare chunks whose survivors disagree are linked one after
-// another.  A second pass walks each chunk's true chain once and decodes its elements in parallel.
+// another.  Then each chunk's true chain is walked twice more, once to count its records and markers
+// (an exclusive scan places them) and once to decode them.  One lane per chunk throughout: a chain is a
+// sequence of dependent steps, so a wave keeps 64 chains going (one chunk per workgroup, walked by one
+// lane, left the other 63 idle and cost ~1 ms per 4 Mi records).
 #pragma once
 
 namespace fw {
 
-constexpr int DEC_CHUNK = 4096;    // bytes per chunk
-constexpr int DEC_THREADS = 128;   // >= DEC_MAXE: one lane per candidate entry offset
+constexpr int DEC_CHUNK = 512;     // bytes per chunk
 constexpr int DEC_MAXE = 4 + 1 + 8 + 8 * FW_DECODE_MAX_FIELDS;   // longest element with its length prefix
-constexpr int DEC_MAXEL = DEC_CHUNK / 13 + 2;   // element starts per chunk (the shortest element: 4 + 9 bytes)
+constexpr int DEC_T = 64;          // chunks per workgroup, one lane of wave 0 each: the workgroup's chunks are
+                                   // staged in LDS with 16-B loads (a lane walking its chunk in global memory
+                                   // issued one uncoalesced byte load per field byte: ~1 line request per lane-byte)
+constexpr int DEC_TW = 256;        // threads per workgroup: all stage the chunks (one round of loads) and decode
+constexpr int DEC_SPILL = 68;      // bytes after a chunk an element starting in it can reach (>= DEC_MAXE)
+constexpr int DEC_STRIDE = DEC_CHUNK + DEC_SPILL;   // LDS bytes per chunk: 145 words apart (odd), so the 64
+                                   // lanes reading the same offset of their chunks hit 64 different banks
+constexpr int DEC_LDS = DEC_T * DEC_STRIDE;
+constexpr int DEC_SCAN = 1024;     // chunks per level-1 scan block
 
 struct DecSpec {
   const uint8_t* bytes;
@@ -43,8 +53,22 @@ __device__ __forceinline__ uint64_t be_u64(const uint8_t* p) {
 __device__ __forceinline__ uint32_t be_u32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
 }
+// the same from 4-byte aligned LDS words: two (three) word reads and byte alignment instead of 4 (8) byte reads
+__device__ __forceinline__ uint32_t lds_be_u32(const uint8_t* p) {
+  const uint32_t a = (uint32_t)(uintptr_t)p & 3u;
+  const uint32_t* w = (const uint32_t*)(p - a);
+  const uint32_t x = __builtin_amdgcn_alignbyte(w[1], w[0], a);
+  return __builtin_bswap32(x);
+}
+__device__ __forceinline__ uint64_t lds_be_u64(const uint8_t* p) {
+  const uint32_t a = (uint32_t)(uintptr_t)p & 3u;
+  const uint32_t* w = (const uint32_t*)(p - a);
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, a), hi = __builtin_amdgcn_alignbyte(w2, w1, a);
+  return ((uint64_t)__builtin_bswap32(lo) << 32) | (uint64_t)__builtin_bswap32(hi);
+}
 
-// kind of the element whose prefix is at p: 0 record, 1 watermark, 2 latency marker, -1 not an element
+// kind of the element with length len and tag: 0 record, 1 watermark, 2 latency marker, -1 not an element
 __device__ __forceinline__ int dec_kind(const DecSpec& d, uint32_t len, uint8_t tag) {
   if (tag == 0 && len == (uint32_t)d.rec_ts_len) return 0;
   if (tag == 1 && len == (uint32_t)d.rec_len) return 0;
@@ -53,136 +77,209 @@ __device__ __forceinline__ int dec_kind(const DecSpec& d, uint32_t len, uint8_t 
   return -1;
 }
 
-// table entry per (chunk, candidate): alive | exit offset + 32768 (<< 1) | records (<< 17) | watermarks
-// (<< 33) | latency markers (<< 49).  exit = where the chain leaves the chunk, relative to its end
-// (negative: the stream ends inside an element that starts in this chunk)
-__device__ __forceinline__ uint64_t dec_pack(bool alive, int exit, uint32_t nr, uint32_t nw, uint32_t nl) {
-  return (alive ? 1ull : 0ull) | ((uint64_t)(exit + 32768) << 1) | ((uint64_t)nr << 17) | ((uint64_t)nw << 33) |
-         ((uint64_t)nl << 49);
+// the chain from offset e of chunk c: DEC_DEAD (a step that is no element), or where it leaves the chunk
+// relative to the chunk's end (negative: the stream ends inside an element starting in this chunk)
+constexpr int DEC_DEAD = INT32_MIN;
+struct DecChunk {
+  const uint8_t* b;   // the chunk's first byte (in LDS)
+  int clen;           // its bytes
+  int64_t rem;        // bytes of the stream from its first byte on
+};
+// the workgroup's DEC_T chunks into LDS, each at DEC_STRIDE with its own copy of the DEC_SPILL bytes after it
+// (the next chunk's first ones), then this lane's chunk.  Global loads of 16 B, LDS stores of 4 B
+__device__ __forceinline__ void dec_put4(uint8_t* buf, int q, uint32_t w) {   // the word at group offset q
+  const int i = q / DEC_CHUNK, o = q % DEC_CHUNK;
+  if (i < DEC_T) *(uint32_t*)(buf + i * DEC_STRIDE + o) = w;
+  if (i > 0 && o < DEC_SPILL) *(uint32_t*)(buf + (i - 1) * DEC_STRIDE + DEC_CHUNK + o) = w;
 }
-__device__ __forceinline__ bool dec_alive(uint64_t t) { return t & 1ull; }
-__device__ __forceinline__ int dec_exit(uint64_t t) { return (int)((t >> 1) & 0xFFFF) - 32768; }
-
-__global__ __launch_bounds__(DEC_THREADS) void k_dec_scan(DecSpec d, uint64_t* table, int32_t* conv) {
-  __shared__ uint8_t buf[DEC_CHUNK + 8];
-  __shared__ int32_t agree;   // the common exit of the surviving chains; INT32_MIN: none survived; INT32_MAX: differ
-  const int64_t c = blockIdx.x;
+__device__ __forceinline__ void dec_put1(uint8_t* buf, int q, uint8_t b) {
+  const int i = q / DEC_CHUNK, o = q % DEC_CHUNK;
+  if (i < DEC_T) buf[i * DEC_STRIDE + o] = b;
+  if (i > 0 && o < DEC_SPILL) buf[(i - 1) * DEC_STRIDE + DEC_CHUNK + o] = b;
+}
+__device__ __forceinline__ DecChunk dec_stage_group(const DecSpec& d, uint8_t* buf) {
+  const int64_t g0 = (int64_t)blockIdx.x * DEC_T * DEC_CHUNK;
+  const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
+  const uint8_t* src = d.bytes + g0;
+  int done = 0;
+  if (((uintptr_t)src & 15) == 0) {
+    const int nv = len >> 4;
+    constexpr int NU = (DEC_T * DEC_CHUNK + DEC_SPILL + 16 * DEC_TW - 1) / (16 * DEC_TW);   // one round of loads
+    for (int i0 = 0; i0 < nv; i0 += NU * DEC_TW) {
+      uint4 v[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) { const int i = i0 + u * DEC_TW + (int)threadIdx.x; if (i < nv) v[u] = ((const uint4*)src)[i]; }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int i = i0 + u * DEC_TW + (int)threadIdx.x;
+        if (i < nv) { dec_put4(buf, 16 * i, v[u].x); dec_put4(buf, 16 * i + 4, v[u].y); dec_put4(buf, 16 * i + 8, v[u].z); dec_put4(buf, 16 * i + 12, v[u].w); }
+      }
+    }
+    done = nv << 4;
+  }
+  for (int i = done + (int)threadIdx.x; i < len; i += DEC_TW) dec_put1(buf, i, src[i]);
+  __syncthreads();
+  const int lane = (int)threadIdx.x & (DEC_T - 1);   // (only wave 0 walks)
+  const int64_t c = (int64_t)blockIdx.x * DEC_T + lane;
   const int64_t start = c * DEC_CHUNK;
-  const int clen = (int)min<int64_t>(DEC_CHUNK, d.nbytes - start);
-  const int slen = (int)min<int64_t>(DEC_CHUNK + 8, d.nbytes - start);
-  for (int i = threadIdx.x; i < slen; i += DEC_THREADS) buf[i] = d.bytes[start + i];
-  if (threadIdx.x == 0) agree = INT32_MIN;
-  __syncthreads();
-  const int e = threadIdx.x;
-  if (e < d.maxe) {
-    int pos = e;
-    bool alive = e < clen;   // a true entry lies inside the chunk (an element cut by the end ends the chain before)
-    uint32_t nr = 0, nw = 0, nl = 0;
-    int exit = 0;
-    while (alive && pos < clen) {
-      if (pos + 5 > slen) { exit = pos - clen; break; }          // prefix + tag beyond the stream's end
-      const uint32_t len = be_u32(buf + pos);
-      const int k = dec_kind(d, len, buf[pos + 4]);
-      if (k < 0) { alive = false; break; }
-      if (start + pos + 4 + (int64_t)len > d.nbytes) { exit = pos - clen; break; }   // cut by the end
-      nr += k == 0; nw += k == 1; nl += k == 2;
-      pos += 4 + (int)len;
-      exit = pos - clen;
-    }
-    if (alive && pos >= clen) exit = pos - clen;
-    table[c * d.maxe + e] = dec_pack(alive, exit, nr, nw, nl);
-    if (alive) {
-      const int cur = atomicCAS(&agree, INT32_MIN, exit);
-      if (cur != INT32_MIN && cur != exit) atomicExch(&agree, INT32_MAX);
-    }
+  return {buf + lane * DEC_STRIDE, (int)max<int64_t>(0, min<int64_t>(DEC_CHUNK, d.nbytes - start)), d.nbytes - start};
+}
+template <typename F>
+__device__ __forceinline__ int dec_walk(const DecSpec& d, const DecChunk& ch, int e, F&& on_element) {
+  int pos = e;
+  while (pos < ch.clen) {
+    if (pos + 5 > ch.rem) return pos - ch.clen;                       // prefix + tag beyond the stream's end
+    const uint32_t len = lds_be_u32(ch.b + pos);
+    const int k = dec_kind(d, len, ch.b[pos + 4]);
+    if (k < 0) return DEC_DEAD;
+    if (pos + 4 + (int64_t)len > ch.rem) return pos - ch.clen;        // cut by the end: the next call's
+    on_element(pos, k);
+    pos += 4 + (int)len;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) conv[c] = agree;
+  return pos - ch.clen;
 }
 
-// entry offset of every chunk (the stream starts at an element boundary), then the exclusive prefix of
-// each chunk's records / watermarks / latency markers.  One workgroup.
-constexpr int DEC_LINK_THREADS = 1024;
-__global__ __launch_bounds__(DEC_LINK_THREADS) void k_dec_link(DecSpec d, const uint64_t* table, const int32_t* conv,
-                                                              int32_t* entry, int64_t* base, int64_t* totals,
-                                                              int64_t* unknown, int32_t* err) {
-  __shared__ int64_t wsum[3][DEC_LINK_THREADS / 64];
-  __shared__ int32_t nunk;
-  const int NT = DEC_LINK_THREADS;
-  const int64_t per = (d.nchunks + NT - 1) / NT;
-  const int64_t c0 = (int64_t)threadIdx.x * per, c1 = min(c0 + per, d.nchunks);
-  // entries known from the previous chunk's agreeing survivors
-  int32_t unk = 0;
-  for (int64_t c = c0; c < c1; ++c) {
-    int32_t en;
-    if (c == 0) en = 0;
-    else {
-      const int32_t a = conv[c - 1];
-      // -3: corrupt, -2: resolve in order, -1: the stream ended inside the previous chunk's last element
-      en = (a == INT32_MIN) ? -3 : (a == INT32_MAX) ? -2 : (a < 0 ? -1 : a);
+// per chunk: the exit every surviving candidate chain agrees on (INT32_MIN: none survived, INT32_MAX: they
+// differ — then every candidate's exit goes to table[c][e] for the in-order resolution)
+__global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* table, int32_t* conv) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
+  const DecChunk ch = dec_stage_group(d, buf);
+  const int64_t c = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
+  if (threadIdx.x >= DEC_T || c >= d.nchunks) return;
+  // every candidate entry (a true one lies inside the chunk), one step per iteration of a single loop: each
+  // lane's steps run back to back whatever candidate they belong to, so the wave does not wait, candidate by
+  // candidate, for the one lane whose true chain it is (nested loops cost ~10x the steps)
+  int32_t agree = INT32_MIN;
+  const int lim = min(d.maxe, ch.clen);
+  int e = 0, pos = 0;
+  while (e < lim) {
+    int x = DEC_DEAD;
+    bool fin = true;
+    if (pos >= ch.clen || pos + 5 > ch.rem) {
+      x = pos - ch.clen;
+    } else {
+      const uint32_t len = lds_be_u32(ch.b + pos);
+      if (dec_kind(d, len, ch.b[pos + 4]) < 0) x = DEC_DEAD;
+      else if (pos + 4 + (int64_t)len > ch.rem) x = pos - ch.clen;
+      else { pos += 4 + (int)len; fin = false; }
     }
-    entry[c] = en;
-    unk += en == -2;
+    if (fin) {
+      if (x != DEC_DEAD) agree = agree == INT32_MIN ? x : (agree == x ? agree : INT32_MAX);
+      pos = ++e;
+    }
   }
-  // the undecided chunks, in order, into one list
-  int64_t u = unk;
+  conv[c] = agree;
+  if (agree == INT32_MAX)
+    for (int e = 0; e < d.maxe; ++e) table[c * d.maxe + e] = e < ch.clen ? dec_walk(d, ch, e, [](int, int) {}) : DEC_DEAD;
+}
+
+// every chunk's entry offset known from the previous chunk's agreeing survivors (-2: undecided, -3: corrupt,
+// -1: the stream ended inside the previous chunk's last element); undecided chunks (rare) listed for k_dec_fix
+__global__ __launch_bounds__(DEC_T) void k_dec_entry(DecSpec d, const int32_t* conv, int32_t* entry, int64_t* unknown,
+                                                    unsigned long long* n_unknown) {
+  const int64_t c = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
+  if (c >= d.nchunks) return;
+  int32_t en = 0;
+  if (c > 0) {
+    const int32_t a = conv[c - 1];
+    en = (a == INT32_MIN) ? -3 : (a == INT32_MAX) ? -2 : (a < 0 ? -1 : a);
+  }
+  entry[c] = en;
+  if (en == -2) unknown[atomicAdd(n_unknown, 1ull)] = c;
+}
+
+// the undecided chunks, in stream order: each one's entry from its predecessor's resolved chain (one thread;
+// nearly always nothing to do)
+__global__ void k_dec_fix(DecSpec d, const int32_t* table, int32_t* entry, int64_t* unknown,
+                          const unsigned long long* n_unknown) {
+  const int64_t nu = (int64_t)*n_unknown;
+  for (int64_t i = 1; i < nu; ++i)   // insertion sort of the list (atomic appends: any order)
+    for (int64_t j = i; j > 0 && unknown[j - 1] > unknown[j]; --j) { const int64_t t = unknown[j]; unknown[j] = unknown[j - 1]; unknown[j - 1] = t; }
+  for (int64_t i = 0; i < nu; ++i) {
+    const int64_t c = unknown[i];
+    const int32_t prev = entry[c - 1];
+    if (prev < 0) { entry[c] = prev == -1 ? -1 : -3; continue; }
+    const int32_t x = table[(c - 1) * d.maxe + prev];   // (c - 1 is a disagreeing chunk: its row is written)
+    entry[c] = x == DEC_DEAD ? -3 : x < 0 ? -1 : x;
+  }
+}
+
+// per chunk along its true chain: records, watermarks, latency markers (cnt3) and the chain's exit; a corrupt
+// chunk (no chain leads to its entry, or the chain dies) flagged
+__global__ __launch_bounds__(DEC_TW) void k_dec_count(DecSpec d, const int32_t* entry, int64_t* cnt3, int32_t* cexit,
+                                                    int32_t* err) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
+  const DecChunk ch = dec_stage_group(d, buf);
+  const int64_t c = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
+  if (threadIdx.x >= DEC_T || c >= d.nchunks) return;
+  const int32_t en = entry[c];
+  int64_t n[3] = {0, 0, 0};
+  int32_t x = DEC_DEAD;
+  if (en == -3) atomicExch(err, 1);
+  if (en >= 0) {
+    x = dec_walk(d, ch, en, [&](int, int k) { n[k]++; });
+    if (x == DEC_DEAD) { atomicExch(err, 1); n[0] = n[1] = n[2] = 0; }
+  }
+  cnt3[3 * c] = n[0]; cnt3[3 * c + 1] = n[1]; cnt3[3 * c + 2] = n[2];
+  cexit[c] = x;
+}
+
+// exclusive prefix of the chunks' counts, level 1: within blocks of DEC_SCAN chunks (base), block totals (btot)
+__global__ __launch_bounds__(DEC_SCAN) void k_dec_bscan(DecSpec d, const int64_t* cnt3, int64_t* base, int64_t* btot) {
+  __shared__ int64_t ws[3][DEC_SCAN / 64];
+  const int64_t c = (int64_t)blockIdx.x * DEC_SCAN + threadIdx.x;
+  int64_t v[3] = {0, 0, 0};
+  if (c < d.nchunks) { v[0] = cnt3[3 * c]; v[1] = cnt3[3 * c + 1]; v[2] = cnt3[3 * c + 2]; }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int64_t incl = u;
-  for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(incl, o); if (lane >= o) incl += y; }
-  if (lane == 63) wsum[0][wv] = incl;
-  __syncthreads();
-  int64_t off = incl - u;
-  for (int w = 0; w < wv; ++w) off += wsum[0][w];
-  if (threadIdx.x == NT - 1) nunk = (int32_t)(off + u);
-  for (int64_t c = c0; c < c1; ++c) if (entry[c] == -2) unknown[off++] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {   // nearly always empty
-    for (int32_t i = 0; i < nunk; ++i) {
-      const int64_t c = unknown[i];
-      const int32_t prev = entry[c - 1];
-      if (prev < 0) { entry[c] = prev == -1 ? -1 : -3; continue; }
-      const uint64_t t = table[(c - 1) * d.maxe + prev];
-      entry[c] = !dec_alive(t) ? -3 : dec_exit(t) < 0 ? -1 : dec_exit(t);
-    }
-  }
-  __syncthreads();
-  // per chunk: its counts along the true chain (the chain past a cut element: the chunks after carry
-  // nothing), then the exclusive prefix
-  int64_t cnt[3] = {0, 0, 0};
-  for (int64_t c = c0; c < c1; ++c) {
-    const int32_t en = entry[c];
-    if (en == -3 || (en >= 0 && !dec_alive(table[c * d.maxe + en]))) { atomicExch(err, 1); continue; }
-    if (en < 0) continue;
-    const uint64_t t = table[c * d.maxe + en];
-    cnt[0] += (t >> 17) & 0xFFFF; cnt[1] += (t >> 33) & 0xFFFF; cnt[2] += (t >> 49) & 0x7FFF;
-  }
-  int64_t offs[3];
+#pragma unroll
   for (int k = 0; k < 3; ++k) {
-    int64_t in = cnt[k];
+    int64_t in = v[k];
     for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(in, o); if (lane >= o) in += y; }
-    __syncthreads();
-    if (lane == 63) wsum[k][wv] = in;
-    __syncthreads();
-    offs[k] = in - cnt[k];
-    for (int w = 0; w < wv; ++w) offs[k] += wsum[k][w];
-    if (threadIdx.x == NT - 1) totals[k] = offs[k] + cnt[k];
+    if (lane == 63) ws[k][wv] = in;
+    v[k] = in - v[k];   // exclusive within the wave
   }
-  for (int64_t c = c0; c < c1; ++c) {
-    base[3 * c + 0] = offs[0]; base[3 * c + 1] = offs[1]; base[3 * c + 2] = offs[2];
-    const int32_t en = entry[c];
-    if (en < 0 || !dec_alive(table[c * d.maxe + en])) continue;
-    const uint64_t t = table[c * d.maxe + en];
-    offs[0] += (t >> 17) & 0xFFFF; offs[1] += (t >> 33) & 0xFFFF; offs[2] += (t >> 49) & 0x7FFF;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    int64_t off = 0, tot = 0;
+    for (int w = 0; w < DEC_SCAN / 64; ++w) { off += w < wv ? ws[k][w] : 0; tot += ws[k][w]; }
+    if (c < d.nchunks) base[3 * c + k] = v[k] + off;
+    if (threadIdx.x == 0) btot[3 * blockIdx.x + k] = tot;
   }
+}
+
+// level 2: the blocks' exclusive offsets (in place), the totals and the bytes of whole elements.  One workgroup
+__global__ __launch_bounds__(DEC_SCAN) void k_dec_top(DecSpec d, const int32_t* entry, const int32_t* cexit, int64_t* btot,
+                                                     int64_t nblk, int64_t* totals) {
+  __shared__ int64_t ws[3][DEC_SCAN / 64];
+  const int64_t per = (nblk + DEC_SCAN - 1) / DEC_SCAN;
+  const int64_t b0 = (int64_t)threadIdx.x * per, b1 = min(b0 + per, nblk);
+  int64_t sum[3] = {0, 0, 0};
+  for (int64_t b = b0; b < b1; ++b) for (int k = 0; k < 3; ++k) sum[k] += btot[3 * b + k];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t ex[3];
+  for (int k = 0; k < 3; ++k) {
+    int64_t in = sum[k];
+    for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(in, o); if (lane >= o) in += y; }
+    if (lane == 63) ws[k][wv] = in;
+    ex[k] = in - sum[k];
+  }
+  __syncthreads();
+  for (int k = 0; k < 3; ++k) {
+    int64_t off = 0, tot = 0;
+    for (int w = 0; w < DEC_SCAN / 64; ++w) { off += w < wv ? ws[k][w] : 0; tot += ws[k][w]; }
+    ex[k] += off;
+    if (threadIdx.x == 0) totals[k] = tot;
+  }
+  for (int64_t b = b0; b < b1; ++b)
+    for (int k = 0; k < 3; ++k) { const int64_t t = btot[3 * b + k]; btot[3 * b + k] = ex[k]; ex[k] += t; }
   // bytes of whole elements: up to the last chunk's chain end
   if (threadIdx.x == 0) {
     int64_t consumed = 0;
     for (int64_t c = d.nchunks - 1; c >= 0; --c) {
-      const int32_t en = entry[c];
-      if (en < 0) continue;
-      const uint64_t t = table[c * d.maxe + en];
+      if (entry[c] < 0 || cexit[c] == DEC_DEAD) continue;
       const int64_t clen = min<int64_t>(DEC_CHUNK, d.nbytes - c * DEC_CHUNK);
-      consumed = c * DEC_CHUNK + clen + dec_exit(t);
+      consumed = c * DEC_CHUNK + clen + cexit[c];
       break;
     }
     totals[3] = consumed;
@@ -195,66 +292,67 @@ struct DecOut {
   int64_t record_cap, marker_cap;
 };
 
-__global__ __launch_bounds__(DEC_THREADS) void k_dec_emit(DecSpec d, const int32_t* entry, const int64_t* base,
-                                                         DecOut o, int32_t* err) {
-  __shared__ uint8_t buf[DEC_CHUNK + DEC_MAXE + 8];
-  __shared__ int16_t el_pos[DEC_MAXEL];     // element start (prefix) within the chunk
-  __shared__ int16_t el_rank[DEC_MAXEL];    // index among the chunk's elements of its kind
-  __shared__ int8_t el_kind[DEC_MAXEL];
-  __shared__ int32_t nel;
-  const int64_t c = blockIdx.x;
-  const int32_t en = entry[c];
-  if (en < 0) return;   // uniform: past the stream's last whole element
-  const int64_t start = c * DEC_CHUNK;
-  const int clen = (int)min<int64_t>(DEC_CHUNK, d.nbytes - start);
-  const int slen = (int)min<int64_t>(DEC_CHUNK + DEC_MAXE + 8, d.nbytes - start);
-  for (int i = threadIdx.x; i < slen; i += DEC_THREADS) buf[i] = d.bytes[start + i];
+// each chunk's true chain once more: every lane lists its records' LDS positions at their rank within the
+// workgroup (its chunks' records are one contiguous run of the output), and the workgroup then decodes them
+// in rank order, so the column stores are coalesced; markers (rare) are written by their lane
+constexpr int DEC_MAXREC = DEC_T * (DEC_CHUNK / 13 + 1);   // records of a workgroup's chunks, at most
+__global__ __launch_bounds__(DEC_TW) void k_dec_emit(DecSpec d, const int32_t* entry, const int64_t* base_in,
+                                                   const int64_t* btop, DecOut o, int32_t* err) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
+  __shared__ uint16_t rpos[DEC_MAXREC];   // LDS position of each record's tag
+  __shared__ int64_t r0_s;
+  __shared__ int32_t nrec_s;
+  const DecChunk ch = dec_stage_group(d, buf);
+  const int64_t c = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
+  const int64_t cfirst = (int64_t)blockIdx.x * DEC_T;
+  const int64_t bfirst = cfirst / DEC_SCAN;
+  if (threadIdx.x == 0) { r0_s = btop[3 * bfirst] + base_in[3 * cfirst]; nrec_s = 0; }
   __syncthreads();
-  if (threadIdx.x == 0) {   // the chunk's true chain, once
-    int pos = en, n = 0, r[3] = {0, 0, 0};
-    while (pos < clen && pos + 5 <= slen && n < DEC_MAXEL) {
-      const uint32_t len = be_u32(buf + pos);
-      const int k = dec_kind(d, len, buf[pos + 4]);
-      if (k < 0) { atomicExch(err, 1); break; }
-      if (start + pos + 4 + (int64_t)len > d.nbytes) break;   // cut by the end: the next call's
-      el_pos[n] = (int16_t)pos; el_kind[n] = (int8_t)k; el_rank[n] = (int16_t)r[k]++;
-      ++n;
-      pos += 4 + (int)len;
-    }
-    nel = n;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nel; i += DEC_THREADS) {
-    const uint8_t* p = buf + el_pos[i] + 4;   // the tag
-    const int k = el_kind[i];
-    if (k == 0) {
-      const int64_t j = base[3 * c] + el_rank[i];
-      if (j >= o.record_cap) { atomicExch(err, 2); continue; }
-      const bool has_ts = p[0] == 0;
-      const int64_t ts = has_ts ? (int64_t)be_u64(p + 1) : INT64_MIN;
-      const uint8_t* t = p + (has_ts ? 9 : 1);
-      const int64_t key = d.key_int ? (int64_t)(int32_t)be_u32(t + d.key_off) : (int64_t)be_u64(t + d.key_off);
-      o.key[j] = key;
-      if (o.key_hash) o.key_hash[j] = (int32_t)key;   // Integer.hashCode
-      o.ts[j] = ts;
-      o.f1[j] = d.f1_off < 0 ? ts : d.f1_int ? (int64_t)(int32_t)be_u32(t + d.f1_off) : (int64_t)be_u64(t + d.f1_off);
-      o.val[j] = (int64_t)be_u64(t + d.val_off);
-    } else {
-      const int64_t j = base[3 * c + k] + el_rank[i];
-      // position: the records before it (this chunk's before element i, found backwards: markers are rare)
-      int32_t before = 0;
-      for (int q = i - 1; q >= 0; --q) if (el_kind[q] == 0) { before = el_rank[q] + 1; break; }
-      const int64_t rpos = base[3 * c] + before;
-      if (j >= o.marker_cap) { atomicExch(err, 2); continue; }
-      if (k == 1) {
-        o.wm[j] = (int64_t)be_u64(p + 1);
-        o.wm_pos[j] = rpos;
-      } else {   // latency marker: markedTime, then vertexId << 32 | subtaskIndex
-        o.lm[2 * j] = (int64_t)be_u64(p + 1);
-        o.lm[2 * j + 1] = (int64_t)(((uint64_t)be_u32(p + 9) << 32) | be_u32(p + 13));
-        o.lm_pos[j] = rpos;
+  const int32_t en = (threadIdx.x < DEC_T && c < d.nchunks) ? entry[c] : -1;
+  int32_t nr = 0;
+  if (en >= 0) {   // past the stream's last whole element (or corrupt: reported by k_dec_count) otherwise
+    const int64_t blk = c / DEC_SCAN;
+    int64_t j[3] = {btop[3 * blk] + base_in[3 * c], btop[3 * blk + 1] + base_in[3 * c + 1], btop[3 * blk + 2] + base_in[3 * c + 2]};
+    const int64_t r0 = r0_s;
+    (void)dec_walk(d, ch, en, [&](int pos, int k) {
+      const uint8_t* p = ch.b + pos + 4;   // the tag
+      if (k == 0) {
+        const int64_t r = j[0]++;
+        const int64_t rl = r - r0;
+        if (rl >= 0 && rl < DEC_MAXREC) rpos[rl] = (uint16_t)(p - buf);
+        ++nr;
+        return;
       }
-    }
+      const int64_t m = j[k]++;
+      if (m >= o.marker_cap) { atomicExch(err, 2); return; }
+      if (k == 1) {
+        o.wm[m] = (int64_t)lds_be_u64(p + 1);
+        o.wm_pos[m] = j[0];   // the records before it
+      } else {   // latency marker: markedTime, then vertexId << 32 | subtaskIndex
+        o.lm[2 * m] = (int64_t)lds_be_u64(p + 1);
+        o.lm[2 * m + 1] = (int64_t)(((uint64_t)lds_be_u32(p + 9) << 32) | lds_be_u32(p + 13));
+        o.lm_pos[m] = j[0];
+      }
+    });
+  }
+  if (nr) atomicAdd(&nrec_s, nr);
+  __syncthreads();
+  // the workgroup's records, in rank order
+  const int nrec = min(nrec_s, DEC_MAXREC);
+  const int64_t r0 = r0_s;
+  for (int rl = threadIdx.x; rl < nrec; rl += DEC_TW) {
+    const int64_t r = r0 + rl;
+    if (r >= o.record_cap) { atomicExch(err, 2); continue; }
+    const uint8_t* p = buf + rpos[rl];
+    const bool has_ts = p[0] == 0;
+    const int64_t ts = has_ts ? (int64_t)lds_be_u64(p + 1) : INT64_MIN;
+    const uint8_t* t = p + (has_ts ? 9 : 1);
+    const int64_t key = d.key_int ? (int64_t)(int32_t)lds_be_u32(t + d.key_off) : (int64_t)lds_be_u64(t + d.key_off);
+    o.key[r] = key;
+    if (o.key_hash) o.key_hash[r] = (int32_t)key;   // Integer.hashCode
+    o.ts[r] = ts;
+    o.f1[r] = d.f1_off < 0 ? ts : d.f1_int ? (int64_t)(int32_t)lds_be_u32(t + d.f1_off) : (int64_t)lds_be_u64(t + d.f1_off);
+    o.val[r] = (int64_t)lds_be_u64(t + d.val_off);
   }
 }
 
@@ -310,8 +408,9 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
     return r;
   };
   const size_t nc = (size_t)d.nchunks;
-  HIPCHK(e, grow(e->dec_table, e->dec_table_cap, nc * (size_t)d.maxe * 8));
-  HIPCHK(e, grow(e->dec_small, e->dec_small_cap, nc * (4 + 4 + 8 + 24) + 64));
+  HIPCHK(e, grow(e->dec_table, e->dec_table_cap, nc * (size_t)d.maxe * 4));
+  const size_t nblk = (nc + DEC_SCAN - 1) / DEC_SCAN;
+  HIPCHK(e, grow(e->dec_small, e->dec_small_cap, nc * (4 + 4 + 4 + 8 + 24 + 24) + nblk * 24 + 128));
   const uint8_t* src = (const uint8_t*)bytes;
   if (mem == FW_MEM_HOST) {
     HIPCHK(e, grow(e->dec_bytes, e->dec_bytes_cap, (size_t)nbytes));
@@ -326,13 +425,21 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   int64_t* base = unknown + nc;
   int64_t* totals = base + 3 * nc;   // [4] records, watermarks, latency markers, consumed bytes
   int32_t* err = (int32_t*)(totals + 4);
-  HIPCHK(e, hipMemsetAsync(err, 0, 4, e->stream));
-  uint64_t* table = (uint64_t*)e->dec_table;
-  hipLaunchKernelGGL(k_dec_scan, dim3((unsigned)nc), dim3(DEC_THREADS), 0, e->stream, d, table, conv);
-  hipLaunchKernelGGL(k_dec_link, dim3(1), dim3(DEC_LINK_THREADS), 0, e->stream, d, table, conv, entry, base, totals,
-                     unknown, err);
+  unsigned long long* n_unknown = (unsigned long long*)(totals + 5);
+  int64_t* cnt3 = totals + 6;   // [3 nc] each chunk's counts along its entry's chain
+  int64_t* btot = cnt3 + 3 * nc;   // [3 nblk] block totals, then their exclusive offsets
+  int32_t* cexit = (int32_t*)(btot + 3 * nblk);   // [nc] where each chunk's true chain leaves it
+  HIPCHK(e, hipMemsetAsync(err, 0, 16, e->stream));   // err and n_unknown
+  int32_t* table = (int32_t*)e->dec_table;
+  const unsigned gb = (unsigned)((nc + DEC_T - 1) / DEC_T);
+  hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, table, conv);
+  hipLaunchKernelGGL(k_dec_entry, dim3(gb), dim3(DEC_T), 0, e->stream, d, conv, entry, unknown, n_unknown);
+  hipLaunchKernelGGL(k_dec_fix, dim3(1), dim3(1), 0, e->stream, d, table, entry, unknown, n_unknown);
+  hipLaunchKernelGGL(k_dec_count, dim3(gb), dim3(DEC_TW), 0, e->stream, d, entry, cnt3, cexit, err);
+  hipLaunchKernelGGL(k_dec_bscan, dim3((unsigned)nblk), dim3(DEC_SCAN), 0, e->stream, d, cnt3, base, btot);
+  hipLaunchKernelGGL(k_dec_top, dim3(1), dim3(DEC_SCAN), 0, e->stream, d, entry, cexit, btot, (int64_t)nblk, totals);
   DecOut o{key, f1, ts, (int64_t*)value, wm, wm_pos, lm, lm_pos, key_hash, record_cap, marker_cap};
-  hipLaunchKernelGGL(k_dec_emit, dim3((unsigned)nc), dim3(DEC_THREADS), 0, e->stream, d, entry, base, o, err);
+  hipLaunchKernelGGL(k_dec_emit, dim3(gb), dim3(DEC_TW), 0, e->stream, d, entry, base, btot, o, err);
   HIPCHK(e, hipGetLastError());
   int64_t tot[4];
   int32_t herr = 0;

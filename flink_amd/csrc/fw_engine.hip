@@ -2566,6 +2566,7 @@ struct fw_engine {
   bool has_client = false;            // set by fw_set_stream; the handle itself may be 0 (the null stream)
   bool serial = false;                // diagnostics (FW_SERIAL=1): k_route on the engine stream too
   bool no_consumed = false;           // diagnostics (FW_NO_CONSUMED=1): no per-push consumption event
+  bool debug_late = false;            // FW_DEBUG_LATE=1: check every skipped late-count read-back (fires_possible)
   bool event_query = true;            // skip stream waits on events already complete (FW_EVENT_QUERY=0: off)
   hipEvent_t ev_in = nullptr;         // client work up to a push (input columns ready)
   static constexpr int NCONS = 8;
@@ -3010,6 +3011,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   e->serial = getenv("FW_SERIAL") && atoi(getenv("FW_SERIAL")) != 0;
   e->event_query = !(getenv("FW_EVENT_QUERY") && atoi(getenv("FW_EVENT_QUERY")) == 0);
   e->no_consumed = getenv("FW_NO_CONSUMED") && atoi(getenv("FW_NO_CONSUMED")) != 0;
+  e->debug_late = getenv("FW_DEBUG_LATE") && atoi(getenv("FW_DEBUG_LATE")) != 0;
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_now, hipEventDisableTiming));
@@ -3434,6 +3436,14 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
                        e->stream, e->s, e->new_list, df1, e->ordinal, n);
     e->phase_end(n);
+  }
+  if (e->debug_late && e->cfg.allowed_lateness > 0 && !e->session && !e->list && !fires_possible(e->s, e->cur_wm)) {
+    // diagnostics: the read-back skipped below must have had nothing to read
+    unsigned long long nl = 0, nf = 0;
+    HIPCHK(e, hipMemcpyAsync(&nl, e->late_count, 8, hipMemcpyDeviceToHost, e->stream));
+    if (e->fire_count) HIPCHK(e, hipMemcpyAsync(&nf, e->fire_count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (nl || nf) return fail(e, FW_ERR_INVALID_ARG, "internal: per-element fires at a watermark fires_possible() ruled out");
   }
   if (e->cfg.allowed_lateness > 0 && !e->session && !e->list && fires_possible(e->s, e->cur_wm)) {
     // per-element fires: the list lengths on the host size the sorts

@@ -185,6 +185,24 @@ def test_zipf_out_of_order_lateness(hip, oracle_engine, mode):
     assert sg["records_late"] == so["records_late"] and so["records_late"] > 0
 
 
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("spec", [(1000, 1000, 370, -6_000), (3000, 1000, 750, 6_000)])
+def test_lateness_read_back_skip(hip, oracle_engine, monkeypatch, mode, spec):
+    """The push skips reading the late-record counts back when no window of the assigner's grid is within its
+    lateness at the watermark (fires_possible: window maxTimestamps are offset + size - 1 modulo the step).
+    With FW_DEBUG_LATE=1 every skipped read-back is checked to have had nothing to read.  Offsets, negative
+    timestamps, and watermarks landing right outside and inside the lateness period (lag swept through it)."""
+    from flink_amd.windowing import SlidingEventTimeWindows, TumblingEventTimeWindows
+    monkeypatch.setenv("FW_DEBUG_LATE", "1")
+    size, slide, off, t0 = spec   # (sliding: no timestamps below offset - slide, whose extra window has no re-fire)
+    a = TumblingEventTimeWindows.of(size, off) if size == slide else SlidingEventTimeWindows.of(size, slide, off)
+    for lag in (0, 1, 99, 100, 101):
+        keys, ts, vals = gen_stream(40_000, 500, rate=1 << 12, ooo=250, t0=t0)
+        cfg = _cfgm(mode, a, ("sum", "count"), first=True, lateness=100)
+        sg, so = _run_both(hip, oracle_engine, cfg, keys, ts, vals, 1000, lag, ["sum_i64", "count"], first=True)
+        assert sg["late_fires"] == so["late_fires"] and sg["records_late"] == so["records_late"]
+
+
 @pytest.mark.parametrize("case", ["sum_count_lateness", "f64_min_max", "max_by", "purging", "min_no_first"])
 def test_hot_buckets_split_over_helpers(hip, oracle_engine, monkeypatch, case):
     """Zipf(1.3) keys concentrate the records in a few directory buckets; with FW_DEBUG_AGG & 64 a share
