@@ -2531,10 +2531,11 @@ struct ListDev {
 };
 
 // session windows (fw_session.hip): per key id `sw` window slots, key-major [D + 1][sw]
-constexpr int SESS_SW_DEFAULT = 32, SESS_SW_MAX = 64;   // in-flight session windows per key
+constexpr int SESS_SW_DEFAULT = 32, SESS_SW_MAX = 256;   // in-flight session windows per key
 struct SessDev {
   int64_t gap;
   int32_t sw;
+  int32_t nw;       // 64-bit words of a key's slot masks (1, 2 or 4)
   int64_t* start;   // window [start, end)
   int64_t* end;
   int64_t* sum;     // accumulator: sum (long / double bits), min / max codes, count
@@ -2970,7 +2971,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->list && (c.agg_flags & FW_AGGF_FOLD)) return unsupported("list state: no fold");
   if (e->list) { c.ingest_mode = 1; c.keep_first_f1 = 1; e->cfg = c; }
   if (e->session) {
-    if (c.max_open_slices > SESS_SW_MAX) return bad("session windows: at most 64 in-flight sessions per key (max_open_slices)");
+    if (c.max_open_slices > SESS_SW_MAX) return bad("session windows: at most 256 in-flight sessions per key (max_open_slices)");
     e->sess.sw = c.max_open_slices > 0 ? c.max_open_slices : SESS_SW_DEFAULT;
     c.slide = c.size; c.offset = 0; c.max_open_slices = 1; c.ingest_mode = 1; e->cfg = c;
   }

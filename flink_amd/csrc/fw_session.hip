@@ -6,10 +6,10 @@
 // EventTimeSessionWindows.withGap (EventTimeSessionWindows.java:53-56) with a reducing state (sum / min / max /
 // count, first-arrival f1, maxBy / minBy) or a list state (WindowedStream.apply: the window's elements).
 //
-// Layout in HBM: per key id (the engine's key directory) `sw` window slots (max_open_slices, default 32),
-// key-major ([D + 1][sw]) so one key's windows share cache lines: window start / end and the accumulator
-// (sum, min / max codes, count); per key two bit masks: slots in flight, slots whose trigger timer is
-// pending.
+// Layout in HBM: per key id (the engine's key directory) `sw` window slots (max_open_slices, default 32, up to
+// 256), key-major ([D + 1][sw]) so one key's windows share cache lines: window start / end and the accumulator
+// (sum, min / max codes, count, f1); per key two bit masks of 1, 2 or 4 words: slots in flight, slots whose
+// trigger timer is pending.
 //
 // A batch (every record of it sees the same watermark): k_sess_prep resolves each record's key id,
 // rocPRIM sorts (key id, arrival index), and k_sess_walk runs one thread per key over that key's records in
@@ -139,9 +139,38 @@ __global__ __launch_bounds__(BLOCK) void k_sess_prep(Spec s, BatchIn b, unsigned
   }
 }
 
+// a key's window slots as a bit set of NW 64-bit words (sw <= 64 NW slots)
+template <int NW>
+struct SBits {
+  uint64_t w[NW];
+  __device__ __forceinline__ static SBits none() { SBits b; for (int i = 0; i < NW; ++i) b.w[i] = 0; return b; }
+  __device__ __forceinline__ static SBits low(int n) {   // slots [0, n)
+    SBits b;
+    for (int i = 0; i < NW; ++i) b.w[i] = n >= 64 * (i + 1) ? ~0ull : (n <= 64 * i ? 0ull : (1ull << (n - 64 * i)) - 1);
+    return b;
+  }
+  __device__ __forceinline__ static SBits load(const unsigned long long* p) { SBits b; for (int i = 0; i < NW; ++i) b.w[i] = p[i]; return b; }
+  __device__ __forceinline__ void store(unsigned long long* p) const { for (int i = 0; i < NW; ++i) p[i] = w[i]; }
+  __device__ __forceinline__ bool any() const { uint64_t x = 0; for (int i = 0; i < NW; ++i) x |= w[i]; return x != 0; }
+  __device__ __forceinline__ int count() const { int c = 0; for (int i = 0; i < NW; ++i) c += __popcll(w[i]); return c; }
+  __device__ __forceinline__ bool test(int q) const { return (w[q >> 6] >> (q & 63)) & 1ull; }
+  __device__ __forceinline__ void set(int q) { w[q >> 6] |= 1ull << (q & 63); }
+  __device__ __forceinline__ void clr(int q) { w[q >> 6] &= ~(1ull << (q & 63)); }
+  __device__ __forceinline__ SBits andnot(const SBits& o) const { SBits b; for (int i = 0; i < NW; ++i) b.w[i] = w[i] & ~o.w[i]; return b; }
+  __device__ __forceinline__ SBits operator|(const SBits& o) const { SBits b; for (int i = 0; i < NW; ++i) b.w[i] = w[i] | o.w[i]; return b; }
+  __device__ __forceinline__ bool operator!=(const SBits& o) const { bool d = false; for (int i = 0; i < NW; ++i) d |= w[i] != o.w[i]; return d; }
+  __device__ __forceinline__ int first() const {   // lowest slot, -1 if none
+    for (int i = 0; i < NW; ++i) if (w[i]) return 64 * i + __ffsll((long long)w[i]) - 1;
+    return -1;
+  }
+  __device__ __forceinline__ int pop() { const int q = first(); if (q >= 0) clr(q); return q; }
+};
+
 // one thread per key (the head of its run in the sorted keys): the key's records in arrival order
+template <int NW>
 __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn b, const unsigned long long* sorted,
                                                      int64_t n, int32_t idx_bits) {
+  typedef SBits<NW> B;
   const int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j0 >= n) return;
   const unsigned long long k0 = sorted[j0];
@@ -154,14 +183,14 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   const int64_t base = kid * d.sw;
   const int64_t* st = d.start + base;
   const int64_t* en = d.end + base;
-  uint64_t live = d.live[kid], trig = d.trig[kid];
-  const uint64_t all = d.sw == 64 ? ~0ull : (1ull << d.sw) - 1;
+  B live = B::load(d.live + kid * NW), trig = B::load(d.trig + kid * NW);
+  const B all = B::low(d.sw);
   unsigned long long late = 0, fires = 0;
   // retire a slot: its trigger and cleanup timers gone; list state frees its elements (a reducing state is
   // overwritten by the slot's next window)
   auto retire = [&](int q) {
-    live &= ~(1ull << q);
-    trig &= ~(1ull << q);
+    live.clr(q);
+    trig.clr(q);
     if (d.list) sess_list_free(d, base + q);
   };
   for (int64_t j = j0; j < n; ++j) {
@@ -180,34 +209,34 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
     a.by = s.by;
     // MergingWindowSet.addWindow: the new window's connected group of intersecting in-flight windows
     int64_t cs = ts, ce = jadd(ts, d.gap);
-    uint64_t mask = 0;
+    B mask = B::none();
     for (;;) {
-      uint64_t grew = 0;
-      for (uint64_t m = live & ~mask; m; m &= m - 1) {
-        const int q = __ffsll((long long)m) - 1;
-        if (cs <= en[q] && ce >= st[q]) { cs = min(cs, st[q]); ce = max(ce, en[q]); grew |= 1ull << q; }
+      B grew = B::none();
+      for (B m = live.andnot(mask); m.any();) {
+        const int q = m.pop();
+        if (cs <= en[q] && ce >= st[q]) { cs = min(cs, st[q]); ce = max(ce, en[q]); grew.set(q); }
       }
-      if (!grew) break;
-      mask |= grew;
+      if (!grew.any()) break;
+      mask = mask | grew;
     }
     int r = -1;          // slot of the resulting window
     bool fresh = false;
-    if (mask == 0) {
+    if (!mask.any()) {
       fresh = true;
     } else {
-      r = __ffsll((long long)mask) - 1;
-      const bool contained = __popcll(mask) == 1 && st[r] == cs && en[r] == ce;   // new window inside an existing one
+      r = mask.first();
+      const bool contained = mask.count() == 1 && st[r] == cs && en[r] == ce;   // new window inside an existing one
       if (!contained) {
         // merge: the group's HashSet holds the merged in-flight windows and the new one (distinct from all of
         // them here); iterated by (bucket, insertion = start order), the first window's state is the target,
         // the others' states reduce in that order into one result added to it.  EventTimeTrigger.onMerge
         // registers the merged window's timer, the merged windows' timers go.
-        const uint32_t cap = sess_set_cap(__popcll(mask) + 1);
+        const uint32_t cap = sess_set_cap(mask.count() + 1);
         auto before = [&](int c, uint32_t bc, int q, uint32_t bq) { return q < 0 || bc < bq || (bc == bq && st[c] < st[q]); };
         int t = -1;
         uint32_t tb = 0;
-        for (uint64_t m = mask; m; m &= m - 1) {   // the target: least (bucket, start)
-          const int c = __ffsll((long long)m) - 1;
+        for (B m = mask; m.any();) {   // the target: least (bucket, start)
+          const int c = m.pop();
           const uint32_t bc = sess_bucket(st[c], en[c], cap);
           if (before(c, bc, t, tb)) { t = c; tb = bc; }
         }
@@ -215,15 +244,17 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
         bool have = false;
         int64_t lh = -1, lt = -1, ll = 0;
         if (d.list) { lh = d.head[base + t]; lt = d.tail[base + t]; ll = d.len[base + t]; }
-        for (uint64_t todo = mask & ~(1ull << t); todo;) {   // the sources in iteration order
+        B todo = mask;
+        todo.clr(t);
+        while (todo.any()) {   // the sources in iteration order
           int q = -1;
           uint32_t bq = 0;
-          for (uint64_t m = todo; m; m &= m - 1) {
-            const int c = __ffsll((long long)m) - 1;
+          for (B m = todo; m.any();) {
+            const int c = m.pop();
             const uint32_t bc = sess_bucket(st[c], en[c], cap);
             if (before(c, bc, q, bq)) { q = c; bq = bc; }
           }
-          todo &= ~(1ull << q);
+          todo.clr(q);
           const int64_t x = base + q;
           if (d.list) {   // the source's elements appended (mergePartitionedStates, list branch :315-333)
             if (d.len[x] > 0) {
@@ -246,8 +277,11 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
         } else if (have) {
           sess_store(d, base + t, sess_combine(s, sess_load(s, d, base + t), res));   // HeapReducingState.add
         }
-        live &= ~(mask & ~(1ull << t));
-        trig = (trig & ~mask) | (1ull << t);
+        B others = mask;
+        others.clr(t);
+        live = live.andnot(others);
+        trig = trig.andnot(mask);
+        trig.set(t);
         r = t;
         d.start[base + r] = cs;
         d.end[base + r] = ce;
@@ -260,11 +294,10 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       continue;
     }
     if (fresh) {
-      const uint64_t freem = ~live & all;
-      if (freem == 0) { cap_error(s, 21); continue; }   // more in-flight sessions for the key than slots
-      r = __ffsll((long long)freem) - 1;
-      live |= 1ull << r;
-      trig &= ~(1ull << r);
+      r = all.andnot(live).first();
+      if (r < 0) { cap_error(s, 21); continue; }   // more in-flight sessions for the key than slots
+      live.set(r);
+      trig.clr(r);
       d.start[base + r] = cs;
       d.end[base + r] = ce;
       if (d.list) d.len[base + r] = 0;
@@ -277,7 +310,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       const int64_t e = ord % d.pcap;
       if (d.pord[e] >= 0) {   // that entry still holds a buffered element: list_capacity exceeded
         cap_error(s, 26);
-        if (fresh) live &= ~(1ull << r);
+        if (fresh) live.clr(r);
         continue;
       }
       d.pord[e] = ord;
@@ -303,49 +336,50 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       ++fires;
       if (purging) retire(r);   // FIRE_AND_PURGE: cleanup(actualWindow)
     } else {
-      trig |= 1ull << r;
+      trig.set(r);
     }
   }
-  d.live[kid] = live;
-  d.trig[kid] = trig;
+  live.store(d.live + kid * NW);
+  trig.store(d.trig + kid * NW);
   if (late) atomicAdd(&s.stats[ST_LATE], late);
   if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
 }
 
 // a watermark: every in-flight window's timers up to wm_new.  One thread per key; lane by lane the it-th window of
 // each key, so the wave's appends stay aggregated (list state: one append per window, its element count)
+template <int NW>
 __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm_new) {
+  typedef SBits<NW> B;
   const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
   const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x; k0 < s.stride; k0 += gstride) {   // uniform per wave
     const int64_t kid = k0 + threadIdx.x;
-    uint64_t live = kid < s.stride ? d.live[kid] : 0, trig = kid < s.stride ? d.trig[kid] : 0;
-    const uint64_t live0 = live, trig0 = trig;
-    int nl = __popcll(live);
+    B live = kid < s.stride ? B::load(d.live + kid * NW) : B::none(), trig = kid < s.stride ? B::load(d.trig + kid * NW) : B::none();
+    const B live0 = live, trig0 = trig;
+    int nl = live.count();
     for (int o = 32; o > 0; o >>= 1) nl = max(nl, __shfl_xor(nl, o));
-    uint64_t todo = live;
+    B todo = live;
     for (int it = 0; it < nl; ++it) {
       bool fire = false;
       int q = -1;
       int64_t start = 0, max_ts = 0;
-      if (todo) {
-        q = __ffsll((long long)todo) - 1;
-        todo &= todo - 1;
+      if (todo.any()) {
+        q = todo.pop();
         const int64_t x = kid * d.sw + q;
         start = d.start[x];
         max_ts = jsub(d.end[x], 1);
         const int64_t ct = cleanup_time(max_ts, s.lateness);
         bool retire = false;
-        if (((trig >> q) & 1ull) && max_ts <= wm_new) {   // onEventTime(maxTimestamp): FIRE
+        if (trig.test(q) && max_ts <= wm_new) {   // onEventTime(maxTimestamp): FIRE
           fire = true;
-          trig &= ~(1ull << q);
+          trig.clr(q);
           if (purging || ct == max_ts) retire = true;       // FIRE_AND_PURGE, or isCleanupTime
         }
         if (!retire && ct <= wm_new) {                    // onEventTime(cleanupTime): cleanup
           if (!fire && ct == max_ts) fire = true;         // (one timer at maxTimestamp == cleanupTime)
           retire = true;
         }
-        if (retire) { live &= ~(1ull << q); trig &= ~(1ull << q); }
+        if (retire) { live.clr(q); trig.clr(q); }
         if (d.list) {   // list state: every element of the window, then (retired) its pool entries freed
           if (fire) sess_list_emit(s, d, x, kid_key(s, kid), start, max_ts);
           if (retire) sess_list_free(d, x);
@@ -357,8 +391,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
       }
       wave_count(&s.stats[ST_FIRED], fire);
     }
-    if (live != live0) d.live[kid] = live;
-    if (trig != trig0) d.trig[kid] = trig;
+    if (live != live0) live.store(d.live + kid * NW);
+    if (trig != trig0) trig.store(d.trig + kid * NW);
   }
 }
 
@@ -393,8 +427,9 @@ int session_create(fw_engine* e) {
     d.pnext = e->alloc<int64_t>((size_t)d.pcap);
     d.pord = e->alloc<int64_t>((size_t)d.pcap);
   }
-  d.live = e->alloc<unsigned long long>((size_t)s.stride);
-  d.trig = e->alloc<unsigned long long>((size_t)s.stride);
+  d.nw = (d.sw + 63) / 64 <= 1 ? 1 : (d.sw + 63) / 64 <= 2 ? 2 : 4;   // words of a key's slot masks
+  d.live = e->alloc<unsigned long long>((size_t)s.stride * d.nw);
+  d.trig = e->alloc<unsigned long long>((size_t)s.stride * d.nw);
   e->s.o.win_start = e->alloc<int64_t>((size_t)e->cfg.out_capacity);
   const size_t nb = (size_t)e->cfg.max_batch;
   e->sess_key = e->alloc<unsigned long long>(nb);
@@ -407,12 +442,12 @@ int session_create(fw_engine* e) {
   e->sess_temp_bytes = tb;
   e->sess_temp = e->alloc<char>(tb);
   for (void* p : e->allocs) if (!p) return FW_ERR_DEVICE;
-  HIPCHK(e, hipMemsetAsync(d.live, 0, 8 * (size_t)s.stride, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.live, 0, 8 * (size_t)s.stride * d.nw, e->stream));
   if (d.list) {
     HIPCHK(e, hipMemsetAsync(d.pord, 0xFF, 8 * (size_t)d.pcap, e->stream));   // every pool entry free (-1)
     HIPCHK(e, hipMemsetAsync(d.len, 0, 8 * cells, e->stream));
   }
-  HIPCHK(e, hipMemsetAsync(d.trig, 0, 8 * (size_t)s.stride, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.trig, 0, 8 * (size_t)s.stride * d.nw, e->stream));
   return FW_OK;
 }
 
@@ -423,8 +458,10 @@ int session_push(fw_engine* e, const BatchIn& b) {
   size_t tb = e->sess_temp_bytes;
   HIPCHK(e, rocprim::radix_sort_keys(e->sess_temp, tb, e->sess_key, e->sess_sorted, (size_t)b.n, 0, e->sess_key_bits,
                                      e->stream));
-  hipLaunchKernelGGL(k_sess_walk, dim3((unsigned)((b.n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, e->stream, e->s, e->sess, b,
-                     e->sess_sorted, b.n, e->sess_idx_bits);
+  const dim3 g((unsigned)((b.n + BLOCK - 1) / BLOCK));
+  if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_walk<1>, g, dim3(BLOCK), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
+  else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_walk<2>, g, dim3(BLOCK), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
+  else hipLaunchKernelGGL(k_sess_walk<4>, g, dim3(BLOCK), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
   e->phase_end(b.n);
   HIPCHK(e, hipGetLastError());
   if (e->cfg.allowed_lateness > 0) e->out_dirty = true;   // per-element fires may have appended
@@ -435,7 +472,9 @@ int session_watermark(fw_engine* e, int64_t wm) {
   if (wm > e->cur_wm) {
     e->phase_begin(FW_PHASE_FIRE);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid));
-    hipLaunchKernelGGL(k_sess_wm, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
+    if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_wm<1>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
+    else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_wm<2>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
+    else hipLaunchKernelGGL(k_sess_wm<4>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
     e->phase_end(e->s.stride);
     e->cur_wm = wm;
     hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);

@@ -66,7 +66,7 @@ extern "C" {
                                     merged windows in the JDK HashSet iteration order TimeWindow.mergeWindows
                                     produces (state window = the first one's; the others reduced / their lists
                                     appended in that order), so f1, ties and double sums match the reference.
-                                    At most 64 in-flight sessions per key (max_open_slices, default 32:
+                                    At most 256 in-flight sessions per key (max_open_slices, default 32:
                                     FW_ERR_CAPACITY beyond).  No checkpoint (the merging-window set is keyed
                                     list state of its own). */
 

@@ -239,6 +239,28 @@ def test_session_rejections(hip):
     e.close()
 
 
+@pytest.mark.parametrize("slots,batch,lag", [(100, 200, 8000), (256, 500, 30_000)])
+def test_session_many_in_flight(hip, oracle_engine, slots, batch, lag):
+    """Far more in-flight sessions per key than one 64-bit slot mask holds (MergingWindowSet has no bound;
+    the engine takes up to 256 per key): a slow watermark over hot keys with short gaps, and late records that
+    bridge sessions, against the oracle."""
+    rng = np.random.default_rng(slots)
+    n = 6000   # ~200 ms apart per key, gap 20: nearly every record a session; at most 84 / 240 in flight per key
+    keys = rng.integers(0, 6, n).astype(np.int64)
+    ts = (np.sort(rng.integers(0, 200_000, n)) - rng.integers(0, 3000, n)).astype(np.int64)
+    vals = rng.integers(-1000, 1000, n).astype(np.int64)
+    cfg = _cfg(20, ("sum", "count"), lateness=400, max_open_slices=slots, max_batch=1 << 14)
+    g = _both(hip, oracle_engine, cfg, keys, ts, vals, batch, lag, ["sum_i64", "count"])
+    assert sum(len(r) for _, r in g) > 1000
+    if slots == 100:   # the same stream with 64 slots runs out of them: the test does exceed one mask word
+        from flink_amd import _abi
+        e = hip(_cfg(20, ("sum", "count"), lateness=400, max_open_slices=64, max_batch=1 << 14))
+        with pytest.raises(_abi.FwError) as ei:
+            drive(e, keys, ts, vals, batch, lag, LONG_MAX)
+        assert ei.value.code == _abi.FW_ERR_CAPACITY
+        e.close()
+
+
 def test_session_capacity_error(hip):
     """More in-flight sessions for one key than the engine's slots: FW_ERR_CAPACITY, not a wrong answer."""
     from flink_amd import _abi
