@@ -272,6 +272,7 @@ def main():
     # wire-format ingest: the batch as Flink network bytes (length-prefixed StreamElementSerializer records of
     # Tuple3<Long key, Long f1, Long value> with timestamps), resident in HBM, decoded by fw_decode
     dec = None
+    dec_sums = []
     if args.decode_steps > 0 and exch is None and vt == "i64":
         k, t, v = cols[0]
         n = k.numel()
@@ -298,6 +299,7 @@ def main():
         for j in range(jd, jd + args.decode_steps):
             k, t, v = stream(j * batch, batch, n_keys, rate, T0, device=dev, value_type=vt, zipf=C["zipf"], ooo=C["ooo"])
             wires.append(torch.cat([head, be(t), be(k), be(t), be(v)], dim=1).reshape(-1).contiguous())
+            dec_sums.append(int(v.sum().item()))   # these batches enter the window state too (checksum below)
         eng.sync()
         torch.cuda.synchronize()
         t3 = time.perf_counter()
@@ -335,6 +337,8 @@ def main():
             pushed = 0
             for k, t, v in pushed_cols:
                 pushed = (pushed + (int(v.sum().item()) & mask)) & mask      # int64 tensor sums wrap
+            for x in dec_sums:
+                pushed = (pushed + (x & mask)) & mask
         else:
             fired = int(np.concatenate([r["count"] for r in collected]).sum())
             pushed = windows_per_record * sum(int(k.numel()) for k, t, v in pushed_cols)

@@ -2568,6 +2568,7 @@ struct fw_engine {
   bool serial = false;                // diagnostics (FW_SERIAL=1): k_route on the engine stream too
   bool no_consumed = false;           // diagnostics (FW_NO_CONSUMED=1): no per-push consumption event
   bool debug_late = false;            // FW_DEBUG_LATE=1: check every skipped late-count read-back (fires_possible)
+  bool debug_sync = false;            // FW_DEBUG_SYNC=1: synchronise after each list / session launch, naming it
   bool event_query = true;            // skip stream waits on events already complete (FW_EVENT_QUERY=0: off)
   hipEvent_t ev_in = nullptr;         // client work up to a push (input columns ready)
   static constexpr int NCONS = 8;
@@ -2771,6 +2772,10 @@ static int fail(fw_engine* e, int code, const std::string& msg) {
 }
 #define HIPCHK(e, x) do { hipError_t _r = (x); if (_r != hipSuccess) \
   return fail(e, FW_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_r)); } while (0)
+// diagnostics (FW_DEBUG_SYNC=1): the launch just made, waited for and named when it failed
+#define DBGSYNC(e, what) do { if ((e)->debug_sync) { hipError_t _r = hipGetLastError(); \
+  if (_r == hipSuccess) _r = hipStreamSynchronize((e)->stream); \
+  if (_r != hipSuccess) return fail(e, FW_ERR_DEVICE, std::string("after ") + (what) + ": " + hipGetErrorString(_r)); } } while (0)
 
 static int launch_fill(fw_engine* e, int64_t* p, int64_t v, int64_t n) {
   if (!p || n <= 0) return FW_OK;
@@ -3013,6 +3018,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   e->event_query = !(getenv("FW_EVENT_QUERY") && atoi(getenv("FW_EVENT_QUERY")) == 0);
   e->no_consumed = getenv("FW_NO_CONSUMED") && atoi(getenv("FW_NO_CONSUMED")) != 0;
   e->debug_late = getenv("FW_DEBUG_LATE") && atoi(getenv("FW_DEBUG_LATE")) != 0;
+  e->debug_sync = getenv("FW_DEBUG_SYNC") && atoi(getenv("FW_DEBUG_SYNC")) != 0;
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_now, hipEventDisableTiming));
@@ -3311,6 +3317,11 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)5 * RT_MAXNB * RT_GS, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
+  if (e->debug_sync && (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess)) {
+    g_create_error = "FW_DEBUG_SYNC: initial fills failed";
+    delete e;
+    return FW_ERR_DEVICE;
+  }
   *out = e;
   return FW_OK;
 }
@@ -3432,7 +3443,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (!e->disarmed.empty() &&
       jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)*e->disarmed.rbegin() * (uint64_t)e->s.size)), e->s.size), 1) > e->cur_wm)
     hipLaunchKernelGGL(k_arm, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0, e->stream, e->s, b);
-  if (e->s.first && !e->routed && !e->fused) {   // the partitioned form sets f1 in k_aggregate, the fused one in k_fused
+  // (the direct form's record-indexed list of f1 fix-ups; the partitioned form sets f1 in k_aggregate, the fused
+  // one in k_fused, and session / list state keep theirs themselves — new_list holds nothing of theirs)
+  if (e->s.first && !e->routed && !e->fused && !e->session && !e->list) {
     e->phase_begin(FW_PHASE_FIXUP);
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
                        e->stream, e->s, e->new_list, df1, e->ordinal, n);

@@ -244,7 +244,9 @@ static int list_sort_window(fw_engine* e, int64_t n, int64_t N);
 int list_push(fw_engine* e, const BatchIn& b) {
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((b.n + BLOCK - 1) / BLOCK, e->grid));
   e->phase_begin(FW_PHASE_INGEST);
+  DBGSYNC(e, "push entry");
   hipLaunchKernelGGL(k_list_ingest, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b, e->lst);
+  DBGSYNC(e, "k_list_ingest");
   e->phase_end(b.n);
   HIPCHK(e, hipGetLastError());
   if (!e->lst.fcnt || !fires_possible(e->s, e->cur_wm)) return FW_OK;
@@ -285,6 +287,7 @@ int list_push(fw_engine* e, const BatchIn& b) {
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((Fn + BLOCK - 1) / BLOCK, e->grid));
     hipLaunchKernelGGL(k_list_fire_count, dim3(blocks), dim3(BLOCK), 0, e->stream, e->lst, e->list_k2, e->list_v1, N, dp,
                        Fn, dp + 2 * Fn);
+    DBGSYNC(e, "k_list_fire_count");
     HIPCHK(e, hipMemcpyAsync(cnt.data(), dp + 2 * Fn, 16 * (size_t)Fn, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     int64_t tot = 0;
@@ -297,6 +300,7 @@ int list_push(fw_engine* e, const BatchIn& b) {
     const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)n * (uint64_t)e->s.slide)), e->s.size), 1);
     hipLaunchKernelGGL(k_list_fire_emit, dim3((unsigned)std::min<int64_t>(Fn, 4096)), dim3(BLOCK), 0, e->stream, e->s,
                        e->lst, e->list_v1, dp + 2 * Fn, dp + 4 * Fn, Fn, e->list_out, max_ts);
+    DBGSYNC(e, "k_list_fire_emit");
     HIPCHK(e, hipStreamSynchronize(e->stream));
     (void)hipFree(dp);
     e->list_out += tot;
@@ -335,13 +339,17 @@ static int list_sort_window(fw_engine* e, int64_t n, int64_t N) {
   const int kid_bits = bits_for((uint64_t)e->s.stride);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((N + BLOCK - 1) / BLOCK, e->grid));
   hipLaunchKernelGGL(k_list_gather, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, n, e->list_k1, e->list_v1);
+  DBGSYNC(e, "k_list_gather");
   size_t tb = e->list_temp_bytes;
   HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v1, e->list_v2, (size_t)N, 0, 64,
                                       e->stream));
+  DBGSYNC(e, "radix sort 1");
   hipLaunchKernelGGL(k_list_kid, dim3(blocks), dim3(BLOCK), 0, e->stream, e->lst, e->list_v2, N, e->list_k1);
+  DBGSYNC(e, "k_list_kid");
   tb = e->list_temp_bytes;
   HIPCHK(e, rocprim::radix_sort_pairs(e->list_temp, tb, e->list_k1, e->list_k2, e->list_v2, e->list_v1, (size_t)N, 0,
                                       kid_bits, e->stream));
+  DBGSYNC(e, "radix sort 2");
   return FW_OK;
 }
 
@@ -359,7 +367,9 @@ int list_watermark(fw_engine* e, int64_t wm) {
     return FW_OK;
   }
   e->phase_begin(FW_PHASE_FIRE);
+  DBGSYNC(e, "watermark entry");
   hipLaunchKernelGGL(k_list_plan, dim3(1), dim3(1024), 0, e->stream, e->s, e->lst, e->cur_wm, wm, e->list_plan);
+  DBGSYNC(e, "k_list_plan");
   HIPCHK(e, hipMemcpyAsync(e->list_plan_h.data(), e->list_plan, 8 * LPLAN_WORDS, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   const int64_t nt = e->list_plan_h[0];
@@ -371,9 +381,11 @@ int list_watermark(fw_engine* e, int64_t wm) {
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((N + BLOCK - 1) / BLOCK, e->grid));
     const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)n * (uint64_t)e->s.slide)), e->s.size), 1);
     hipLaunchKernelGGL(k_list_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, e->list_v1, N, e->list_out, max_ts);
+    DBGSYNC(e, "k_list_emit");
     e->list_out += N;
   }
   hipLaunchKernelGGL(k_list_finish, dim3(1), dim3(1024), 0, e->stream, e->s, e->lst, e->list_plan, e->list_out);
+  DBGSYNC(e, "k_list_finish");
   hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
   e->phase_end(e->s.stride);
   HIPCHK(e, hipGetLastError());
