@@ -81,6 +81,8 @@ def parse():
                          "timed events serialise kernels, so the timed region runs without them")
     ap.add_argument("--decode-steps", type=int, default=4,
                     help="wire-format decode leg (fw_decode of the batch as Flink network bytes; 0 = skip)")
+    ap.add_argument("--drain-steps", type=int, default=8,
+                    help="steps of the leg that collects fired results to the host after every step (0 = skip)")
     ap.add_argument("--h2d-steps", type=int, default=8,
                     help="steps after the timed region pushed from pinned host columns (PCIe-inclusive rate; 0 = skip)")
     return ap.parse_args()
@@ -159,7 +161,7 @@ def main():
     C = CONFIGS[args.config]
     n_keys, rate, batch, key_cap = C["keys"], C["rate"], C["batch"], C["key_cap"]
     fields, vt = C["reduce"]
-    total_steps = args.warmup + args.steps + args.prof_steps + args.h2d_steps + args.decode_steps + 2
+    total_steps = args.warmup + args.steps + args.prof_steps + args.h2d_steps + args.decode_steps + args.drain_steps + 2
 
     from flink_amd.keygroups import compute_key_group_range_for_operator_index
     mp = 128
@@ -272,7 +274,8 @@ def main():
     # wire-format ingest: the batch as Flink network bytes (length-prefixed StreamElementSerializer records of
     # Tuple3<Long key, Long f1, Long value> with timestamps), resident in HBM, decoded by fw_decode
     dec = None
-    dec_sums = []
+    dec_sums = []   # value sums / record counts of batches pushed outside `cols` (checksum below)
+    extra_n = 0
     if args.decode_steps > 0 and exch is None and vt == "i64":
         k, t, v = cols[0]
         n = k.numel()
@@ -300,6 +303,7 @@ def main():
             k, t, v = stream(j * batch, batch, n_keys, rate, T0, device=dev, value_type=vt, zipf=C["zipf"], ooo=C["ooo"])
             wires.append(torch.cat([head, be(t), be(k), be(t), be(v)], dim=1).reshape(-1).contiguous())
             dec_sums.append(int(v.sum().item()))   # these batches enter the window state too (checksum below)
+            extra_n += int(k.numel())
         eng.sync()
         torch.cuda.synchronize()
         t3 = time.perf_counter()
@@ -316,6 +320,37 @@ def main():
                                         "batch (the drop-in path from network buffers), host-synchronous decode"}
         collected.append(eng.collect())
         del wires
+
+    # results drained as they fire: push + watermark + fw_collect (host columns) every step, the way the
+    # reference's operator hands fired windows downstream; fresh batches after the decode leg's
+    drain_leg = None
+    if args.drain_steps > 0 and exch is None:
+        jr = args.warmup + args.steps + args.prof_steps + args.h2d_steps + 2 + args.decode_steps
+        fresh = []
+        for j in range(jr, jr + args.drain_steps):
+            k, t, v = stream(j * batch, batch, n_keys, rate, T0, device=dev, value_type=vt, zipf=C["zipf"], ooo=C["ooo"])
+            fresh.append((k, t, v))
+            if vt == "i64":
+                dec_sums.append(int(v.sum().item()))
+            extra_n += int(k.numel())
+        eng.sync()
+        torch.cuda.synchronize()
+        n_out = 0
+        t4 = time.perf_counter()
+        for q, (k, t, v) in enumerate(fresh):
+            eng.push(k, t, v)
+            eng.advance_watermark(wm_of(jr + q))
+            r = eng.collect()
+            n_out += r["n"]
+            collected.append(r)
+        torch.cuda.synchronize()
+        dtr = (time.perf_counter() - t4) / args.drain_steps
+        drain_leg = {"value": batch / dtr, "unit": "events/s", "steps": args.drain_steps, "results": n_out,
+                     "ms_per_step": dtr * 1e3,
+                     "note": "push + watermark + fw_collect of the fired results into host columns after every "
+                             "step (host-synchronous: no overlap across steps); the headline leaves them in the "
+                             "device output log, drained after the timed region"}
+        del fresh
 
     if world > 1:
         import torch.distributed as dist
@@ -341,7 +376,7 @@ def main():
                 pushed = (pushed + (x & mask)) & mask
         else:
             fired = int(np.concatenate([r["count"] for r in collected]).sum())
-            pushed = windows_per_record * sum(int(k.numel()) for k, t, v in pushed_cols)
+            pushed = windows_per_record * (sum(int(k.numel()) for k, t, v in pushed_cols) + extra_n)
         if world > 1:
             import torch.distributed as dist
             signed = lambda x: x - (1 << 64) if x >= (1 << 63) else x
@@ -425,6 +460,8 @@ def main():
         line["h2d_ingest"] = h2d
     if dec is not None:
         line["wire_decode"] = dec
+    if drain_leg is not None:
+        line["with_drain"] = drain_leg
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         line["cpu_baseline"] = cpu_baseline(cfg, C, args.cpu_sample)
     if rank == 0:
