@@ -2553,6 +2553,10 @@ struct SessDev {
   int64_t* len;
   int64_t *pv, *pf1, *pnext, *pord;
   int64_t pcap;
+  // hot keys (a batch run of >= hot records, reducing state): walked by one wave each (k_sess_walk_hot)
+  int32_t hot;
+  int64_t* hot_list;                 // run heads (sorted positions)
+  unsigned long long* hot_count;
 };
 
 }  // namespace
@@ -2715,6 +2719,12 @@ struct fw_engine {
   int64_t part_blocks_cap = 0;
   // host output copies
   std::vector<int64_t> h_key, h_f1, h_ts, h_sum, h_mn, h_mx, h_cnt, h_mark_wm, h_mark_pos, h_dev_pos, h_start;
+  // fw_collect(FW_MEM_HOST): pinned staging of the result columns (DMA copies, one wait), grown on demand up
+  // to COLLECT_PIN_MAX rows (larger drains use pageable vectors); two pinned words for the counts
+  static constexpr int64_t COLLECT_PIN_MAX = 1 << 22;
+  int64_t* h_pin = nullptr;
+  int64_t h_pin_rows = 0;
+  unsigned long long* h_pin_cnt = nullptr;
   // watermark marks since the last collect, in emission order.  A firing watermark's kernel (and a
   // k_mark_only) writes a device mark; a quiet watermark with no output appended since the previous
   // device mark launches nothing: its position is that mark's (dev < 0: the start of the log)
@@ -2751,6 +2761,8 @@ struct fw_engine {
     if (bload_host) (void)hipHostFree(bload_host);
     if (dir_keys_host) (void)hipHostFree(dir_keys_host);
     for (void* p : {dec_table, dec_small, dec_bytes}) if (p) (void)hipFree(p);
+    if (h_pin) (void)hipHostFree(h_pin);
+    if (h_pin_cnt) (void)hipHostFree(h_pin_cnt);
     for (void* p : {(void*)list_k1, (void*)list_k2, (void*)list_v1, (void*)list_v2, list_temp}) if (p) (void)hipFree(p);
   }
 };
@@ -3605,9 +3617,18 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
   int rc = check_device_error(e);
   if (rc) return rc;
   unsigned long long cnt = 0, mc = 0;
-  HIPCHK(e, hipMemcpyAsync(&cnt, e->s.o.count, 8, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipMemcpyAsync(&mc, e->s.o.mark_count, 8, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (!e->h_pin_cnt && hipHostMalloc((void**)&e->h_pin_cnt, 16, hipHostMallocDefault) != hipSuccess) e->h_pin_cnt = nullptr;
+  if (e->h_pin_cnt) {
+    HIPCHK(e, hipMemcpyAsync(e->h_pin_cnt, e->s.o.count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->h_pin_cnt + 1, e->s.o.mark_count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    cnt = e->h_pin_cnt[0];
+    mc = e->h_pin_cnt[1];
+  } else {
+    HIPCHK(e, hipMemcpyAsync(&cnt, e->s.o.count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(&mc, e->s.o.mark_count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
   if ((int64_t)cnt > e->s.o.capacity) return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded");
   const OutLog& L = e->s.o;
   // the marks in emission order: device marks as written, the others at the position of the device mark
@@ -3645,8 +3666,25 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
     o->mark_wm = L.mark_wm; o->mark_pos = L.mark_pos;
     o->win_start = L.win_start;
   } else {
+    if (n > e->h_pin_rows && n <= fw_engine::COLLECT_PIN_MAX) {
+      if (e->h_pin) (void)hipHostFree(e->h_pin);
+      const int64_t rows = std::min<int64_t>(std::max<int64_t>(2 * n, 4096), fw_engine::COLLECT_PIN_MAX);
+      if (hipHostMalloc((void**)&e->h_pin, 8 * 8 * (size_t)rows, hipHostMallocDefault) != hipSuccess) {
+        e->h_pin = nullptr;
+        e->h_pin_rows = 0;
+      } else {
+        e->h_pin_rows = rows;
+      }
+    }
+    const bool pinned = e->h_pin && n <= e->h_pin_rows;
+    int col = 0;
     auto cp = [&](std::vector<int64_t>& h, const int64_t* d, int64_t cnt_) -> const int64_t* {
       if (!d) return nullptr;
+      if (pinned) {   // column `col` of the pinned staging
+        int64_t* dst = e->h_pin + (size_t)(col++) * (size_t)e->h_pin_rows;
+        if (cnt_ > 0) (void)hipMemcpyAsync(dst, d, 8 * cnt_, hipMemcpyDeviceToHost, e->stream);
+        return dst;
+      }
       h.resize((size_t)std::max<int64_t>(cnt_, 1));
       if (cnt_ > 0) (void)hipMemcpyAsync(h.data(), d, 8 * cnt_, hipMemcpyDeviceToHost, e->stream);
       return h.data();

@@ -164,7 +164,15 @@ struct SBits {
     return -1;
   }
   __device__ __forceinline__ int pop() { const int q = first(); if (q >= 0) clr(q); return q; }
+  __device__ __forceinline__ uint32_t group(int g) const { return (uint32_t)(w[g >> 3] >> ((g & 7) * 8)) & 0xffu; }
 };
+
+// slots [8g, 8g + 8) of one key's column, loaded together: one memory round trip per group of slots instead of
+// one per slot (the columns carry 8 slots of padding past the last key)
+__device__ __forceinline__ void sess_load8(const int64_t* col, int g, int64_t* v) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = col[8 * g + k];
+}
 
 // one thread per key (the head of its run in the sorted keys): the key's records in arrival order
 template <int NW>
@@ -177,6 +185,10 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   if (k0 == ~0ull) return;
   const int64_t kid = (int64_t)(k0 >> idx_bits);
   if (j0 > 0 && (sorted[j0 - 1] >> idx_bits) == (unsigned long long)kid) return;   // not the head of its run
+  if (d.hot > 0 && j0 + d.hot - 1 < n && (sorted[j0 + d.hot - 1] >> idx_bits) == (unsigned long long)kid) {
+    d.hot_list[atomicAdd(d.hot_count, 1ull)] = j0;   // a hot key: one wave walks it (k_sess_walk_hot)
+    return;
+  }
   const int64_t key = kid_key(s, kid);
   const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
   const int64_t wm = b.wm;
@@ -193,28 +205,53 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
     trig.clr(q);
     if (d.list) sess_list_free(d, base + q);
   };
-  for (int64_t j = j0; j < n; ++j) {
-    const unsigned long long kj = sorted[j];
-    if ((kj >> idx_bits) != (unsigned long long)kid) break;
-    const int64_t i = (int64_t)(kj & ((1ull << idx_bits) - 1));
-    const int64_t ts = b.ts[i];
-    const int64_t v = b.val[i];
+  // the accumulator of the slot last written, kept in registers (only this thread writes its key's slots):
+  // a hot key's consecutive records into one session read it back without a memory round trip
+  int cq = -1;
+  LateAcc cacc;
+  auto acc_load = [&](int q) -> LateAcc { return q == cq ? cacc : sess_load(s, d, base + q); };
+  auto acc_store = [&](int q, const LateAcc& a) { sess_store(d, base + q, a); cq = q; cacc = a; };
+  // the next record's columns are loaded while the current one is processed
+  const unsigned long long imask = (1ull << idx_bits) - 1;
+  int64_t ni = (int64_t)(k0 & imask);
+  int64_t nts = b.ts[ni], nv = b.val[ni], nf1 = b.f1 ? b.f1[ni] : nts;
+  bool more = true;
+  for (int64_t j = j0; more; ++j) {
+    const int64_t i = ni, ts = nts, v = nv, f1 = nf1;
+    more = false;
+    if (j + 1 < n) {
+      const unsigned long long kn = sorted[j + 1];
+      if ((kn >> idx_bits) == (unsigned long long)kid) {
+        more = true;
+        ni = (int64_t)(kn & imask);
+        nts = b.ts[ni];
+        nv = b.val[ni];
+        nf1 = b.f1 ? b.f1[ni] : nts;
+      }
+    }
     LateAcc a;
     a.vt = s.vt;
     a.sum = v;
     a.mn = min_code(s.vt, s.cmpto, v);
     a.mx = max_code(s.vt, s.cmpto, v);
     a.cnt = 1;
-    a.f1 = b.f1 ? b.f1[i] : ts;
+    a.f1 = f1;
     a.by = s.by;
     // MergingWindowSet.addWindow: the new window's connected group of intersecting in-flight windows
     int64_t cs = ts, ce = jadd(ts, d.gap);
     B mask = B::none();
-    for (;;) {
+    for (;;) {   // (the fixed point — the connected group — does not depend on the order slots are tested in)
       B grew = B::none();
-      for (B m = live.andnot(mask); m.any();) {
-        const int q = m.pop();
-        if (cs <= en[q] && ce >= st[q]) { cs = min(cs, st[q]); ce = max(ce, en[q]); grew.set(q); }
+      const B cand = live.andnot(mask);
+      for (int g = 0; g < 8 * NW; ++g) {
+        const uint32_t bits = cand.group(g);
+        if (!bits) continue;
+        int64_t s8[8], e8[8];
+        sess_load8(st, g, s8);
+        sess_load8(en, g, e8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (((bits >> k) & 1u) && cs <= e8[k] && ce >= s8[k]) { cs = min(cs, s8[k]); ce = max(ce, e8[k]); grew.set(8 * g + k); }
       }
       if (!grew.any()) break;
       mask = mask | grew;
@@ -265,7 +302,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
               d.len[x] = 0;
             }
           } else {
-            const LateAcc sv = sess_load(s, d, x);
+            const LateAcc sv = acc_load(q);
             res = have ? sess_combine(s, res, sv) : sv;
             have = true;
           }
@@ -275,7 +312,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
           d.tail[base + t] = lt;
           d.len[base + t] = ll;
         } else if (have) {
-          sess_store(d, base + t, sess_combine(s, sess_load(s, d, base + t), res));   // HeapReducingState.add
+          acc_store(t, sess_combine(s, acc_load(t), res));   // HeapReducingState.add
         }
         B others = mask;
         others.clr(t);
@@ -322,8 +359,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       d.tail[x] = e;
       d.len[x] += 1;
     } else {
-      cur = fresh ? a : sess_combine(s, sess_load(s, d, x), a);
-      sess_store(d, x, cur);
+      cur = fresh ? a : sess_combine(s, acc_load(r), a);
+      acc_store(r, cur);
     }
     // EventTimeTrigger.onElement on the (possibly merged) window
     if (max_ts <= wm) {
@@ -345,6 +382,227 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
 }
 
+// a hot key's run (>= d.hot records of the batch, reducing state): the same per-record state machine as
+// k_sess_walk, one wave per key.  Lane l holds slots l + 64 w (window bounds and accumulator in registers);
+// the record columns are loaded 64 at a time, one per lane, and processed in arrival order from registers
+// (wave-uniform control flow: every lane takes every decision with the same values)
+template <int NW>
+struct SLane {   // one wave's copy of a key's slots, slot q at lane q & 63, word q >> 6
+  int64_t st[NW], en[NW], sum[NW], mn[NW], mx[NW], cnt[NW], f1[NW];
+};
+template <int NW>
+__device__ __forceinline__ int64_t slane_get(const int64_t (&v)[NW], int q) {
+  int64_t x = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) if (w == (q >> 6)) x = v[w];
+  return __shfl(x, q & 63);
+}
+template <int NW>
+__device__ __forceinline__ void slane_set(int64_t (&v)[NW], int q, int64_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) if (w == (q >> 6) && lane == (q & 63)) v[w] = x;
+}
+template <int NW>
+__device__ __forceinline__ LateAcc slane_acc(const Spec& s, const SLane<NW>& L, int q) {
+  LateAcc a;
+  a.vt = s.vt;
+  a.sum = slane_get<NW>(L.sum, q);
+  a.mn = slane_get<NW>(L.mn, q);
+  a.mx = slane_get<NW>(L.mx, q);
+  a.cnt = slane_get<NW>(L.cnt, q);
+  a.f1 = slane_get<NW>(L.f1, q);
+  a.by = s.by;
+  return a;
+}
+template <int NW>
+__device__ __forceinline__ void slane_put(SLane<NW>& L, int q, const LateAcc& a) {
+  slane_set<NW>(L.sum, q, a.sum);
+  slane_set<NW>(L.mn, q, a.mn);
+  slane_set<NW>(L.mx, q, a.mx);
+  slane_set<NW>(L.cnt, q, a.cnt);
+  slane_set<NW>(L.f1, q, a.f1);
+}
+__device__ __forceinline__ int64_t wave_min64(int64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (int64_t)__shfl_xor((long long)x, o));
+  return x;
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t x) {
+  for (int o = 32; o > 0; o >>= 1) x = max(x, (int64_t)__shfl_xor((long long)x, o));
+  return x;
+}
+
+template <int NW>
+__global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn b, const unsigned long long* sorted,
+                                                      int64_t n, int32_t idx_bits) {
+  typedef SBits<NW> B;
+  if ((unsigned long long)blockIdx.x >= *d.hot_count) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t j0 = d.hot_list[blockIdx.x];
+  const int64_t kid = (int64_t)(sorted[j0] >> idx_bits);
+  const int64_t key = kid_key(s, kid);
+  const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
+  const int64_t wm = b.wm;
+  const int64_t base = kid * d.sw;
+  const unsigned long long imask = (1ull << idx_bits) - 1;
+  SLane<NW> L;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int q = lane + 64 * w;
+    const bool in = q < d.sw;
+    const int64_t x = base + q;
+    L.st[w] = in ? d.start[x] : 0;
+    L.en[w] = in ? d.end[x] : 0;
+    L.sum[w] = in && d.sum ? d.sum[x] : 0;
+    L.mn[w] = in && d.mn ? d.mn[x] : INT64_MAX;
+    L.mx[w] = in && d.mx ? d.mx[x] : INT64_MIN;
+    L.cnt[w] = in && d.cnt ? d.cnt[x] : 0;
+    L.f1[w] = in && d.f1 ? d.f1[x] : 0;
+  }
+  B live = B::load(d.live + kid * NW), trig = B::load(d.trig + kid * NW);
+  const B all = B::low(d.sw);
+  unsigned long long late = 0, fires = 0;
+  bool done = false;
+  for (int64_t jc = j0; !done; jc += 64) {
+    // 64 records of the run, one per lane
+    const int64_t j = jc + lane;
+    bool mine = false;
+    int64_t rts = 0, rv = 0, rf1 = 0;
+    if (j < n) {
+      const unsigned long long kj = sorted[j];
+      if ((kj >> idx_bits) == (unsigned long long)kid) {
+        const int64_t i = (int64_t)(kj & imask);
+        mine = true;
+        rts = b.ts[i];
+        rv = b.val[i];
+        rf1 = b.f1 ? b.f1[i] : rts;
+      }
+    }
+    const uint64_t have = __ballot(mine);
+    const int cnt_here = __popcll(have);   // the run's records are a prefix of the 64
+    if (cnt_here < 64) done = true;
+    for (int t = 0; t < cnt_here; ++t) {
+      const int64_t ts = __shfl(rts, t), v = __shfl(rv, t), f1 = __shfl(rf1, t);
+      LateAcc a;
+      a.vt = s.vt;
+      a.sum = v;
+      a.mn = min_code(s.vt, s.cmpto, v);
+      a.mx = max_code(s.vt, s.cmpto, v);
+      a.cnt = 1;
+      a.f1 = f1;
+      a.by = s.by;
+      // the connected group of intersecting in-flight windows (a fixed point, as k_sess_walk's)
+      int64_t cs = ts, ce = jadd(ts, d.gap);
+      B mask = B::none();
+      for (;;) {
+        B grew = B::none();
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const int q = lane + 64 * w;
+          const bool c = live.test(q) && !mask.test(q) && cs <= L.en[w] && ce >= L.st[w];
+          grew.w[w] = __ballot(c);
+          if (c) { lo = min(lo, L.st[w]); hi = max(hi, L.en[w]); }
+        }
+        if (!grew.any()) break;
+        mask = mask | grew;
+        cs = min(cs, wave_min64(lo));
+        ce = max(ce, wave_max64(hi));
+      }
+      int r = -1;
+      bool fresh = false;
+      if (!mask.any()) {
+        fresh = true;
+      } else {
+        r = mask.first();
+        const bool contained = mask.count() == 1 && slane_get<NW>(L.st, r) == cs && slane_get<NW>(L.en, r) == ce;
+        if (!contained) {   // merge, in the JDK HashSet order (see k_sess_walk)
+          const uint32_t cap = sess_set_cap(mask.count() + 1);
+          int tq = -1;
+          uint32_t tb = 0;
+          int64_t tst = 0;
+          for (B m = mask; m.any();) {
+            const int c = m.pop();
+            const int64_t sc = slane_get<NW>(L.st, c);
+            const uint32_t bc = sess_bucket(sc, slane_get<NW>(L.en, c), cap);
+            if (tq < 0 || bc < tb || (bc == tb && sc < tst)) { tq = c; tb = bc; tst = sc; }
+          }
+          LateAcc res;
+          bool hv = false;
+          B todo = mask;
+          todo.clr(tq);
+          while (todo.any()) {
+            int q = -1;
+            uint32_t bq = 0;
+            int64_t sq = 0;
+            for (B m = todo; m.any();) {
+              const int c = m.pop();
+              const int64_t sc = slane_get<NW>(L.st, c);
+              const uint32_t bc = sess_bucket(sc, slane_get<NW>(L.en, c), cap);
+              if (q < 0 || bc < bq || (bc == bq && sc < sq)) { q = c; bq = bc; sq = sc; }
+            }
+            todo.clr(q);
+            const LateAcc sv = slane_acc<NW>(s, L, q);
+            res = hv ? sess_combine(s, res, sv) : sv;
+            hv = true;
+          }
+          if (hv) slane_put<NW>(L, tq, sess_combine(s, slane_acc<NW>(s, L, tq), res));
+          B others = mask;
+          others.clr(tq);
+          live = live.andnot(others);
+          trig = trig.andnot(mask);
+          trig.set(tq);
+          r = tq;
+          slane_set<NW>(L.st, r, cs);
+          slane_set<NW>(L.en, r, ce);
+        }
+      }
+      const int64_t max_ts = jsub(ce, 1);
+      if (cleanup_time(max_ts, s.lateness) <= wm) {   // isLate(actualWindow)
+        ++late;
+        if (r >= 0) { live.clr(r); trig.clr(r); }
+        continue;
+      }
+      if (fresh) {
+        r = all.andnot(live).first();
+        if (r < 0) { if (lane == 0) cap_error(s, 21); continue; }
+        live.set(r);
+        trig.clr(r);
+        slane_set<NW>(L.st, r, cs);
+        slane_set<NW>(L.en, r, ce);
+      }
+      const LateAcc cur = fresh ? a : sess_combine(s, slane_acc<NW>(s, L, r), a);
+      slane_put<NW>(L, r, cur);
+      if (max_ts <= wm) {   // EventTimeTrigger.onElement: FIRE
+        if (lane == 0) sess_emit(s, atomicAdd(s.o.count, 1ull), key, cs, max_ts, cur);
+        ++fires;
+        if (purging) { live.clr(r); trig.clr(r); }
+      } else {
+        trig.set(r);
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int q = lane + 64 * w;
+    if (q >= d.sw) continue;
+    const int64_t x = base + q;
+    d.start[x] = L.st[w];
+    d.end[x] = L.en[w];
+    if (d.sum) d.sum[x] = L.sum[w];
+    if (d.mn) d.mn[x] = L.mn[w];
+    if (d.mx) d.mx[x] = L.mx[w];
+    if (d.cnt) d.cnt[x] = L.cnt[w];
+    if (d.f1) d.f1[x] = L.f1[w];
+  }
+  if (lane == 0) {
+    live.store(d.live + kid * NW);
+    trig.store(d.trig + kid * NW);
+    if (late) atomicAdd(&s.stats[ST_LATE], late);
+    if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
+  }
+}
+
 // a watermark: every in-flight window's timers up to wm_new.  One thread per key; lane by lane the it-th window of
 // each key, so the wave's appends stay aggregated (list state: one append per window, its element count)
 template <int NW>
@@ -356,9 +614,42 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
     const int64_t kid = k0 + threadIdx.x;
     B live = kid < s.stride ? B::load(d.live + kid * NW) : B::none(), trig = kid < s.stride ? B::load(d.trig + kid * NW) : B::none();
     const B live0 = live, trig0 = trig;
-    int nl = live.count();
+    // the slots' timers decided from their ends, 8 slots per memory round trip
+    B fire_m = B::none(), ret_m = B::none();
+    if (live.any()) {
+      const int64_t* en = d.end + kid * d.sw;
+      for (int g = 0; g < 8 * NW; ++g) {
+        const uint32_t bits = live.group(g);
+        if (!bits) continue;
+        int64_t e8[8];
+        sess_load8(en, g, e8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (!((bits >> k) & 1u)) continue;
+          const int q = 8 * g + k;
+          const int64_t max_ts = jsub(e8[k], 1);
+          const int64_t ct = cleanup_time(max_ts, s.lateness);
+          bool fire = false, retire = false;
+          if (trig.test(q) && max_ts <= wm_new) {   // onEventTime(maxTimestamp): FIRE
+            fire = true;
+            trig.clr(q);
+            if (purging || ct == max_ts) retire = true;       // FIRE_AND_PURGE, or isCleanupTime
+          }
+          if (!retire && ct <= wm_new) {                    // onEventTime(cleanupTime): cleanup
+            if (!fire && ct == max_ts) fire = true;         // (one timer at maxTimestamp == cleanupTime)
+            retire = true;
+          }
+          if (fire) fire_m.set(q);
+          if (retire) ret_m.set(q);
+        }
+      }
+      live = live.andnot(ret_m);
+      trig = trig.andnot(ret_m);
+    }
+    // the fires (list state: and the retired windows' elements freed), the wave's appends aggregated
+    B todo = d.list ? (fire_m | ret_m) : fire_m;
+    int nl = todo.count();
     for (int o = 32; o > 0; o >>= 1) nl = max(nl, __shfl_xor(nl, o));
-    B todo = live;
     for (int it = 0; it < nl; ++it) {
       bool fire = false;
       int q = -1;
@@ -366,23 +657,12 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
       if (todo.any()) {
         q = todo.pop();
         const int64_t x = kid * d.sw + q;
+        fire = fire_m.test(q);
         start = d.start[x];
         max_ts = jsub(d.end[x], 1);
-        const int64_t ct = cleanup_time(max_ts, s.lateness);
-        bool retire = false;
-        if (trig.test(q) && max_ts <= wm_new) {   // onEventTime(maxTimestamp): FIRE
-          fire = true;
-          trig.clr(q);
-          if (purging || ct == max_ts) retire = true;       // FIRE_AND_PURGE, or isCleanupTime
-        }
-        if (!retire && ct <= wm_new) {                    // onEventTime(cleanupTime): cleanup
-          if (!fire && ct == max_ts) fire = true;         // (one timer at maxTimestamp == cleanupTime)
-          retire = true;
-        }
-        if (retire) { live.clr(q); trig.clr(q); }
         if (d.list) {   // list state: every element of the window, then (retired) its pool entries freed
           if (fire) sess_list_emit(s, d, x, kid_key(s, kid), start, max_ts);
-          if (retire) sess_list_free(d, x);
+          if (ret_m.test(q)) sess_list_free(d, x);
         }
       }
       if (!d.list) {
@@ -405,8 +685,8 @@ int session_create(fw_engine* e) {
   SessDev& d = e->sess;
   d.gap = e->cfg.size;
   const size_t cells = (size_t)d.sw * (size_t)s.stride;
-  d.start = e->alloc<int64_t>(cells);
-  d.end = e->alloc<int64_t>(cells);
+  d.start = e->alloc<int64_t>(cells + 8);   // (+ 8: sess_load8's groups past the last key's slots)
+  d.end = e->alloc<int64_t>(cells + 8);
   d.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>(cells) : nullptr;
   d.mn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(cells) : nullptr;
   d.mx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>(cells) : nullptr;
@@ -428,6 +708,16 @@ int session_create(fw_engine* e) {
     d.pord = e->alloc<int64_t>((size_t)d.pcap);
   }
   d.nw = (d.sw + 63) / 64 <= 1 ? 1 : (d.sw + 63) / 64 <= 2 ? 2 : 4;   // words of a key's slot masks
+  // hot keys: runs of >= FW_SESS_HOT records (default 0 = off) walked a wave each; reducing state only
+  {
+    const char* hv = getenv("FW_SESS_HOT");
+    d.hot = e->list ? 0 : hv ? std::max(0, atoi(hv)) : 0;
+    if (d.hot == 1) d.hot = 2;
+  }
+  if (d.hot > 0) {
+    d.hot_list = e->alloc<int64_t>((size_t)(e->cfg.max_batch / d.hot + 1));
+    d.hot_count = e->alloc<unsigned long long>(1);
+  }
   d.live = e->alloc<unsigned long long>((size_t)s.stride * d.nw);
   d.trig = e->alloc<unsigned long long>((size_t)s.stride * d.nw);
   e->s.o.win_start = e->alloc<int64_t>((size_t)e->cfg.out_capacity);
@@ -459,9 +749,16 @@ int session_push(fw_engine* e, const BatchIn& b) {
   HIPCHK(e, rocprim::radix_sort_keys(e->sess_temp, tb, e->sess_key, e->sess_sorted, (size_t)b.n, 0, e->sess_key_bits,
                                      e->stream));
   const dim3 g((unsigned)((b.n + BLOCK - 1) / BLOCK));
+  if (e->sess.hot > 0) HIPCHK(e, hipMemsetAsync(e->sess.hot_count, 0, 8, e->stream));
   if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_walk<1>, g, dim3(BLOCK), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
   else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_walk<2>, g, dim3(BLOCK), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
   else hipLaunchKernelGGL(k_sess_walk<4>, g, dim3(BLOCK), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
+  if (e->sess.hot > 0 && b.n >= e->sess.hot) {   // the hot keys' runs: one wave each (at most n / hot of them)
+    const dim3 gh((unsigned)(b.n / e->sess.hot));
+    if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_walk_hot<1>, gh, dim3(64), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
+    else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_walk_hot<2>, gh, dim3(64), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
+    else hipLaunchKernelGGL(k_sess_walk_hot<4>, gh, dim3(64), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
+  }
   e->phase_end(b.n);
   HIPCHK(e, hipGetLastError());
   if (e->cfg.allowed_lateness > 0) e->out_dirty = true;   // per-element fires may have appended
