@@ -708,10 +708,10 @@ int session_create(fw_engine* e) {
     d.pord = e->alloc<int64_t>((size_t)d.pcap);
   }
   d.nw = (d.sw + 63) / 64 <= 1 ? 1 : (d.sw + 63) / 64 <= 2 ? 2 : 4;   // words of a key's slot masks
-  // hot keys: runs of >= FW_SESS_HOT records (default 0 = off) walked a wave each; reducing state only
+  // hot keys: runs of >= FW_SESS_HOT records (default 256; 0 = off) walked a wave each; reducing state only
   {
     const char* hv = getenv("FW_SESS_HOT");
-    d.hot = e->list ? 0 : hv ? std::max(0, atoi(hv)) : 0;
+    d.hot = e->list ? 0 : hv ? std::max(0, atoi(hv)) : 256;
     if (d.hot == 1) d.hot = 2;
   }
   if (d.hot > 0) {
