@@ -423,6 +423,12 @@ __device__ __forceinline__ void slane_put(SLane<NW>& L, int q, const LateAcc& a)
   slane_set<NW>(L.cnt, q, a.cnt);
   slane_set<NW>(L.f1, q, a.f1);
 }
+// a wave-uniform value made visibly uniform to the compiler (scalar registers, scalar branches)
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ int64_t wave_min64(int64_t x) {
   for (int o = 32; o > 0; o >>= 1) x = min(x, (int64_t)__shfl_xor((long long)x, o));
   return x;
@@ -460,8 +466,18 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
     L.f1[w] = in && d.f1 ? d.f1[x] : 0;
   }
   B live = B::load(d.live + kid * NW), trig = B::load(d.trig + kid * NW);
+#pragma unroll
+  for (int w = 0; w < NW; ++w) { live.w[w] = (uint64_t)uni64((int64_t)live.w[w]); trig.w[w] = (uint64_t)uni64((int64_t)trig.w[w]); }
   const B all = B::low(d.sw);
   unsigned long long late = 0, fires = 0;
+  // the slot the previous record went to, replicated in every lane (a hot key's records mostly extend one
+  // session: its bounds and accumulator are then read without cross-lane reads)
+  int cr = -1;
+  int64_t c_st = 0, c_en = 0;
+  LateAcc c_acc;
+  auto gst = [&](int q) -> int64_t { return q == cr ? c_st : slane_get<NW>(L.st, q); };
+  auto gen = [&](int q) -> int64_t { return q == cr ? c_en : slane_get<NW>(L.en, q); };
+  auto gacc = [&](int q) -> LateAcc { return q == cr ? c_acc : slane_acc<NW>(s, L, q); };
   bool done = false;
   for (int64_t jc = j0; !done; jc += 64) {
     // 64 records of the run, one per lane
@@ -482,7 +498,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
     const int cnt_here = __popcll(have);   // the run's records are a prefix of the 64
     if (cnt_here < 64) done = true;
     for (int t = 0; t < cnt_here; ++t) {
-      const int64_t ts = __shfl(rts, t), v = __shfl(rv, t), f1 = __shfl(rf1, t);
+      const int64_t ts = uni64(__shfl(rts, t)), v = uni64(__shfl(rv, t)), f1 = uni64(__shfl(rf1, t));
       LateAcc a;
       a.vt = s.vt;
       a.sum = v;
@@ -506,8 +522,14 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
         }
         if (!grew.any()) break;
         mask = mask | grew;
-        cs = min(cs, wave_min64(lo));
-        ce = max(ce, wave_max64(hi));
+        if (grew.count() == 1) {   // (the usual case: one window grows the group)
+          const int q = grew.first();
+          cs = uni64(min(cs, gst(q)));
+          ce = uni64(max(ce, gen(q)));
+        } else {
+          cs = uni64(min(cs, wave_min64(lo)));
+          ce = uni64(max(ce, wave_max64(hi)));
+        }
       }
       int r = -1;
       bool fresh = false;
@@ -515,7 +537,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
         fresh = true;
       } else {
         r = mask.first();
-        const bool contained = mask.count() == 1 && slane_get<NW>(L.st, r) == cs && slane_get<NW>(L.en, r) == ce;
+        const bool contained = mask.count() == 1 && gst(r) == cs && gen(r) == ce;
         if (!contained) {   // merge, in the JDK HashSet order (see k_sess_walk)
           const uint32_t cap = sess_set_cap(mask.count() + 1);
           int tq = -1;
@@ -523,8 +545,8 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
           int64_t tst = 0;
           for (B m = mask; m.any();) {
             const int c = m.pop();
-            const int64_t sc = slane_get<NW>(L.st, c);
-            const uint32_t bc = sess_bucket(sc, slane_get<NW>(L.en, c), cap);
+            const int64_t sc = gst(c);
+            const uint32_t bc = sess_bucket(sc, gen(c), cap);
             if (tq < 0 || bc < tb || (bc == tb && sc < tst)) { tq = c; tb = bc; tst = sc; }
           }
           LateAcc res;
@@ -537,16 +559,20 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
             int64_t sq = 0;
             for (B m = todo; m.any();) {
               const int c = m.pop();
-              const int64_t sc = slane_get<NW>(L.st, c);
-              const uint32_t bc = sess_bucket(sc, slane_get<NW>(L.en, c), cap);
+              const int64_t sc = gst(c);
+              const uint32_t bc = sess_bucket(sc, gen(c), cap);
               if (q < 0 || bc < bq || (bc == bq && sc < sq)) { q = c; bq = bc; sq = sc; }
             }
             todo.clr(q);
-            const LateAcc sv = slane_acc<NW>(s, L, q);
+            const LateAcc sv = gacc(q);
             res = hv ? sess_combine(s, res, sv) : sv;
             hv = true;
           }
-          if (hv) slane_put<NW>(L, tq, sess_combine(s, slane_acc<NW>(s, L, tq), res));
+          if (hv) {
+            const LateAcc m2 = sess_combine(s, gacc(tq), res);
+            slane_put<NW>(L, tq, m2);
+            if (tq == cr) c_acc = m2;
+          }
           B others = mask;
           others.clr(tq);
           live = live.andnot(others);
@@ -555,6 +581,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
           r = tq;
           slane_set<NW>(L.st, r, cs);
           slane_set<NW>(L.en, r, ce);
+          if (r == cr) { c_st = cs; c_en = ce; }
         }
       }
       const int64_t max_ts = jsub(ce, 1);
@@ -571,8 +598,12 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
         slane_set<NW>(L.st, r, cs);
         slane_set<NW>(L.en, r, ce);
       }
-      const LateAcc cur = fresh ? a : sess_combine(s, slane_acc<NW>(s, L, r), a);
+      const LateAcc cur = fresh ? a : sess_combine(s, gacc(r), a);
       slane_put<NW>(L, r, cur);
+      cr = __builtin_amdgcn_readfirstlane(r);   // slot r now holds [cs, ce) and cur in every lane's copy
+      c_st = cs;
+      c_en = ce;
+      c_acc = cur;
       if (max_ts <= wm) {   // EventTimeTrigger.onElement: FIRE
         if (lane == 0) sess_emit(s, atomicAdd(s.o.count, 1ull), key, cs, max_ts, cur);
         ++fires;
