@@ -161,7 +161,7 @@ def main():
     C = CONFIGS[args.config]
     n_keys, rate, batch, key_cap = C["keys"], C["rate"], C["batch"], C["key_cap"]
     fields, vt = C["reduce"]
-    total_steps = args.warmup + args.steps + args.prof_steps + args.h2d_steps + args.decode_steps + args.drain_steps + 2
+    total_steps = args.warmup + args.steps + args.prof_steps + args.h2d_steps + args.decode_steps + 2 * args.drain_steps + 2
 
     from flink_amd.keygroups import compute_key_group_range_for_operator_index
     mp = 128
@@ -321,36 +321,56 @@ def main():
         collected.append(eng.collect())
         del wires
 
-    # results drained as they fire: push + watermark + fw_collect (host columns) every step, the way the
-    # reference's operator hands fired windows downstream; fresh batches after the decode leg's
+    # results drained as they fire, the way the reference's operator hands fired windows downstream: push +
+    # watermark + an asynchronous drain (fw_collect_begin / fw_collect_end) every step, results of step j landing
+    # in pinned host columns while step j + 1 runs (they need only precede watermark j downstream); and the same
+    # with the synchronous fw_collect for comparison.  Fresh batches after the decode leg's
     drain_leg = None
     if args.drain_steps > 0 and exch is None:
         jr = args.warmup + args.steps + args.prof_steps + args.h2d_steps + 2 + args.decode_steps
-        fresh = []
-        for j in range(jr, jr + args.drain_steps):
-            k, t, v = stream(j * batch, batch, n_keys, rate, T0, device=dev, value_type=vt, zipf=C["zipf"], ooo=C["ooo"])
-            fresh.append((k, t, v))
-            if vt == "i64":
-                dec_sums.append(int(v.sum().item()))
-            extra_n += int(k.numel())
-        eng.sync()
-        torch.cuda.synchronize()
-        n_out = 0
-        t4 = time.perf_counter()
-        for q, (k, t, v) in enumerate(fresh):
-            eng.push(k, t, v)
-            eng.advance_watermark(wm_of(jr + q))
-            r = eng.collect()
-            n_out += r["n"]
-            collected.append(r)
-        torch.cuda.synchronize()
-        dtr = (time.perf_counter() - t4) / args.drain_steps
-        drain_leg = {"value": batch / dtr, "unit": "events/s", "steps": args.drain_steps, "results": n_out,
-                     "ms_per_step": dtr * 1e3,
-                     "note": "push + watermark + fw_collect of the fired results into host columns after every "
-                             "step (host-synchronous: no overlap across steps); the headline leaves them in the "
-                             "device output log, drained after the timed region"}
-        del fresh
+        legs = {}
+        for mode in ("async", "sync"):
+            fresh = []
+            for j in range(jr, jr + args.drain_steps):
+                k, t, v = stream(j * batch, batch, n_keys, rate, T0, device=dev, value_type=vt, zipf=C["zipf"], ooo=C["ooo"])
+                fresh.append((k, t, v))
+                if vt == "i64":
+                    dec_sums.append(int(v.sum().item()))
+                extra_n += int(k.numel())
+            eng.sync()
+            torch.cuda.synchronize()
+            n_out = 0
+            t4 = time.perf_counter()
+            prev = None
+            for q, (k, t, v) in enumerate(fresh):
+                eng.push(k, t, v)
+                eng.advance_watermark(wm_of(jr + q))
+                if mode == "sync":
+                    r = eng.collect()
+                    n_out += r["n"]
+                    collected.append(r)
+                    continue
+                cur = eng.collect_begin()
+                if prev is not None:
+                    r = eng.collect_end(prev)
+                    n_out += r["n"]
+                    collected.append(r)
+                prev = cur
+            if prev is not None:
+                r = eng.collect_end(prev)
+                n_out += r["n"]
+                collected.append(r)
+            torch.cuda.synchronize()
+            dtr = (time.perf_counter() - t4) / args.drain_steps
+            legs[mode] = {"value": batch / dtr, "unit": "events/s", "steps": args.drain_steps, "results": n_out,
+                          "ms_per_step": dtr * 1e3}
+            jr += args.drain_steps
+            del fresh
+        drain_leg = dict(legs["async"])
+        drain_leg["note"] = ("push + watermark + fw_collect_begin every step, fw_collect_end of the previous step's drain "
+                             "(pinned host columns; results of watermark j land while batch j + 1 runs); the headline "
+                             "leaves them in the device output log, drained after the timed region")
+        drain_leg["sync"] = dict(legs["sync"], note="the same with the host-synchronous fw_collect after every step")
 
     if world > 1:
         import torch.distributed as dist
@@ -399,9 +419,12 @@ def main():
     wm_ms, wm_n = per(_abi.FW_PHASE_FIRE)
     late_ms, late_n = per(_abi.FW_PHASE_LATE)
     wm_per_step = wm_n / max(args.prof_steps, 1)
-    # algorithmic bytes: 24 B per event (key, ts, value) + per fired pane 96 B (C3: 112 B)
+    # algorithmic bytes: 24 B per event (key, ts, value) + per fired pane 96 B (C3:
+    # 112 B); at N > 1 the keyBy exchange sends each GPU's (N-1)/N share of its events to the other GPUs (21 B/event
+    # at N = 8: SURVEY.md 8(e)), which the receivers write to HBM: B_alg = 24 N + 96 P_fired + 24 (N-1)/N N
     ev_gpu = batch
-    alg_step = 24.0 * ev_gpu + C["pane_bytes"] * fired_per_step / max(world, 1)
+    xchg_step = 24.0 * ev_gpu * (world - 1) / world if world > 1 else 0.0
+    alg_step = 24.0 * ev_gpu + C["pane_bytes"] * fired_per_step / max(world, 1) + xchg_step
     achieved = alg_step / (ms_step / 1e3) / 1e9
     pmc, pmc_src = pmc_traffic(args.config)
     kernels = {}
@@ -456,13 +479,21 @@ def main():
         "stats": {k: stats[k] for k in ("records_in", "records_late", "panes_fired", "late_fires", "ingest_form")},
         "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
     }
+    if world > 1:
+        # xGMI: the sent share over the point-to-point links to the other N-1 GPUs (7 x ~153 GB/s per GPU at N = 8,
+        # SURVEY.md 8(e)); the bound of C5
+        peak_x = 153.0 * min(world - 1, 7)
+        got_x = xchg_step / (ms_step / 1e3) / 1e9
+        line["xgmi"] = {"bytes_sent_per_step": xchg_step, "achieved": got_x, "peak": peak_x, "unit": "GB/s",
+                        "frac": got_x / peak_x, "links": min(world - 1, 7),
+                        "note": "keyBy exchange payload (24 B x the (N-1)/N share of a rank's events) over ms_per_step"}
     if h2d is not None:
         line["h2d_ingest"] = h2d
     if dec is not None:
         line["wire_decode"] = dec
     if drain_leg is not None:
         line["with_drain"] = drain_leg
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and args.cpu_sample > 0:   # at every N: the CPU job on the host's cores, beside the GPU line
         line["cpu_baseline"] = cpu_baseline(cfg, C, args.cpu_sample)
     if rank == 0:
         print(json.dumps(line), flush=True)

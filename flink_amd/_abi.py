@@ -18,6 +18,7 @@ FW_ERR_CAPACITY = 3
 FW_ERR_KEY_GROUP = 4
 FW_ERR_UNSUPPORTED = 5
 FW_ERR_DEVICE = 6
+FW_ERR_RESIDENCY = 7
 
 FW_TUMBLING = 0
 FW_SLIDING = 1
@@ -43,7 +44,8 @@ FW_MEM_DEVICE = 1
 EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sync", "fw_collect",
                     "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
                     "fw_get_profile", "fw_debug_counters", "fw_debug_stamps", "fw_set_stream", "fw_stream_wait_input",
-                    "fw_version", "fw_snapshot_kg", "fw_restore_kg", "fw_snapshot_kg_flink", "fw_restore_kg_flink", "fw_decode")
+                    "fw_version", "fw_snapshot_kg", "fw_restore_kg", "fw_snapshot_kg_flink", "fw_restore_kg_flink", "fw_decode",
+                    "fw_collect_begin", "fw_collect_end")
 FW_SNAP_MAGIC, FW_SNAP_HEADER_WORDS, FW_SNAP_ENTRY_WORDS = 0x31474b5746574b, 14, 8
 # state tuple fields of the Flink-layout checkpoint (fw_state_layout)
 FW_SF_KEY, FW_SF_F1, FW_SF_SUM, FW_SF_MIN, FW_SF_MAX, FW_SF_COUNT, FW_SF_VALUE, FW_SF_MAX_FIELDS = 1, 2, 3, 4, 5, 6, 7, 8
@@ -101,6 +103,8 @@ def declare(lib, prefix="fw"):
         "advance_watermark": (_i32, [_p, _i64]),
         "sync": (_i32, [_p]),
         "collect": (_i32, [_p, P(FwOut)] + ([_i32] if prefix == "fw" else [])),
+        "collect_begin": (_i32, [_p, P(_i32)]),
+        "collect_end": (_i32, [_p, _i32, P(FwOut)]),
         "get_stats": (_i32, [_p, P(FwStats)]),
         "last_error": (ctypes.c_char_p, [_p]),
         "destroy": (None, [_p]),

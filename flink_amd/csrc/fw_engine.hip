@@ -113,6 +113,8 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   uint64_t dir_mask;
   int64_t D;
   int32_t kb_bits;  // log2(slots per directory bucket); probing stays inside the home bucket
+  uint32_t home_mask;   // probe start inside the bucket = home & home_mask: ~0 (the home slot) or ~7 (the start of
+                        // its 64-B line of 8 slots: the fused form reads a key's candidates as one aligned line)
   int32_t nb;       // directory buckets = D >> kb_bits
   // slices
   int32_t P;
@@ -188,7 +190,7 @@ __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
 // stale) load can only under-report, which the CAS then corrects; a key found EMPTY at slot j cannot
 // sit at a later slot.
 __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
-                                                         int32_t kb_bits, int64_t D, int64_t key,
+                                                         int32_t kb_bits, uint32_t home_mask, int64_t D, int64_t key,
                                                          unsigned long long* inserted) {
   if (key == EMPTY_KEY) {
     if (dir_min_used[0] == 0) dir_min_used[0] = 1;
@@ -197,7 +199,7 @@ __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int3
   const uint64_t home = fmix64((uint64_t)key) & dir_mask;
   const uint64_t kbm = (1ull << kb_bits) - 1;
   const uint64_t base = home & ~kbm;
-  uint64_t off = home & kbm;
+  uint64_t off = home & kbm & (uint64_t)home_mask;
   for (uint64_t probe = 0; probe <= kbm; ++probe) {
     const uint64_t h = base + off;
     const int64_t cur = dir_keys[h];
@@ -213,17 +215,17 @@ __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int3
   return -1;
 }
 __device__ __noinline__ int64_t dir_find_or_insert_call(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
-                                                        int32_t kb_bits, int64_t D, int64_t key,
+                                                        int32_t kb_bits, uint32_t home_mask, int64_t D, int64_t key,
                                                         unsigned long long* inserted) {
-  return dir_find_or_insert_at(dir_keys, dir_min_used, dir_mask, kb_bits, D, key, inserted);
+  return dir_find_or_insert_at(dir_keys, dir_min_used, dir_mask, kb_bits, home_mask, D, key, inserted);
 }
 // inline: the direct form's per-record lookup
 __device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key) {
-  return dir_find_or_insert_at(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key, s.stats + ST_DIR_KEYS);
+  return dir_find_or_insert_at(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.home_mask, s.D, key, s.stats + ST_DIR_KEYS);
 }
 // out of line: the rare lookups of the partitioned form (new keys, direct-list records) and restore
 __device__ __forceinline__ int64_t dir_lookup(const Spec& s, int64_t key) {
-  return dir_find_or_insert_call(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key, s.stats + ST_DIR_KEYS);
+  return dir_find_or_insert_call(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.home_mask, s.D, key, s.stats + ST_DIR_KEYS);
 }
 
 // slice number m -> slot p, claiming a FREE slot.  Returns -1 when slot p holds another live slice.
@@ -2217,7 +2219,7 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
       continue;
     }
     // re-insert: the same probe sequence as dir_find_or_insert, in the fresh LDS layout
-    uint32_t y = (uint32_t)fmix64((uint64_t)key) & kbm;
+    uint32_t y = (uint32_t)fmix64((uint64_t)key) & kbm & s.home_mask;
     for (;;) {
       const unsigned long long prev =
           atomicCAS((unsigned long long*)&nkey[y], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
@@ -2323,6 +2325,40 @@ __global__ __launch_bounds__(1024) void k_quirk_apply(Spec s, int64_t* list, uns
   }
   __syncthreads();
   if (threadIdx.x == 0) *count = 0;
+}
+
+// asynchronous drain (fw_collect_begin): the output log's rows and device marks since the last collect, copied into
+// pinned host staging (column-major, `rows` per column) with coalesced stores over PCIe; hdr[0..3] = rows, device
+// marks, fits, the engine's error word.  A log larger than the staging is left in place (fits = 0)
+constexpr int DR_COLS = 8;   // key, f1, ts, sum, min, max, count, window start
+__global__ __launch_bounds__(BLOCK) void k_drain(OutLog L, const int32_t* err, int64_t rows, int64_t* stage, int64_t* marks,
+                                                 int64_t* hdr) {
+  const int64_t n = (int64_t)*L.count, nm = (int64_t)*L.mark_count;
+  const bool fits = n <= rows && n <= L.capacity && nm <= L.mark_capacity;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    hdr[0] = n;
+    hdr[1] = nm;
+    hdr[2] = fits ? 1 : 0;
+    hdr[3] = *err;
+  }
+  if (!fits) return;
+  const int64_t* src[DR_COLS] = {L.key, L.f1, L.ts, L.sum, L.mn, L.mx, L.cnt, L.win_start};
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+#pragma unroll
+    for (int c = 0; c < DR_COLS; ++c)
+      if (src[c]) stage[(int64_t)c * rows + i] = src[c][i];
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = threadIdx.x; i < nm; i += blockDim.x) marks[i] = L.mark_pos[i];
+}
+// ... then the log restarts (a separate launch: every k_drain block has read the counts)
+__global__ void k_drain_reset(OutLog L, int64_t rows) {
+  const unsigned long long n = *L.count, nm = *L.mark_count;
+  if ((int64_t)n <= rows && (int64_t)n <= L.capacity && (int64_t)nm <= L.mark_capacity) {
+    *L.count = 0;
+    *L.mark_count = 0;
+  }
 }
 
 __global__ void k_mark_only(Spec s, int64_t wm) {
@@ -2733,6 +2769,19 @@ struct fw_engine {
   int64_t dev_marks = 0;        // device marks enqueued since the last collect
   bool out_dirty = false;       // output appended (per-element fires) after the last device mark
   std::vector<double> h_sum_d, h_mn_d, h_mx_d;
+  // asynchronous drains (fw_collect_begin / fw_collect_end): two pinned host staging buffers, alternating
+  struct Drain {
+    int64_t* host = nullptr;        // [DR_COLS][rows] columns, then [mark_capacity] device mark positions, then hdr[4]
+    int64_t* dptr = nullptr;        // the same memory as the device sees it
+    hipEvent_t done = nullptr;
+    bool pending = false;           // begun, not yet ended
+    std::vector<HostMark> marks;    // the host marks of the drain
+    int64_t dev_marks = 0;
+    std::vector<int64_t> mark_wm, mark_pos;
+  };
+  Drain drains[2];
+  int64_t drain_rows = 0;
+  int64_t drain_seq = 0;
   int dev = 0;
 
   template <class T>
@@ -2762,6 +2811,7 @@ struct fw_engine {
     if (dir_keys_host) (void)hipHostFree(dir_keys_host);
     for (void* p : {dec_table, dec_small, dec_bytes}) if (p) (void)hipFree(p);
     if (h_pin) (void)hipHostFree(h_pin);
+    for (auto& d : drains) { if (d.host) (void)hipHostFree(d.host); if (d.done) (void)hipEventDestroy(d.done); }
     if (h_pin_cnt) (void)hipHostFree(h_pin_cnt);
     for (void* p : {(void*)list_k1, (void*)list_k2, (void*)list_v1, (void*)list_v2, list_temp}) if (p) (void)hipFree(p);
   }
@@ -2862,19 +2912,23 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
 }
 
 // fused form (fw_fused.hip): one launch per batch, FU_GRID workgroups, after any other engine's fused launch
+// (the dynamic-LDS attribute is set once per instantiation, under the device-wide lock, in fused_prepare_t)
+template <int VT, int AGG, bool FIRST>
+static void fused_prepare_t(fw_engine* e, hipError_t* rc) {
+  static bool attr_set = false;
+  std::lock_guard<std::mutex> lk(g_fused_mu);
+  if (attr_set) return;
+  hipFuncAttributes fa{};
+  *rc = hipFuncGetAttributes(&fa, (const void*)k_fused<VT, AGG, FIRST>);
+  if (*rc == hipSuccess)
+    *rc = hipFuncSetAttribute((const void*)k_fused<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(160 * 1024 - fa.sharedSizeBytes));
+  attr_set = *rc == hipSuccess;
+}
 template <int VT, int AGG, bool FIRST>
 static void launch_fused_t(fw_engine* e, const BatchIn& b, const int64_t* f1col) {
-  static bool attr_set = false;
-  if (!attr_set) {   // all of LDS less the kernel's static part (none expected)
-    hipFuncAttributes fa{};
-    const size_t stat = hipFuncGetAttributes(&fa, (const void*)k_fused<VT, AGG, FIRST>) == hipSuccess ? fa.sharedSizeBytes : 0;
-    (void)hipFuncSetAttribute((const void*)k_fused<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(160 * 1024 - stat));
-    attr_set = true;
-  }
   FusedBuf f = e->fb;
-  const int64_t per_round = (int64_t)FU_GRID * FU_CH;
-  f.rounds = (int32_t)((b.n + per_round - 1) / per_round);
+  f.rounds = (int32_t)((b.n + FU_ROUND - 1) / FU_ROUND);
   f.epoch = e->fused_launches;
   for (int q = 0; q < FU_S; ++q) f.uses[q] = e->fused_uses[q];
   std::lock_guard<std::mutex> lk(g_fused_mu);
@@ -3074,9 +3128,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
 
   // fused ingest (ingest_mode 3, fw_fused.hip): reduce / fold of tumbling or sliding windows without allowed
   // lateness, on a device that holds the whole grid resident (one workgroup per CU), with an owner's range of
-  // the directory (D / 32 slots, D = 2 x key capacity) and its accumulators in LDS.  Only on request
-  // (ingest_mode 3, or FW_FUSED=1 in auto mode): measured at 23 G events/s against the partitioned form's
-  // 56 G on C1 (round-serial phases, tools/fused_stamps.py)
+  // the directory (D / 32 slots, D = 2 x key capacity) and its accumulators in LDS beside the producers' staging
   const int nacc_f = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
   const int64_t d_fused = next_pow2(std::max<int64_t>(2 * c.key_capacity, 2048));
   const int so_bits_f = bits_for((uint64_t)d_fused) - 1 - 5;
@@ -3086,7 +3138,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
                     prop.multiProcessorCount >= FU_GRID && fused_lds_bytes(so_bits_f, nacc_f) <= 160 * 1024;
     if (c.ingest_mode == 3 && !ok)
       return unsupported("fused ingest (ingest_mode 3): tumbling or sliding reduce / fold without allowed lateness, "
-                         "key_capacity <= 64 Ki (sum) / 32 Ki (sum, min, max, count), on a 256-CU device");
+                         "key_capacity <= 64 Ki (sum) / 16 Ki (sum, min, max, count), on a 256-CU device");
     e->fused = ok && (c.ingest_mode == 3 || (c.ingest_mode == 0 && fv && atoi(fv) != 0 && c.max_batch >= (1 << 16)));
   }
   // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys, and for the fused form): short linear-probe
@@ -3099,6 +3151,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (e->fused) kb = std::min(9, dbits - 5);                 // fused: >= 32 buckets (one owner range is whole buckets)
     s.kb_bits = kb;
     s.nb = (int32_t)(s.D >> kb);
+    s.home_mask = e->fused ? ~7u : ~0u;   // fused: a key's probe starts at its home line (fw_fused.hip)
   }
   s.stride = s.D + 1;
   int32_t P = c.max_open_slices;
@@ -3229,16 +3282,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->fused) {
     FusedBuf& f = e->fb;
     f.so_bits = so_bits_f;
-    f.owner_shift = bits_for((uint64_t)s.D) - 1 - 5;
-    f.ring = e->alloc<unsigned char>((size_t)FU_GRID * FU_S * FU_SLOT);
-    f.ctr = e->alloc<unsigned long long>(FU_C_N);
+    f.ring = e->alloc<unsigned char>((size_t)FU_GROUPS * FU_NP * FU_S * FU_UNIT);
+    f.ctr = e->alloc<unsigned long long>((size_t)FU_C_N * FU_C_PAD);
     f.xcc = e->alloc<int32_t>(FU_GRID);
-    const size_t np = (size_t)FU_GROUPS * (size_t)s.D;   // [32 ranges][8 groups][D / 32 slots]
-    f.psum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>(np) : nullptr;
-    f.pmn = (s.agg & FW_AGG_MIN) ? e->alloc<int64_t>(np) : nullptr;
-    f.pmx = (s.agg & FW_AGG_MAX) ? e->alloc<int64_t>(np) : nullptr;
-    f.pcnt = (s.agg & FW_AGG_COUNT) ? e->alloc<int64_t>(np) : nullptr;
-    f.pfirst = e->alloc<uint32_t>(np);
     const char* fs = getenv("FW_FUSED_SAFE");
     f.force_safe = fs && atoi(fs) != 0 ? 1 : 0;
     const char* dbg = getenv("FW_DEBUG_AGG");
@@ -3247,6 +3293,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     f.stamps = e->rb.stamps;
     // at least 81 KiB: one workgroup per CU, so the 256 of a launch are resident together on 256 CUs
     e->fused_lds = std::max<size_t>(fused_lds_bytes(so_bits_f, nacc_f), 81 * 1024);
+    hipError_t rc = hipSuccess;
+    FW_DISPATCH_FUSED(fused_prepare_t, e, &rc);
+    HIPCHK(e, rc);
   }
   e->wm_done = e->alloc<unsigned int>(1);
   if (s.first && !e->routed) {
@@ -3325,7 +3374,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
   if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
   if (e->bload) HIPCHK(e, hipMemsetAsync(e->bload, 0, 4 * 4 * RT_MAXNB, e->stream));
-  if (e->fb.ctr) HIPCHK(e, hipMemsetAsync(e->fb.ctr, 0, 8 * FU_C_N, e->stream));
+  if (e->fb.ctr) HIPCHK(e, hipMemsetAsync(e->fb.ctr, 0, 8 * (size_t)FU_C_N * FU_C_PAD, e->stream));
+  if (e->fb.ring) HIPCHK(e, hipMemsetAsync(e->fb.ring, 0, (size_t)FU_GROUPS * FU_NP * FU_S * FU_UNIT, e->stream));
   if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)5 * RT_MAXNB * RT_GS, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
@@ -3338,10 +3388,15 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   return FW_OK;
 }
 
+static int device_error(fw_engine* e, int32_t derr);
 static int check_device_error(fw_engine* e) {
   int32_t derr = 0;
   HIPCHK(e, hipMemcpyAsync(&derr, e->s.err, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  return device_error(e, derr);
+}
+// the device error word as the engine's sticky error, with the reference's message where it has one
+static int device_error(fw_engine* e, int32_t derr) {
   if (derr != 0 && e->sticky == FW_OK) {
     const char* msg = "device error";
     switch (derr) {
@@ -3351,6 +3406,8 @@ static int check_device_error(fw_engine* e) {
         break;
       case FW_ERR_KEY_GROUP: msg = "Unexpected key group index. This indicates a bug."; break;
       case FW_ERR_CAPACITY: msg = "capacity exceeded (key directory, slice pool, per-element fire list or output log)"; break;
+      case FW_ERR_RESIDENCY: msg = "fused ingest: the 256 workgroups of a launch were not resident together (other work "
+                                   "held CUs); ingest_mode 3 needs the device to itself"; break;
       case FW_ERR_UNSUPPORTED: msg = "a record's extra sliding window (timestamp below offset - slide, Java % of a negative "
                                      "numerator) is already behind the watermark, or maxBy/minBy with such a record: "
                                      "per-element fire of a window pane not supported"; break;
@@ -3713,6 +3770,91 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
   HIPCHK(e, hipMemsetAsync(L.count, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(L.mark_count, 0, 8, e->stream));
   if (mem == FW_MEM_HOST) HIPCHK(e, hipStreamSynchronize(e->stream));
+  return FW_OK;
+}
+
+int fw_collect_begin(fw_engine* e, int32_t* ticket) {
+  if (!e || !ticket) return FW_ERR_INVALID_ARG;
+  if (e->sticky) return e->sticky;
+  HIPCHK(e, hipSetDevice(e->dev));
+  const int b = (int)(e->drain_seq & 1);
+  fw_engine::Drain& d = e->drains[b];
+  if (d.pending) { e->err = "fw_collect_begin: two drains outstanding (fw_collect_end the older first)"; return FW_ERR_INVALID_ARG; }
+  const OutLog& L = e->s.o;
+  if (!d.host) {
+    e->drain_rows = std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX);
+    const size_t bytes = 8 * ((size_t)DR_COLS * (size_t)e->drain_rows + (size_t)L.mark_capacity + 4);
+    if (hipHostMalloc((void**)&d.host, bytes, hipHostMallocMapped) != hipSuccess) {
+      d.host = nullptr;
+      return fail(e, FW_ERR_DEVICE, "fw_collect_begin: pinned staging allocation failed");
+    }
+    HIPCHK(e, hipHostGetDevicePointer((void**)&d.dptr, d.host, 0));
+    HIPCHK(e, hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+  }
+  int64_t* marks = d.dptr + (size_t)DR_COLS * (size_t)e->drain_rows;
+  int64_t* hdr = marks + L.mark_capacity;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->drain_rows + BLOCK - 1) / BLOCK, 512));
+  hipLaunchKernelGGL(k_drain, dim3(blocks), dim3(BLOCK), 0, e->stream, L, (const int32_t*)e->s.err, e->drain_rows, d.dptr,
+                     marks, hdr);
+  hipLaunchKernelGGL(k_drain_reset, dim3(1), dim3(1), 0, e->stream, L, e->drain_rows);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipEventRecord(d.done, e->stream));
+  // the marks since the last collect belong to this drain; the log restarts on the device
+  d.marks.swap(e->hmarks);
+  e->hmarks.clear();
+  d.dev_marks = e->dev_marks;
+  e->dev_marks = 0;
+  e->out_dirty = false;
+  e->list_out = 0;
+  d.pending = true;
+  *ticket = (int32_t)(e->drain_seq++ & 0x7FFFFFFF);
+  return FW_OK;
+}
+
+int fw_collect_end(fw_engine* e, int32_t ticket, fw_out* o) {
+  if (!e || !o || ticket < 0) return FW_ERR_INVALID_ARG;
+  fw_engine::Drain& d = e->drains[ticket & 1];
+  if (!d.pending || ((e->drain_seq - 1 - ticket) & 0x7FFFFFFF) > 1) {
+    e->err = "fw_collect_end: no such drain outstanding";
+    return FW_ERR_INVALID_ARG;
+  }
+  HIPCHK(e, hipSetDevice(e->dev));
+  HIPCHK(e, hipEventSynchronize(d.done));
+  d.pending = false;
+  const OutLog& L = e->s.o;
+  const int64_t* marks = d.host + (size_t)DR_COLS * (size_t)e->drain_rows;
+  const int64_t* hdr = marks + L.mark_capacity;
+  if (int rc = device_error(e, (int32_t)hdr[3])) return rc;
+  if (!hdr[2]) return fail(e, FW_ERR_CAPACITY, "fw_collect_end: more results than an asynchronous drain holds (collect more often)");
+  if (hdr[1] != d.dev_marks) return fail(e, FW_ERR_CAPACITY, "watermark mark log capacity exceeded");
+  const int64_t n = hdr[0], nm = (int64_t)d.marks.size();
+  d.mark_wm.resize((size_t)std::max<int64_t>(nm, 1));
+  d.mark_pos.resize((size_t)std::max<int64_t>(nm, 1));
+  for (int64_t i = 0; i < nm; ++i) {
+    d.mark_wm[(size_t)i] = d.marks[(size_t)i].wm;
+    d.mark_pos[(size_t)i] = d.marks[(size_t)i].dev >= 0 ? marks[d.marks[(size_t)i].dev] : 0;
+  }
+  std::memset(o, 0, sizeof(*o));
+  o->n = n;
+  o->n_marks = nm;
+  auto col = [&](int c, const void* present) -> const int64_t* { return present ? d.host + (size_t)c * (size_t)e->drain_rows : nullptr; };
+  o->key = col(0, L.key);
+  o->f1 = col(1, L.f1);
+  o->ts = col(2, L.ts);
+  const int64_t* su = col(3, L.sum);
+  const int64_t* mn = col(4, L.mn);
+  const int64_t* mx = col(5, L.mx);
+  o->count = col(6, L.cnt);
+  o->win_start = col(7, L.win_start);
+  if (e->s.vt == FW_VALUE_F64) { o->sum_f64 = (const double*)su; o->min_f64 = (const double*)mn; o->max_f64 = (const double*)mx; }
+  else { o->sum_i64 = su; o->min_i64 = mn; o->max_i64 = mx; }
+  o->mark_wm = d.mark_wm.data();
+  o->mark_pos = d.mark_pos.data();
+  const int32_t um = e->list ? FW_AGG_SUM : e->cfg.agg_mask;   // only the fields the reduce function asked for
+  if (!(um & FW_AGG_SUM)) { o->sum_i64 = nullptr; o->sum_f64 = nullptr; }
+  if (!(um & (FW_AGG_MIN | FW_AGG_MINBY))) { o->min_i64 = nullptr; o->min_f64 = nullptr; }
+  if (!(um & (FW_AGG_MAX | FW_AGG_MAXBY))) { o->max_i64 = nullptr; o->max_f64 = nullptr; }
+  if (!(um & FW_AGG_COUNT)) o->count = nullptr;
   return FW_OK;
 }
 

@@ -1,210 +1,291 @@
-// fw_fused.hip — ingest form 3: one persistent launch per batch in which the records of a
-// chunk are handed from the workgroup that read them to the workgroup that owns their keys through the
-// L2 of the XCD both run on, so the routed intermediate of the two-kernel form (k_route -> k_aggregate,
-// ~40 B per event of HBM / Infinity-Cache traffic) never leaves the chip.  Included by fw_engine.hip.
+// fw_fused.hip — ingest form 3: one persistent launch per batch.  The records a workgroup reads
+// are handed to the workgroup that owns their keys through the L2 of the XCD both run on, and each owner reduces
+// its share in LDS, so no routed intermediate has to survive a kernel boundary.  Included by fw_engine.hip.
 //
 // Reference path: WindowOperator.processElement (SJ/runtime/operators/windowing/WindowOperator.java:222-333)
 // -> HeapReducingState.add (RT/state/heap/HeapReducingState.java:84-122), for a batch of records between two
-// watermarks (StreamInputProcessor.java:147-177).  Exact for integer reduces and the first-arrival f1;
-// double sums change association (the tolerance path), as in the other forms.
+// watermarks (StreamInputProcessor.java:147-177).  Exact for integer reduces and the first-arrival f1; double
+// sums change association (the tolerance path), as in the other forms.
 //
-// Geometry.  FU_GRID = 256 workgroups of 1024 threads, one per CU (LDS > 80 KiB), in FU_GROUPS = 8 groups
-// g = blockIdx % 8 of FU_MEMBERS = 32 members (blockIdx / 8).  The dispatcher deals workgroups to the 8
-// XCDs round-robin, so a group is normally the 32 CUs of one XCD.  Placement is only ever a speed matter:
-// every workgroup reads HW_REG_XCC_ID, and a group whose members do not all report the same XCD hands off
-// with the agent-scope release/acquire recipe (MI355X_MICROARCH.md § visibility) instead of the same-L2
-// path (plain stores drained with vmcnt(0) before a memory-side counter add; every consumer load L1-bypassing).
+// Geometry.  FU_GRID = 256 workgroups of 1024 threads, one per CU, in FU_GROUPS = 8 groups g = blockIdx % 8 of
+// FU_MEMBERS = 32 members (blockIdx / 8).  The dispatcher deals workgroups to the XCDs round-robin, so a group is
+// normally the 32 CUs of one XCD.  Placement is only ever a speed matter: every workgroup registers its
+// HW_REG_XCC_ID, and a group whose members do not all report one XCD hands off with the agent-scope
+// release / acquire recipe (MI355X_MICROARCH.md, inter-workgroup visibility) instead of the same-L2 path.
 //
-// Ownership.  Member j of each group owns directory slots [j SO, (j+1) SO), SO = D / 32: whole directory
-// buckets, and linear probing never leaves a bucket, so every key lives in its owner's range.  The owner
-// keeps an LDS copy of its slots' key hashes and LDS accumulators of the batch's primary slice m0 (the
-// slice of the middle record: an in-order batch has one slice).
+// Ownership.  Member j of each group owns directory slots [j SO, (j + 1) SO), SO = D / 32: whole directory
+// buckets, and probing never leaves a bucket, so every key lives in its owner's range.  The owner keeps an LDS
+// copy of its slots' key hashes and LDS accumulators of the batch's primary slice m0 (the slice of the middle
+// record: an in-order batch has one).  A key's probe starts at the first slot of its home line of 8 slots
+// (Spec::home_mask), so its candidates are one aligned 64-B line of that copy.
 //
-// Round k (chunk c = 256 k + blockIdx, FU_CH records, loaded into registers during round k - 1):
-//   produce  the operator work of k_route (timestamp, key group, windows, lateness), a wave multisplit of
-//            the records of slice m0 by owner, an LDS counting sort, and the chunk stored bin-sorted as
-//            (fmix64(key), value) + chunk index into this workgroup's ring slot k % FU_S; one counter add
-//            tells the group.  Records of any other slice and the Long.MIN_VALUE key update the dense
-//            columns directly (device atomics, as k_ingest_direct; rare for in-order streams).
-//   consume  round k - 1: this owner's bin of each of the group's 32 slots, resolved against the LDS
-//            directory copy, reduced with LDS atomics (first arrival = least batch index).
-// Then every owner publishes its partial accumulators (write-through), and the 8 owners of one directory
-// range (one per group) each fold one eighth of the range over the 8 partials into the dense columns,
-// plain read-modify-write: in this launch they are the only writers of those panes.
+// Roles.  Waves 0..FU_PW-1 of a workgroup are producers, the others consumers; neither waits on the other
+// inside the workgroup (no workgroup barrier between the prologue and the flush).
+//   producer  per unit of FU_U records (four per lane, the next unit's columns in flight meanwhile): the
+//             operator work (timestamp, key group, window, lateness), fmix64 of the key, the owner; a
+//             counting sort of the unit by owner in the wave's LDS staging; the unit stored to its ring slot
+//             as (fmix64(key), value) + the record's index in the unit, then a header of 32 words (segment
+//             start, length, tag) once every store of the unit has completed.  Records of another slice and the
+//             Long.MIN_VALUE key update the dense columns directly (device atomics, as k_ingest_direct).
+//   consumer  round after round, the owner's segment of each of the group's FU_NP units (8 lanes per unit,
+//             headers polled by tag), resolved against the LDS directory copy and reduced with LDS atomics
+//             (first arrival = least batch index).  The last consumer wave of a workgroup done with a round
+//             tells the group, and a producer re-fills a ring slot only after all 32 owners have read it.
+// Flush.  Every owner adds its accumulators to the dense columns of slice m0 with device atomics (one lane per
+// slot, consecutive slots in consecutive lanes); the last workgroup of the launch stores the f1 of the panes the
+// batch created (their final first-arrival ordinal).
 //
-// Counters are monotonic across launches (targets from the launch count and the ring slots' uses), every
-// wait is bounded (a launch that cannot make progress reports FW_ERR_CAPACITY site 30 and runs to its end
-// instead of hanging the device), and the host serialises fused launches device-wide, so two of them
-// never hold half of the CUs each.
+// Counters are monotonic across launches (targets from the launch count and the ring slots' uses), every wait is
+// bounded (a launch that cannot make progress, e.g. because other work holds CUs so that the 256 workgroups are
+// not resident together, reports FW_ERR_RESIDENCY and runs to its end instead of hanging the device), and the
+// host serialises fused launches device-wide, so two of them never hold half of the CUs each.
 namespace fw {
 
-constexpr int FU_THREADS = 1024;
+constexpr int FU_THREADS = 512;   // one workgroup per CU, two waves per SIMD (256 VGPRs a lane)
 constexpr int FU_WAVES = FU_THREADS / 64;
-constexpr int FU_CH = 2 * FU_THREADS;       // records per chunk: two per thread
+#ifndef FW_FU_PW
+#define FW_FU_PW 4
+#endif
+constexpr int FU_PW = FW_FU_PW;             // producer waves per workgroup
+constexpr int FU_CW = FU_WAVES - FU_PW;     // consumer waves
+constexpr int FU_RPL = 8;                   // records per lane of a producer unit
+constexpr int FU_U = 64 * FU_RPL;           // records per producer unit
 constexpr int FU_GROUPS = 8;
 constexpr int FU_MEMBERS = 32;
 constexpr int FU_GRID = FU_GROUPS * FU_MEMBERS;
-constexpr int FU_S = 2;                     // ring slots per workgroup
-constexpr int FU_HDR = 128;                 // slot header: bin starts uint16[33], round tag uint64 at byte 96
-constexpr size_t FU_SLOT = FU_HDR + (size_t)FU_CH * 16 + (size_t)FU_CH * 2;
+constexpr int FU_NP = FU_MEMBERS * FU_PW;   // producer units per group and round
+#ifndef FW_FU_S
+#define FW_FU_S 4
+#endif
+constexpr int FU_S = FW_FU_S;               // ring slots (rounds in flight) per producer wave
+constexpr int64_t FU_ROUND = (int64_t)FU_GROUPS * FU_NP * FU_U;   // records per round
+constexpr size_t FU_HDR = 32 * 8;           // per owner: start | length << 16 | tag << 32
+constexpr size_t FU_UNIT = FU_HDR + (size_t)FU_U * 18;            // header, (hash, value) pairs, unit indices (u16)
+static_assert(FU_NP % (8 * FU_CW) == 0, "consumer steps of 8 units per wave");
+static_assert(FU_S <= 8, "consumer round counters: misc[4, 12)");
 // counter block (64-bit, monotonic)
-constexpr int FU_C_REG = 0;                               // [g]      workgroups registered (32 per launch)
-constexpr int FU_C_PROD = FU_C_REG + FU_GROUPS;           // [g][s]   chunks stored in slot s
-constexpr int FU_C_DONE = FU_C_PROD + FU_GROUPS * FU_S;   // [g][s]   owners done reading slot s
-constexpr int FU_C_FOLD = FU_C_DONE + FU_GROUPS * FU_S;   // [j]      partials of range j published (8 per launch)
-constexpr int FU_C_FIN = FU_C_FOLD + FU_MEMBERS;          //          workgroups finished (256 per launch)
+constexpr int FU_C_REG = 0;                               // [g]     workgroups registered (32 per launch)
+constexpr int FU_C_DONE = FU_C_REG + FU_GROUPS;           // [g][s]  owners done reading the units of slot s
+constexpr int FU_C_PUB = FU_C_DONE + FU_GROUPS * FU_S;    // [g][s]  units of slot s published (FU_NP per use)
+constexpr int FU_C_FIN = FU_C_PUB + FU_GROUPS * FU_S;     //         workgroups finished (256 per launch)
 constexpr int FU_C_N = FU_C_FIN + 1;
+constexpr int FU_C_PAD = 64;   // u64 words between counters: each on its own 512-B stretch (memory channel), so pollers
+                               // of one counter never queue behind another's
+#define FU_CTR(f, i) ((f).ctr + (size_t)(i) * FU_C_PAD)
 
 struct FusedBuf {
-  unsigned char* ring;          // [FU_GRID][FU_S] slots of FU_SLOT bytes
-  unsigned long long* ctr;      // [FU_C_N]
+  unsigned char* ring;          // [FU_GROUPS][FU_NP][FU_S] units of FU_UNIT bytes
+  unsigned long long* ctr;      // [FU_C_N][FU_C_PAD]
   int32_t* xcc;                 // [FU_GRID] HW_REG_XCC_ID of each workgroup (this launch)
-  int64_t *psum, *pmn, *pmx, *pcnt;   // partial accumulators [FU_MEMBERS][FU_GROUPS][SO]
-  uint32_t* pfirst;             // ... least batch index (NO_FIRST: slot untouched by that group)
   unsigned long long uses[FU_S];  // rounds that used each ring slot in earlier launches
   int64_t epoch;                // fused launches before this one
-  int32_t rounds;               // chunks per workgroup
+  int32_t rounds;               // units per producer wave
   int32_t so_bits;              // log2(SO)
-  int32_t owner_shift;          // log2(D) - 5: (fmix64(key) & dir_mask) >> owner_shift = owning member
   int32_t force_safe;           // diagnostics (FW_FUSED_SAFE=1): the release/acquire hand-off for every group
   long long* stamps;            // diagnostics (FW_DEBUG_AGG & 16): per-workgroup realtime stamps, 64 per workgroup
 };
-// stamp i of this workgroup: 0 start, 1 placement known, 2 + 4k + {0 produced, 1 published, 2 round k - 1 arrived,
-// 3 consumed}, 60 partials published, 61 fold range ready, 62 end; 63 = xcc | one_l2 << 8
-#define FU_STAMP(i) do { if (f.stamps && tid == 0 && (i) < 63) f.stamps[(int64_t)w * 64 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// stamp i of this workgroup: 0 start, 1 prologue done, 2 producers done, 3 consumers done, 4 flushed, 5 end,
+// 63 = xcc | one_l2 << 8
+#define FU_STAMP(i) do { if (f.stamps && (i) < 63) f.stamps[(int64_t)w * 64 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-// LDS bytes of k_fused: staging of one chunk, bin counts, the owner's directory copy and accumulators
+// LDS bytes of k_fused: the producers' staging, the owner's directory copy and accumulators, counters
+__host__ __device__ constexpr size_t fused_stage_bytes() { return (size_t)FU_PW * (128 + (size_t)FU_U * 18); }
 __host__ __device__ constexpr size_t fused_lds_bytes(int so_bits, int nacc) {
-  return (size_t)FU_CH * 18 + 4 * (size_t)(FU_WAVES * 32 + 48 + 16) + ((size_t)8 << so_bits) +
-         (((size_t)1 << so_bits) + 64) * (8 * (size_t)nacc + 4) + 64;
+  return fused_stage_bytes() + 64 + ((size_t)8 << so_bits) + ((size_t)1 << so_bits) * (8 * (size_t)nacc + 4);
 }
 
 __device__ __forceinline__ int fu_xcc_id() { return (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15); }
 
-// one lane: wait until counter ci reaches target, bounded.  Returns false (and reports FW_ERR_CAPACITY
-// site 30 once) when it gave up; a workgroup that gave up skips its later waits (broken)
-__device__ __noinline__ bool fu_wait_at(int32_t* err, unsigned long long* stats, unsigned long long* c,
-                                        unsigned long long target) {
+// one lane: wait until counter c reaches target, bounded (~0.5 s).  Returns false (and reports
+// FW_ERR_RESIDENCY once) when it gave up; a wave that gave up skips its later waits (broken)
+__device__ __noinline__ bool fu_wait_at(int32_t* err, unsigned long long* c, unsigned long long target) {
   for (uint32_t spins = 0;; ++spins) {
     if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    if (spins > (1u << 21)) {
-      set_error(err, FW_ERR_CAPACITY);
-      atomicCAS(&stats[7], 0ull, 30ull);
+    // another wave of the launch gave up already: so does this one (the launch drains quickly)
+    const bool gone = (spins & 255) == 255 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FW_ERR_RESIDENCY;
+    if (spins > (1u << 23) || gone) {
+      set_error(err, FW_ERR_RESIDENCY);
       return false;
     }
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(8);
   }
 }
-#define fu_wait(s, ctr, ci, target, broken) \
-  ((broken) ? false : ((broken) = !fu_wait_at((s).err, (s).stats, (ctr) + (ci), (target)), !(broken)))
+
+// a wave-uniform poll through the scalar unit (s_load ... glc: the scalar cache is bypassed).  Scalar loads are
+// counted by lgkmcnt, not vmcnt, so waiting for one does not wait for the wave's vector loads in flight (vmcnt
+// retires in issue order: a vector poll would wait for the next unit's columns).  Counters only grow, so a stale
+// value can only delay a wait, never end it early
+__device__ __forceinline__ unsigned long long fu_sload(const unsigned long long* p) {
+  unsigned long long v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ int32_t fu_sload32(const int32_t* p) {
+  int32_t v;
+  asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+// the whole wave: wait until counter c reaches target, bounded like fu_wait_at
+__device__ __forceinline__ bool fu_swait(int32_t* err, const unsigned long long* c, unsigned long long target) {
+  for (uint32_t spins = 0;; ++spins) {
+    if (fu_sload(c) >= target) return true;
+    const bool gone = (spins & 255) == 255 && fu_sload32(err) == FW_ERR_RESIDENCY;
+    if (spins > (1u << 23) || gone) {
+      set_error(err, FW_ERR_RESIDENCY);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
 
 typedef long long fu_v2 __attribute__((ext_vector_type(2)));
-typedef int fu_i2 __attribute__((ext_vector_type(2)));
+typedef unsigned long long fu_u2 __attribute__((ext_vector_type(2)));
+typedef int fu_i4 __attribute__((ext_vector_type(4)));
+
+// the owner's LDS directory copy (lh, fmix64 of its slots): slot of hash h, inserting the key (fmix64_inv(h))
+// into the global directory if absent.  The probe sequence of dir_find_or_insert_at with home_mask ~7: from the
+// first slot of h's home line, linearly through the bucket.  Out of line: taken by a lane only when its key is not
+// on its home line
+__device__ __noinline__ int32_t fu_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint32_t start, uint64_t h,
+                                                unsigned long long* inserted) {
+  uint32_t x = start;
+  for (uint32_t probe = 0; probe <= kbm; ++probe) {
+    const uint64_t cur = lh[x];
+    if (cur == h) return (int32_t)x;
+    if (cur == EMPTY_H) {
+      const int64_t key = (int64_t)fmix64_inv(h);
+      const unsigned long long prev = atomicCAS((unsigned long long*)&dir_keys[x], (unsigned long long)EMPTY_KEY,
+                                                (unsigned long long)key);
+      if ((int64_t)prev == EMPTY_KEY) atomicAdd(inserted, 1ull);
+      const uint64_t now = (int64_t)prev == EMPTY_KEY ? h : fmix64(prev);
+      lh[x] = now;   // only globally confirmed keys enter the copy
+      if (now == h) return (int32_t)x;
+    }
+    x = (x + 1) & kbm;
+  }
+  return -1;
+}
 
 template <int VT, int AGG, bool FIRST>
-__global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBuf f, const int64_t* f1col) {
+__global__ __launch_bounds__(FU_THREADS, 2) void k_fused(Spec s, BatchIn b, FusedBuf f, const int64_t* f1col) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool HAS_MIN = (AGG & FW_AGG_MIN) != 0, HAS_MAX = (AGG & FW_AGG_MAX) != 0;
   constexpr bool HAS_CNT = (AGG & FW_AGG_COUNT) != 0;
   const int w = blockIdx.x, g = w & (FU_GROUPS - 1), me = w / FU_GROUPS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int SO = 1 << f.so_bits;
-  const int KA = SO + 64;
-  longlong2* st_kv = (longlong2*)smem;                 // [FU_CH] the chunk's routed records, bin-sorted
-  uint16_t* st_idx = (uint16_t*)(st_kv + FU_CH);       // [FU_CH] ... their index in the chunk
-  int32_t* wc = (int32_t*)(st_idx + FU_CH);            // [FU_WAVES][32] records of wave v in bin b, then offsets
-  int32_t* bst = wc + FU_WAVES * 32;                   // [48] bin starts, [32] = routed records
-  int32_t* misc = bst + 48;                            // [16] 0: same-L2 group, 2: pane slot of m0
-  uint64_t* lh = (uint64_t*)(misc + 16);               // [SO] fmix64 of the owned directory slots
-  int64_t* lsum = (int64_t*)(lh + SO);                 // [KA]
-  int64_t* lmin = lsum + KA;
-  int64_t* lmax = lmin + (HAS_MIN ? KA : 0);
-  int64_t* lcnt = lmax + (HAS_MAX ? KA : 0);
-  uint32_t* lfirst = (uint32_t*)(lcnt + (HAS_CNT ? KA : 0));
+  unsigned char* stage = smem;                                             // [FU_PW] staging areas
+  int32_t* misc = (int32_t*)(smem + fused_stage_bytes());                  // [16]
+  uint64_t* lh = (uint64_t*)(misc + 16);                                   // [SO] fmix64 of the owned slots
+  int64_t* lsum = (int64_t*)(lh + SO);                                     // [SO]
+  int64_t* lmin = lsum + SO;
+  int64_t* lmax = lmin + (HAS_MIN ? SO : 0);
+  int64_t* lcnt = lmax + (HAS_MAX ? SO : 0);
+  uint32_t* lfirst = (uint32_t*)(lcnt + (HAS_CNT ? SO : 0));
   const AggLds L{lsum, lmin, lmax, lcnt, lfirst, nullptr};
   const bool cmpto = s.cmpto != 0;
   const int64_t n = b.n;
   const unsigned long long ep = (unsigned long long)f.epoch;
   const int R = f.rounds;
-  bool broken = false;   // (thread 0) a bounded wait gave up
+  const int64_t dbase = (int64_t)me * SO;
+  const uint32_t kbm = (1u << s.kb_bits) - 1u;
+  if (tid == 0) FU_STAMP(0);
   // the batch's primary slice: the middle record's
   int64_t m0 = 0;
   {
     const int64_t tm = b.ts[n >> 1];
     if (tm != INT64_MIN) m0 = uniform64(record_windows(s, tm, b.wm).m);
   }
-  FU_STAMP(0);
   // registration: this workgroup's XCD, published write-through, then counted
   const int my_xcc = fu_xcc_id();
   if (tid == 0) {
     __hip_atomic_store(f.xcc + w, my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(f.ctr + FU_C_REG + g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(FU_CTR(f, FU_C_REG + g), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // chunk k of this workgroup into registers (two records per thread; whole chunks with 16-B loads)
-  int64_t nk[2], nt[2], nv[2];
-  int32_t nh[2] = {0, 0};
-  auto load_chunk = [&](int k) {
-    const int64_t i = ((int64_t)k * FU_GRID + w) * FU_CH + 2 * tid;
-    if (i + 1 < n) {
-      const fu_v2 a = __builtin_nontemporal_load((const fu_v2*)(b.key + i));
-      const fu_v2 c = __builtin_nontemporal_load((const fu_v2*)(b.ts + i));
-      const fu_v2 d = __builtin_nontemporal_load((const fu_v2*)(b.val + i));
-      nk[0] = a.x; nk[1] = a.y; nt[0] = c.x; nt[1] = c.y; nv[0] = d.x; nv[1] = d.y;
-      if (b.key_hash) { const fu_i2 h = *(const fu_i2*)(b.key_hash + i); nh[0] = h.x; nh[1] = h.y; }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const bool in = i + e < n;
-        nk[e] = in ? b.key[i + e] : 0;
-        nt[e] = in ? b.ts[i + e] : 0;
-        nv[e] = in ? b.val[i + e] : 0;
-        if (b.key_hash) nh[e] = in ? b.key_hash[i + e] : 0;
-      }
-    }
-  };
-  if (R > 0) load_chunk(0);
   // the owned directory slots and their accumulators
-  const int64_t dbase = (int64_t)me * SO;
-  for (int x = tid; x < SO; x += FU_THREADS) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
-  for (int x = tid; x < KA; x += FU_THREADS) {
+  for (int x = tid; x < SO; x += FU_THREADS) {
+    lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
     lsum[x] = sum_identity(VT);
     if (HAS_MIN) lmin[x] = INT64_MAX;
     if (HAS_MAX) lmax[x] = INT64_MIN;
     if (HAS_CNT) lcnt[x] = 0;
     lfirst[x] = NO_FIRST;
   }
+  if (tid < 16) misc[tid] = 0;
   // the group's placement: one L2 (the fast hand-off) unless some member runs on another XCD
   if (tid == 0) {
     bool one_l2 = false;
-    if (fu_wait(s, f.ctr, FU_C_REG + g, (ep + 1) * FU_MEMBERS, broken)) {
+    if (fu_wait_at(s.err, FU_CTR(f, FU_C_REG + g), (ep + 1) * FU_MEMBERS)) {
       one_l2 = !f.force_safe;
       for (int j = 0; j < FU_MEMBERS; ++j)
         one_l2 &= __hip_atomic_load(f.xcc + j * FU_GROUPS + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == my_xcc;
       if (!one_l2 && me == 0) atomicAdd(&s.stats[6], 1ull);   // diagnostics: group-launches on the safe path
+    } else {
+      misc[1] = 1;   // broken: every later wait is skipped
     }
     misc[0] = one_l2 ? 1 : 0;
   }
   __syncthreads();
   const bool one_l2 = misc[0] != 0;
-  FU_STAMP(1);
-  if (f.stamps && tid == 0) f.stamps[(int64_t)w * 64 + 63] = my_xcc | (one_l2 ? 256 : 0);
+  bool broken = misc[1] != 0;
+  if (tid == 0) { FU_STAMP(1); if (f.stamps) f.stamps[(int64_t)w * 64 + 63] = my_xcc | (one_l2 ? 256 : 0); }
   const bool all_kg = s.kg_start == 0 && s.kg_end == s.mp - 1;
-  const uint32_t kbm = (1u << s.kb_bits) - 1u;
   unsigned long long late_pairs = 0;
+  unsigned char* gbase = f.ring + (size_t)g * FU_NP * FU_S * FU_UNIT;
 
-  for (int k = 0; k <= R; ++k) {   // uniform
-    if (k < R) {
-      // ---------------- produce chunk k ----------------
-      int64_t kk[2] = {nk[0], nk[1]}, tt[2] = {nt[0], nt[1]}, vv[2] = {nv[0], nv[1]};
-      int32_t hh[2] = {nh[0], nh[1]};
-      const int64_t cbase = ((int64_t)k * FU_GRID + w) * FU_CH;
-      if (k + 1 < R) load_chunk(k + 1);   // in flight during this round
+  if (wave < FU_PW) {
+    // =============================== producer wave ===============================
+    const int pw = wave;
+    const int pu = me * FU_PW + pw;                       // this wave's unit index in the group
+    int32_t* wcnt = (int32_t*)(stage + (size_t)pw * (128 + (size_t)FU_U * 18));   // [32] per owner: count, then start
+    longlong2* skv = (longlong2*)(wcnt + 32);             // [FU_U]
+    uint16_t* sidx = (uint16_t*)(skv + FU_U);             // [FU_U]
+    // two units' columns in registers, ping-pong: unit r in X while unit r + 1 is in flight in Y; X takes unit
+    // r + 2 once unit r is stored (no register copies, so no wait for Y's loads before they are used)
+    int64_t ak[FU_RPL], at[FU_RPL], av[FU_RPL], bk[FU_RPL], bt[FU_RPL], bv[FU_RPL];
+    bool a_vec = false, b_vec = false;   // the buffer's loads were the 12 wide loads of every lane (nothing else)
+    auto unit_base = [&](int r) { return ((int64_t)(r * FU_GROUPS + g) * FU_NP + pu) * FU_U; };
+    // lane: records [FU_RPL lane, FU_RPL (lane + 1)) of unit r
+    auto load_unit = [&](int r, int64_t* nk, int64_t* nt, int64_t* nv) -> bool {
+      const int64_t i = unit_base(r) + FU_RPL * lane;
+      const bool whole = __all(i + FU_RPL - 1 < n);
+      if (whole) {
+#pragma unroll
+        for (int q = 0; q < FU_RPL / 2; ++q) {
+          const fu_v2 a = __builtin_nontemporal_load((const fu_v2*)(b.key + i + 2 * q));
+          const fu_v2 c = __builtin_nontemporal_load((const fu_v2*)(b.ts + i + 2 * q));
+          const fu_v2 d = __builtin_nontemporal_load((const fu_v2*)(b.val + i + 2 * q));
+          nk[2 * q] = a.x; nk[2 * q + 1] = a.y; nt[2 * q] = c.x; nt[2 * q + 1] = c.y; nv[2 * q] = d.x; nv[2 * q + 1] = d.y;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < FU_RPL; ++e) {
+          const bool in = i + e < n;
+          nk[e] = in ? b.key[i + e] : 0;
+          nt[e] = in ? b.ts[i + e] : 0;
+          nv[e] = in ? b.val[i + e] : 0;
+        }
+      }
+      return whole;
+    };
+    if (R > 0) a_vec = load_unit(0, ak, at, av);
+    if (R > 1) b_vec = load_unit(1, bk, bt, bv);
+    // the previous unit's header, published once its stores have completed (one unit later, so the wait for
+    // them overlaps this unit's work)
+    bool pend = false;
+    int pend_sl = 0;
+    // unit r from buffer X (kk, tt, vv, hh); Y's loads (unit r + 1, y_vec) are the youngest memory operations
+    auto unit_body = [&](int r, int64_t* kk, int64_t* tt, int64_t* vv, bool& x_vec, const bool y_vec) {
+      const bool next_vec = y_vec;
+      if (pw == 0 && lane == 0 && r < 8) FU_STAMP(8 + 3 * r);
+      const int64_t ubase = unit_base(r);
+      const int64_t lbase = ubase + FU_RPL * lane;   // batch index of this lane's first record
       // the wave's reference slice (first valid lane), valid for every record whose timestamp lies in it
       RecWin w0;
       w0.m = 0; w0.n_late = 0; w0.n_fire = 0; w0.n_windows = 0; w0.quirk = false; w0.lo = 1; w0.hi = 0;
       {
-        const bool c0 = cbase + 2 * tid < n && tt[0] > -(1LL << 61) && tt[0] < (1LL << 61);
+        const bool c0 = lbase < n && tt[0] > -(1LL << 61) && tt[0] < (1LL << 61);
         const uint64_t cm = __ballot(c0);
         if (cm && s.size < (1LL << 60)) {
           const int64_t ts0 = uniform64(__shfl(tt[0], __ffsll((long long)cm) - 1));
@@ -215,49 +296,61 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
           w0.n_windows = __builtin_amdgcn_readfirstlane(w0.n_windows);
         }
       }
-      uint32_t route = 0, spill = 0;
-      int64_t mm[2];
+      if (lane < 32) wcnt[lane] = 0;
+      uint32_t route = 0, spill = 0, slow = 0;
+      const bool w0_live = w0.n_windows - w0.n_late > 0;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int64_t i = cbase + 2 * tid + e;
+      for (int e = 0; e < FU_RPL; ++e) {
+        const int64_t i = lbase + e;
         bool ok = i < n;
         if (ok && tt[e] == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
         if (ok && !all_kg) {
-          const int32_t h = b.key_hash ? hh[e] : long_hash_code(kk[e]);
+          const int32_t h = b.key_hash ? b.key_hash[i] : long_hash_code(kk[e]);   // (Java hashes: rare, loaded here)
           const int32_t kg = record_key_group(s, h);   // AbstractKeyedStateBackend.setCurrentKey :167-170
           if (kg < s.kg_start || kg > s.kg_end) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
         }
-        RecWin rw = w0;
-        if (ok && !(tt[e] >= w0.lo && tt[e] <= w0.hi)) {
-          rw = record_windows(s, tt[e], b.wm);
-          if (rw.quirk) quirk_record(s, b, kk[e], i, rw.qn, rw.q_late, rw.q_fire);
-        }
-        if (ok) late_pairs += (unsigned long long)rw.n_late;
-        const bool live = ok && rw.n_windows - rw.n_late > 0;
-        if (live && rw.n_fire > 0) set_error(s.err, FW_ERR_UNSUPPORTED);   // no per-element fires: lateness is 0
-        const bool rt = live && rw.m == m0 && kk[e] != EMPTY_KEY;
+        const bool fast = ok && tt[e] >= w0.lo && tt[e] <= w0.hi;
+        slow |= (ok && !fast ? 1u : 0u) << e;
+        if (fast) late_pairs += (unsigned long long)w0.n_late;
+        const bool live = fast && w0_live;
+        if (live && w0.n_fire > 0) set_error(s.err, FW_ERR_UNSUPPORTED);   // no per-element fires: lateness is 0
+        const bool rt = live && w0.m == m0 && kk[e] != EMPTY_KEY;
         route |= (rt ? 1u : 0u) << e;
         spill |= (live && !rt ? 1u : 0u) << e;
-        mm[e] = rw.m;
       }
-      // records of another slice, and the Long.MIN_VALUE key: the dense columns directly
-      if (__any(spill != 0)) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int64_t i = cbase + 2 * tid + e;
-          bool fresh = false;
-          int64_t idx = 0;
-          if ((spill >> e) & 1u) {
-            const int32_t p = slice_slot(s, mm[e]);
-            const int64_t kid = p < 0 ? -1 : dir_lookup(s, kk[e]);   // (Long.MIN_VALUE: kid D)
+      // records outside the wave's reference slice: the full window assignment (rare: not unrolled); a record
+      // of another slice than the primary one (or the Long.MIN_VALUE key) updates the dense columns directly
+      if (__any((slow | spill) != 0)) {
+#pragma unroll 1
+        for (int e = 0; e < FU_RPL; ++e) {
+          const int64_t i = lbase + e;
+          bool sp = (spill >> e) & 1u;
+          int64_t m = w0.m;
+          if ((slow >> e) & 1u) {
+            const int64_t ts = b.ts[i], key = b.key[i];
+            const RecWin rw = record_windows(s, ts, b.wm);
+            if (rw.quirk) quirk_record(s, b, key, i, rw.qn, rw.q_late, rw.q_fire);
+            late_pairs += (unsigned long long)rw.n_late;
+            const bool live = rw.n_windows - rw.n_late > 0;
+            if (live && rw.n_fire > 0) set_error(s.err, FW_ERR_UNSUPPORTED);
+            const bool rt = live && rw.m == m0 && key != EMPTY_KEY;
+            route |= (rt ? 1u : 0u) << e;
+            sp = live && !rt;
+            m = rw.m;
+          }
+          int64_t idx = -1;
+          if (sp) {
+            const int32_t p = slice_slot(s, m);
+            const int64_t kid = p < 0 ? -1 : dir_lookup(s, b.key[i]);   // (Long.MIN_VALUE: kid D)
             if (p < 0 || kid < 0) {
               cap_error(s, 31);
             } else {
-              idx = (int64_t)p * s.stride + kid;
-              fresh = pane_update<VT, AGG, FIRST>(s, idx, vv[e], b.ord_base + i);
+              const int64_t pi = (int64_t)p * s.stride + kid;
+              if (pane_update<VT, AGG, FIRST>(s, pi, b.val[i], b.ord_base + i)) idx = pi;
             }
           }
           if (FIRST) {   // the panes this batch created: their f1 is set after every workgroup is done
+            const bool fresh = idx >= 0;
             const unsigned long long pos = wave_append(b.new_count, fresh);
             if (fresh) {
               if ((int64_t)pos < b.new_capacity)
@@ -268,259 +361,256 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
           }
         }
       }
-      // owner of each routed record, and its rank among the wave's records of that owner
-      uint64_t hk[2];
-      int32_t bin[2], rank[2];
+      // owner of each routed record, and its rank among the unit's records of that owner (LDS counters of
+      // this wave only: in-order LDS operations of one wave need no barrier)
+      int32_t br[FU_RPL];   // owner << 16 | rank among the unit's records of that owner (fmix64 recomputed below:
+                            // fewer registers live across the scan)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the counters are zero
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        hk[e] = fmix64((uint64_t)kk[e]);
-        bin[e] = (int32_t)((hk[e] & s.dir_mask) >> f.owner_shift);
+      for (int e = 0; e < FU_RPL; ++e) {
+        const int32_t bin = (int32_t)((fmix64((uint64_t)kk[e]) & s.dir_mask) >> f.so_bits);
+        br[e] = ((route >> e) & 1u) ? (bin << 16) | atomicAdd(&wcnt[bin], 1) : 0;
       }
-      if (tid < FU_WAVES * 32) wc[tid] = 0;
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const bool act = (route >> e) & 1u;
-        uint64_t peers = __ballot(act);
-#pragma unroll
-        for (int bb = 0; bb < 5; ++bb) {
-          const bool bit = (bin[e] >> bb) & 1;
-          const uint64_t m = __ballot(bit);
-          peers &= bit ? m : ~m;
-        }
-        const int32_t below = __popcll(peers & lanemask_lt());
-        int32_t base = 0;
-        if (e == 1 && act) base = wc[wave * 32 + bin[e]];
-        rank[e] = base + below;
-        if (act && below == 0) wc[wave * 32 + bin[e]] = base + __popcll(peers);
-      }
-      __syncthreads();
-      // bin starts, and each wave's offset inside each bin (wave 0, one lane per bin)
-      if (wave == 0) {
-        int32_t c[FU_WAVES];
-        int32_t tot = 0;
-#pragma unroll
-        for (int v = 0; v < FU_WAVES; ++v) { c[v] = lane < 32 ? wc[v * 32 + lane] : 0; tot += c[v]; }
-        int32_t incl = tot;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every rank taken
+      // segment starts (lanes 0..31, one owner each) and the header words
+      uint64_t hword = 0;
+      {
+        const int32_t c = lane < 32 ? __hip_atomic_load(&wcnt[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+        int32_t incl = c;
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) {
           const int32_t y = __shfl_up(incl, o);
           if (lane >= o) incl += y;
         }
-        int32_t run = incl - tot;
-        if (lane < 32) {
-          bst[lane] = run;
-#pragma unroll
-          for (int v = 0; v < FU_WAVES; ++v) { wc[v * 32 + lane] = run; run += c[v]; }
-        }
-        if (lane == 31) bst[32] = incl;
+        const int32_t st = incl - c;
+        if (lane < 32) __hip_atomic_store(&wcnt[lane], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        hword = (uint64_t)(uint32_t)st | ((uint64_t)(uint32_t)c << 16);
       }
-      __syncthreads();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the starts are in place
+      int32_t rc = __popc(route);
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
+      for (int o = 32; o > 0; o >>= 1) rc += __shfl_xor(rc, o);
+      const int32_t routed = __builtin_amdgcn_readfirstlane(rc);   // records staged by the unit
+#pragma unroll
+      for (int e = 0; e < FU_RPL; ++e) {
         if ((route >> e) & 1u) {
-          const int32_t pos = wc[wave * 32 + bin[e]] + rank[e];
-          st_kv[pos] = make_longlong2((long long)hk[e], (long long)vv[e]);
-          st_idx[pos] = (uint16_t)(2 * tid + e);
+          const int32_t pos = __hip_atomic_load(&wcnt[br[e] >> 16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + (br[e] & 0xFFFF);
+          skv[pos] = make_longlong2((long long)fmix64((uint64_t)kk[e]), (long long)vv[e]);
+          sidx[pos] = (uint16_t)(FU_RPL * lane + e);
         }
       }
-      FU_STAMP(2 + 4 * k);
-      // the ring slot is free once every owner of the group read its previous use
-      const int sl = k % FU_S;
-      if (tid == 0) (void)fu_wait(s, f.ctr, FU_C_DONE + g * FU_S + sl, (f.uses[sl] + (unsigned long long)(k / FU_S)) * FU_MEMBERS, broken);
-      __syncthreads();
-      unsigned char* slot = f.ring + ((size_t)w * FU_S + sl) * FU_SLOT;
-      const int32_t total = bst[32];
-      longlong2* gkv = (longlong2*)(slot + FU_HDR);
-      uint32_t* gidx = (uint32_t*)(slot + FU_HDR + (size_t)FU_CH * 16);
-      for (int x = tid; x < total; x += FU_THREADS) gkv[x] = st_kv[x];
-      for (int x = tid; 2 * x < total; x += FU_THREADS) gidx[x] = ((const uint32_t*)st_idx)[x];
-      if (tid <= 32) ((uint16_t*)slot)[tid] = (uint16_t)bst[tid];
-      if (tid == 64) *(unsigned long long*)(slot + 96) = (ep << 16) | (unsigned long long)(k + 1);
-      // publish: every storing wave drained, then one counter add (same L2), or release + add (safe path)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the staging is written
+      // publish unit r - 1 (before waiting for this unit's ring slot, which needs the consumers to progress): its stores (header included) are older than unit r + 1's loads (issued after them),
+      // so waiting for all but those 12 wide loads waits for the stores only (vmcnt counts in issue order)
+      if (pend) {
+        if (next_vec && one_l2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!one_l2) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __hip_atomic_fetch_add(f.ctr + FU_C_PROD + g * FU_S + sl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_fetch_add(FU_CTR(f, FU_C_PUB + g * FU_S + pend_sl), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      FU_STAMP(3 + 4 * k);
+      // the ring slot is free once every owner of the group read its previous use
+      const int sl = r % FU_S;
+      const unsigned long long use = f.uses[sl] + (unsigned long long)(r / FU_S);
+      if (use > 0 && !broken) {
+        bool okw = true;
+        if (lane == 0) okw = fu_wait_at(s.err, FU_CTR(f, FU_C_DONE + g * FU_S + sl), use * FU_MEMBERS);
+        broken = !__builtin_amdgcn_readfirstlane(okw ? 1 : 0);
+      }
+      if (pw == 0 && lane == 0 && r < 8) FU_STAMP(9 + 3 * r);
+      // (the slot's address made scalar here, not hoisted into vector registers for the whole loop)
+      unsigned char* unit = (unsigned char*)uniform64((int64_t)(gbase + ((size_t)pu * FU_S + sl) * FU_UNIT));
+      longlong2* gkv = (longlong2*)(unit + FU_HDR);
+      uint16_t* gidx = (uint16_t*)(gkv + FU_U);
+#pragma unroll 1
+      for (int x = lane; x < routed; x += 64) gkv[x] = skv[x];
+#pragma unroll 1
+      for (int x = 2 * lane; x < routed; x += 128) *(uint32_t*)(gidx + x) = *(const uint32_t*)(sidx + x);
+      if (lane < 32) ((unsigned long long*)unit)[lane] = hword | ((use + 1) << 32);
+      pend = true;
+      pend_sl = sl;
+      if (pw == 0 && lane == 0 && r < 8) FU_STAMP(10 + 3 * r);
+      if (r + 2 < R) x_vec = load_unit(r + 2, kk, tt, vv);   // after the stores: see the publish above
+      else x_vec = false;
+    };
+    for (int r = 0; r < R; r += 2) {   // uniform
+      unit_body(r, ak, at, av, a_vec, b_vec);
+      if (r + 1 < R) unit_body(r + 1, bk, bt, bv, b_vec, a_vec);
     }
-    if (k >= 1) {
-      // ---------------- consume round kc = k - 1 ----------------
-      const int kc = k - 1;
-      const int sl = kc % FU_S;
-      if (tid == 0) {
-        if (fu_wait(s, f.ctr, FU_C_PROD + g * FU_S + sl, (f.uses[sl] + (unsigned long long)(kc / FU_S) + 1) * FU_MEMBERS,
-                    broken) && !one_l2)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (pend) {   // the last unit
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!one_l2) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      __syncthreads();
-      FU_STAMP(4 + 4 * kc);
-      // 32 threads per producer: its segment for this owner, 16-B L1-bypassing loads from the XCD's L2
-      const int p = tid >> 5, u = tid & 31;
-      const int wp = p * FU_GROUPS + g;
-      const unsigned char* slot = f.ring + ((size_t)wp * FU_S + sl) * FU_SLOT;
-      int32_t a = 0, z = 0;
-      if (u == 0) {
-        a = __builtin_nontemporal_load((const uint16_t*)slot + me);
-        z = __builtin_nontemporal_load((const uint16_t*)slot + me + 1);
-        const unsigned long long tag = __builtin_nontemporal_load((const unsigned long long*)(slot + 96));
-        if (tag != ((ep << 16) | (unsigned long long)(kc + 1))) { cap_error(s, 33); z = a; }   // not this round's chunk
-      }
-      a = __shfl(a, lane & 32);
-      z = __shfl(z, lane & 32);
-      z = min(z, FU_CH);   // (bounds a torn header could break; the tag check reports it)
-      a = min(a, z);
-      const longlong2* gkv = (const longlong2*)(slot + FU_HDR);
-      const uint16_t* gidx = (const uint16_t*)(slot + FU_HDR + (size_t)FU_CH * 16);
-      const uint32_t cb = (uint32_t)(((int64_t)kc * FU_GRID + wp) * FU_CH);   // batch index of the chunk's record 0
-      auto add = [&](const fu_v2 r, uint32_t ix) {
-        const uint64_t h = (uint64_t)r.x;
-        const uint32_t loc = (uint32_t)((h & s.dir_mask) - (uint64_t)dbase);   // slot relative to the owned range
-        if (loc >= (uint32_t)SO) { cap_error(s, 35); return; }                 // (another owner's key: a torn slot)
-        const uint32_t bb = loc & ~kbm, h0 = (uint32_t)h & kbm;
-        uint32_t kl = 0;
-        bool found = false;
-#pragma unroll
-        for (int j = 7; j >= 0; --j) {   // the nearest match wins
-          const uint32_t x = bb + ((h0 + (uint32_t)j) & kbm);
-          const bool m = lh[x] == h;
-          kl = m ? x : kl;
-          found |= m;
-        }
-        if (!found) {
-          const int32_t x = agg_probe_insert(lh + bb, s.dir_keys + dbase + bb, kbm, h, s.stats + ST_DIR_KEYS);
-          if (x < 0) { cap_error(s, 34); return; }
-          kl = bb + (uint32_t)x;
-        }
-        acc_add<VT, AGG>(L, cmpto, false, 0, kl, (int64_t)r.y, cb + ix);
-      };
-      for (int x = a + u; x < z; x += 64) {
-        const bool two = x + 32 < z;
-        const fu_v2 r0 = __builtin_nontemporal_load((const fu_v2*)(gkv + x));
-        const uint32_t i0 = __builtin_nontemporal_load(gidx + x);
-        fu_v2 r1 = r0;
-        uint32_t i1 = i0;
-        if (two) { r1 = __builtin_nontemporal_load((const fu_v2*)(gkv + x + 32)); i1 = __builtin_nontemporal_load(gidx + x + 32); }
-        add(r0, i0);
-        if (two) add(r1, i1);
-      }
-      __syncthreads();
-      FU_STAMP(5 + 4 * kc);
-      if (tid == 0) __hip_atomic_fetch_add(f.ctr + FU_C_DONE + g * FU_S + sl, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_fetch_add(FU_CTR(f, FU_C_PUB + g * FU_S + pend_sl), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (lane == 0) FU_STAMP(2);
+  } else {
+    // =============================== consumer wave ===============================
+    const int cw = wave - FU_PW;
+    int32_t* lcd = misc + 4;   // [FU_S <= 8] consumer waves done with the rounds of ring slot s
+    constexpr int UPW = FU_NP / FU_CW;   // units per consumer wave and round (lanes 0..UPW-1 poll their headers)
+    constexpr int STEPS = UPW / 8;       // 8 lanes per unit's segment
+    constexpr int KPRE = 2;              // records per lane and step loaded up front (segments up to 16 records)
+    static_assert(UPW <= 64, "one header per lane");
+    const int sub = lane & 7;
+    bool got = false;   // this lane reduced a record
+    auto unit_of = [&](int r, int u) {
+      return gbase + ((size_t)(cw * UPW + u) * FU_S + (size_t)(r % FU_S)) * FU_UNIT;
+    };
+    auto tag_of = [&](int r) { return (uint32_t)(f.uses[r % FU_S] + (unsigned long long)(r / FU_S) + 1); };
+    // one record of the segment into the accumulators
+    auto reduce_one = [&](const fu_v2 rv, uint32_t bi) {
+      const uint64_t h = (uint64_t)rv.x;
+      const uint32_t loc = (uint32_t)((h & s.dir_mask) - (uint64_t)dbase);   // slot relative to the owned range
+      if (loc >= (uint32_t)SO) { cap_error(s, 35); return; }                 // (another owner's key: a torn unit)
+      const uint32_t bb = loc & ~kbm, h0 = loc & kbm & s.home_mask;
+      const fu_u2* wl = (const fu_u2*)(lh + bb + h0);
+      const fu_u2 a0 = wl[0], a1 = wl[1], a2 = wl[2], a3 = wl[3];
+      int32_t kl = -1;
+      kl = a3.y == h ? 7 : kl; kl = a3.x == h ? 6 : kl; kl = a2.y == h ? 5 : kl; kl = a2.x == h ? 4 : kl;
+      kl = a1.y == h ? 3 : kl; kl = a1.x == h ? 2 : kl; kl = a0.y == h ? 1 : kl; kl = a0.x == h ? 0 : kl;
+      if (kl >= 0) kl += (int32_t)h0;
+      else kl = fu_probe_insert(lh + bb, s.dir_keys + dbase + bb, kbm, h0, h, s.stats + ST_DIR_KEYS);
+      if (kl < 0) { cap_error(s, 34); return; }
+      acc_add<VT, AGG>(L, cmpto, false, 0, bb + (uint32_t)kl, (int64_t)rv.y, bi);
+      got = true;
+    };
+    // headers: lane u < UPW holds the header word of unit cw * UPW + u of the round, read once the group's
+    // publication counter of the ring slot says every unit of the round is complete (one polling lane per wave)
+    for (int r = 0; r < R; ++r) {   // uniform
+      const int sl = r % FU_S;
+      const uint32_t tag = tag_of(r);
+      const unsigned long long use = f.uses[sl] + (unsigned long long)(r / FU_S);
+      if (!broken) {
+        bool okw = true;
+        if (lane == 0) okw = fu_wait_at(s.err, FU_CTR(f, FU_C_PUB + g * FU_S + sl), (use + 1) * FU_NP);
+        broken = !__builtin_amdgcn_readfirstlane(okw ? 1 : 0);
+      }
+      if (!one_l2) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (cw == 0 && lane == 0 && r < 8) FU_STAMP(32 + 3 * r);
+      uint64_t hw = 0;
+      if (lane < UPW && !broken)
+        hw = __hip_atomic_load((const unsigned long long*)unit_of(r, lane) + me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < UPW && !broken && (uint32_t)(hw >> 32) != tag) { cap_error(s, 33); hw = 0; }   // (a torn publication)
+      if (lane >= UPW) hw = 0;
+      // every lane's first KPRE records of each step's segment, loaded before any is reduced
+      fu_v2 rv[STEPS][KPRE];
+      uint32_t bi[STEPS][KPRE];
+      int32_t cnt[STEPS], st[STEPS];
+#pragma unroll
+      for (int q = 0; q < STEPS; ++q) {
+        const int u = q * 8 + (lane >> 3);
+        const uint64_t w = __shfl(hw, u);
+        st[q] = (int32_t)(w & 0xFFFF);
+        cnt[q] = min((int32_t)((w >> 16) & 0xFFFF), FU_U - st[q]);   // (bounds a torn header could break)
+        const unsigned char* unit = unit_of(r, u);
+        const fu_v2* gkv = (const fu_v2*)(unit + FU_HDR);
+        const uint16_t* gidx = (const uint16_t*)(unit + FU_HDR + (size_t)FU_U * 16);
+        const uint32_t ub = (uint32_t)(((int64_t)(r * FU_GROUPS + g) * FU_NP + cw * UPW + u) * FU_U);
+#pragma unroll
+        for (int k = 0; k < KPRE; ++k) {
+          const int i = sub + 8 * k;
+          if (i < cnt[q]) {
+            rv[q][k] = __builtin_nontemporal_load(gkv + st[q] + i);
+            bi[q][k] = ub + __builtin_nontemporal_load(gidx + st[q] + i);
+          }
+        }
+      }
+      if (cw == 0 && lane == 0 && r < 8) FU_STAMP(33 + 3 * r);
+#pragma unroll
+      for (int q = 0; q < STEPS; ++q) {
+#pragma unroll
+        for (int k = 0; k < KPRE; ++k)
+          if (sub + 8 * k < cnt[q]) reduce_one(rv[q][k], bi[q][k]);
+      }
+      if (cw == 0 && lane == 0 && r < 8) FU_STAMP(34 + 3 * r);
+      // segments longer than KPRE * 8 records (rare)
+#pragma unroll 1
+      for (int q = 0; q < STEPS; ++q) {
+        if (!__any(cnt[q] > 8 * KPRE)) continue;
+        const int u = q * 8 + (lane >> 3);
+        const unsigned char* unit = unit_of(r, u);
+        const fu_v2* gkv = (const fu_v2*)(unit + FU_HDR);
+        const uint16_t* gidx = (const uint16_t*)(unit + FU_HDR + (size_t)FU_U * 16);
+        const uint32_t ub = (uint32_t)(((int64_t)(r * FU_GROUPS + g) * FU_NP + cw * UPW + u) * FU_U);
+        for (int i = sub + 8 * KPRE; i < cnt[q]; i += 8)
+          reduce_one(__builtin_nontemporal_load(gkv + st[q] + i), ub + __builtin_nontemporal_load(gidx + st[q] + i));
+      }
+      // this wave is done with round r; the last consumer wave of the workgroup tells the group
+      if (lane == 0) {
+        const int old = atomicAdd(&lcd[sl], 1);
+        if (old + 1 == FU_CW * (r / FU_S + 1))
+          __hip_atomic_fetch_add(FU_CTR(f, FU_C_DONE + g * FU_S + sl), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (__any(got) && lane == 0) misc[12] = 1;
+    if (lane == 0) FU_STAMP(3);
   }
   if (__any(late_pairs != 0)) {
     for (int off = 32; off > 0; off >>= 1) late_pairs += __shfl_xor(late_pairs, off);
     if (lane == 0) atomicAdd(&s.stats[ST_LATE], late_pairs);
   }
+  __syncthreads();
 
-  // ---------------- publish the partials of the owned slots (write-through 4- and 8-B stores) ----------------
-  const size_t pb = ((size_t)me * FU_GROUPS + g) << f.so_bits;
-  for (int x = tid; x < SO; x += FU_THREADS) {
-    const uint32_t lf = lfirst[x];
-    __hip_atomic_store(f.pfirst + pb + x, lf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lf != NO_FIRST) {
-      if (AGG & FW_AGG_SUM)
-        __hip_atomic_store((unsigned long long*)f.psum + pb + x, (unsigned long long)lsum[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (HAS_MIN)
-        __hip_atomic_store((unsigned long long*)f.pmn + pb + x, (unsigned long long)lmin[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (HAS_MAX)
-        __hip_atomic_store((unsigned long long*)f.pmx + pb + x, (unsigned long long)lmax[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (HAS_CNT)
-        __hip_atomic_store((unsigned long long*)f.pcnt + pb + x, (unsigned long long)lcnt[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // ---------------- flush: the owned slots' accumulators into the dense columns of slice m0 ----------------
+  if (tid == 0) {   // the slot of slice m0, claimed (idempotently) by every owner that reduced a record
+    int32_t p0 = -1;
+    if (misc[12]) {
+      p0 = slice_slot(s, m0);
+      if (p0 < 0) cap_error(s, 32);
     }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  FU_STAMP(60);
-  if (tid == 0) {
-    __hip_atomic_fetch_add(f.ctr + FU_C_FOLD + me, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    (void)fu_wait(s, f.ctr, FU_C_FOLD + me, (ep + 1) * FU_GROUPS, broken);
+    misc[2] = p0;
   }
   __syncthreads();
-  FU_STAMP(61);
-
-  // ---------------- fold: slots [g SH, (g+1) SH) of range me over the 8 groups' partials ----------------
-  const int SH = SO / FU_GROUPS;
-  for (int x0 = 0; x0 < SH; x0 += FU_THREADS) {   // uniform
-    const int x = g * SH + x0 + tid;
-    bool touched = false;
-    int64_t tsum = sum_identity(VT), tmin = INT64_MAX, tmax = INT64_MIN, tcnt = 0;
-    uint32_t tfirst = NO_FIRST;
-    if (x0 + tid < SH) {
-#pragma unroll
-      for (int gg = 0; gg < FU_GROUPS; ++gg) {   // group order: a fixed association for double sums
-        const size_t pi = (((size_t)me * FU_GROUPS + gg) << f.so_bits) + (size_t)x;
-        const uint32_t pf = __hip_atomic_load(f.pfirst + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (pf == NO_FIRST) continue;
-        touched = true;
-        tfirst = pf < tfirst ? pf : tfirst;
-        if (AGG & FW_AGG_SUM) {
-          const int64_t v = (int64_t)__hip_atomic_load((unsigned long long*)f.psum + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (VT == FW_VALUE_I64) tsum = jadd(tsum, v);
-          else tsum = __double_as_longlong(__longlong_as_double(tsum) + __longlong_as_double(v));
-        }
-        if (HAS_MIN) {
-          const int64_t v = (int64_t)__hip_atomic_load((unsigned long long*)f.pmn + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          tmin = v < tmin ? v : tmin;
-        }
-        if (HAS_MAX) {
-          const int64_t v = (int64_t)__hip_atomic_load((unsigned long long*)f.pmx + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          tmax = v > tmax ? v : tmax;
-        }
-        if (HAS_CNT) {
-          const int64_t v = (int64_t)__hip_atomic_load((unsigned long long*)f.pcnt + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          tcnt = jadd(tcnt, v);
+  const int32_t p0 = misc[2];
+  if (p0 >= 0) {
+    for (int x = tid; x < SO; x += FU_THREADS) {   // whole waves (SO is a power of two >= 64)
+      const uint32_t lf = lfirst[x];
+      const int64_t idx = (int64_t)p0 * s.stride + dbase + x;
+      bool fresh = false;
+      if (lf != NO_FIRST) {
+      if (AGG & FW_AGG_SUM) {
+        if (VT == FW_VALUE_I64) atomicAdd((unsigned long long*)&s.c.sum[idx], (unsigned long long)lsum[x]);
+        else unsafeAtomicAdd((double*)&s.c.sum[idx], __longlong_as_double(lsum[x]));
+      }
+      if (HAS_MIN) atomicMin((long long*)&s.c.mn[idx], (long long)lmin[x]);
+      if (HAS_MAX) atomicMax((long long*)&s.c.mx[idx], (long long)lmax[x]);
+      if (HAS_CNT) atomicAdd((unsigned long long*)&s.c.cnt[idx], (unsigned long long)lcnt[x]);
+      if (FIRST) {
+        // a pane present before this batch keeps its (earlier) first arrival; first only decreases within the
+        // launch, so a plain load already at or below this batch's ordinal proves there is nothing to do
+        const int64_t ord = b.ord_base + (int64_t)lf;
+        if (ord < s.c.first[idx]) fresh = atomicMin((long long*)&s.c.first[idx], (long long)ord) == INT64_MAX;
+      } else {
+        s.c.present[idx] = 1;
+      }
+      }
+      if (FIRST) {   // the panes this batch created (one creator each): their f1 once every workgroup is done
+        const unsigned long long pos = wave_append(b.new_count, fresh);
+        if (fresh) {
+          if ((int64_t)pos < b.new_capacity)
+            __hip_atomic_store((unsigned long long*)b.new_list + pos, (unsigned long long)idx, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          else cap_error(s, 5);
         }
       }
     }
-    // the primary slice's pane slot: claimed (idempotently) once some slot of this share was touched
-    // (a block-wide OR through LDS: all of this kernel's LDS stays dynamic)
-    if (tid == 0) misc[4] = 0;
-    __syncthreads();
-    if (__any(touched) && lane == 0) misc[4] = 1;
-    __syncthreads();
-    if (misc[4]) {   // uniform
-      if (tid == 0) misc[2] = slice_slot(s, m0);
-      __syncthreads();
-      const int32_t p0 = misc[2];
-      if (p0 < 0) {
-        if (tid == 0) cap_error(s, 32);
-      } else if (touched) {
-        const int64_t idx = (int64_t)p0 * s.stride + dbase + x;
-        if (AGG & FW_AGG_SUM) {
-          if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], tsum);
-          else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(tsum));
-        }
-        if (HAS_MIN) { if (tmin < s.c.mn[idx]) s.c.mn[idx] = tmin; }
-        if (HAS_MAX) { if (tmax > s.c.mx[idx]) s.c.mx[idx] = tmax; }
-        if (HAS_CNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], tcnt);
-        if (FIRST) {
-          // a pane present before this batch keeps its (earlier) first arrival
-          if (s.c.first[idx] == INT64_MAX && (int64_t)tfirst < n) {
-            s.c.first[idx] = b.ord_base + (int64_t)tfirst;
-            s.c.f1v[idx] = f1col[tfirst];
-          }
-        } else {
-          s.c.present[idx] = 1;
-        }
-      }
-      __syncthreads();   // misc[2] is rewritten by the next share
-    }
   }
+  if (tid == 0) FU_STAMP(4);
 
-  // ---------------- the last workgroup: f1 of the panes the direct records created ----------------
+  // ---------------- the last workgroup: f1 of the panes this batch created ----------------
   if (FIRST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      const unsigned long long done = __hip_atomic_fetch_add(f.ctr + FU_C_FIN, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long done = __hip_atomic_fetch_add(FU_CTR(f, FU_C_FIN), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       misc[3] = done + 1 == (ep + 1) * FU_GRID ? 1 : 0;
     }
     __syncthreads();
@@ -536,7 +626,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(Spec s, BatchIn b, FusedBu
       if (tid == 0) __hip_atomic_store(b.new_count, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  FU_STAMP(62);
+  if (tid == 0) FU_STAMP(5);
 }
 
 }  // namespace fw

@@ -312,6 +312,7 @@ class WindowEngine:
             raise _abi.FwError(rc, self._fn("last_error")(None).decode() or "fw_create failed")
         self.h = h
         self._inflight = []   # device columns pushed since the last sync/collect (read asynchronously)
+        self._drain_keep = {}   # drain ticket -> inputs pushed before it (collect_begin / collect_end)
 
     def _fn(self, name):
         return getattr(self.lib, f"{self.prefix}_{name}")
@@ -357,6 +358,25 @@ class WindowEngine:
         if self.prefix == "fw":
             self._check(self._fn("sync")(self.h))
             self._inflight.clear()
+            self._drain_keep = {t: 0 for t in self._drain_keep}
+
+    def collect_begin(self):
+        """Start an asynchronous drain of the results since the last collect (fw_collect_begin): returns a ticket for
+        collect_end; the batches pushed meanwhile run while the results travel to the host."""
+        t = ctypes.c_int32()
+        self._check(self._fn("collect_begin")(self.h, ctypes.byref(t)))
+        self._drain_keep[t.value] = len(self._inflight)   # inputs pushed before the drain: read once it lands
+        return t.value
+
+    def collect_end(self, ticket):
+        """The drain `ticket` (collect_begin) once it has landed: the same dict as collect()."""
+        o = _abi.FwOut()
+        self._check(self._fn("collect_end")(self.h, ticket, ctypes.byref(o)))
+        done = self._drain_keep.pop(ticket, 0)
+        del self._inflight[:done]
+        for t in self._drain_keep:
+            self._drain_keep[t] = max(0, self._drain_keep[t] - done)
+        return self._out_dict(o)
 
     def collect(self):
         """Results since the last collect: dict of numpy columns + (mark_wm, mark_pos)."""
@@ -364,8 +384,12 @@ class WindowEngine:
         if self.prefix == "fw":
             self._check(self._fn("collect")(self.h, ctypes.byref(o), _abi.FW_MEM_HOST))
             self._inflight.clear()
+            self._drain_keep = {t: 0 for t in self._drain_keep}
         else:
             self._check(self._fn("collect")(self.h, ctypes.byref(o)))
+        return self._out_dict(o)
+
+    def _out_dict(self, o):
         n = o.n
         res = {"n": n}
         for name in ("key", "f1", "ts", "sum_i64", "min_i64", "max_i64", "count", "sum_f64", "min_f64", "max_f64"):

@@ -54,6 +54,7 @@ extern "C" {
 #define FW_ERR_KEY_GROUP      4  /* key group of a record outside [kg_start, kg_end] of this subtask         */
 #define FW_ERR_UNSUPPORTED    5  /* configuration this backend does not implement                            */
 #define FW_ERR_DEVICE         6  /* HIP runtime failure                                                      */
+#define FW_ERR_RESIDENCY      7  /* fused ingest (ingest_mode 3): its workgroups were not all resident at once */
 
 /* ---- window assigner (SJ/api/windowing/assigners) ---- */
 #define FW_TUMBLING 0            /* TumblingEventTimeWindows.of(size[, offset])  (offset already % size)     */
@@ -200,6 +201,15 @@ int         fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_h
 int         fw_advance_watermark(fw_engine* e, int64_t wm);
 int         fw_sync(fw_engine* e);
 int         fw_collect(fw_engine* e, fw_out* out, int32_t mem);
+/* Asynchronous drain of the same results (the operator hands fired windows downstream while the next batch already
+ * runs; they need only precede their watermark, AbstractStreamOperator.java:803-808).  fw_collect_begin enqueues on
+ * the engine stream a copy of every result and watermark mark since the last collect into pinned host staging (two
+ * buffers, alternating) and restarts the log; it returns at once with a ticket.  fw_collect_end(ticket) waits for
+ * that copy and fills `out` (FW_MEM_HOST layout) with columns valid until the next fw_collect_begin after it.  At
+ * most two drains are outstanding; one holds at most min(out_capacity, 2^22) results (more: FW_ERR_CAPACITY at
+ * fw_collect_end).  Device errors surface at fw_collect_end. */
+int         fw_collect_begin(fw_engine* e, int32_t* ticket);
+int         fw_collect_end(fw_engine* e, int32_t ticket, fw_out* out);
 int         fw_get_stats(fw_engine* e, fw_stats* st);
 const char* fw_last_error(const fw_engine* e);
 void        fw_destroy(fw_engine* e);

@@ -251,3 +251,51 @@ def test_c2_ten_million_keys():
     sg, so = _run(cfg, 4, batch, 10_000_000, 1 << 22, 1)
     assert sg["ingest_form"] == 1   # direct: a 10 M-key directory bucket does not fit LDS
     assert sg["panes_fired"] == so["panes_fired"] > 0
+
+
+def test_c5_one_rank_shard():
+    """One rank of BASELINE config C5 (8 x MI355X keyBy shuffle, maxParallelism 128, 100 M uniform keys), on one
+    GPU: rank 3 owns key groups [48, 63] (KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex(128, 8, 3),
+    KeyGroupRangeAssignment.java:78-89) and receives the records of all eight sources whose key group it owns
+    (:105-107), ~4 Mi per step, into an engine sized like bench.py's C5 rank (12.5 M keys of its share; the direct
+    ingest form).  Two steps of the global stream (8 sources x 2^22 events, R = 2^27 events per second) with a
+    watermark after each, then MAX_WATERMARK; bit-exact against the oracle restricted to the same key groups."""
+    from flink_amd.keygroups import compute_key_group_range_for_operator_index, operator_index_np
+    from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, WindowEngine, make_config
+    from oracle.oracle import OracleEngine
+    mp, world, rank, n_keys, rate, src_batch = 128, 8, 3, 100_000_000, 1 << 27, 1 << 22
+    kg = compute_key_group_range_for_operator_index(mp, world, rank)
+    assert kg == (48, 63)
+    key_cap = int(n_keys * (kg[1] - kg[0] + 1) / mp * 1.05) + 4096
+    cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", keep_first_f1=True),
+                      max_parallelism=mp, key_group_range=kg, key_capacity=key_cap, max_batch=5 << 20,
+                      out_capacity=1 << 24)
+    from flink_amd.synth import stream
+    eg, eo = WindowEngine(cfg), OracleEngine(cfg)
+    rg, ro = [], []
+    for step in range(2):
+        k, t, v = stream(step * world * src_batch, world * src_batch, n_keys, rate, T0, device="cuda")
+        kn = k.cpu().numpy()
+        sel = np.nonzero(operator_index_np(kn, mp, world) == rank)[0]
+        assert 3_900_000 < len(sel) < 4_500_000    # the rank's share of the step
+        idx = torch.from_numpy(sel).cuda()
+        kr, tr, vr = k[idx].contiguous(), t[idx].contiguous(), v[idx].contiguous()
+        wm = int(t.max().item()) - 1
+        eg.push(kr, tr, vr)
+        eg.advance_watermark(wm)
+        rg.append(eg.collect())
+        eo.push(kr.cpu().numpy(), tr.cpu().numpy(), vr.cpu().numpy())
+        eo.advance_watermark(wm)
+        ro.append(eo.collect())
+    for e, out in ((eg, rg), (eo, ro)):
+        e.advance_watermark(LONG_MAX)
+        out.append(e.collect())
+    sg, so = eg.stats(), eo.stats()
+    eg.close()
+    eo.close()
+    assert sg["ingest_form"] == 1   # direct: a 12.5 M-key share does not fit LDS buckets
+    a, b = _epochs_np(rg, ("sum_i64",)), _epochs_np(ro, ("sum_i64",))
+    assert [w for w, _ in a] == [w for w, _ in b]
+    for (w, x), (_, y) in zip(a, b):
+        assert x.shape == y.shape and np.array_equal(x, y), f"wm {w}"
+    assert sg["panes_fired"] == so["panes_fired"] > 3_000_000
