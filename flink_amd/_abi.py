@@ -18,7 +18,6 @@ FW_ERR_CAPACITY = 3
 FW_ERR_KEY_GROUP = 4
 FW_ERR_UNSUPPORTED = 5
 FW_ERR_DEVICE = 6
-FW_ERR_RESIDENCY = 7
 
 FW_TUMBLING = 0
 FW_SLIDING = 1

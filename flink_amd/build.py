@@ -17,7 +17,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 ENGINE_SOURCES = ["fw_engine.hip"]
 ENGINE_DEPS = ["java_semantics.h", os.path.join("..", "..", "include", "flink_window.h"), "flink_kg_format.h", "fw_decode.hip",
-               "fw_session.hip", "fw_list.hip", "fw_fused.hip"]
+               "fw_session.hip", "fw_list.hip"]
 
 
 def _stale(target, deps):

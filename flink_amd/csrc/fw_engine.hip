@@ -56,7 +56,9 @@ namespace fw {
 
 constexpr int64_t FREE_TAG = INT64_MIN;
 constexpr int64_t EMPTY_KEY = INT64_MIN;
-constexpr int MAX_K = 64;          // max slices per window
+constexpr int MAX_K = 1024;        // max slices per window (k_watermark's LDS table of a window's slice slots)
+constexpr int MAX_P = 4096;        // max slice slots
+constexpr int LIST_MAX_K = 64;     // list state: slices per window (k_list_gather's per-thread slice table)
 constexpr int BLOCK = 256;
 
 // ST_SHARES: helper shares run; ST_DIR_KEYS: keys in the directory buckets (inserts since the last compaction + the keys it kept)
@@ -113,8 +115,6 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   uint64_t dir_mask;
   int64_t D;
   int32_t kb_bits;  // log2(slots per directory bucket); probing stays inside the home bucket
-  uint32_t home_mask;   // probe start inside the bucket = home & home_mask: ~0 (the home slot) or ~7 (the start of
-                        // its 64-B line of 8 slots: the fused form reads a key's candidates as one aligned line)
   int32_t nb;       // directory buckets = D >> kb_bits
   // slices
   int32_t P;
@@ -190,7 +190,7 @@ __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
 // stale) load can only under-report, which the CAS then corrects; a key found EMPTY at slot j cannot
 // sit at a later slot.
 __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
-                                                         int32_t kb_bits, uint32_t home_mask, int64_t D, int64_t key,
+                                                         int32_t kb_bits, int64_t D, int64_t key,
                                                          unsigned long long* inserted) {
   if (key == EMPTY_KEY) {
     if (dir_min_used[0] == 0) dir_min_used[0] = 1;
@@ -199,7 +199,7 @@ __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int3
   const uint64_t home = fmix64((uint64_t)key) & dir_mask;
   const uint64_t kbm = (1ull << kb_bits) - 1;
   const uint64_t base = home & ~kbm;
-  uint64_t off = home & kbm & (uint64_t)home_mask;
+  uint64_t off = home & kbm;
   for (uint64_t probe = 0; probe <= kbm; ++probe) {
     const uint64_t h = base + off;
     const int64_t cur = dir_keys[h];
@@ -215,17 +215,17 @@ __device__ __forceinline__ int64_t dir_find_or_insert_at(int64_t* dir_keys, int3
   return -1;
 }
 __device__ __noinline__ int64_t dir_find_or_insert_call(int64_t* dir_keys, int32_t* dir_min_used, uint64_t dir_mask,
-                                                        int32_t kb_bits, uint32_t home_mask, int64_t D, int64_t key,
+                                                        int32_t kb_bits, int64_t D, int64_t key,
                                                         unsigned long long* inserted) {
-  return dir_find_or_insert_at(dir_keys, dir_min_used, dir_mask, kb_bits, home_mask, D, key, inserted);
+  return dir_find_or_insert_at(dir_keys, dir_min_used, dir_mask, kb_bits, D, key, inserted);
 }
 // inline: the direct form's per-record lookup
 __device__ __forceinline__ int64_t dir_find_or_insert(const Spec& s, int64_t key) {
-  return dir_find_or_insert_at(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.home_mask, s.D, key, s.stats + ST_DIR_KEYS);
+  return dir_find_or_insert_at(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key, s.stats + ST_DIR_KEYS);
 }
 // out of line: the rare lookups of the partitioned form (new keys, direct-list records) and restore
 __device__ __forceinline__ int64_t dir_lookup(const Spec& s, int64_t key) {
-  return dir_find_or_insert_call(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.home_mask, s.D, key, s.stats + ST_DIR_KEYS);
+  return dir_find_or_insert_call(s.dir_keys, s.dir_min_used, s.dir_mask, s.kb_bits, s.D, key, s.stats + ST_DIR_KEYS);
 }
 
 // slice number m -> slot p, claiming a FREE slot.  Returns -1 when slot p holds another live slice.
@@ -1994,7 +1994,7 @@ __global__ void k_fire_emit(Spec s, const unsigned long long* sorted_key, int64_
 // ------------------------------------------------------------------------------------------------
 constexpr int WM_THREADS = 1024;
 constexpr int WM_MAXT = 2048;      // windows firing at one watermark
-constexpr int WM_MAXP = 1024;      // slices purged at one watermark (>= P)
+constexpr int WM_MAXP = MAX_P;     // slices purged at one watermark (>= P)
 
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old, int64_t wm_new, unsigned int* done) {
@@ -2219,7 +2219,7 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
       continue;
     }
     // re-insert: the same probe sequence as dir_find_or_insert, in the fresh LDS layout
-    uint32_t y = (uint32_t)fmix64((uint64_t)key) & kbm & s.home_mask;
+    uint32_t y = (uint32_t)fmix64((uint64_t)key) & kbm;
     for (;;) {
       const unsigned long long prev =
           atomicCAS((unsigned long long*)&nkey[y], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
@@ -2327,9 +2327,9 @@ __global__ __launch_bounds__(1024) void k_quirk_apply(Spec s, int64_t* list, uns
   if (threadIdx.x == 0) *count = 0;
 }
 
-// asynchronous drain (fw_collect_begin): the output log's rows and device marks since the last collect, copied into
-// pinned host staging (column-major, `rows` per column) with coalesced stores over PCIe; hdr[0..3] = rows, device
-// marks, fits, the engine's error word.  A log larger than the staging is left in place (fits = 0)
+// asynchronous drain (fw_collect_begin), step 1 on the engine stream: the output log's rows and device marks since
+// the last collect copied into device staging (column-major, `rows` per column; HBM to HBM), with hdr[0..3] = rows,
+// device marks, fits, the engine's error word.  A log larger than the staging is left in place (fits = 0)
 constexpr int DR_COLS = 8;   // key, f1, ts, sum, min, max, count, window start
 __global__ __launch_bounds__(BLOCK) void k_drain(OutLog L, const int32_t* err, int64_t rows, int64_t* stage, int64_t* marks,
                                                  int64_t* hdr) {
@@ -2358,6 +2358,23 @@ __global__ void k_drain_reset(OutLog L, int64_t rows) {
   if ((int64_t)n <= rows && (int64_t)n <= L.capacity && (int64_t)nm <= L.mark_capacity) {
     *L.count = 0;
     *L.mark_count = 0;
+  }
+}
+// step 2 on the drain stream (beside the next batch's kernels): the staged rows, marks and header into the pinned
+// host buffer (zero-copy stores over PCIe), only the columns present and only the rows staged
+__global__ __launch_bounds__(BLOCK) void k_drain_host(const int64_t* stage, const int64_t* dmarks, const int64_t* dhdr,
+                                                      int64_t rows, int64_t mark_cap, uint32_t colmask, int64_t* host) {
+  const int64_t n = dhdr[2] ? dhdr[0] : 0, nm = dhdr[2] ? dhdr[1] : 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+#pragma unroll
+    for (int c = 0; c < DR_COLS; ++c)
+      if ((colmask >> c) & 1u) host[(int64_t)c * rows + i] = stage[(int64_t)c * rows + i];
+  }
+  int64_t* hmarks = host + (size_t)DR_COLS * rows;
+  if (blockIdx.x == 0) {
+    for (int64_t i = threadIdx.x; i < nm; i += blockDim.x) hmarks[i] = dmarks[i];
+    if (threadIdx.x < 4) hmarks[mark_cap + threadIdx.x] = dhdr[threadIdx.x];
   }
 }
 
@@ -2527,17 +2544,9 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
 
 }  // namespace fw
 
-#include "fw_fused.hip"
 
 #include <mutex>
 struct fw_engine;
-namespace {
-// fused launches are serialised device-wide: each one needs every CU of the device resident at once, so two
-// engines' launches must not split the CUs between them (fw_fused.hip)
-std::mutex g_fused_mu;
-hipEvent_t g_fused_ev[64] = {};
-const fw_engine* g_fused_owner[64] = {};
-}  // namespace
 
 // ==================================================================================================
 // host side
@@ -2581,13 +2590,16 @@ struct SessDev {
   int64_t* f1;      // first-arrival f1 (keep_first_f1) / the extremal record's f1 (maxBy / minBy), or null
   unsigned long long* live;   // [D + 1] slots in flight
   unsigned long long* trig;   // [D + 1] slots whose trigger timer (at maxTimestamp) is pending
-  // list state (FW_AGG_LIST): per slot the window's elements as a linked list through an element pool, a ring
-  // of pcap entries indexed by arrival ordinal (pord = -1: entry free)
+  // list state (FW_AGG_LIST): per slot the window's elements as a linked list through an element pool of pcap
+  // entries, handed out from a ring of free entry indices (freeq; pool[0] head, pool[1] end of the free ones,
+  // pool[2] entries freed during the current launch, listed in fpend)
   int32_t list;
   int64_t* head;
   int64_t* tail;
   int64_t* len;
-  int64_t *pv, *pf1, *pnext, *pord;
+  int64_t *pv, *pf1, *pnext;
+  int64_t *freeq, *fpend;
+  unsigned long long* pool;
   int64_t pcap;
   // hot keys (a batch run of >= hot records, reducing state): walked by one wave each (k_sess_walk_hot)
   int32_t hot;
@@ -2697,12 +2709,6 @@ struct fw_engine {
   unsigned int* wm_done = nullptr;   // k_watermark's workgroup completion counter
   // partitioned ingest (ingest_mode 2)
   bool routed = false;
-  // fused ingest (ingest_mode 3, fw_fused.hip)
-  bool fused = false;
-  FusedBuf fb{};
-  size_t fused_lds = 0;
-  int64_t fused_launches = 0;
-  unsigned long long fused_uses[FU_S] = {};
   RouteBuf rb{};                            // fields shared by both parities (dbg, stamps)
   RouteBuf rbs[NBUF] = {};                  // routed-batch buffers, one set per buffer slot
   unsigned int* dflags = nullptr;           // direct-record flags, a ring of FLAG_RING
@@ -2773,6 +2779,8 @@ struct fw_engine {
   struct Drain {
     int64_t* host = nullptr;        // [DR_COLS][rows] columns, then [mark_capacity] device mark positions, then hdr[4]
     int64_t* dptr = nullptr;        // the same memory as the device sees it
+    int64_t* dev = nullptr;         // device staging of the same layout (k_drain's copy)
+    hipEvent_t staged = nullptr;    // the engine stream's copy done (the drain stream waits for it)
     hipEvent_t done = nullptr;
     bool pending = false;           // begun, not yet ended
     std::vector<HostMark> marks;    // the host marks of the drain
@@ -2780,6 +2788,7 @@ struct fw_engine {
     std::vector<int64_t> mark_wm, mark_pos;
   };
   Drain drains[2];
+  hipStream_t dstream = nullptr;     // drain stream: staged results to pinned host memory beside the next batches
   int64_t drain_rows = 0;
   int64_t drain_seq = 0;
   int dev = 0;
@@ -2792,10 +2801,6 @@ struct fw_engine {
     return (T*)p;
   }
   ~fw_engine() {
-    {
-      std::lock_guard<std::mutex> lk(g_fused_mu);
-      if (g_fused_owner[dev & 63] == this) g_fused_owner[dev & 63] = nullptr;
-    }
     if (rstream) (void)hipStreamSynchronize(rstream);
     if (stream) (void)hipStreamSynchronize(stream);
     if (rstream) (void)hipStreamDestroy(rstream);
@@ -2811,7 +2816,13 @@ struct fw_engine {
     if (dir_keys_host) (void)hipHostFree(dir_keys_host);
     for (void* p : {dec_table, dec_small, dec_bytes}) if (p) (void)hipFree(p);
     if (h_pin) (void)hipHostFree(h_pin);
-    for (auto& d : drains) { if (d.host) (void)hipHostFree(d.host); if (d.done) (void)hipEventDestroy(d.done); }
+    if (dstream) { (void)hipStreamSynchronize(dstream); (void)hipStreamDestroy(dstream); }
+    for (auto& d : drains) {
+      if (d.host) (void)hipHostFree(d.host);
+      if (d.dev) (void)hipFree(d.dev);
+      if (d.done) (void)hipEventDestroy(d.done);
+      if (d.staged) (void)hipEventDestroy(d.staged);
+    }
     if (h_pin_cnt) (void)hipHostFree(h_pin_cnt);
     for (void* p : {(void*)list_k1, (void*)list_k2, (void*)list_v1, (void*)list_v2, list_temp}) if (p) (void)hipFree(p);
   }
@@ -2911,37 +2922,6 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   // (ev_agg[par] is recorded by fw_push_batch once the batch's extra-window list is applied too)
 }
 
-// fused form (fw_fused.hip): one launch per batch, FU_GRID workgroups, after any other engine's fused launch
-// (the dynamic-LDS attribute is set once per instantiation, under the device-wide lock, in fused_prepare_t)
-template <int VT, int AGG, bool FIRST>
-static void fused_prepare_t(fw_engine* e, hipError_t* rc) {
-  static bool attr_set = false;
-  std::lock_guard<std::mutex> lk(g_fused_mu);
-  if (attr_set) return;
-  hipFuncAttributes fa{};
-  *rc = hipFuncGetAttributes(&fa, (const void*)k_fused<VT, AGG, FIRST>);
-  if (*rc == hipSuccess)
-    *rc = hipFuncSetAttribute((const void*)k_fused<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(160 * 1024 - fa.sharedSizeBytes));
-  attr_set = *rc == hipSuccess;
-}
-template <int VT, int AGG, bool FIRST>
-static void launch_fused_t(fw_engine* e, const BatchIn& b, const int64_t* f1col) {
-  FusedBuf f = e->fb;
-  f.rounds = (int32_t)((b.n + FU_ROUND - 1) / FU_ROUND);
-  f.epoch = e->fused_launches;
-  for (int q = 0; q < FU_S; ++q) f.uses[q] = e->fused_uses[q];
-  std::lock_guard<std::mutex> lk(g_fused_mu);
-  const int d = e->dev & 63;
-  if (!g_fused_ev[d]) (void)hipEventCreateWithFlags(&g_fused_ev[d], hipEventDisableTiming);
-  if (g_fused_owner[d] && g_fused_owner[d] != e && g_fused_ev[d]) (void)hipStreamWaitEvent(e->stream, g_fused_ev[d], 0);
-  hipLaunchKernelGGL((k_fused<VT, AGG, FIRST>), dim3(FU_GRID), dim3(FU_THREADS), e->fused_lds, e->stream, e->s, b, f, f1col);
-  if (g_fused_ev[d]) (void)hipEventRecord(g_fused_ev[d], e->stream);
-  g_fused_owner[d] = e;
-  e->fused_launches++;
-  for (int k = 0; k < f.rounds; ++k) e->fused_uses[k % FU_S]++;
-}
-
 // no window of the assigner has its maxTimestamp or its cleanup time in (old, new]: the advance fires
 // and purges nothing (a live slice's fire and cleanup times lie above the watermark it was created
 // under), only the watermark's mark is due.  Conservative near the int64 edges.
@@ -2996,26 +2976,6 @@ static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
         case 1: if (_f) FN<1, 1, true>(e, ##__VA_ARGS__); else FN<1, 1, false>(e, ##__VA_ARGS__); break;   \
         case 16: FN<1, 16, true>(e, ##__VA_ARGS__); break;                                       \
         case 32: FN<1, 32, true>(e, ##__VA_ARGS__); break;                                       \
-        case 9: if (_f) FN<1, 9, true>(e, ##__VA_ARGS__); else FN<1, 9, false>(e, ##__VA_ARGS__); break;   \
-        default: if (_f) FN<1, 15, true>(e, ##__VA_ARGS__); else FN<1, 15, false>(e, ##__VA_ARGS__); break; \
-      }                                                                                          \
-    }                                                                                            \
-  } while (0)
-
-// the fused form's instantiated reduce shapes (no maxBy / minBy)
-#define FW_DISPATCH_FUSED(FN, e, ...)                                                            \
-  do {                                                                                           \
-    const Spec& _s = (e)->s;                                                                     \
-    const bool _f = _s.first != 0;                                                               \
-    if (_s.vt == FW_VALUE_I64) {                                                                 \
-      switch (_s.agg) {                                                                          \
-        case 1: if (_f) FN<0, 1, true>(e, ##__VA_ARGS__); else FN<0, 1, false>(e, ##__VA_ARGS__); break;   \
-        case 9: if (_f) FN<0, 9, true>(e, ##__VA_ARGS__); else FN<0, 9, false>(e, ##__VA_ARGS__); break;   \
-        default: if (_f) FN<0, 15, true>(e, ##__VA_ARGS__); else FN<0, 15, false>(e, ##__VA_ARGS__); break; \
-      }                                                                                          \
-    } else {                                                                                     \
-      switch (_s.agg) {                                                                          \
-        case 1: if (_f) FN<1, 1, true>(e, ##__VA_ARGS__); else FN<1, 1, false>(e, ##__VA_ARGS__); break;   \
         case 9: if (_f) FN<1, 9, true>(e, ##__VA_ARGS__); else FN<1, 9, false>(e, ##__VA_ARGS__); break;   \
         default: if (_f) FN<1, 15, true>(e, ##__VA_ARGS__); else FN<1, 15, false>(e, ##__VA_ARGS__); break; \
       }                                                                                          \
@@ -3108,7 +3068,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.inv_size = 1.0 / (double)s.size;
   s.inv_g = 1.0 / (double)s.g;
   s.R = (int32_t)(s.slide / s.g);
-  if (s.K > MAX_K) return unsupported("more than 64 slices per window (size / gcd(size, slide))");
+  if (s.K > MAX_K) return unsupported("more than 1024 slices per window (size / gcd(size, slide))");
   s.mp = c.max_parallelism;
   s.mp_mask = (c.max_parallelism & (c.max_parallelism - 1)) == 0 ? c.max_parallelism - 1 : 0;
   s.kg_start = c.kg_start;
@@ -3126,40 +3086,25 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.fold_init = c.fold_initial;
   s.first = c.keep_first_f1 || by ? 1 : 0;   // maxBy/minBy: the pane's presence and the extremal f1
 
-  // fused ingest (ingest_mode 3, fw_fused.hip): reduce / fold of tumbling or sliding windows without allowed
-  // lateness, on a device that holds the whole grid resident (one workgroup per CU), with an owner's range of
-  // the directory (D / 32 slots, D = 2 x key capacity) and its accumulators in LDS beside the producers' staging
-  const int nacc_f = 1 + ((s.agg & FW_AGG_MIN) ? 1 : 0) + ((s.agg & FW_AGG_MAX) ? 1 : 0) + ((s.agg & FW_AGG_COUNT) ? 1 : 0);
-  const int64_t d_fused = next_pow2(std::max<int64_t>(2 * c.key_capacity, 2048));
-  const int so_bits_f = bits_for((uint64_t)d_fused) - 1 - 5;
-  {
-    const char* fv = getenv("FW_FUSED");
-    const bool ok = !e->session && !e->list && !by && c.allowed_lateness == 0 && c.max_batch <= (1ll << 26) &&
-                    prop.multiProcessorCount >= FU_GRID && fused_lds_bytes(so_bits_f, nacc_f) <= 160 * 1024;
-    if (c.ingest_mode == 3 && !ok)
-      return unsupported("fused ingest (ingest_mode 3): tumbling or sliding reduce / fold without allowed lateness, "
-                         "key_capacity <= 64 Ki (sum) / 16 Ki (sum, min, max, count), on a 256-CU device");
-    e->fused = ok && (c.ingest_mode == 3 || (c.ingest_mode == 0 && fv && atoi(fv) != 0 && c.max_batch >= (1 << 16)));
-  }
-  // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys, and for the fused form): short linear-probe
-  // sequences
-  s.D = e->fused ? d_fused : next_pow2(std::max<int64_t>((c.key_capacity <= (1 << 20) ? 4 : 2) * c.key_capacity, 64));
+  // ingest_mode 3 was the fused form (one persistent launch per batch, XCD-local hand-off of the routed records):
+  // measured slower than the partitioned form in rounds 3 and 4 (23 / 14 G vs 51-56 G events/s on C1), removed
+  if (c.ingest_mode == 3) return unsupported("ingest_mode 3 (fused) was removed: the partitioned form (2) is faster; DESIGN.md section 4");
+  // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys): short linear-probe sequences
+  s.D = next_pow2(std::max<int64_t>((c.key_capacity <= (1 << 20) ? 4 : 2) * c.key_capacity, 64));
   s.dir_mask = (uint64_t)s.D - 1;
   {
     int dbits = bits_for((uint64_t)s.D) - 1;                  // D = 2^dbits
     int kb = std::max(std::min(dbits, 9), dbits - 8);          // <= 256 buckets of >= 512 slots
-    if (e->fused) kb = std::min(9, dbits - 5);                 // fused: >= 32 buckets (one owner range is whole buckets)
     s.kb_bits = kb;
     s.nb = (int32_t)(s.D >> kb);
-    s.home_mask = e->fused ? ~7u : ~0u;   // fused: a key's probe starts at its home line (fw_fused.hip)
   }
   s.stride = s.D + 1;
   int32_t P = c.max_open_slices;
   if (P <= 0) {
     int64_t late_slices = (c.allowed_lateness + s.g - 1) / s.g;
-    P = (int32_t)std::min<int64_t>(2 * s.K + late_slices + 8, 1024);
+    P = (int32_t)std::min<int64_t>(2 * s.K + late_slices + 8, MAX_P);
   }
-  if (P > 1024) P = 1024;
+  if (P > MAX_P) P = MAX_P;
   s.P = P;
 
   s.dir_keys = e->alloc<int64_t>((size_t)s.D);
@@ -3241,7 +3186,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
                       c.max_batch <= (1ll << 26);
     if (c.ingest_mode == 2 && !fits)
       return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
-    e->routed = !e->session && !e->fused && (c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by)));
+    e->routed = !e->session && (c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by)));
     if (by && !e->routed && !e->session)
       return unsupported("maxBy / minBy need the partitioned ingest form (key_capacity <= 256 Ki)");
     if (e->routed) {
@@ -3279,24 +3224,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       e->agg_lds = agg_need;   // at launch: less the unused tiles, at least agg_min_lds
     }
   }
-  if (e->fused) {
-    FusedBuf& f = e->fb;
-    f.so_bits = so_bits_f;
-    f.ring = e->alloc<unsigned char>((size_t)FU_GROUPS * FU_NP * FU_S * FU_UNIT);
-    f.ctr = e->alloc<unsigned long long>((size_t)FU_C_N * FU_C_PAD);
-    f.xcc = e->alloc<int32_t>(FU_GRID);
-    const char* fs = getenv("FW_FUSED_SAFE");
-    f.force_safe = fs && atoi(fs) != 0 ? 1 : 0;
-    const char* dbg = getenv("FW_DEBUG_AGG");
-    e->rb.dbg = dbg ? atoi(dbg) : 0;
-    e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
-    f.stamps = e->rb.stamps;
-    // at least 81 KiB: one workgroup per CU, so the 256 of a launch are resident together on 256 CUs
-    e->fused_lds = std::max<size_t>(fused_lds_bytes(so_bits_f, nacc_f), 81 * 1024);
-    hipError_t rc = hipSuccess;
-    FW_DISPATCH_FUSED(fused_prepare_t, e, &rc);
-    HIPCHK(e, rc);
-  }
   e->wm_done = e->alloc<unsigned int>(1);
   if (s.first && !e->routed) {
     e->new_list = e->alloc<int64_t>((size_t)c.max_batch);
@@ -3311,7 +3238,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     int pane_bits = bits_for((uint64_t)P * (uint64_t)s.stride);
     if (e->idx_bits + pane_bits > 64) { delete e; return FW_ERR_UNSUPPORTED; }
     // sliding: a late record fires once per window of its slice in its lateness period
-    if (c.assigner == FW_SLIDING) e->fire_cap = c.max_batch * (int64_t)((s.K + s.R - 1) / s.R);
+    // (bounded: a batch of late records whose windows' per-element fires exceed it reports FW_ERR_CAPACITY)
+    if (c.assigner == FW_SLIDING) e->fire_cap = std::min<int64_t>(c.max_batch * (int64_t)((s.K + s.R - 1) / s.R), (int64_t)1 << 27);
     const size_t nb = (size_t)std::max<int64_t>(c.max_batch, e->fire_cap);
     if (e->fire_cap) {
       e->fire_key = e->alloc<unsigned long long>((size_t)e->fire_cap);
@@ -3341,6 +3269,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (int rc = session_create(e)) { g_create_error = "session window state allocation failed"; delete e; return rc; }
   }
   if (e->list && !e->session) {
+    if (s.K > LIST_MAX_K) return unsupported("list state: more than 64 slices per window (size / gcd(size, slide))");
     if (int rc = list_create(e)) { g_create_error = "list state allocation failed"; delete e; return rc; }
   }
   // initial state
@@ -3374,8 +3303,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->new_counts) HIPCHK(e, hipMemsetAsync(e->new_counts, 0, 16, e->stream));
   if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
   if (e->bload) HIPCHK(e, hipMemsetAsync(e->bload, 0, 4 * 4 * RT_MAXNB, e->stream));
-  if (e->fb.ctr) HIPCHK(e, hipMemsetAsync(e->fb.ctr, 0, 8 * (size_t)FU_C_N * FU_C_PAD, e->stream));
-  if (e->fb.ring) HIPCHK(e, hipMemsetAsync(e->fb.ring, 0, (size_t)FU_GROUPS * FU_NP * FU_S * FU_UNIT, e->stream));
   if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)5 * RT_MAXNB * RT_GS, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
@@ -3406,8 +3333,6 @@ static int device_error(fw_engine* e, int32_t derr) {
         break;
       case FW_ERR_KEY_GROUP: msg = "Unexpected key group index. This indicates a bug."; break;
       case FW_ERR_CAPACITY: msg = "capacity exceeded (key directory, slice pool, per-element fire list or output log)"; break;
-      case FW_ERR_RESIDENCY: msg = "fused ingest: the 256 workgroups of a launch were not resident together (other work "
-                                   "held CUs); ingest_mode 3 needs the device to itself"; break;
       case FW_ERR_UNSUPPORTED: msg = "a record's extra sliding window (timestamp below offset - slide, Java % of a negative "
                                      "numerator) is already behind the watermark, or maxBy/minBy with such a record: "
                                      "per-element fire of a window pane not supported"; break;
@@ -3462,8 +3387,8 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     HIPCHK(e, hipEventSynchronize(e->ev_route[par]));
     if (in_stream != e->stream && !e->routed) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_route[par], 0));
   }
-  if ((e->routed || e->fused) && mem == FW_MEM_DEVICE) {
-    // k_route / k_fused stream the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
+  if (e->routed && mem == FW_MEM_DEVICE) {
+    // k_route streams the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
     auto mis = [](const void* ptr, uintptr_t a) { return ((uintptr_t)ptr & (a - 1)) != 0; };
     if (mis(dk, 16)) { HIPCHK(e, hipMemcpyAsync(e->stg_key[par], dk, 8 * n, hipMemcpyDeviceToDevice, in_stream)); dk = e->stg_key[par]; }
     if (mis(dts, 16)) { HIPCHK(e, hipMemcpyAsync(e->stg_ts[par], dts, 8 * n, hipMemcpyDeviceToDevice, in_stream)); dts = e->stg_ts[par]; }
@@ -3487,7 +3412,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.quirk_capacity = e->s.W > 0 ? e->cfg.max_batch : 0;
   b.f1 = df1;
   b.new_list = e->new_list;
-  b.new_count = e->new_counts;   // (the fused form's appended list; the direct form indexes by record)
+  b.new_count = e->new_counts;   // (the direct form's list is indexed by record; the count stays unused)
   b.new_capacity = e->new_list ? e->cfg.max_batch : 0;
   if (e->session) {
     if (int rc = session_push(e, b)) return rc;
@@ -3495,10 +3420,6 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     if (int rc = list_push(e, b)) return rc;
   } else if (e->routed) {
     FW_DISPATCH(launch_routed_t, e, b, df1, par);
-  } else if (e->fused) {
-    e->phase_begin(FW_PHASE_INGEST);
-    FW_DISPATCH_FUSED(launch_fused_t, e, b, df1);
-    e->phase_end(n);
   } else {
     e->phase_begin(FW_PHASE_INGEST);
     FW_DISPATCH(launch_ingest_t, e, b);
@@ -3512,9 +3433,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   if (!e->disarmed.empty() &&
       jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)*e->disarmed.rbegin() * (uint64_t)e->s.size)), e->s.size), 1) > e->cur_wm)
     hipLaunchKernelGGL(k_arm, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0, e->stream, e->s, b);
-  // (the direct form's record-indexed list of f1 fix-ups; the partitioned form sets f1 in k_aggregate, the fused
-  // one in k_fused, and session / list state keep theirs themselves — new_list holds nothing of theirs)
-  if (e->s.first && !e->routed && !e->fused && !e->session && !e->list) {
+  // (the direct form's record-indexed list of f1 fix-ups; the partitioned form sets f1 in k_aggregate, and session /
+  // list state keep theirs themselves — new_list holds nothing of theirs)
+  if (e->s.first && !e->routed && !e->session && !e->list) {
     e->phase_begin(FW_PHASE_FIXUP);
     hipLaunchKernelGGL(k_fix_first_f1, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0,
                        e->stream, e->s, e->new_list, df1, e->ordinal, n);
@@ -3781,24 +3702,36 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
   fw_engine::Drain& d = e->drains[b];
   if (d.pending) { e->err = "fw_collect_begin: two drains outstanding (fw_collect_end the older first)"; return FW_ERR_INVALID_ARG; }
   const OutLog& L = e->s.o;
+  const size_t words = (size_t)DR_COLS * (size_t)std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX) +
+                       (size_t)L.mark_capacity + 4;
   if (!d.host) {
     e->drain_rows = std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX);
-    const size_t bytes = 8 * ((size_t)DR_COLS * (size_t)e->drain_rows + (size_t)L.mark_capacity + 4);
-    if (hipHostMalloc((void**)&d.host, bytes, hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc((void**)&d.host, 8 * words, hipHostMallocMapped) != hipSuccess) {
       d.host = nullptr;
       return fail(e, FW_ERR_DEVICE, "fw_collect_begin: pinned staging allocation failed");
     }
     HIPCHK(e, hipHostGetDevicePointer((void**)&d.dptr, d.host, 0));
+    HIPCHK(e, hipMalloc((void**)&d.dev, 8 * words));
     HIPCHK(e, hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    HIPCHK(e, hipEventCreateWithFlags(&d.staged, hipEventDisableTiming));
+    if (!e->dstream) HIPCHK(e, hipStreamCreateWithFlags(&e->dstream, hipStreamNonBlocking));
   }
-  int64_t* marks = d.dptr + (size_t)DR_COLS * (size_t)e->drain_rows;
+  int64_t* marks = d.dev + (size_t)DR_COLS * (size_t)e->drain_rows;
   int64_t* hdr = marks + L.mark_capacity;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->drain_rows + BLOCK - 1) / BLOCK, 512));
-  hipLaunchKernelGGL(k_drain, dim3(blocks), dim3(BLOCK), 0, e->stream, L, (const int32_t*)e->s.err, e->drain_rows, d.dptr,
+  hipLaunchKernelGGL(k_drain, dim3(blocks), dim3(BLOCK), 0, e->stream, L, (const int32_t*)e->s.err, e->drain_rows, d.dev,
                      marks, hdr);
   hipLaunchKernelGGL(k_drain_reset, dim3(1), dim3(1), 0, e->stream, L, e->drain_rows);
   HIPCHK(e, hipGetLastError());
-  HIPCHK(e, hipEventRecord(d.done, e->stream));
+  HIPCHK(e, hipEventRecord(d.staged, e->stream));
+  // to the host on the drain stream, beside whatever the engine stream runs next
+  HIPCHK(e, hipStreamWaitEvent(e->dstream, d.staged, 0));
+  const uint32_t colmask = (L.key ? 1u : 0u) | (L.f1 ? 2u : 0u) | (L.ts ? 4u : 0u) | (L.sum ? 8u : 0u) | (L.mn ? 16u : 0u) |
+                           (L.mx ? 32u : 0u) | (L.cnt ? 64u : 0u) | (L.win_start ? 128u : 0u);
+  hipLaunchKernelGGL(k_drain_host, dim3(64), dim3(BLOCK), 0, e->dstream, d.dev, marks, hdr, e->drain_rows, L.mark_capacity,
+                     colmask, d.dptr);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipEventRecord(d.done, e->dstream));
   // the marks since the last collect belong to this drain; the log restarts on the device
   d.marks.swap(e->hmarks);
   e->hmarks.clear();
@@ -3875,7 +3808,7 @@ int fw_get_stats(fw_engine* e, fw_stats* st) {
   for (int64_t t : tags) live += t != FREE_TAG;
   st->slices_live = live;
   st->keys_resident = (int64_t)d[ST_DIR_KEYS];   // the Long.MIN_VALUE key's own column not counted
-  st->ingest_form = e->fused ? 3 : e->routed ? 2 : 1;
+  st->ingest_form = e->routed ? 2 : 1;
   st->compactions = e->compactions;
   return FW_OK;
 }

@@ -125,8 +125,8 @@ __global__ __launch_bounds__(1024) void k_list_plan(Spec s, ListDev L, int64_t w
 
 // window n's elements: sort keys (arrival ordinal) and their buffer positions
 __global__ __launch_bounds__(BLOCK) void k_list_gather(Spec s, ListDev L, int64_t n, unsigned long long* key, int64_t* idx) {
-  int64_t off[MAX_K + 1];
-  int32_t slot[MAX_K];
+  int64_t off[LIST_MAX_K + 1];
+  int32_t slot[LIST_MAX_K];
   off[0] = 0;
   for (int k = 0; k < s.K; ++k) {
     const int64_t mm = n * s.R + k;

@@ -95,13 +95,23 @@ __device__ __forceinline__ uint32_t sess_set_cap(int n) {
 }
 
 // list state: free a window's elements (their pool entries may be reused)
+// (pool entries are handed out from a ring of free entry indices: freeq[(head, ftail)] mod pcap, pool[0] = head,
+// pool[1] = ftail; an entry freed during a launch is listed in fpend (pool[2] entries) and joins the ring at
+// k_sess_pool_recycle after it, so a launch only ever takes entries that were free when it started)
 __device__ __forceinline__ void sess_list_free(const SessDev& d, int64_t x) {
   for (int64_t e = d.head[x], n = d.len[x]; n > 0 && e >= 0; --n) {
     const int64_t nx = d.pnext[e];
-    d.pord[e] = -1;
+    const unsigned long long pos = atomicAdd(&d.pool[2], 1ull);
+    if ((int64_t)pos < d.pcap) d.fpend[pos] = e;
     e = nx;
   }
   d.len[x] = 0;
+}
+// a pool entry for a new element, or -1 when every entry free at the launch's start is taken
+__device__ __forceinline__ int64_t sess_pool_take(const SessDev& d) {
+  const unsigned long long h = atomicAdd(&d.pool[0], 1ull);
+  if (h >= d.pool[1]) { atomicAdd(&d.pool[0], ~0ull); return -1; }   // (pool[1] does not change during the launch)
+  return d.freeq[h % (unsigned long long)d.pcap];
 }
 // list state: one output row per element of the window, in list order (InternalIterableWindowFunction)
 __device__ __forceinline__ void sess_list_emit(const Spec& s, const SessDev& d, int64_t x, int64_t key, int64_t start,
@@ -217,7 +227,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   int64_t nts = b.ts[ni], nv = b.val[ni], nf1 = b.f1 ? b.f1[ni] : nts;
   bool more = true;
   for (int64_t j = j0; more; ++j) {
-    const int64_t i = ni, ts = nts, v = nv, f1 = nf1;
+    const int64_t ts = nts, v = nv, f1 = nf1;
     more = false;
     if (j + 1 < n) {
       const unsigned long long kn = sorted[j + 1];
@@ -342,15 +352,13 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
     const int64_t x = base + r;
     LateAcc cur;
     if (d.list) {
-      // HeapListState.add: the element appended; its pool entry is the ring slot of its arrival ordinal
-      const int64_t ord = b.ord_base + i;
-      const int64_t e = ord % d.pcap;
-      if (d.pord[e] >= 0) {   // that entry still holds a buffered element: list_capacity exceeded
+      // HeapListState.add: the element appended in a free pool entry
+      const int64_t e = sess_pool_take(d);
+      if (e < 0) {   // more elements buffered at once than list_capacity
         cap_error(s, 26);
         if (fresh) live.clr(r);
         continue;
       }
-      d.pord[e] = ord;
       d.pv[e] = v;
       d.pf1[e] = a.f1;
       d.pnext[e] = -1;
@@ -707,9 +715,33 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
   }
 }
 
+// after a launch that freed pool entries: they join the free ring (one workgroup; a batch frees at most pcap)
+__global__ __launch_bounds__(1024) void k_sess_pool_recycle(SessDev d) {
+  const unsigned long long nf = min(d.pool[2], (unsigned long long)d.pcap), t = d.pool[1];
+  for (unsigned long long i = threadIdx.x; i < nf; i += blockDim.x) d.freeq[(t + i) % (unsigned long long)d.pcap] = d.fpend[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d.pool[1] = t + nf;
+    d.pool[2] = 0;
+  }
+}
+__global__ void k_sess_pool_init(SessDev d) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.pcap; i += (int64_t)gridDim.x * blockDim.x)
+    d.freeq[i] = i;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.pool[0] = 0;
+    d.pool[1] = (unsigned long long)d.pcap;
+    d.pool[2] = 0;
+  }
+}
+
 }  // namespace fw
 
 using namespace fw;
+
+static void session_pool_recycle(fw_engine* e) {
+  if (e->sess.list) hipLaunchKernelGGL(k_sess_pool_recycle, dim3(1), dim3(1024), 0, e->stream, e->sess);
+}
 
 int session_create(fw_engine* e) {
   const Spec& s = e->s;
@@ -736,7 +768,9 @@ int session_create(fw_engine* e) {
     d.pv = e->alloc<int64_t>((size_t)d.pcap);
     d.pf1 = e->alloc<int64_t>((size_t)d.pcap);
     d.pnext = e->alloc<int64_t>((size_t)d.pcap);
-    d.pord = e->alloc<int64_t>((size_t)d.pcap);
+    d.freeq = e->alloc<int64_t>((size_t)d.pcap);
+    d.fpend = e->alloc<int64_t>((size_t)d.pcap);
+    d.pool = e->alloc<unsigned long long>(4);
   }
   d.nw = (d.sw + 63) / 64 <= 1 ? 1 : (d.sw + 63) / 64 <= 2 ? 2 : 4;   // words of a key's slot masks
   // hot keys: runs of >= FW_SESS_HOT records (default 256; 0 = off) walked a wave each; reducing state only
@@ -765,7 +799,7 @@ int session_create(fw_engine* e) {
   for (void* p : e->allocs) if (!p) return FW_ERR_DEVICE;
   HIPCHK(e, hipMemsetAsync(d.live, 0, 8 * (size_t)s.stride * d.nw, e->stream));
   if (d.list) {
-    HIPCHK(e, hipMemsetAsync(d.pord, 0xFF, 8 * (size_t)d.pcap, e->stream));   // every pool entry free (-1)
+    hipLaunchKernelGGL(k_sess_pool_init, dim3(64), dim3(BLOCK), 0, e->stream, d);   // every pool entry free
     HIPCHK(e, hipMemsetAsync(d.len, 0, 8 * cells, e->stream));
   }
   HIPCHK(e, hipMemsetAsync(d.trig, 0, 8 * (size_t)s.stride * d.nw, e->stream));
@@ -791,6 +825,7 @@ int session_push(fw_engine* e, const BatchIn& b) {
     else hipLaunchKernelGGL(k_sess_walk_hot<4>, gh, dim3(64), 0, e->stream, e->s, e->sess, b, e->sess_sorted, b.n, e->sess_idx_bits);
   }
   e->phase_end(b.n);
+  session_pool_recycle(e);   // the entries this batch's merges and retirements freed
   HIPCHK(e, hipGetLastError());
   if (e->cfg.allowed_lateness > 0) e->out_dirty = true;   // per-element fires may have appended
   return FW_OK;
@@ -804,6 +839,7 @@ int session_watermark(fw_engine* e, int64_t wm) {
     else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_wm<2>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
     else hipLaunchKernelGGL(k_sess_wm<4>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
     e->phase_end(e->s.stride);
+    session_pool_recycle(e);   // the entries of the windows purged
     e->cur_wm = wm;
     hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
     e->hmarks.push_back({wm, e->dev_marks++, true});

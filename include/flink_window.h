@@ -54,7 +54,6 @@ extern "C" {
 #define FW_ERR_KEY_GROUP      4  /* key group of a record outside [kg_start, kg_end] of this subtask         */
 #define FW_ERR_UNSUPPORTED    5  /* configuration this backend does not implement                            */
 #define FW_ERR_DEVICE         6  /* HIP runtime failure                                                      */
-#define FW_ERR_RESIDENCY      7  /* fused ingest (ingest_mode 3): its workgroups were not all resident at once */
 
 /* ---- window assigner (SJ/api/windowing/assigners) ---- */
 #define FW_TUMBLING 0            /* TumblingEventTimeWindows.of(size[, offset])  (offset already % size)     */
@@ -99,10 +98,11 @@ extern "C" {
  * pane slice) and a firing window returns every element of every key, grouped by key, in arrival order, one
  * result row per element (value in the sum column, the element's f1, ts = window.maxTimestamp()); the host runs
  * the window function over each group.  Tumbling / sliding: an element arriving for a window that already
- * fired (allowed lateness) fails with FW_ERR_UNSUPPORTED.  Session windows: each window's elements in list
- * order (a merge appends the sources' lists to the target's, AbstractKeyedStateBackend.mergePartitionedStates
- * :315-333), a late element's per-element fire re-emits the whole list; list_capacity bounds the elements
- * buffered at once (a pool indexed by arrival ordinal).  Used alone. */
+ * fired (allowed lateness) re-fires the window for its key with every element so far (under PurgingTrigger:
+ * FW_ERR_UNSUPPORTED).  Session windows: each window's elements in list order (a merge appends the sources' lists
+ * to the target's, AbstractKeyedStateBackend.mergePartitionedStates :315-333), a late element's per-element fire
+ * re-emits the whole list; list_capacity bounds the elements buffered at once (a pool of free entries; entries
+ * freed by a batch or watermark are reused from the next one on).  Used alone. */
 #define FW_AGG_LIST   64
 
 /* agg_flags */
@@ -146,13 +146,12 @@ typedef struct {
   int64_t key_capacity;      /* distinct keys over the engine lifetime                          */
   int64_t max_batch;         /* max records per fw_push_batch                                   */
   int64_t out_capacity;      /* max fired records between two fw_collect calls                  */
-  int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate,    */
-                             /* 3 = fused (one launch per batch, XCD-local hand-off; reduce /  */
-                             /*     fold without allowed lateness, key_capacity <= 64 Ki)     */
+  int32_t ingest_mode;       /* 0 = auto, 1 = direct atomics, 2 = partition + LDS aggregate     */
+                             /* (3, the fused form, was removed: FW_ERR_UNSUPPORTED)          */
   int32_t agg_flags;         /* OR of FW_AGGF_*                                                 */
   int64_t fold_initial;      /* FW_AGGF_FOLD: the fold's initial accumulator                    */
   int64_t list_capacity;     /* FW_AGG_LIST: elements buffered per pane slice (session windows: */
-                             /* ... in all, a ring by arrival ordinal); 0 = 4 x max_batch      */
+                             /* ... in all, live at once); 0 = 4 x max_batch                    */
 } fw_config;
 
 /* Output between two collects: records and watermark marks.  Records [mark_pos[i-1], mark_pos[i])
@@ -185,7 +184,7 @@ typedef struct {
   int64_t late_fires;        /* per-element fires (allowed lateness > 0)      */
   int64_t keys_resident;     /* distinct keys in the key directory            */
   int64_t slices_live;       /* pane slices resident                          */
-  int64_t ingest_form;       /* 1 = direct atomics, 2 = partitioned + LDS, 3 = fused */
+  int64_t ingest_form;       /* 1 = direct atomics, 2 = partitioned + LDS aggregate */
   int64_t compactions;       /* key-directory compactions (dead keys evicted) */
 } fw_stats;
 

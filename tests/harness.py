@@ -33,16 +33,9 @@ LIST_FIXTURES = ["list_sliding_apply", "list_tumbling_apply", "list_cleanup_time
 
 
 def hip_engine(cfg):
-    """WindowEngine(cfg); a config the fused ingest form (ingest_mode 3: reduce / fold without allowed
-    lateness) does not take skips the calling test instead of failing it."""
-    import pytest
+    """WindowEngine(cfg) (the HIP engine the GPU parity tests drive)."""
     from flink_amd.windowing import WindowEngine
-    try:
-        return WindowEngine(cfg)
-    except _abi.FwError as ex:
-        if cfg.ingest_mode == 3 and ex.code == _abi.FW_ERR_UNSUPPORTED:
-            pytest.skip(f"not a fused-form config: {ex}")
-        raise
+    return WindowEngine(cfg)
 
 
 def fixture_config(c, **kw):

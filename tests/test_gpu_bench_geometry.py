@@ -91,17 +91,6 @@ def test_c1_bench_geometry():
     assert sg["panes_fired"] == so["panes_fired"] > 0
 
 
-def test_c1_bench_geometry_fused():
-    """The same C1 stream through the fused form (ingest_mode 3)."""
-    from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, make_config
-    batch = 1 << 22
-    cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", keep_first_f1=True),
-                      max_parallelism=128, key_capacity=1 << 16, max_batch=batch, out_capacity=1 << 20, ingest_mode=3)
-    sg, so = _run(cfg, 5, batch, 1 << 16, 1 << 24, 1)
-    assert sg["ingest_form"] == 3
-    assert sg["panes_fired"] == so["panes_fired"] > 0
-
-
 def test_c4_zipf_lateness_bench_geometry():
     from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, make_config
     batch = 1 << 22

@@ -128,7 +128,7 @@ def _checkpoint_roundtrip(hip, oracle_engine, make_cfg, keys, ts, vals, batch, l
     return n_entries
 
 
-MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned"), pytest.param(3, id="fused")]
+MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned")]
 
 
 @pytest.mark.parametrize("mode", MODES)

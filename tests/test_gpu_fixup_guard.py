@@ -45,9 +45,9 @@ def test_session_and_list_never_launch_direct_fixup():
     assert _fixups(sess, k, t, v) == 0
     sess_list = make_config(EventTimeSessionWindows.withGap(30), ListStateDescriptor("i64", list_capacity=1 << 16), **common)
     assert _fixups(sess_list, k, t, v) == 0
-    lst = make_config(TumblingEventTimeWindows.of(100), ListStateDescriptor("i64"), **common)
+    lst = make_config(TumblingEventTimeWindows.of(1000), ListStateDescriptor("i64"), **common)
     assert _fixups(lst, k, t, v) == 0
     # positive control: the direct form with a first-arrival f1 launches it once per push
-    direct = make_config(TumblingEventTimeWindows.of(100), ReduceFunction(("sum",), "i64", keep_first_f1=True),
+    direct = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", keep_first_f1=True),
                          ingest_mode=1, **common)
     assert _fixups(direct, k, t, v) == (len(k) + (1 << 12) - 1) >> 12

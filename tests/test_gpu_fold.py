@@ -11,7 +11,7 @@ from harness import FOLD_FIXTURES, drive, epochs_of, expected_epochs, gen_stream
 pytestmark = pytest.mark.gpu
 
 LONG_MAX = (1 << 63) - 1
-MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned"), pytest.param(3, id="fused")]
+MODES = [pytest.param(1, id="direct"), pytest.param(2, id="partitioned")]
 
 
 @pytest.fixture(scope="module")

@@ -230,6 +230,32 @@ def test_session_list_capacity(hip):
     e.close()
 
 
+def test_session_list_pool_reuse(hip, oracle_engine):
+    """list_capacity bounds the elements buffered AT ONCE: one long session (key 0, a record every
+    100 ms, gap 1 s) stays open over 40 batches while 60 new keys per batch open short sessions that the watermark
+    closes a second later.  2,440 arrivals pass through a 1,024-entry pool with at most ~700 elements live; the
+    pool reuses the entries of purged windows (an arrival-ordinal ring would have failed at the 1,025th arrival
+    while key 0's first element is still buffered)."""
+    from flink_amd.windowing import ListStateDescriptor
+    keys, ts = [], []
+    for b in range(40):
+        keys += [0] + list(range(1 + 60 * b, 61 + 60 * b))
+        ts += [100 * b] + [100 * b + 1 + j for j in range(60)]
+    keys, ts = np.array(keys, np.int64), np.array(ts, np.int64)
+    vals = np.arange(len(keys), dtype=np.int64) * 3 - 7
+    f1 = np.arange(len(keys), dtype=np.int64) + 100
+    cfg = _red_cfg(1000, ListStateDescriptor("i64", list_capacity=1024))
+    out = []
+    for f in (hip, oracle_engine):
+        e = f(cfg)
+        r = drive(e, keys, ts, vals, 61, 0, LONG_MAX, f1=f1)
+        out.append(_list_groups(r))
+        e.close()
+    g, o = out
+    assert g == o
+    assert max(len(x) for _, grp in g for x in grp.values()) == 40   # key 0's one session, every element
+
+
 def test_session_rejections(hip):
     from flink_amd import _abi
     e = hip(_cfg(10, ("sum",)))
