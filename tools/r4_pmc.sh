@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over a short bench run (one counter group per pass, no trace domains): MODE = ingest mode, CFG = config
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-A="--config ${CFG:-c1} --steps 6 --warmup 2 --prof-steps 0 --cpu-sample 0 --no-check --decode-steps 0 --h2d-steps 0 --drain-steps 0 --ingest-mode ${MODE:-3}"
+A="--config ${CFG:-c1} --steps 6 --warmup 2 --prof-steps 0 --cpu-sample 0 --no-check --decode-steps 0 --h2d-steps 0 --drain-steps 0 --ingest-mode ${MODE:-0}"
 i=0
 for pass in ${PASSES:-FETCH_SIZE WRITE_SIZE}; do ctrs="${pass//_SQ_/ SQ_}"; ctrs="${ctrs//_TCC_/ TCC_}";
   i=$((i+1)); rm -rf gpurun_out/pmc_$i
