@@ -81,7 +81,7 @@ def parse():
                          "timed events serialise kernels, so the timed region runs without them")
     ap.add_argument("--decode-steps", type=int, default=4,
                     help="wire-format decode leg (fw_decode of the batch as Flink network bytes; 0 = skip)")
-    ap.add_argument("--drain-steps", type=int, default=8,
+    ap.add_argument("--drain-steps", type=int, default=32,
                     help="steps of the leg that collects fired results to the host after every step (0 = skip)")
     ap.add_argument("--h2d-steps", type=int, default=8,
                     help="steps after the timed region pushed from pinned host columns (PCIe-inclusive rate; 0 = skip)")
@@ -337,14 +337,14 @@ def main():
                 if vt == "i64":
                     dec_sums.append(int(v.sum().item()))
                 extra_n += int(k.numel())
-            if mode == "async":   # the drains' pinned host staging (two buffers) is allocated by their first use
-                for _ in range(2):
+            if mode == "async":   # the drains' pinned host staging (three buffers) is allocated by their first use
+                for _ in range(3):
                     collected.append(eng.collect_end(eng.collect_begin()))
             eng.sync()
             torch.cuda.synchronize()
             n_out = 0
             t4 = time.perf_counter()
-            prev = None
+            pend = []
             for q, (k, t, v) in enumerate(fresh):
                 eng.push(k, t, v)
                 eng.advance_watermark(wm_of(jr + q))
@@ -353,14 +353,13 @@ def main():
                     n_out += r["n"]
                     collected.append(r)
                     continue
-                cur = eng.collect_begin()
-                if prev is not None:
-                    r = eng.collect_end(prev)
+                if len(pend) == 3:   # three drains in flight: the oldest (two batches back) has landed by now
+                    r = eng.collect_end(pend.pop(0))
                     n_out += r["n"]
                     collected.append(r)
-                prev = cur
-            if prev is not None:
-                r = eng.collect_end(prev)
+                pend.append(eng.collect_begin())
+            for tk in pend:
+                r = eng.collect_end(tk)
                 n_out += r["n"]
                 collected.append(r)
             torch.cuda.synchronize()
@@ -370,8 +369,8 @@ def main():
             jr += args.drain_steps
             del fresh
         drain_leg = dict(legs["async"])
-        drain_leg["note"] = ("push + watermark + fw_collect_begin every step, fw_collect_end of the previous step's drain "
-                             "(pinned host columns; results of watermark j land while batch j + 1 runs); the headline "
+        drain_leg["note"] = ("push + watermark + fw_collect_begin every step, fw_collect_end of the drain begun two steps "
+                             "before (pinned host columns; results of watermark j land while batches j + 1, j + 2 run); the headline "
                              "leaves them in the device output log, drained after the timed region")
         drain_leg["sync"] = dict(legs["sync"], note="the same with the host-synchronous fw_collect after every step")
 

@@ -173,80 +173,71 @@ __device__ __forceinline__ int dec_walk(const DecSpec& d, const DecChunk& ch, in
   return pos - ch.clen;
 }
 
-// a candidate chain's outcome in one word: DEC_CDEAD, or its exit (biased by DEC_XB) and the records, watermarks
-// and latency markers along it (a 512-byte chunk holds at most 39 elements: 6 bits each)
-constexpr int32_t DEC_CDEAD = INT32_MIN;
+// a candidate chain's outcome in one word: its exit (biased by DEC_XB) and the records, watermarks and latency
+// markers along it (a 512-byte chunk holds at most 39 elements: 6 bits each)
 constexpr int DEC_XB = 512;
 __device__ __forceinline__ int32_t dec_cpack(int x, int n0, int n1, int n2) {
   return (x + DEC_XB) | (n0 << 10) | (n1 << 16) | (n2 << 22);
 }
 __device__ __forceinline__ int dec_cexit(int32_t v) { return (v & 1023) - DEC_XB; }
-constexpr int DEC_S = 8;   // survivors kept per chunk (entry offset << 32 | packed outcome); more: walked again
+constexpr int DEC_W = DEC_TW / 64;       // waves per workgroup: each takes every DEC_W-th candidate of every chunk
+constexpr int DEC_SW = 2;                // survivors kept per wave and chunk (entry offset << 32 | outcome)
+constexpr int DEC_S = DEC_W * DEC_SW;    // ... per chunk; beyond them a chunk's count is walked again
+__device__ __forceinline__ int32_t dec_agree(int32_t a, int32_t x) {
+  return a == INT32_MIN ? x : (x == INT32_MIN || a == x) ? a : INT32_MAX;
+}
 
-// per chunk: the exit every surviving candidate chain agrees on (INT32_MIN: none survived, INT32_MAX: they
-// differ — then every candidate's exit goes to table[c][e] for the in-order resolution), and the survivors
-// with their counts, so the true chain's counts are known once its entry is (no second walk).  The 4 waves
-// share a chunk's candidates (wave w takes e = w, w + 4, ...; lane = chunk), so 4 chains per chunk run at once
-__global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* table, int32_t* conv, int64_t* surv,
-                                                    int32_t* nsurv) {
+// per chunk and wave: the exit its surviving candidate chains agree on (INT32_MIN: none survived, INT32_MAX: they
+// differ) and up to DEC_SW survivors with their counts, so the true chain's counts are known once its entry is
+// (no second walk).  The workgroup's waves share a chunk's candidates (wave w takes e = w, w + DEC_W, ...; lane =
+// chunk), so DEC_W chains per chunk run at once; each wave writes its own results (no LDS beyond the chunks)
+__global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, int64_t* surv, int32_t* nsurv) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
-  __shared__ int32_t cand[DEC_T][DEC_MAXE + 1];   // each candidate's outcome (odd row pitch: lanes hit distinct banks)
   const DecChunk ch = dec_stage_group(d, buf);
   const int lane = (int)threadIdx.x & (DEC_T - 1), wv = (int)threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * DEC_T + lane;
+  if (c >= d.nchunks) return;
   const int lim = min(d.maxe, ch.clen);
-  if (c < d.nchunks) {
-    // one step per iteration of a single loop whatever candidate it belongs to (nested loops cost ~10x the steps)
-    int e = wv, pos = wv, n0 = 0, n1 = 0, n2 = 0;
-    while (e < lim) {
-      int x = DEC_DEAD;
-      bool fin = true;
-      if (pos >= ch.clen || pos + 5 > ch.rem) {
-        x = pos - ch.clen;
-      } else {
-        uint32_t len, tag;
-        dec_header(ch.b + pos, len, tag);
-        const int k = dec_kind(d, len, (uint8_t)tag);
-        if (k < 0) x = DEC_DEAD;
-        else if (pos + 4 + (int64_t)len > ch.rem) x = pos - ch.clen;
-        else {
-          pos += 4 + (int)len;
-          n0 += k == 0; n1 += k == 1; n2 += k == 2;
-          if (k == 0) {
-            const int m = dec_ff(ch, pos, len, tag);
-            pos += m * (4 + (int)len);
-            n0 += m;
-          }
-          fin = false;
-        }
-      }
-      if (fin) {
-        cand[lane][e] = x == DEC_DEAD ? DEC_CDEAD : dec_cpack(x, n0, n1, n2);
-        e += 4;
-        pos = e;
-        n0 = n1 = n2 = 0;
-      }
-    }
-  }
-  __syncthreads();
-  if (wv != 0 || c >= d.nchunks) return;
   int32_t agree = INT32_MIN;
   int ns = 0;
-  for (int e = 0; e < lim; ++e) {
-    const int32_t v = cand[lane][e];
-    if (v == DEC_CDEAD) continue;
-    const int x = dec_cexit(v);
-    agree = agree == INT32_MIN ? x : (agree == x ? agree : INT32_MAX);
-    if (ns < DEC_S) surv[c * DEC_S + ns] = ((int64_t)e << 32) | (uint32_t)v;
-    ++ns;
-  }
-  conv[c] = agree;
-  nsurv[c] = ns;
-  if (agree == INT32_MAX)
-    for (int e = 0; e < d.maxe; ++e) {
-      const int32_t v = e < lim ? cand[lane][e] : DEC_CDEAD;
-      table[c * d.maxe + e] = v == DEC_CDEAD ? DEC_DEAD : dec_cexit(v);
+  int64_t* sv = surv + c * DEC_S + wv * DEC_SW;
+  // one step per iteration of a single loop whatever candidate it belongs to (nested loops cost ~10x the steps)
+  int e = wv, pos = wv, n0 = 0, n1 = 0, n2 = 0;
+  while (e < lim) {
+    int x = DEC_DEAD;
+    bool fin = true;
+    if (pos >= ch.clen || pos + 5 > ch.rem) {
+      x = pos - ch.clen;
+    } else {
+      uint32_t len, tag;
+      dec_header(ch.b + pos, len, tag);
+      const int k = dec_kind(d, len, (uint8_t)tag);
+      if (k < 0) x = DEC_DEAD;
+      else if (pos + 4 + (int64_t)len > ch.rem) x = pos - ch.clen;
+      else {
+        pos += 4 + (int)len;
+        n0 += k == 0; n1 += k == 1; n2 += k == 2;
+        if (k == 0) {
+          const int m = dec_ff(ch, pos, len, tag);
+          pos += m * (4 + (int)len);
+          n0 += m;
+        }
+        fin = false;
+      }
     }
+    if (fin) {
+      if (x != DEC_DEAD) {
+        agree = dec_agree(agree, x);
+        if (ns < DEC_SW) sv[ns] = ((int64_t)e << 32) | (uint32_t)dec_cpack(x, n0, n1, n2);
+        ++ns;
+      }
+      e += DEC_W;
+      pos = e;
+      n0 = n1 = n2 = 0;
+    }
+  }
+  conv[c * DEC_W + wv] = agree;
+  nsurv[c * DEC_W + wv] = ns;
 }
 
 // the counts and exit of chunk c's chain from entry en >= 0, from its survivors; false: not among the kept ones
@@ -254,9 +245,10 @@ __device__ __forceinline__ bool dec_surv_counts(const DecSpec& d, const int64_t*
                                                 int32_t en, int64_t* cnt3, int32_t* cexit) {
   const int clen = (int)min<int64_t>(DEC_CHUNK, d.nbytes - c * DEC_CHUNK);
   if (en >= clen) { cexit[c] = en - clen; return true; }   // the previous element covers the (last, short) chunk
-  const int ns = min(nsurv[c], DEC_S);
+  const int w = en % DEC_W;                                  // the wave that walked candidate en
+  const int ns = min(nsurv[c * DEC_W + w], DEC_SW);
   for (int i = 0; i < ns; ++i) {
-    const int64_t s = surv[c * DEC_S + i];
+    const int64_t s = surv[c * DEC_S + w * DEC_SW + i];
     if ((int32_t)(s >> 32) != en) continue;
     const int32_t v = (int32_t)(uint32_t)s;
     cnt3[3 * c] = (v >> 10) & 63;
@@ -266,6 +258,16 @@ __device__ __forceinline__ bool dec_surv_counts(const DecSpec& d, const int64_t*
     return true;
   }
   return false;
+}
+// a chunk's entry known, its counts: from the survivors, else listed for a walk (the wave kept fewer survivors than
+// it found), else corrupt (no chain from the entry through the chunk)
+__device__ __forceinline__ void dec_entry_counts(const DecSpec& d, const int64_t* surv, const int32_t* nsurv, int64_t c,
+                                                 int32_t en, int64_t* cnt3, int32_t* cexit, int64_t* walk,
+                                                 unsigned long long* n_walk, int32_t* err) {
+  if (en == -3) atomicExch(err, 1);
+  if (en < 0 || dec_surv_counts(d, surv, nsurv, c, en, cnt3, cexit)) return;
+  if (nsurv[c * DEC_W + en % DEC_W] > DEC_SW) walk[atomicAdd(n_walk, 1ull)] = c;
+  else atomicExch(err, 1);
 }
 
 // every chunk's entry offset known from the previous chunk's agreeing survivors (-2: undecided, -3: corrupt,
@@ -279,25 +281,40 @@ __global__ __launch_bounds__(DEC_T) void k_dec_entry(DecSpec d, const int32_t* c
   if (c >= d.nchunks) return;
   int32_t en = 0;
   if (c > 0) {
-    const int32_t a = conv[c - 1];
+    int32_t a = INT32_MIN;
+    for (int w = 0; w < DEC_W; ++w) a = dec_agree(a, conv[(c - 1) * DEC_W + w]);
     en = (a == INT32_MIN) ? -3 : (a == INT32_MAX) ? -2 : (a < 0 ? -1 : a);
   }
   entry[c] = en;
   cnt3[3 * c] = cnt3[3 * c + 1] = cnt3[3 * c + 2] = 0;
   cexit[c] = DEC_DEAD;
-  if (en == -3) atomicExch(err, 1);
   if (en == -2) unknown[atomicAdd(n_unknown, 1ull)] = c;
-  if (en >= 0 && !dec_surv_counts(d, surv, nsurv, c, en, cnt3, cexit)) {
-    if (nsurv[c] > DEC_S) walk[atomicAdd(n_walk, 1ull)] = c;
-    else atomicExch(err, 1);   // no chain from the entry through the chunk
+  else dec_entry_counts(d, surv, nsurv, c, en, cnt3, cexit, walk, n_walk, err);
+}
+
+// chunk c's chain from pos in global memory (the rare paths): its exit or DEC_DEAD, and its counts
+__device__ __forceinline__ int32_t dec_walk_global(const DecSpec& d, int64_t c, int pos, int64_t n[3]) {
+  const int64_t start = c * DEC_CHUNK;
+  const int clen = (int)min<int64_t>(DEC_CHUNK, d.nbytes - start);
+  const int64_t rem = d.nbytes - start;
+  const uint8_t* b = d.bytes + start;
+  n[0] = n[1] = n[2] = 0;
+  while (true) {
+    if (pos >= clen || pos + 5 > rem) return pos - clen;
+    const uint32_t len = be_u32(b + pos);
+    const int k = dec_kind(d, len, b[pos + 4]);
+    if (k < 0) return DEC_DEAD;
+    if (pos + 4 + (int64_t)len > rem) return pos - clen;
+    n[k]++;
+    pos += 4 + (int)len;
   }
 }
 
-// the undecided chunks, in stream order: each one's entry from its predecessor's resolved chain, then its
-// counts (one thread; nearly always nothing to do)
-__global__ void k_dec_fix(DecSpec d, const int32_t* table, int32_t* entry, int64_t* unknown,
-                          const unsigned long long* n_unknown, const int64_t* surv, const int32_t* nsurv, int64_t* cnt3,
-                          int32_t* cexit, int64_t* walk, unsigned long long* n_walk, int32_t* err) {
+// the undecided chunks, in stream order: each one's entry where its predecessor's true chain leaves it (walked in
+// global memory), then its counts (one thread; nearly always nothing to do)
+__global__ void k_dec_fix(DecSpec d, int32_t* entry, int64_t* unknown, const unsigned long long* n_unknown,
+                          const int64_t* surv, const int32_t* nsurv, int64_t* cnt3, int32_t* cexit, int64_t* walk,
+                          unsigned long long* n_walk, int32_t* err) {
   const int64_t nu = (int64_t)*n_unknown;
   for (int64_t i = 1; i < nu; ++i)   // insertion sort of the list (atomic appends: any order)
     for (int64_t j = i; j > 0 && unknown[j - 1] > unknown[j]; --j) { const int64_t t = unknown[j]; unknown[j] = unknown[j - 1]; unknown[j - 1] = t; }
@@ -308,15 +325,12 @@ __global__ void k_dec_fix(DecSpec d, const int32_t* table, int32_t* entry, int64
     if (prev < 0) {
       en = prev == -1 ? -1 : -3;
     } else {
-      const int32_t x = table[(c - 1) * d.maxe + prev];   // (c - 1 is a disagreeing chunk: its row is written)
+      int64_t n[3];
+      const int32_t x = dec_walk_global(d, c - 1, prev, n);
       en = x == DEC_DEAD ? -3 : x < 0 ? -1 : x;
     }
     entry[c] = en;
-    if (en == -3) atomicExch(err, 1);
-    if (en >= 0 && !dec_surv_counts(d, surv, nsurv, c, en, cnt3, cexit)) {
-      if (nsurv[c] > DEC_S) walk[atomicAdd(n_walk, 1ull)] = c;
-      else atomicExch(err, 1);
-    }
+    dec_entry_counts(d, surv, nsurv, c, en, cnt3, cexit, walk, n_walk, err);
   }
 }
 
@@ -327,21 +341,8 @@ __global__ __launch_bounds__(DEC_T) void k_dec_count(DecSpec d, const int32_t* e
   const int64_t nw = (int64_t)*n_walk;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t c = walk[i];
-    const int64_t start = c * DEC_CHUNK;
-    const DecChunk ch{d.bytes + start, (int)min<int64_t>(DEC_CHUNK, d.nbytes - start), d.nbytes - start};
-    int64_t n[3] = {0, 0, 0};
-    int pos = entry[c];
-    int32_t x = DEC_DEAD;
-    while (true) {   // dec_walk over global bytes
-      if (pos >= ch.clen) { x = pos - ch.clen; break; }
-      if (pos + 5 > ch.rem) { x = pos - ch.clen; break; }
-      const uint32_t len = be_u32(ch.b + pos);
-      const int k = dec_kind(d, len, ch.b[pos + 4]);
-      if (k < 0) break;
-      if (pos + 4 + (int64_t)len > ch.rem) { x = pos - ch.clen; break; }
-      n[k]++;
-      pos += 4 + (int)len;
-    }
+    int64_t n[3];
+    const int32_t x = dec_walk_global(d, c, entry[c], n);
     if (x == DEC_DEAD) { atomicExch(err, 1); n[0] = n[1] = n[2] = 0; }
     cnt3[3 * c] = n[0]; cnt3[3 * c + 1] = n[1]; cnt3[3 * c + 2] = n[2];
     cexit[c] = x;
@@ -532,9 +533,8 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
     return r;
   };
   const size_t nc = (size_t)d.nchunks;
-  HIPCHK(e, grow(e->dec_table, e->dec_table_cap, nc * (size_t)d.maxe * 4));
   const size_t nblk = (nc + DEC_SCAN - 1) / DEC_SCAN;
-  HIPCHK(e, grow(e->dec_small, e->dec_small_cap, nc * (4 + 4 + 4 + 4 + 8 + 8 + 24 + 24 + 8 * DEC_S) + nblk * 24 + 256));
+  HIPCHK(e, grow(e->dec_small, e->dec_small_cap, nc * (4 * DEC_W + 4 + 4 + 4 * DEC_W + 8 + 8 + 24 + 24 + 8 * DEC_S) + nblk * 24 + 256));
   const uint8_t* src = (const uint8_t*)bytes;
   if (mem == FW_MEM_HOST) {
     HIPCHK(e, grow(e->dec_bytes, e->dec_bytes_cap, (size_t)nbytes));
@@ -543,8 +543,8 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   }
   d.bytes = src;
   uint8_t* sm = (uint8_t*)e->dec_small;
-  int32_t* conv = (int32_t*)sm;
-  int32_t* entry = conv + nc;
+  int32_t* conv = (int32_t*)sm;   // [nc][DEC_W] each wave's agreeing exit
+  int32_t* entry = conv + nc * DEC_W;
   int64_t* unknown = (int64_t*)(((uintptr_t)(entry + nc) + 7) & ~(uintptr_t)7);
   int64_t* base = unknown + nc;
   int64_t* totals = base + 3 * nc;   // [4] records, watermarks, latency markers, consumed bytes
@@ -553,19 +553,18 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   int64_t* cnt3 = totals + 6;   // [3 nc] each chunk's counts along its entry's chain
   int64_t* btot = cnt3 + 3 * nc;   // [3 nblk] block totals, then their exclusive offsets
   int32_t* cexit = (int32_t*)(btot + 3 * nblk);   // [nc] where each chunk's true chain leaves it
-  int32_t* nsurv = cexit + nc;                     // [nc] candidates that survived each chunk
-  int64_t* surv = (int64_t*)(((uintptr_t)(nsurv + nc) + 7) & ~(uintptr_t)7);   // [nc][DEC_S] kept survivors
+  int32_t* nsurv = cexit + nc;                     // [nc][DEC_W] survivors each wave found
+  int64_t* surv = (int64_t*)(((uintptr_t)(nsurv + nc * DEC_W) + 7) & ~(uintptr_t)7);   // [nc][DEC_S] kept survivors
   int64_t* walk = surv + nc * DEC_S;               // [nc] chunks to walk again (entry not a kept survivor)
   unsigned long long* n_walk = (unsigned long long*)(walk + nc);
   HIPCHK(e, hipMemsetAsync(err, 0, 16, e->stream));   // err and n_unknown
   HIPCHK(e, hipMemsetAsync(n_walk, 0, 8, e->stream));
-  int32_t* table = (int32_t*)e->dec_table;
   const unsigned gb = (unsigned)((nc + DEC_T - 1) / DEC_T);
-  hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, table, conv, surv, nsurv);
+  hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, conv, surv, nsurv);
   hipLaunchKernelGGL(k_dec_entry, dim3(gb), dim3(DEC_T), 0, e->stream, d, conv, surv, nsurv, entry, cnt3, cexit, unknown,
                      n_unknown, walk, n_walk, err);
-  hipLaunchKernelGGL(k_dec_fix, dim3(1), dim3(1), 0, e->stream, d, table, entry, unknown, n_unknown, surv, nsurv, cnt3,
-                     cexit, walk, n_walk, err);
+  hipLaunchKernelGGL(k_dec_fix, dim3(1), dim3(1), 0, e->stream, d, entry, unknown, n_unknown, surv, nsurv, cnt3, cexit,
+                     walk, n_walk, err);
   hipLaunchKernelGGL(k_dec_count, dim3(64), dim3(DEC_T), 0, e->stream, d, entry, walk, n_walk, cnt3, cexit, err);
   hipLaunchKernelGGL(k_dec_bscan, dim3((unsigned)nblk), dim3(DEC_SCAN), 0, e->stream, d, cnt3, base, btot);
   hipLaunchKernelGGL(k_dec_top, dim3(1), dim3(DEC_SCAN), 0, e->stream, d, entry, cexit, btot, (int64_t)nblk, totals);

@@ -137,6 +137,12 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   // record re-armed its timer (armed[p * stride + kid], EventTimeTrigger.onElement :37-45).  Null otherwise
   uint8_t* disarm;
   uint8_t* armed;
+  // PurgingTrigger + allowed lateness (tumbling): a fired window's purge clears its state but keeps each key's
+  // cleanup timer until the cleanup time (WindowOperator.java:365-371 purges contents only; the timer goes at
+  // :420-428).  gfirst[p * stride + kid] = the arrival ordinal that registered the timer of (key, window gtag[p])
+  // (0 without first-arrival tracking), INT64_MAX = none; the timers' only trace, written to checkpoints.  Null else
+  int64_t* gtag;
+  int64_t* gfirst;
 };
 
 __device__ __forceinline__ void set_error(int32_t* err, int32_t code) { atomicCAS(err, 0, code); }
@@ -1897,7 +1903,12 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
   if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) {
     // FIRE_AND_PURGE after the last element: pane cleared (AbstractHeapState.clear).  (Sliding: the slice
     // also feeds windows that have not fired; a purged window's later per-element fires emit the record
-    // alone, k_fire_emit)
+    // alone, k_fire_emit).  The cleanup timer the segment's first record registered stays (s.gfirst)
+    if (s.gfirst) {
+      int64_t o = s.first ? ord_base + (int64_t)(sorted_key[headpos[j]] & ((1ull << idx_bits) - 1)) : 0;
+      if (s.first && s.c.first[idx] < o) o = s.c.first[idx];
+      if (o < s.gfirst[idx]) s.gfirst[idx] = o;
+    }
     if (s.c.sum) s.c.sum[idx] = sum_identity(s.vt);
     if (s.c.mn) s.c.mn[idx] = INT64_MAX;
     if (s.c.mx) s.c.mx[idx] = INT64_MIN;
@@ -1995,6 +2006,7 @@ __global__ void k_fire_emit(Spec s, const unsigned long long* sorted_key, int64_
 constexpr int WM_THREADS = 1024;
 constexpr int WM_MAXT = 2048;      // windows firing at one watermark
 constexpr int WM_MAXP = MAX_P;     // slices purged at one watermark (>= P)
+constexpr int32_t PURGE_GHOST = 1 << 30;   // purge list flag: keep the panes' cleanup timers (Spec::gfirst)
 
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old, int64_t wm_new, unsigned int* done) {
@@ -2013,12 +2025,12 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     if (m == FREE_TAG) continue;
     const int64_t n_hi = floor_div(m, s.R);
     const int64_t n_lo = floor_div(m - s.K, s.R) + 1;
-    bool purge_now = false;
+    bool purge_now = false, fire_purge = false;
     for (int64_t n = n_lo; n <= n_hi; ++n) {
       const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
       const bool fires = max_ts > wm_old && max_ts <= wm_new;
       if (!fires) continue;
-      if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) purge_now = true;   // the slice is the window
+      if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) purge_now = fire_purge = true;   // the slice is the window
       bool owner = true;                                                    // first live slice of window n
       for (int64_t mm = n * s.R; mm < m; ++mm) {
         if (s.slice_tag[floor_mod(mm, s.P)] == mm) { owner = false; break; }
@@ -2032,7 +2044,8 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     if (ct <= wm_new) purge_now = true;
     if (purge_now) {
       const int32_t q = atomicAdd(&n_purge, 1);
-      if (q < WM_MAXP) purge[q] = p;
+      // a fire's purge keeps the panes' cleanup timers (as ghost ordinals) until the cleanup time
+      if (q < WM_MAXP) purge[q] = p | ((s.gfirst && fire_purge && ct > wm_new) ? PURGE_GHOST : 0);
     }
   }
   // window panes (sliding: the assigner's extra windows): a firing window without any live slice is a task
@@ -2125,9 +2138,14 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   }
   // purge this workgroup's share of the expired slices (it fired that share above)
   for (int32_t q = 0; q < np; ++q) {
-    const int64_t pbase = (int64_t)purge[q] * s.stride;
+    const bool ghost = (purge[q] & PURGE_GHOST) != 0;
+    const int64_t pbase = (int64_t)(purge[q] & ~PURGE_GHOST) * s.stride;
     for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < s.stride; kid += gstride) {
       const int64_t idx = pbase + kid;
+      if (ghost) {
+        const int64_t o = s.first ? s.c.first[idx] : (s.c.present[idx] ? 0 : INT64_MAX);
+        if (o < s.gfirst[idx]) s.gfirst[idx] = o;
+      }
       if (s.c.sum) s.c.sum[idx] = sum_identity(s.vt);
       if (s.c.mn) s.c.mn[idx] = INT64_MAX;
       if (s.c.mx) s.c.mx[idx] = INT64_MIN;
@@ -2154,7 +2172,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   __syncthreads();
   if (!last) return;
   // last workgroup: free the purged slots, then record the watermark's position in the log
-  for (int32_t q = threadIdx.x; q < np; q += WM_THREADS) s.slice_tag[purge[q]] = FREE_TAG;
+  for (int32_t q = threadIdx.x; q < np; q += WM_THREADS) s.slice_tag[purge[q] & ~PURGE_GHOST] = FREE_TAG;
   for (int32_t q = threadIdx.x; q < nwp; q += WM_THREADS) s.wtag[wpurge[q]] = FREE_TAG;
   if (threadIdx.x == 0) {
     *done = 0u;
@@ -2214,6 +2232,8 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
       if (tags[p] != FREE_TAG) live = pane_present(s, (int64_t)p * s.stride + dbase + x);
     for (int w = 0; w < s.W && !live; ++w)   // window panes (sliding extra windows)
       if (s.wtag[w] != FREE_TAG) live = cols_present(s, s.wc, (int64_t)w * s.stride + dbase + x);
+    for (int p = 0; s.gtag && p < s.P && !live; ++p)   // cleanup timers of purged windows
+      if (s.gtag[p] != FREE_TAG) live = s.gfirst[(int64_t)p * s.stride + dbase + x] != INT64_MAX;
     if (!live) {
       kg_evicted[key_group_for_hash(long_hash_code(key), s.mp)] = 1;
       continue;
@@ -2270,6 +2290,15 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
       }
     }
   }
+  if (s.gtag)
+    for (int p = 0; p < s.P; ++p) {   // uniform
+      if (s.gtag[p] == FREE_TAG) continue;
+      int64_t* c = s.gfirst + (int64_t)p * s.stride + dbase;
+      for (int x = threadIdx.x; x < KB; x += CP_THREADS) tmp[x] = c[x];
+      __syncthreads();
+      for (int y = threadIdx.x; y < KB; y += CP_THREADS) c[y] = inv[y] >= 0 ? tmp[inv[y]] : INT64_MAX;
+      __syncthreads();
+    }
   if (s.c.sum) move(s.c.sum, sum_identity(s.vt));
   if (s.c.mn) move(s.c.mn, INT64_MAX);
   if (s.c.mx) move(s.c.mx, INT64_MIN);
@@ -2407,6 +2436,11 @@ __global__ void k_restore(Spec s, const int64_t* ent, int64_t n, int32_t wpane) 
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t* x = ent + j * FW_SNAP_ENTRY_WORDS;
     const int64_t kid = dir_lookup(s, x[1]);
+    if (wpane == 2) {   // a cleanup timer without state (purged window): its ghost ordinal (slot tag set by the host)
+      if (kid < 0) { cap_error(s, 15); continue; }
+      s.gfirst[floor_mod(x[0], s.P) * s.stride + kid] = x[6];
+      continue;
+    }
     const int32_t p = wpane ? slice_slot_at(s.wtag, s.W, x[0]) : slice_slot(s, x[0]);
     if (kid < 0 || p < 0) { cap_error(s, 15); continue; }
     const int64_t idx = (int64_t)p * s.stride + kid;
@@ -2644,6 +2678,10 @@ struct fw_engine {
   // restored tumbling windows (slice numbers) whose trigger timers fired before the checkpoint, still ahead of
   // the watermark (Spec::disarm / armed); and the restored windows that did carry their trigger timers
   std::set<int64_t> disarmed, armed_windows;
+  // PurgingTrigger + allowed lateness: windows whose cleanup timers may outlive their state (Spec::gtag), each
+  // held until the watermark reaches its cleanup time
+  std::set<int64_t> ghost_windows;
+  std::vector<std::vector<int64_t>> snap_gkg;   // per key group: (window, key, ordinal) of such timers
   std::set<std::pair<int64_t, int64_t>> snap_unarmed;   // build_snapshot: (slice, key) panes not re-armed
   // fw_snapshot_kg: entries of every key group, built once per engine state (state_epoch)
   int64_t state_epoch = 0, snap_epoch = -1;
@@ -2723,8 +2761,8 @@ struct fw_engine {
   double compact_fill = 0.5;                // FW_COMPACT_FILL
   int64_t compactions = 0;
   // fw_decode scratch (grow-only)
-  void *dec_table = nullptr, *dec_small = nullptr, *dec_bytes = nullptr;
-  size_t dec_table_cap = 0, dec_small_cap = 0, dec_bytes_cap = 0;
+  void *dec_small = nullptr, *dec_bytes = nullptr;
+  size_t dec_small_cap = 0, dec_bytes_cap = 0;
   int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
   int agg_split = AG_SPLIT_CHAIN;           // shares per hot bucket, at most (FW_AGG_SPLIT)
   int agg_chunk_pct = 200;                  // records per share: at least this % of the mean load (FW_AGG_CHUNK_PCT)
@@ -2775,7 +2813,7 @@ struct fw_engine {
   int64_t dev_marks = 0;        // device marks enqueued since the last collect
   bool out_dirty = false;       // output appended (per-element fires) after the last device mark
   std::vector<double> h_sum_d, h_mn_d, h_mx_d;
-  // asynchronous drains (fw_collect_begin / fw_collect_end): two pinned host staging buffers, alternating
+  // asynchronous drains (fw_collect_begin / fw_collect_end): NDRAIN pinned host staging buffers, in turn
   struct Drain {
     int64_t* host = nullptr;        // [DR_COLS][rows] columns, then [mark_capacity] device mark positions, then hdr[4]
     int64_t* dptr = nullptr;        // the same memory as the device sees it
@@ -2783,11 +2821,13 @@ struct fw_engine {
     hipEvent_t staged = nullptr;    // the engine stream's copy done (the drain stream waits for it)
     hipEvent_t done = nullptr;
     bool pending = false;           // begun, not yet ended
+    int32_t ticket = -1;            // the ticket fw_collect_begin handed out for it
     std::vector<HostMark> marks;    // the host marks of the drain
     int64_t dev_marks = 0;
     std::vector<int64_t> mark_wm, mark_pos;
   };
-  Drain drains[2];
+  static constexpr int NDRAIN = 3;   // drains outstanding at once
+  Drain drains[NDRAIN];
   hipStream_t dstream = nullptr;     // drain stream: staged results to pinned host memory beside the next batches
   int64_t drain_rows = 0;
   int64_t drain_seq = 0;
@@ -2814,7 +2854,7 @@ struct fw_engine {
     for (void* p : allocs) (void)hipFree(p);
     if (bload_host) (void)hipHostFree(bload_host);
     if (dir_keys_host) (void)hipHostFree(dir_keys_host);
-    for (void* p : {dec_table, dec_small, dec_bytes}) if (p) (void)hipFree(p);
+    for (void* p : {dec_small, dec_bytes}) if (p) (void)hipFree(p);
     if (h_pin) (void)hipHostFree(h_pin);
     if (dstream) { (void)hipStreamSynchronize(dstream); (void)hipStreamDestroy(dstream); }
     for (auto& d : drains) {
@@ -3124,6 +3164,10 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     s.c.f1v = nullptr;
     s.c.present = e->alloc<uint8_t>(cells);
   }
+  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0 && c.assigner == FW_TUMBLING) {
+    s.gtag = e->alloc<int64_t>((size_t)P);   // purged windows' cleanup timers (Spec::gfirst)
+    s.gfirst = e->alloc<int64_t>(cells);
+  }
   if (c.assigner == FW_SLIDING) {   // window panes for the assigner's extra windows
     s.W = P;
     s.wtag = e->alloc<int64_t>((size_t)P);
@@ -3280,6 +3324,8 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   launch_fill(e, s.c.mx, INT64_MIN, (int64_t)cells);
   launch_fill(e, s.c.cnt, 0, (int64_t)cells);
   launch_fill(e, s.c.first, INT64_MAX, (int64_t)cells);
+  launch_fill(e, s.gtag, FREE_TAG, P);
+  launch_fill(e, s.gfirst, INT64_MAX, (int64_t)cells);
   if (s.c.present) HIPCHK(e, hipMemsetAsync(s.c.present, 0, cells, e->stream));
   if (s.W > 0) {
     launch_fill(e, s.wtag, FREE_TAG, s.W);
@@ -3530,6 +3576,53 @@ int fw_stream_wait_input(fw_engine* e, void* stream, int32_t back) {
   return FW_OK;
 }
 
+// PurgingTrigger + allowed lateness: window m's cleanup timers outlive its purged state until its cleanup time;
+// its slot's ghost column holds them (Spec::gfirst), tagged with m
+static int64_t host_max_ts(const fw::Spec& s, int64_t m) {
+  return fw::jsub(fw::jadd(fw::jadd(s.offset, (int64_t)((uint64_t)m * (uint64_t)s.size)), s.size), 1);
+}
+static int ghost_track(fw_engine* e, int64_t m) {
+  if (e->ghost_windows.count(m)) return FW_OK;
+  const int32_t p = (int32_t)floor_mod(m, e->s.P);
+  for (int64_t o : e->ghost_windows)
+    if (floor_mod(o, e->s.P) == p)
+      return fail(e, FW_ERR_CAPACITY, "purged windows' cleanup timers: two windows in one slice slot (raise max_open_slices)");
+  e->ghost_windows.insert(m);
+  return launch_fill(e, e->s.gtag + p, m, 1);
+}
+// the watermark moves from wm_old to wm_new: windows whose cleanup time it reaches drop their timers; windows it
+// fires (maxTimestamp in (wm_old, wm_new]) that stay within their lateness get a ghost column
+static int ghost_advance(fw_engine* e, int64_t wm_old, int64_t wm_new) {
+  const fw::Spec& s = e->s;
+  for (auto it = e->ghost_windows.begin(); it != e->ghost_windows.end();) {
+    const int64_t m = *it;
+    if (fw::cleanup_time(host_max_ts(s, m), s.lateness) > wm_new) { ++it; continue; }
+    const int32_t p = (int32_t)floor_mod(m, s.P);
+    int rc = launch_fill(e, s.gfirst + (size_t)p * (size_t)s.stride, INT64_MAX, s.stride);
+    if (!rc) rc = launch_fill(e, s.gtag + p, FREE_TAG, 1);
+    if (rc) return rc;
+    it = e->ghost_windows.erase(it);
+  }
+  // m with maxTimestamp in (max(wm_old, wm_new - lateness), wm_new]: maxTimestamp = offset + (m + 1) size - 1
+  const __int128 lo = std::max<__int128>((__int128)wm_old, (__int128)wm_new - (__int128)s.lateness);
+  const __int128 base = (__int128)s.offset - 1;
+  auto m_at_or_below = [&](__int128 t) {   // largest m with maxTimestamp <= t
+    const __int128 x = t - base;
+    __int128 q = x / s.size;
+    if (x % s.size != 0 && x < 0) --q;
+    return q - 1;
+  };
+  const __int128 m_hi = m_at_or_below(wm_new), m_lo = m_at_or_below(lo) + 1;
+  if (m_hi - m_lo > (__int128)s.P) return fail(e, FW_ERR_CAPACITY, "purged windows' cleanup timers: more windows within their lateness than slice slots");
+  for (__int128 m = m_lo; m <= m_hi; ++m) {
+    if (m < (__int128)INT64_MIN / 2 || m > (__int128)INT64_MAX / 2) continue;
+    if (fw::cleanup_time(host_max_ts(s, (int64_t)m), s.lateness) <= wm_new) continue;
+    int rc = ghost_track(e, (int64_t)m);
+    if (rc) return rc;
+  }
+  return FW_OK;
+}
+
 int fw_advance_watermark(fw_engine* e, int64_t wm) {
   if (!e) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
@@ -3537,6 +3630,10 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   e->state_epoch++;
   if (e->session) return session_watermark(e, wm);
   if (e->list) return list_watermark(e, wm);
+  if (e->s.gtag && wm > e->cur_wm) {
+    int rc = ghost_advance(e, e->cur_wm, wm);
+    if (rc) return rc;
+  }
   if (wm <= e->cur_wm || wm_quiet(e->s, e->cur_wm, wm)) {   // nothing fires or purges: the mark only
     if (e->out_dirty) {   // per-element fires appended since the last device mark: the mark needs the count
       hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
@@ -3698,9 +3795,9 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
   if (!e || !ticket) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
   HIPCHK(e, hipSetDevice(e->dev));
-  const int b = (int)(e->drain_seq & 1);
+  const int b = (int)(e->drain_seq % fw_engine::NDRAIN);
   fw_engine::Drain& d = e->drains[b];
-  if (d.pending) { e->err = "fw_collect_begin: two drains outstanding (fw_collect_end the older first)"; return FW_ERR_INVALID_ARG; }
+  if (d.pending) { e->err = "fw_collect_begin: three drains outstanding (fw_collect_end the oldest first)"; return FW_ERR_INVALID_ARG; }
   const OutLog& L = e->s.o;
   const size_t words = (size_t)DR_COLS * (size_t)std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX) +
                        (size_t)L.mark_capacity + 4;
@@ -3740,17 +3837,21 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
   e->out_dirty = false;
   e->list_out = 0;
   d.pending = true;
-  *ticket = (int32_t)(e->drain_seq++ & 0x7FFFFFFF);
+  d.ticket = (int32_t)(e->drain_seq++ & 0x7FFFFFFF);
+  *ticket = d.ticket;
   return FW_OK;
 }
 
 int fw_collect_end(fw_engine* e, int32_t ticket, fw_out* o) {
   if (!e || !o || ticket < 0) return FW_ERR_INVALID_ARG;
-  fw_engine::Drain& d = e->drains[ticket & 1];
-  if (!d.pending || ((e->drain_seq - 1 - ticket) & 0x7FFFFFFF) > 1) {
+  fw_engine::Drain* dp = nullptr;
+  for (fw_engine::Drain& x : e->drains)
+    if (x.pending && x.ticket == ticket) dp = &x;
+  if (!dp) {
     e->err = "fw_collect_end: no such drain outstanding";
     return FW_ERR_INVALID_ARG;
   }
+  fw_engine::Drain& d = *dp;
   HIPCHK(e, hipSetDevice(e->dev));
   HIPCHK(e, hipEventSynchronize(d.done));
   d.pending = false;
@@ -4010,6 +4111,19 @@ static int build_snapshot(fw_engine* e) {
       }
     }
   }
+  // purged windows' cleanup timers (PurgingTrigger + allowed lateness)
+  e->snap_gkg.assign((size_t)mp, {});
+  for (int64_t m : e->ghost_windows) {
+    const size_t off = (size_t)floor_mod(m, s.P) * st;
+    std::vector<int64_t> g(st);
+    HIPCHK(e, hipMemcpy(g.data(), s.gfirst + off, 8 * st, hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < st; ++k) {
+      if (g[k] == INT64_MAX || kid_kg[k] < 0) continue;
+      const int64_t key = (int64_t)k == s.D ? fw::EMPTY_KEY : keys[k];
+      auto& v = e->snap_gkg[(size_t)kid_kg[k]];
+      v.insert(v.end(), {m, key, s.first ? g[k] - e->ordinal : -1});
+    }
+  }
   e->snap_epoch = e->state_epoch;
   return FW_OK;
 }
@@ -4246,9 +4360,9 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   int rc = check_state_layout(e, layout);
   if (rc) return rc;
   const fw_config& c = e->cfg;
-  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0)
-    return reject(e, FW_ERR_UNSUPPORTED, "PurgingTrigger with allowed lateness: purged panes keep timers the "
-                                         "engine does not hold");
+  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0 && c.assigner != FW_TUMBLING)
+    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows under PurgingTrigger with allowed lateness: purged windows "
+                                         "keep timers the engine does not hold");
   HIPCHK(e, hipSetDevice(e->dev));
   rc = build_snapshot(e);
   if (rc) return rc;
@@ -4309,6 +4423,17 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
     if (max_ts > e->cur_wm && !p.unarmed) tv.push_back({p.key, p.start, p.end, max_ts, p.first, 0, INT64_MAX});
     if (ct != max_ts || max_ts <= e->cur_wm) tv.push_back({p.key, p.start, p.end, ct, p.first, 1, INT64_MAX});
   }
+  // purged windows' cleanup timers (no state; a key whose window holds state again has the timer above)
+  if (!e->snap_gkg.empty()) {
+    std::set<std::pair<int64_t, int64_t>> has;
+    for (const KgPane& p : panes) has.insert({p.start, p.key});
+    const std::vector<int64_t>& g = e->snap_gkg[(size_t)kg];
+    for (size_t j = 0; j + 3 <= g.size(); j += 3) {
+      const int64_t start = host_window_start(c, g[j]), end = fw::jadd(start, c.size);
+      if (has.count({start, g[j + 1]})) continue;
+      tv.push_back({g[j + 1], start, end, fw::cleanup_time(fw::jsub(end, 1), c.allowed_lateness), g[j + 2], 1, INT64_MAX});
+    }
+  }
   if (!e->restored_timer_rank.empty())
     for (Tm& t : tv) {
       auto it = e->restored_timer_rank.find({t.key, t.start, t.end, t.ts});
@@ -4362,8 +4487,6 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   if (sliding && c.allowed_lateness > 0)
     return reject(e, FW_ERR_UNSUPPORTED, "sliding windows with allowed lateness: window-level state restores into "
                                          "tumbling windows, or sliding without lateness");
-  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0)
-    return reject(e, FW_ERR_UNSUPPORTED, "PurgingTrigger with allowed lateness");
   if (e->restored && watermark != e->cur_wm)
     return reject(e, FW_ERR_INVALID_ARG, "key groups restored at different watermarks");
   const bool f64 = s.vt == FW_VALUE_F64;
@@ -4456,8 +4579,28 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
     if (ct != max_ts) want.push_back({p.key, p.start, p.end, ct});
   }
   std::sort(want.begin(), want.end());
-  if (got != want)
+  // PurgingTrigger + allowed lateness: a window purged by its fire keeps its keys' cleanup timers without state
+  std::vector<int64_t> ghosts;   // restore entries (window, key, .., ordinal)
+  if (s.gtag && got != want) {
+    std::vector<std::array<int64_t, 4>> extra;
+    if (!std::includes(got.begin(), got.end(), want.begin(), want.end()))
+      return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
+    std::set_difference(got.begin(), got.end(), want.begin(), want.end(), std::back_inserter(extra));
+    std::set<std::pair<int64_t, int64_t>> has;
+    for (const KgPane& p : panes) has.insert({p.start, p.key});
+    for (const auto& t : extra) {
+      const int64_t key = t[0], start = t[1], end = t[2], ts = t[3];
+      const int64_t m = fw::floor_div(fw::jsub(start, c.offset), c.size);
+      const int64_t max_ts = fw::jsub(end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+      if (host_window_start(c, m) != start || end != fw::jadd(start, c.size) || ts != ct || ct == max_ts || ct <= watermark ||
+          has.count({start, key}) || host_key_group(s, key) != kg)
+        return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
+      const int64_t w[FW_SNAP_ENTRY_WORDS] = {m, key, 0, 0, 0, 0, 0, 0};
+      ghosts.insert(ghosts.end(), w, w + FW_SNAP_ENTRY_WORDS);
+    }
+  } else if (got != want) {
     return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
+  }
   if (!dis_now.empty() && !e->s.disarm) {   // per-slot flags and per-pane re-arm marks, first needed here
     e->s.disarm = e->alloc<uint8_t>((size_t)s.P);
     e->s.armed = e->alloc<uint8_t>((size_t)s.P * (size_t)s.stride);
@@ -4483,7 +4626,18 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   for (const auto& t : got_in_order) e->restored_timer_rank[t] = (int64_t)e->restored_timer_rank.size();
   if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(s.kg_end - s.kg_start + 1), 0);
   if (present) e->kg_touched[(size_t)(kg - s.kg_start)] = 1;
-  return restore_entries(e, watermark, ent.data(), (int64_t)panes.size(), sliding ? 1 : 0);
+  rc = restore_entries(e, watermark, ent.data(), (int64_t)panes.size(), sliding ? 1 : 0);
+  if (rc || !s.gtag) return rc;
+  // windows within their lateness at the restore watermark (later per-element fires purge them again), and the
+  // restored cleanup timers without state, each with its arrival ordinal (after the panes', in blob order)
+  rc = ghost_advance(e, INT64_MIN, watermark);
+  const int64_t ng = (int64_t)(ghosts.size() / FW_SNAP_ENTRY_WORDS);
+  for (int64_t j = 0; j < ng && !rc; ++j) {
+    ghosts[(size_t)j * FW_SNAP_ENTRY_WORDS + 6] = s.first ? e->restore_ord++ : 0;
+    rc = ghost_track(e, ghosts[(size_t)j * FW_SNAP_ENTRY_WORDS]);
+  }
+  if (rc) return rc;
+  return restore_entries(e, watermark, ghosts.data(), ng, 2);
 }
 
 int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,

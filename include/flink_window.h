@@ -202,10 +202,10 @@ int         fw_sync(fw_engine* e);
 int         fw_collect(fw_engine* e, fw_out* out, int32_t mem);
 /* Asynchronous drain of the same results (the operator hands fired windows downstream while the next batch already
  * runs; they need only precede their watermark, AbstractStreamOperator.java:803-808).  fw_collect_begin enqueues on
- * the engine stream a copy of every result and watermark mark since the last collect into pinned host staging (two
- * buffers, alternating) and restarts the log; it returns at once with a ticket.  fw_collect_end(ticket) waits for
+ * the engine stream a copy of every result and watermark mark since the last collect into pinned host staging (three
+ * buffers, in turn) and restarts the log; it returns at once with a ticket.  fw_collect_end(ticket) waits for
  * that copy and fills `out` (FW_MEM_HOST layout) with columns valid until the next fw_collect_begin after it.  At
- * most two drains are outstanding; one holds at most min(out_capacity, 2^22) results (more: FW_ERR_CAPACITY at
+ * most three drains are outstanding; one holds at most min(out_capacity, 2^22) results (more: FW_ERR_CAPACITY at
  * fw_collect_end).  Device errors surface at fw_collect_end. */
 int         fw_collect_begin(fw_engine* e, int32_t* ticket);
 int         fw_collect_end(fw_engine* e, int32_t ticket, fw_out* out);

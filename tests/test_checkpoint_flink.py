@@ -396,3 +396,83 @@ def test_restore_rejections():
     st0, tm0 = e.snapshot_kg_flink(0, sc["layout"])
     assert st0 == b"" and tm0 == bytes(8)
     e.close()
+
+
+def _purging_lateness_run(factory_g, mode, restore_at):
+    """PurgingTrigger + allowed lateness 400 (tumbling 1 s): a window's fire purges its state but each key keeps its
+    cleanup timer until maxTimestamp + 400 (WindowOperator.java:365-371 clears the contents only; the timer is
+    deleted at cleanup, :420-428), and a per-element fire within the lateness registers one for a key that had
+    none.  Snapshot at a watermark with purged windows inside their lateness; restore (at that watermark, or at
+    Long.MIN_VALUE as the reference restarts its timers) and continue."""
+    from flink_amd.windowing import (EventTimeTrigger, PurgingTrigger, ReduceFunction, TumblingEventTimeWindows,
+                                     make_config)
+    from harness import drive, gen_stream
+    from oracle.oracle import OracleEngine
+    keys, ts, vals = gen_stream(48_000, 2000, rate=1 << 13, zipf=1.1, ooo=300)   # ~6 s of event time
+    f1 = np.arange(len(keys), dtype=np.int64) * 3 + 1
+    kw = dict(max_parallelism=128, key_capacity=1 << 13, max_batch=1 << 13, out_capacity=1 << 20)
+    if mode:
+        kw["ingest_mode"] = mode
+    cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "max"), "i64", True),
+                      PurgingTrigger.of(EventTimeTrigger.create()), 400, **kw)
+    layout = ("f1", "key", "max", "sum")
+    n = int(3.25 * (1 << 13)) + 17   # checkpoint watermark ~3.13 s: window [2 s, 3 s) fired, within its lateness
+    wm_cut = int(ts[:n].max()) - 120
+    assert 2999 < wm_cut < 3399
+    blobs = {}
+    for name, factory in (("g", factory_g), ("o", OracleEngine)):
+        if factory is None:
+            continue
+        e = factory(cfg)
+        drive(e, keys[:n], ts[:n], vals[:n], 2048, 120, None, f1=f1[:n])
+        blobs[name] = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        e.close()
+    # cleanup timers without state: (key, window) pairs in the timer section that the state section lacks
+    ghosts = 0
+    for kg, (st, tm) in blobs["o"].items():
+        have = set()
+        if st and st[6]:
+            pos, (nns,) = 11, struct.unpack(">i", st[7:11])
+            for _ in range(nns):
+                start, end, ne = struct.unpack(">qqi", st[pos:pos + 20])
+                pos += 20
+                for _ in range(ne):
+                    (k,) = struct.unpack(">q", st[pos:pos + 8])
+                    have.add((k, start))
+                    pos += 8 * (1 + len(layout))
+        (nt,) = struct.unpack(">i", tm[:4])
+        for j in range(nt):
+            k, start, end, t = struct.unpack(">qqqq", tm[4 + 32 * j:36 + 32 * j])
+            ghosts += (k, start) not in have
+    assert ghosts > 50, ghosts
+    wm = wm_cut if restore_at == "checkpoint" else LONG_MIN
+    outs = {}
+    for name, factory in (("g", factory_g), ("o", OracleEngine)):
+        if factory is None:
+            continue
+        e = factory(cfg)
+        for kg, (st, tm) in blobs["o"].items():
+            e.restore_kg_flink(kg, layout, st, tm, wm)
+        back = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        assert _diff(back, blobs["o"]) is None, _diff(back, blobs["o"])
+        outs[name] = _canon(epochs_of(drive(e, keys[n:], ts[n:], vals[n:], 2048, 120, LONG_MAX, f1=f1[n:]),
+                                      ["sum_i64", "max_i64"], True))
+        e.close()
+    return blobs, outs
+
+
+@pytest.mark.parametrize("restore_at", ["checkpoint", "long_min"])
+def test_oracle_purging_lateness_round_trip(restore_at):
+    _purging_lateness_run(None, 0, restore_at)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("restore_at", ["checkpoint", "long_min"])
+def test_purging_lateness_checkpoint(mode, restore_at):
+    """The engine's sections byte-identical with the oracle's (purged windows' cleanup timers included), its
+    restore writes them back, and the restored engine continues as the restored oracle."""
+    from flink_amd.windowing import WindowEngine
+    blobs, outs = _purging_lateness_run(WindowEngine, mode, restore_at)
+    assert _diff(blobs["g"], blobs["o"]) is None, _diff(blobs["g"], blobs["o"])
+    assert outs["g"] == outs["o"]

@@ -1,6 +1,6 @@
 """Asynchronous drains (fw_collect_begin / fw_collect_end): the results and watermark marks of every drain equal
 what the synchronous fw_collect returns at the same point of the same stream (two engines fed identically), with
-one or two drains outstanding while later batches run, quiet watermarks (marks without results) included, and
+one to three drains outstanding while later batches run, quiet watermarks (marks without results) included, and
 for tumbling, sliding and session windows (the window-start column).  The operator may hand watermark j's results
 downstream after batch j + 1 is pushed: results need only precede their watermark
 (AbstractStreamOperator.java:803-808)."""
@@ -35,7 +35,7 @@ def _rows(r):
 
 
 @pytest.mark.parametrize("kind", ["tumbling", "sliding", "session"])
-@pytest.mark.parametrize("lag", [0, 1])   # drains left outstanding before the next begins (two at most at once)
+@pytest.mark.parametrize("lag", [0, 1, 2])   # drains left outstanding before the next begins (three at most at once)
 def test_async_drain_matches_collect(kind, lag):
     from flink_amd.windowing import (EventTimeSessionWindows, ReduceFunction, SlidingEventTimeWindows,
                                      TumblingEventTimeWindows, WindowEngine, make_config)
@@ -61,7 +61,7 @@ def test_async_drain_matches_collect(kind, lag):
         want += _rows(b.collect())
     for e in (a, b):
         e.advance_watermark(LONG_MAX)
-    if len(pending) > 1:
+    while len(pending) > 2:
         got += _rows(a.collect_end(pending.pop(0)))
     pending.append(a.collect_begin())
     while pending:
@@ -93,8 +93,16 @@ def test_async_drain_limits():
     e.advance_watermark(LONG_MAX)
     t1 = e.collect_begin()
     t2 = e.collect_begin()
-    with pytest.raises(_abi.FwError):   # a third drain while two are outstanding
+    t3 = e.collect_begin()
+    with pytest.raises(_abi.FwError):   # a fourth drain while three are outstanding
         e.collect_begin()
-    r1, r2 = e.collect_end(t1), e.collect_end(t2)
-    assert r1["n"] > 0 and r2["n"] == 0 and list(r1["mark_wm"]) == [LONG_MAX] and len(r2["mark_wm"]) == 0
+    with pytest.raises(_abi.FwError):   # no such ticket
+        e.collect_end(t3 + 1)
+    r2, r1, r3 = e.collect_end(t2), e.collect_end(t1), e.collect_end(t3)   # any order
+    assert r1["n"] > 0 and r2["n"] == 0 and r3["n"] == 0
+    assert list(r1["mark_wm"]) == [LONG_MAX] and len(r2["mark_wm"]) == 0
+    with pytest.raises(_abi.FwError):   # ended already
+        e.collect_end(t1)
+    t4 = e.collect_begin()   # the ring turns over
+    assert e.collect_end(t4)["n"] == 0
     e.close()
