@@ -286,8 +286,9 @@ def main():
         ok = out["n_records"] == n and bool(torch.equal(out["key"], k)) and bool(torch.equal(out["value"], v))
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        for _ in range(args.decode_steps):
-            eng.decode(wire, ["long", "long", "long"], key=0, f1=1, value=2, record_cap=n, device=True)
+        for _ in range(args.decode_steps):   # into the same output columns (allocated by the first call)
+            eng.decode(wire, ["long", "long", "long"], key=0, f1=1, value=2, record_cap=n, device=True,
+                       buffers=out["buffers"])
         torch.cuda.synchronize()
         dtd = (time.perf_counter() - t2) / args.decode_steps
         dec = {"value": n / dtd, "unit": "records/s", "GB_s_in": wire.numel() / dtd / 1e9, "bytes_per_record": 37,
@@ -308,6 +309,7 @@ def main():
         torch.cuda.synchronize()
         t3 = time.perf_counter()
         for q, w in enumerate(wires):
+            # fresh output columns per batch: the push reads them on the engine's route stream after this call returns
             o = eng.decode(w, ["long", "long", "long"], key=0, f1=1, value=2, record_cap=n, device=True)
             m = o["n_records"]
             eng.push(o["key"][:m], o["ts"][:m], o["value"][:m], f1=o["f1"][:m])
@@ -326,6 +328,16 @@ def main():
     # in pinned host columns while step j + 1 runs (they need only precede watermark j downstream); and the same
     # with the synchronous fw_collect for comparison.  Fresh batches after the decode leg's
     drain_leg = None
+
+    def _digest(r):   # read every drained value once, as an operator emitting them would (for the checksum below)
+        d = {"n": r["n"]}
+        for c in ("sum_i64", "count"):
+            a = r.get(c)
+            if a is not None:
+                d[c] = np.array([a.view(np.uint64).sum(dtype=np.uint64)], np.uint64).view(np.int64)
+        return d
+
+    drained = []
     if args.drain_steps > 0 and exch is None:
         jr = args.warmup + args.steps + args.prof_steps + args.h2d_steps + 2 + args.decode_steps
         legs = {}
@@ -354,14 +366,14 @@ def main():
                     collected.append(r)
                     continue
                 if len(pend) == 3:   # three drains in flight: the oldest (two batches back) has landed by now
-                    r = eng.collect_end(pend.pop(0))
+                    r = eng.collect_end(pend.pop(0), copy=False)   # the pinned columns, read in place
                     n_out += r["n"]
-                    collected.append(r)
+                    drained.append(_digest(r))
                 pend.append(eng.collect_begin())
             for tk in pend:
-                r = eng.collect_end(tk)
+                r = eng.collect_end(tk, copy=False)
                 n_out += r["n"]
-                collected.append(r)
+                drained.append(_digest(r))
             torch.cuda.synchronize()
             dtr = (time.perf_counter() - t4) / args.drain_steps
             legs[mode] = {"value": batch / dtr, "unit": "events/s", "steps": args.drain_steps, "results": n_out,
@@ -390,14 +402,14 @@ def main():
         pushed_cols = [c for c in cols] + ([] if h2d is None else [tuple(x for x in hc) for hc in host])
         if vt == "i64":
             mask = (1 << 64) - 1
-            fired = int(np.concatenate([r["sum_i64"] for r in collected]).astype(np.uint64).sum(dtype=np.uint64)) & mask
+            fired = int(np.concatenate([r["sum_i64"] for r in collected + drained]).astype(np.uint64).sum(dtype=np.uint64)) & mask
             pushed = 0
             for k, t, v in pushed_cols:
                 pushed = (pushed + (int(v.sum().item()) & mask)) & mask      # int64 tensor sums wrap
             for x in dec_sums:
                 pushed = (pushed + (x & mask)) & mask
         else:
-            fired = int(np.concatenate([r["count"] for r in collected]).sum())
+            fired = int(np.concatenate([r["count"] for r in collected + drained]).sum())
             pushed = windows_per_record * (sum(int(k.numel()) for k, t, v in pushed_cols) + extra_n)
         if world > 1:
             import torch.distributed as dist

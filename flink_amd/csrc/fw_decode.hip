@@ -83,7 +83,7 @@ constexpr int DEC_DEAD = INT32_MIN;
 struct DecChunk {
   const uint8_t* b;   // the chunk's first byte (in LDS)
   int clen;           // its bytes
-  int64_t rem;        // bytes of the stream from its first byte on
+  int rem;            // bytes of the stream from its first byte on (capped at 2^30: every test is within a chunk + spill)
 };
 // the workgroup's DEC_T chunks into LDS, each at DEC_STRIDE with its own copy of the DEC_SPILL bytes after it
 // (the next chunk's first ones), then this lane's chunk.  Global loads of 16 B, LDS stores of 4 B
@@ -122,7 +122,8 @@ __device__ __forceinline__ DecChunk dec_stage_group(const DecSpec& d, uint8_t* b
   const int lane = (int)threadIdx.x & (DEC_T - 1);   // (only wave 0 walks)
   const int64_t c = (int64_t)blockIdx.x * DEC_T + lane;
   const int64_t start = c * DEC_CHUNK;
-  return {buf + lane * DEC_STRIDE, (int)max<int64_t>(0, min<int64_t>(DEC_CHUNK, d.nbytes - start)), d.nbytes - start};
+  return {buf + lane * DEC_STRIDE, (int)max<int64_t>(0, min<int64_t>(DEC_CHUNK, d.nbytes - start)),
+          (int)min<int64_t>(d.nbytes - start, (int64_t)1 << 30)};
 }
 // the element header at LDS position p (4-byte BE length, then the tag) from two aligned word reads
 __device__ __forceinline__ void dec_header(const uint8_t* p, uint32_t& len, uint32_t& tag) {
@@ -144,7 +145,7 @@ __device__ __forceinline__ int dec_ff(const DecChunk& ch, int pos, uint32_t len,
 #pragma unroll
   for (int j = 0; j < DEC_FF; ++j) {
     const int p = pos + j * L;
-    const bool in = p < ch.clen && p + (int64_t)L <= ch.rem;
+    const bool in = p < ch.clen && p + L <= ch.rem;
     uint32_t hl = 0, ht = 0;
     dec_header(ch.b + (in ? p : 0), hl, ht);
     ok = ok && in && hl == len && ht == tag;
@@ -161,7 +162,7 @@ __device__ __forceinline__ int dec_walk(const DecSpec& d, const DecChunk& ch, in
     dec_header(ch.b + pos, len, tag);
     const int k = dec_kind(d, len, (uint8_t)tag);
     if (k < 0) return DEC_DEAD;
-    if (pos + 4 + (int64_t)len > ch.rem) return pos - ch.clen;        // cut by the end: the next call's
+    if (pos + 4 + (int)len > ch.rem) return pos - ch.clen;            // cut by the end: the next call's
     on_element(pos, k);
     pos += 4 + (int)len;
     if (k == 0) {
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, i
       dec_header(ch.b + pos, len, tag);
       const int k = dec_kind(d, len, (uint8_t)tag);
       if (k < 0) x = DEC_DEAD;
-      else if (pos + 4 + (int64_t)len > ch.rem) x = pos - ch.clen;
+      else if (pos + 4 + (int)len > ch.rem) x = pos - ch.clen;
       else {
         pos += 4 + (int)len;
         n0 += k == 0; n1 += k == 1; n2 += k == 2;
@@ -240,58 +241,6 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, i
   nsurv[c * DEC_W + wv] = ns;
 }
 
-// the counts and exit of chunk c's chain from entry en >= 0, from its survivors; false: not among the kept ones
-__device__ __forceinline__ bool dec_surv_counts(const DecSpec& d, const int64_t* surv, const int32_t* nsurv, int64_t c,
-                                                int32_t en, int64_t* cnt3, int32_t* cexit) {
-  const int clen = (int)min<int64_t>(DEC_CHUNK, d.nbytes - c * DEC_CHUNK);
-  if (en >= clen) { cexit[c] = en - clen; return true; }   // the previous element covers the (last, short) chunk
-  const int w = en % DEC_W;                                  // the wave that walked candidate en
-  const int ns = min(nsurv[c * DEC_W + w], DEC_SW);
-  for (int i = 0; i < ns; ++i) {
-    const int64_t s = surv[c * DEC_S + w * DEC_SW + i];
-    if ((int32_t)(s >> 32) != en) continue;
-    const int32_t v = (int32_t)(uint32_t)s;
-    cnt3[3 * c] = (v >> 10) & 63;
-    cnt3[3 * c + 1] = (v >> 16) & 63;
-    cnt3[3 * c + 2] = (v >> 22) & 63;
-    cexit[c] = dec_cexit(v);
-    return true;
-  }
-  return false;
-}
-// a chunk's entry known, its counts: from the survivors, else listed for a walk (the wave kept fewer survivors than
-// it found), else corrupt (no chain from the entry through the chunk)
-__device__ __forceinline__ void dec_entry_counts(const DecSpec& d, const int64_t* surv, const int32_t* nsurv, int64_t c,
-                                                 int32_t en, int64_t* cnt3, int32_t* cexit, int64_t* walk,
-                                                 unsigned long long* n_walk, int32_t* err) {
-  if (en == -3) atomicExch(err, 1);
-  if (en < 0 || dec_surv_counts(d, surv, nsurv, c, en, cnt3, cexit)) return;
-  if (nsurv[c * DEC_W + en % DEC_W] > DEC_SW) walk[atomicAdd(n_walk, 1ull)] = c;
-  else atomicExch(err, 1);
-}
-
-// every chunk's entry offset known from the previous chunk's agreeing survivors (-2: undecided, -3: corrupt,
-// -1: the stream ended inside the previous chunk's last element) and its counts from its own survivors;
-// undecided chunks (rare) listed for k_dec_fix, chunks whose entry is not a kept survivor for k_dec_count
-__global__ __launch_bounds__(DEC_T) void k_dec_entry(DecSpec d, const int32_t* conv, const int64_t* surv,
-                                                    const int32_t* nsurv, int32_t* entry, int64_t* cnt3, int32_t* cexit,
-                                                    int64_t* unknown, unsigned long long* n_unknown, int64_t* walk,
-                                                    unsigned long long* n_walk, int32_t* err) {
-  const int64_t c = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
-  if (c >= d.nchunks) return;
-  int32_t en = 0;
-  if (c > 0) {
-    int32_t a = INT32_MIN;
-    for (int w = 0; w < DEC_W; ++w) a = dec_agree(a, conv[(c - 1) * DEC_W + w]);
-    en = (a == INT32_MIN) ? -3 : (a == INT32_MAX) ? -2 : (a < 0 ? -1 : a);
-  }
-  entry[c] = en;
-  cnt3[3 * c] = cnt3[3 * c + 1] = cnt3[3 * c + 2] = 0;
-  cexit[c] = DEC_DEAD;
-  if (en == -2) unknown[atomicAdd(n_unknown, 1ull)] = c;
-  else dec_entry_counts(d, surv, nsurv, c, en, cnt3, cexit, walk, n_walk, err);
-}
-
 // chunk c's chain from pos in global memory (the rare paths): its exit or DEC_DEAD, and its counts
 __device__ __forceinline__ int32_t dec_walk_global(const DecSpec& d, int64_t c, int pos, int64_t n[3]) {
   const int64_t start = c * DEC_CHUNK;
@@ -309,52 +258,66 @@ __device__ __forceinline__ int32_t dec_walk_global(const DecSpec& d, int64_t c, 
     pos += 4 + (int)len;
   }
 }
-
-// the undecided chunks, in stream order: each one's entry where its predecessor's true chain leaves it (walked in
-// global memory), then its counts (one thread; nearly always nothing to do)
-__global__ void k_dec_fix(DecSpec d, int32_t* entry, int64_t* unknown, const unsigned long long* n_unknown,
-                          const int64_t* surv, const int32_t* nsurv, int64_t* cnt3, int32_t* cexit, int64_t* walk,
-                          unsigned long long* n_walk, int32_t* err) {
-  const int64_t nu = (int64_t)*n_unknown;
-  for (int64_t i = 1; i < nu; ++i)   // insertion sort of the list (atomic appends: any order)
-    for (int64_t j = i; j > 0 && unknown[j - 1] > unknown[j]; --j) { const int64_t t = unknown[j]; unknown[j] = unknown[j - 1]; unknown[j - 1] = t; }
-  for (int64_t i = 0; i < nu; ++i) {
-    const int64_t c = unknown[i];
-    const int32_t prev = entry[c - 1];
-    int32_t en;
-    if (prev < 0) {
-      en = prev == -1 ? -1 : -3;
-    } else {
-      int64_t n[3];
-      const int32_t x = dec_walk_global(d, c - 1, prev, n);
-      en = x == DEC_DEAD ? -3 : x < 0 ? -1 : x;
-    }
-    entry[c] = en;
-    dec_entry_counts(d, surv, nsurv, c, en, cnt3, cexit, walk, n_walk, err);
-  }
+// the entry a chunk's predecessor's survivors agree on (-2: they differ, -3: none survived: corrupt, -1: the
+// stream ended inside the predecessor's last element)
+__device__ __forceinline__ int32_t dec_agreed_entry(const int32_t* conv, int64_t c) {
+  if (c == 0) return 0;
+  int32_t a = INT32_MIN;
+  for (int w = 0; w < DEC_W; ++w) a = dec_agree(a, conv[(c - 1) * DEC_W + w]);
+  return (a == INT32_MIN) ? -3 : (a == INT32_MAX) ? -2 : (a < 0 ? -1 : a);
 }
 
-// the listed chunks (entry not among the kept survivors: rare), walked along their true chain in global memory
-__global__ __launch_bounds__(DEC_T) void k_dec_count(DecSpec d, const int32_t* entry, const int64_t* walk,
-                                                    const unsigned long long* n_walk, int64_t* cnt3, int32_t* cexit,
-                                                    int32_t* err) {
-  const int64_t nw = (int64_t)*n_walk;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = walk[i];
-    int64_t n[3];
-    const int32_t x = dec_walk_global(d, c, entry[c], n);
-    if (x == DEC_DEAD) { atomicExch(err, 1); n[0] = n[1] = n[2] = 0; }
-    cnt3[3 * c] = n[0]; cnt3[3 * c + 1] = n[1]; cnt3[3 * c + 2] = n[2];
-    cexit[c] = x;
-  }
-}
-
-// exclusive prefix of the chunks' counts, level 1: within blocks of DEC_SCAN chunks (base), block totals (btot)
-__global__ __launch_bounds__(DEC_SCAN) void k_dec_bscan(DecSpec d, const int64_t* cnt3, int64_t* base, int64_t* btot) {
+// per chunk: its entry (from its predecessor's agreeing survivors; where they differ — rare — from the last
+// chunk whose entry they fix, walking the chunks after it in global memory), its counts along its true chain
+// (from its survivors, else walked), then the exclusive prefix of the counts within blocks of DEC_SCAN chunks
+// (base) and the block totals (btot)
+__global__ __launch_bounds__(DEC_SCAN) void k_dec_bscan(DecSpec d, const int32_t* conv, const int64_t* surv,
+                                                       const int32_t* nsurv, int32_t* entry, int32_t* cexit,
+                                                       int64_t* base, int64_t* btot, int32_t* err) {
   __shared__ int64_t ws[3][DEC_SCAN / 64];
   const int64_t c = (int64_t)blockIdx.x * DEC_SCAN + threadIdx.x;
   int64_t v[3] = {0, 0, 0};
-  if (c < d.nchunks) { v[0] = cnt3[3 * c]; v[1] = cnt3[3 * c + 1]; v[2] = cnt3[3 * c + 2]; }
+  if (c < d.nchunks) {
+    int32_t en = dec_agreed_entry(conv, c);
+    if (en == -2) {
+      int64_t j = c - 1;
+      int32_t ej = dec_agreed_entry(conv, j);
+      while (ej == -2) ej = dec_agreed_entry(conv, --j);
+      for (; j < c && ej >= 0; ++j) {   // entry of j known: its chain's exit is the entry of j + 1
+        int64_t n[3];
+        const int32_t x = dec_walk_global(d, j, ej, n);
+        ej = x == DEC_DEAD ? -3 : x < 0 ? -1 : x;
+      }
+      en = ej;
+    }
+    int32_t x = DEC_DEAD;
+    if (en == -3) atomicExch(err, 1);
+    if (en >= 0) {
+      const int clen = (int)min<int64_t>(DEC_CHUNK, d.nbytes - c * DEC_CHUNK);
+      bool found = false;
+      if (en >= clen) {   // the previous element covers the (last, short) chunk
+        x = en - clen;
+        found = true;
+      } else {
+        const int w = en % DEC_W;   // the wave that walked candidate en
+        const int ns = min(nsurv[c * DEC_W + w], DEC_SW);
+        for (int i = 0; i < ns && !found; ++i) {
+          const int64_t sv = surv[c * DEC_S + w * DEC_SW + i];
+          if ((int32_t)(sv >> 32) != en) continue;
+          const int32_t pk = (int32_t)(uint32_t)sv;
+          v[0] = (pk >> 10) & 63; v[1] = (pk >> 16) & 63; v[2] = (pk >> 22) & 63;
+          x = dec_cexit(pk);
+          found = true;
+        }
+      }
+      if (!found) {   // not among the kept survivors (the wave found more): walked again
+        x = dec_walk_global(d, c, en, v);
+        if (x == DEC_DEAD) { atomicExch(err, 1); v[0] = v[1] = v[2] = 0; }
+      }
+    }
+    entry[c] = en;
+    cexit[c] = x;
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -435,7 +398,7 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_emit(DecSpec d, const int32_t* e
   __syncthreads();
   const int32_t en = (threadIdx.x < DEC_T && c < d.nchunks) ? entry[c] : -1;
   int32_t nr = 0;
-  if (en >= 0) {   // past the stream's last whole element (or corrupt: reported by k_dec_count) otherwise
+  if (en >= 0) {   // past the stream's last whole element (or corrupt: reported by k_dec_bscan) otherwise
     const int64_t blk = c / DEC_SCAN;
     int64_t j[3] = {btop[3 * blk] + base_in[3 * c], btop[3 * blk + 1] + base_in[3 * c + 1], btop[3 * blk + 2] + base_in[3 * c + 2]};
     const int64_t r0 = r0_s;
@@ -534,7 +497,7 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   };
   const size_t nc = (size_t)d.nchunks;
   const size_t nblk = (nc + DEC_SCAN - 1) / DEC_SCAN;
-  HIPCHK(e, grow(e->dec_small, e->dec_small_cap, nc * (4 * DEC_W + 4 + 4 + 4 * DEC_W + 8 + 8 + 24 + 24 + 8 * DEC_S) + nblk * 24 + 256));
+  HIPCHK(e, grow(e->dec_small, e->dec_small_cap, nc * (4 * DEC_W + 4 + 24 + 4 + 4 * DEC_W + 8 * DEC_S) + nblk * 24 + 256));
   const uint8_t* src = (const uint8_t*)bytes;
   if (mem == FW_MEM_HOST) {
     HIPCHK(e, grow(e->dec_bytes, e->dec_bytes_cap, (size_t)nbytes));
@@ -545,37 +508,26 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   uint8_t* sm = (uint8_t*)e->dec_small;
   int32_t* conv = (int32_t*)sm;   // [nc][DEC_W] each wave's agreeing exit
   int32_t* entry = conv + nc * DEC_W;
-  int64_t* unknown = (int64_t*)(((uintptr_t)(entry + nc) + 7) & ~(uintptr_t)7);
-  int64_t* base = unknown + nc;
-  int64_t* totals = base + 3 * nc;   // [4] records, watermarks, latency markers, consumed bytes
+  int64_t* base = (int64_t*)(((uintptr_t)(entry + nc) + 7) & ~(uintptr_t)7);
+  int64_t* totals = base + 3 * nc;   // [4] records, watermarks, latency markers, consumed bytes; then err
   int32_t* err = (int32_t*)(totals + 4);
-  unsigned long long* n_unknown = (unsigned long long*)(totals + 5);
-  int64_t* cnt3 = totals + 6;   // [3 nc] each chunk's counts along its entry's chain
-  int64_t* btot = cnt3 + 3 * nc;   // [3 nblk] block totals, then their exclusive offsets
+  int64_t* btot = totals + 6;   // [3 nblk] block totals, then their exclusive offsets
   int32_t* cexit = (int32_t*)(btot + 3 * nblk);   // [nc] where each chunk's true chain leaves it
   int32_t* nsurv = cexit + nc;                     // [nc][DEC_W] survivors each wave found
   int64_t* surv = (int64_t*)(((uintptr_t)(nsurv + nc * DEC_W) + 7) & ~(uintptr_t)7);   // [nc][DEC_S] kept survivors
-  int64_t* walk = surv + nc * DEC_S;               // [nc] chunks to walk again (entry not a kept survivor)
-  unsigned long long* n_walk = (unsigned long long*)(walk + nc);
-  HIPCHK(e, hipMemsetAsync(err, 0, 16, e->stream));   // err and n_unknown
-  HIPCHK(e, hipMemsetAsync(n_walk, 0, 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(err, 0, 4, e->stream));
   const unsigned gb = (unsigned)((nc + DEC_T - 1) / DEC_T);
   hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, conv, surv, nsurv);
-  hipLaunchKernelGGL(k_dec_entry, dim3(gb), dim3(DEC_T), 0, e->stream, d, conv, surv, nsurv, entry, cnt3, cexit, unknown,
-                     n_unknown, walk, n_walk, err);
-  hipLaunchKernelGGL(k_dec_fix, dim3(1), dim3(1), 0, e->stream, d, entry, unknown, n_unknown, surv, nsurv, cnt3, cexit,
-                     walk, n_walk, err);
-  hipLaunchKernelGGL(k_dec_count, dim3(64), dim3(DEC_T), 0, e->stream, d, entry, walk, n_walk, cnt3, cexit, err);
-  hipLaunchKernelGGL(k_dec_bscan, dim3((unsigned)nblk), dim3(DEC_SCAN), 0, e->stream, d, cnt3, base, btot);
+  hipLaunchKernelGGL(k_dec_bscan, dim3((unsigned)nblk), dim3(DEC_SCAN), 0, e->stream, d, conv, surv, nsurv, entry, cexit,
+                     base, btot, err);
   hipLaunchKernelGGL(k_dec_top, dim3(1), dim3(DEC_SCAN), 0, e->stream, d, entry, cexit, btot, (int64_t)nblk, totals);
   DecOut o{key, f1, ts, (int64_t*)value, wm, wm_pos, lm, lm_pos, key_hash, record_cap, marker_cap};
   hipLaunchKernelGGL(k_dec_emit, dim3(gb), dim3(DEC_TW), 0, e->stream, d, entry, base, btot, o, err);
   HIPCHK(e, hipGetLastError());
-  int64_t tot[4];
-  int32_t herr = 0;
+  int64_t tot[5];   // the totals and the error word, one read-back
   HIPCHK(e, hipMemcpyAsync(tot, totals, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  const int32_t herr = (int32_t)(tot[4] & 0xffffffff);
   if (herr == 1) return reject(e, FW_ERR_INVALID_ARG, "corrupt stream: no element chain through the bytes");
   out->n_records = tot[0];
   out->n_watermarks = tot[1];

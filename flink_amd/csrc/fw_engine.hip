@@ -2361,14 +2361,22 @@ __global__ __launch_bounds__(1024) void k_quirk_apply(Spec s, int64_t* list, uns
 // device marks, fits, the engine's error word.  A log larger than the staging is left in place (fits = 0)
 constexpr int DR_COLS = 8;   // key, f1, ts, sum, min, max, count, window start
 __global__ __launch_bounds__(BLOCK) void k_drain(OutLog L, const int32_t* err, int64_t rows, int64_t* stage, int64_t* marks,
-                                                 int64_t* hdr) {
-  const int64_t n = (int64_t)*L.count, nm = (int64_t)*L.mark_count;
+                                                 int64_t* hdr, unsigned int* done) {
+  __shared__ int64_t cnt_s[2];
+  if (threadIdx.x == 0) { cnt_s[0] = (int64_t)*L.count; cnt_s[1] = (int64_t)*L.mark_count; }
+  __syncthreads();
+  const int64_t n = cnt_s[0], nm = cnt_s[1];
   const bool fits = n <= rows && n <= L.capacity && nm <= L.mark_capacity;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     hdr[0] = n;
     hdr[1] = nm;
     hdr[2] = fits ? 1 : 0;
     hdr[3] = *err;
+  }
+  // the log restarts once every block has read the counts: the last block to arrive resets them
+  if (threadIdx.x == 0 && atomicAdd(done, 1u) == gridDim.x - 1) {
+    *done = 0u;
+    if (fits) { *L.count = 0; *L.mark_count = 0; }
   }
   if (!fits) return;
   const int64_t* src[DR_COLS] = {L.key, L.f1, L.ts, L.sum, L.mn, L.mx, L.cnt, L.win_start};
@@ -2380,14 +2388,6 @@ __global__ __launch_bounds__(BLOCK) void k_drain(OutLog L, const int32_t* err, i
   }
   if (blockIdx.x == 0)
     for (int64_t i = threadIdx.x; i < nm; i += blockDim.x) marks[i] = L.mark_pos[i];
-}
-// ... then the log restarts (a separate launch: every k_drain block has read the counts)
-__global__ void k_drain_reset(OutLog L, int64_t rows) {
-  const unsigned long long n = *L.count, nm = *L.mark_count;
-  if ((int64_t)n <= rows && (int64_t)n <= L.capacity && (int64_t)nm <= L.mark_capacity) {
-    *L.count = 0;
-    *L.mark_count = 0;
-  }
 }
 // step 2 on the drain stream (beside the next batch's kernels): the staged rows, marks and header into the pinned
 // host buffer (zero-copy stores over PCIe), only the columns present and only the rows staged
@@ -2822,6 +2822,7 @@ struct fw_engine {
     hipEvent_t done = nullptr;
     bool pending = false;           // begun, not yet ended
     int32_t ticket = -1;            // the ticket fw_collect_begin handed out for it
+    bool host_ready = false;        // the device arrival counter initialised
     std::vector<HostMark> marks;    // the host marks of the drain
     int64_t dev_marks = 0;
     std::vector<int64_t> mark_wm, mark_pos;
@@ -3800,7 +3801,7 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
   if (d.pending) { e->err = "fw_collect_begin: three drains outstanding (fw_collect_end the oldest first)"; return FW_ERR_INVALID_ARG; }
   const OutLog& L = e->s.o;
   const size_t words = (size_t)DR_COLS * (size_t)std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX) +
-                       (size_t)L.mark_capacity + 4;
+                       (size_t)L.mark_capacity + 8;   // + hdr[4], the blocks' arrival counter
   if (!d.host) {
     e->drain_rows = std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX);
     if (hipHostMalloc((void**)&d.host, 8 * words, hipHostMallocMapped) != hipSuccess) {
@@ -3816,9 +3817,12 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
   int64_t* marks = d.dev + (size_t)DR_COLS * (size_t)e->drain_rows;
   int64_t* hdr = marks + L.mark_capacity;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->drain_rows + BLOCK - 1) / BLOCK, 512));
+  if (!d.host_ready) {   // the arrival counter starts at zero (k_drain returns it there)
+    HIPCHK(e, hipMemsetAsync(hdr + 4, 0, 8, e->stream));
+    d.host_ready = true;
+  }
   hipLaunchKernelGGL(k_drain, dim3(blocks), dim3(BLOCK), 0, e->stream, L, (const int32_t*)e->s.err, e->drain_rows, d.dev,
-                     marks, hdr);
-  hipLaunchKernelGGL(k_drain_reset, dim3(1), dim3(1), 0, e->stream, L, e->drain_rows);
+                     marks, hdr, (unsigned int*)(hdr + 4));
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(d.staged, e->stream));
   // to the host on the drain stream, beside whatever the engine stream runs next

@@ -368,15 +368,17 @@ class WindowEngine:
         self._drain_keep[t.value] = len(self._inflight)   # inputs pushed before the drain: read once it lands
         return t.value
 
-    def collect_end(self, ticket):
-        """The drain `ticket` (collect_begin) once it has landed: the same dict as collect()."""
+    def collect_end(self, ticket, copy=True):
+        """The drain `ticket` (collect_begin) once it has landed: the same dict as collect().  copy=False returns
+        views of the pinned host columns instead (no copy; valid until the next collect_begin, as the C-ABI
+        says), the way a JNI operator reads them."""
         o = _abi.FwOut()
         self._check(self._fn("collect_end")(self.h, ticket, ctypes.byref(o)))
         done = self._drain_keep.pop(ticket, 0)
         del self._inflight[:done]
         for t in self._drain_keep:
             self._drain_keep[t] = max(0, self._drain_keep[t] - done)
-        return self._out_dict(o)
+        return self._out_dict(o, copy)
 
     def collect(self):
         """Results since the last collect: dict of numpy columns + (mark_wm, mark_pos)."""
@@ -389,17 +391,18 @@ class WindowEngine:
             self._check(self._fn("collect")(self.h, ctypes.byref(o)))
         return self._out_dict(o)
 
-    def _out_dict(self, o):
+    def _out_dict(self, o, copy=True):
         n = o.n
         res = {"n": n}
+        cp = (lambda a: a.copy()) if copy else (lambda a: a)
         for name in ("key", "f1", "ts", "sum_i64", "min_i64", "max_i64", "count", "sum_f64", "min_f64", "max_f64"):
             p = getattr(o, name)
             if n == 0:
                 res[name] = np.zeros(0, np.float64 if name.endswith("f64") else np.int64)
             else:
-                res[name] = np.ctypeslib.as_array(p, shape=(n,)).copy() if p else None
+                res[name] = cp(np.ctypeslib.as_array(p, shape=(n,))) if p else None
         nm = o.n_marks
-        res["win_start"] = (np.ctypeslib.as_array(o.win_start, shape=(n,)).copy() if o.win_start
+        res["win_start"] = (cp(np.ctypeslib.as_array(o.win_start, shape=(n,))) if o.win_start
                             else (np.zeros(0, np.int64) if n == 0 else None))
         res["mark_wm"] = np.ctypeslib.as_array(o.mark_wm, shape=(nm,)).copy() if nm > 0 else np.zeros(0, np.int64)
         res["mark_pos"] = np.ctypeslib.as_array(o.mark_pos, shape=(nm,)).copy() if nm > 0 else np.zeros(0, np.int64)
@@ -445,14 +448,16 @@ class WindowEngine:
         self._check(self._fn("restore_kg_flink")(self.h, kg, ctypes.byref(L), watermark, sb, len(state), tb,
                                                  len(timers)))
 
-    def decode(self, data, fields, key=0, value=None, f1=None, record_cap=None, marker_cap=1 << 16, device=False):
+    def decode(self, data, fields, key=0, value=None, f1=None, record_cap=None, marker_cap=1 << 16, device=False,
+               buffers=None):
         """Decode Flink network-buffer bytes (fw_decode: length-prefixed StreamElementSerializer elements over a
         TupleSerializer tuple) into record columns, watermarks and latency markers in stream order.
 
         data: bytes / numpy uint8 (host) or a torch uint8 tensor on the GPU; fields: the tuple's field types
         ("long", "double", "int"); key / value / f1: field indices (f1 None: the record timestamp).  Returns a
         dict of numpy arrays (device=True: torch tensors on the engine's GPU, ready for push) and the counts;
-        "consumed" < len(data) when the bytes end inside an element."""
+        "consumed" < len(data) when the bytes end inside an element.  buffers: a previous result's "buffers" (the same
+        capacities) to decode into again instead of allocating the output columns."""
         types = {"long": _abi.FW_FT_LONG, "double": _abi.FW_FT_DOUBLE, "int": _abi.FW_FT_INT}
         sc = _abi.FwTupleSchema()
         sc.n_fields = len(fields)
@@ -476,9 +481,14 @@ class WindowEngine:
             mk = lambda n, dt=np.int64: np.empty(max(n, 1), dtype=np.int32 if dt is not np.int64 else np.int64)
             ptr = lambda t: ctypes.c_void_p(t.ctypes.data)
         i32 = torch.int32 if on_gpu else np.int32
-        cols = dict(key=mk(cap), f1=mk(cap), ts=mk(cap), value=mk(cap), wm=mk(marker_cap), wm_pos=mk(marker_cap),
-                    lm=mk(2 * marker_cap), lm_pos=mk(marker_cap))
-        cols["key_hash"] = mk(cap, i32) if int_key else None
+        if buffers is not None:
+            cols = buffers
+            if cols["key"].shape[0] < cap or cols["wm"].shape[0] < marker_cap or (int_key and cols["key_hash"] is None):
+                raise ValueError("decode buffers smaller than the capacities asked for")
+        else:
+            cols = dict(key=mk(cap), f1=mk(cap), ts=mk(cap), value=mk(cap), wm=mk(marker_cap), wm_pos=mk(marker_cap),
+                        lm=mk(2 * marker_cap), lm_pos=mk(marker_cap))
+            cols["key_hash"] = mk(cap, i32) if int_key else None
         cnt = _abi.FwDecodeCounts()
         src = ctypes.c_void_p(data.data_ptr()) if dev_in else ctypes.c_void_p(data.ctypes.data)
         self._check(self._fn("decode")(self.h, ctypes.byref(sc), src, nbytes,
@@ -488,7 +498,7 @@ class WindowEngine:
                                        ptr(cols["wm_pos"]), ptr(cols["lm"]), ptr(cols["lm_pos"]), marker_cap,
                                        ctypes.byref(cnt)))
         n, nw, nl = cnt.n_records, cnt.n_watermarks, cnt.n_latency_markers
-        out = {"n_records": n, "n_watermarks": nw, "n_latency_markers": nl, "consumed": cnt.consumed}
+        out = {"n_records": n, "n_watermarks": nw, "n_latency_markers": nl, "consumed": cnt.consumed, "buffers": cols}
         for k in ("key", "key_hash", "f1", "ts", "value"):
             out[k] = None if cols[k] is None else cols[k][:n]
         out["wm"], out["wm_pos"] = cols["wm"][:nw], cols["wm_pos"][:nw]
@@ -496,7 +506,7 @@ class WindowEngine:
         if fields[sc.value_field] == "double":
             out["value"] = out["value"].view(torch.float64 if on_gpu else np.float64)
         if on_gpu and not device:
-            out = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in out.items()}
+            out = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in out.items() if k != "buffers"}
         return out
 
     def stats(self):
