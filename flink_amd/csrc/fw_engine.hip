@@ -2359,9 +2359,10 @@ __global__ __launch_bounds__(1024) void k_quirk_apply(Spec s, int64_t* list, uns
 // asynchronous drain (fw_collect_begin), step 1 on the engine stream: the output log's rows and device marks since
 // the last collect copied into device staging (column-major, `rows` per column; HBM to HBM), with hdr[0..3] = rows,
 // device marks, fits, the engine's error word.  A log larger than the staging is left in place (fits = 0)
-constexpr int DR_COLS = 8;   // key, f1, ts, sum, min, max, count, window start
+constexpr int DR_COLS = 8;   // key, f1, ts, sum, min, max, count, window start (those the log has, packed in this order)
+__host__ __device__ __forceinline__ int dr_slot(uint32_t colmask, int c) { return __builtin_popcount(colmask & ((1u << c) - 1u)); }
 __global__ __launch_bounds__(BLOCK) void k_drain(OutLog L, const int32_t* err, int64_t rows, int64_t* stage, int64_t* marks,
-                                                 int64_t* hdr, unsigned int* done) {
+                                                 int64_t* hdr, unsigned int* done, uint32_t colmask) {
   __shared__ int64_t cnt_s[2];
   if (threadIdx.x == 0) { cnt_s[0] = (int64_t)*L.count; cnt_s[1] = (int64_t)*L.mark_count; }
   __syncthreads();
@@ -2384,7 +2385,7 @@ __global__ __launch_bounds__(BLOCK) void k_drain(OutLog L, const int32_t* err, i
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
 #pragma unroll
     for (int c = 0; c < DR_COLS; ++c)
-      if (src[c]) stage[(int64_t)c * rows + i] = src[c][i];
+      if (src[c]) stage[(int64_t)dr_slot(colmask, c) * rows + i] = src[c][i];
   }
   if (blockIdx.x == 0)
     for (int64_t i = threadIdx.x; i < nm; i += blockDim.x) marks[i] = L.mark_pos[i];
@@ -2398,9 +2399,12 @@ __global__ __launch_bounds__(BLOCK) void k_drain_host(const int64_t* stage, cons
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
 #pragma unroll
     for (int c = 0; c < DR_COLS; ++c)
-      if ((colmask >> c) & 1u) host[(int64_t)c * rows + i] = stage[(int64_t)c * rows + i];
+      if ((colmask >> c) & 1u) {
+        const int64_t o = (int64_t)dr_slot(colmask, c) * rows + i;
+        host[o] = stage[o];
+      }
   }
-  int64_t* hmarks = host + (size_t)DR_COLS * rows;
+  int64_t* hmarks = host + (size_t)__builtin_popcount(colmask) * rows;
   if (blockIdx.x == 0) {
     for (int64_t i = threadIdx.x; i < nm; i += blockDim.x) hmarks[i] = dmarks[i];
     if (threadIdx.x < 4) hmarks[mark_cap + threadIdx.x] = dhdr[threadIdx.x];
@@ -2802,6 +2806,7 @@ struct fw_engine {
   // fw_collect(FW_MEM_HOST): pinned staging of the result columns (DMA copies, one wait), grown on demand up
   // to COLLECT_PIN_MAX rows (larger drains use pageable vectors); two pinned words for the counts
   static constexpr int64_t COLLECT_PIN_MAX = 1 << 22;
+  static constexpr int64_t DRAIN_ROWS_MAX = 1 << 25;   // results one asynchronous drain holds at most
   int64_t* h_pin = nullptr;
   int64_t h_pin_rows = 0;
   unsigned long long* h_pin_cnt = nullptr;
@@ -2815,7 +2820,7 @@ struct fw_engine {
   std::vector<double> h_sum_d, h_mn_d, h_mx_d;
   // asynchronous drains (fw_collect_begin / fw_collect_end): NDRAIN pinned host staging buffers, in turn
   struct Drain {
-    int64_t* host = nullptr;        // [DR_COLS][rows] columns, then [mark_capacity] device mark positions, then hdr[4]
+    int64_t* host = nullptr;        // [log columns][rows], then [mark_capacity] device mark positions, then hdr[4]
     int64_t* dptr = nullptr;        // the same memory as the device sees it
     int64_t* dev = nullptr;         // device staging of the same layout (k_drain's copy)
     hipEvent_t staged = nullptr;    // the engine stream's copy done (the drain stream waits for it)
@@ -3792,6 +3797,11 @@ int fw_collect(fw_engine* e, fw_out* o, int32_t mem) {
   return FW_OK;
 }
 
+static uint32_t drain_colmask(const OutLog& L) {
+  return (L.key ? 1u : 0u) | (L.f1 ? 2u : 0u) | (L.ts ? 4u : 0u) | (L.sum ? 8u : 0u) | (L.mn ? 16u : 0u) | (L.mx ? 32u : 0u) |
+         (L.cnt ? 64u : 0u) | (L.win_start ? 128u : 0u);
+}
+
 int fw_collect_begin(fw_engine* e, int32_t* ticket) {
   if (!e || !ticket) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
@@ -3800,10 +3810,12 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
   fw_engine::Drain& d = e->drains[b];
   if (d.pending) { e->err = "fw_collect_begin: three drains outstanding (fw_collect_end the oldest first)"; return FW_ERR_INVALID_ARG; }
   const OutLog& L = e->s.o;
-  const size_t words = (size_t)DR_COLS * (size_t)std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX) +
+  const uint32_t colmask = drain_colmask(L);
+  const int ncols = __builtin_popcount(colmask);
+  const size_t words = (size_t)ncols * (size_t)std::min<int64_t>(L.capacity, fw_engine::DRAIN_ROWS_MAX) +
                        (size_t)L.mark_capacity + 8;   // + hdr[4], the blocks' arrival counter
   if (!d.host) {
-    e->drain_rows = std::min<int64_t>(L.capacity, fw_engine::COLLECT_PIN_MAX);
+    e->drain_rows = std::min<int64_t>(L.capacity, fw_engine::DRAIN_ROWS_MAX);
     if (hipHostMalloc((void**)&d.host, 8 * words, hipHostMallocMapped) != hipSuccess) {
       d.host = nullptr;
       return fail(e, FW_ERR_DEVICE, "fw_collect_begin: pinned staging allocation failed");
@@ -3814,7 +3826,7 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
     HIPCHK(e, hipEventCreateWithFlags(&d.staged, hipEventDisableTiming));
     if (!e->dstream) HIPCHK(e, hipStreamCreateWithFlags(&e->dstream, hipStreamNonBlocking));
   }
-  int64_t* marks = d.dev + (size_t)DR_COLS * (size_t)e->drain_rows;
+  int64_t* marks = d.dev + (size_t)ncols * (size_t)e->drain_rows;
   int64_t* hdr = marks + L.mark_capacity;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->drain_rows + BLOCK - 1) / BLOCK, 512));
   if (!d.host_ready) {   // the arrival counter starts at zero (k_drain returns it there)
@@ -3822,13 +3834,11 @@ int fw_collect_begin(fw_engine* e, int32_t* ticket) {
     d.host_ready = true;
   }
   hipLaunchKernelGGL(k_drain, dim3(blocks), dim3(BLOCK), 0, e->stream, L, (const int32_t*)e->s.err, e->drain_rows, d.dev,
-                     marks, hdr, (unsigned int*)(hdr + 4));
+                     marks, hdr, (unsigned int*)(hdr + 4), colmask);
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(d.staged, e->stream));
   // to the host on the drain stream, beside whatever the engine stream runs next
   HIPCHK(e, hipStreamWaitEvent(e->dstream, d.staged, 0));
-  const uint32_t colmask = (L.key ? 1u : 0u) | (L.f1 ? 2u : 0u) | (L.ts ? 4u : 0u) | (L.sum ? 8u : 0u) | (L.mn ? 16u : 0u) |
-                           (L.mx ? 32u : 0u) | (L.cnt ? 64u : 0u) | (L.win_start ? 128u : 0u);
   hipLaunchKernelGGL(k_drain_host, dim3(64), dim3(BLOCK), 0, e->dstream, d.dev, marks, hdr, e->drain_rows, L.mark_capacity,
                      colmask, d.dptr);
   HIPCHK(e, hipGetLastError());
@@ -3860,7 +3870,8 @@ int fw_collect_end(fw_engine* e, int32_t ticket, fw_out* o) {
   HIPCHK(e, hipEventSynchronize(d.done));
   d.pending = false;
   const OutLog& L = e->s.o;
-  const int64_t* marks = d.host + (size_t)DR_COLS * (size_t)e->drain_rows;
+  const uint32_t colmask = drain_colmask(L);
+  const int64_t* marks = d.host + (size_t)__builtin_popcount(colmask) * (size_t)e->drain_rows;
   const int64_t* hdr = marks + L.mark_capacity;
   if (int rc = device_error(e, (int32_t)hdr[3])) return rc;
   if (!hdr[2]) return fail(e, FW_ERR_CAPACITY, "fw_collect_end: more results than an asynchronous drain holds (collect more often)");
@@ -3875,7 +3886,9 @@ int fw_collect_end(fw_engine* e, int32_t ticket, fw_out* o) {
   std::memset(o, 0, sizeof(*o));
   o->n = n;
   o->n_marks = nm;
-  auto col = [&](int c, const void* present) -> const int64_t* { return present ? d.host + (size_t)c * (size_t)e->drain_rows : nullptr; };
+  auto col = [&](int c, const void* present) -> const int64_t* {
+    return present ? d.host + (size_t)dr_slot(colmask, c) * (size_t)e->drain_rows : nullptr;
+  };
   o->key = col(0, L.key);
   o->f1 = col(1, L.f1);
   o->ts = col(2, L.ts);

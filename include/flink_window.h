@@ -205,7 +205,7 @@ int         fw_collect(fw_engine* e, fw_out* out, int32_t mem);
  * the engine stream a copy of every result and watermark mark since the last collect into pinned host staging (three
  * buffers, in turn) and restarts the log; it returns at once with a ticket.  fw_collect_end(ticket) waits for
  * that copy and fills `out` (FW_MEM_HOST layout) with columns valid until the next fw_collect_begin after it.  At
- * most three drains are outstanding; one holds at most min(out_capacity, 2^22) results (more: FW_ERR_CAPACITY at
+ * most three drains are outstanding; one holds at most min(out_capacity, 2^25) results (more: FW_ERR_CAPACITY at
  * fw_collect_end).  Device errors surface at fw_collect_end. */
 int         fw_collect_begin(fw_engine* e, int32_t* ticket);
 int         fw_collect_end(fw_engine* e, int32_t ticket, fw_out* out);
