@@ -4501,9 +4501,6 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   const fw_config& c = e->cfg;
   const fw::Spec& s = e->s;
   const bool sliding = c.assigner == FW_SLIDING;
-  if (sliding && c.allowed_lateness > 0)
-    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows with allowed lateness: window-level state restores into "
-                                         "tumbling windows, or sliding without lateness");
   if (e->restored && watermark != e->cur_wm)
     return reject(e, FW_ERR_INVALID_ARG, "key groups restored at different watermarks");
   const bool f64 = s.vt == FW_VALUE_F64;
@@ -4587,6 +4584,9 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   for (int64_t m : dis_now)
     if (armed_now.count(m) || e->armed_windows.count(m) || c.allowed_lateness == 0)
       return reject(e, FW_ERR_UNSUPPORTED, "a window with and without trigger timers (not an aligned checkpoint)");
+  if (sliding && !dis_now.empty())   // (disarmed windows are slice slots: tumbling only)
+    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows that fired before the checkpoint, restored below their "
+                                         "maxTimestamp (restore at the checkpoint's watermark)");
   for (int64_t m : armed_now)
     if (e->disarmed.count(m)) return reject(e, FW_ERR_UNSUPPORTED, "a window with and without trigger timers (not an aligned checkpoint)");
   for (size_t i = 0; i < panes.size(); ++i) {

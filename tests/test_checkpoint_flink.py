@@ -385,7 +385,7 @@ def test_restore_rejections():
         e.restore_kg_flink((kg + 1) % 8, sc["layout"], *want[(kg + 1) % 8], sc["checkpoint_wm"] + 1)
     e.close()
     sl = dict(SCEN["sliding_i64"])
-    sl["config"] = dict(sl["config"], lateness=100)   # sliding + allowed lateness: no window-level restore
+    sl["config"] = dict(sl["config"], lateness=100)   # timers of a lateness-0 checkpoint: rejected
     e = WindowEngine(_cfg(sl))
     with pytest.raises(_abi.FwError) as ei:
         e.restore_kg_flink(0, sl["layout"], *_expected(sl)[0])
@@ -476,3 +476,50 @@ def test_purging_lateness_checkpoint(mode, restore_at):
     blobs, outs = _purging_lateness_run(WindowEngine, mode, restore_at)
     assert _diff(blobs["g"], blobs["o"]) is None, _diff(blobs["g"], blobs["o"])
     assert outs["g"] == outs["o"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_sliding_lateness_checkpoint(mode):
+    """SlidingEventTimeWindows.of(3 s, 1 s) with allowed lateness 1.5 s, checkpointed while fired windows are kept
+    for their lateness: the engine's sections equal the oracle's, restore (at the checkpoint's watermark) writes them
+    back — each window's state in its own window pane — and the restored engine's per-element fires and watermark
+    fires continue as the restored oracle's.  Restored at Long.MIN_VALUE, a window that fired before the checkpoint
+    would need a disarmed window pane: rejected."""
+    from flink_amd import _abi
+    from flink_amd.windowing import ReduceFunction, SlidingEventTimeWindows, WindowEngine, make_config
+    from harness import drive, gen_stream
+    from oracle.oracle import OracleEngine
+    keys, ts, vals = gen_stream(48_000, 1500, rate=1 << 13, zipf=1.1, ooo=400)
+    f1 = np.arange(len(keys), dtype=np.int64) * 5 + 2
+    cfg = make_config(SlidingEventTimeWindows.of(3000, 1000), ReduceFunction(("sum", "count"), "i64", True), None, 1500,
+                      max_parallelism=128, key_capacity=1 << 13, max_batch=1 << 13, out_capacity=1 << 20, ingest_mode=mode)
+    layout = ("key", "f1", "sum", "count")
+    n = int(3.25 * (1 << 13)) + 29
+    wm_cut = int(ts[:n].max()) - 120
+    blobs = {}
+    for name, factory in (("g", WindowEngine), ("o", OracleEngine)):
+        e = factory(cfg)
+        drive(e, keys[:n], ts[:n], vals[:n], 2048, 120, None, f1=f1[:n])
+        blobs[name] = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        e.close()
+    assert _diff(blobs["g"], blobs["o"]) is None, _diff(blobs["g"], blobs["o"])
+    outs = {}
+    for name, factory in (("g", WindowEngine), ("o", OracleEngine)):
+        e = factory(cfg)
+        for kg, (st, tm) in blobs["o"].items():
+            e.restore_kg_flink(kg, layout, st, tm, wm_cut)
+        back = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        assert _diff(back, blobs["o"]) is None, _diff(back, blobs["o"])
+        outs[name] = _canon(epochs_of(drive(e, keys[n:], ts[n:], vals[n:], 2048, 120, LONG_MAX, f1=f1[n:]),
+                                      ["sum_i64", "count"], True))
+        e.close()
+    assert outs["g"] == outs["o"]
+    late = [r for w, recs in outs["o"] if w != "tail" for r in recs if r[1] < wm_cut]
+    assert late, "windows kept for their lateness fired again after the restore"
+    e = WindowEngine(cfg)
+    kg = max(blobs["o"], key=lambda k: len(blobs["o"][k][1]))
+    with pytest.raises(_abi.FwError) as ei:
+        e.restore_kg_flink(kg, layout, *blobs["o"][kg], LONG_MIN)
+    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+    e.close()
