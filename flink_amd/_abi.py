@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sy
                     "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
                     "fw_get_profile", "fw_debug_counters", "fw_debug_stamps", "fw_set_stream", "fw_stream_wait_input",
                     "fw_version", "fw_snapshot_kg", "fw_restore_kg", "fw_snapshot_kg_flink", "fw_restore_kg_flink", "fw_decode",
-                    "fw_collect_begin", "fw_collect_end")
+                    "fw_collect_begin", "fw_collect_end", "fw_decode_begin", "fw_decode_end")
 FW_SNAP_MAGIC, FW_SNAP_HEADER_WORDS, FW_SNAP_ENTRY_WORDS = 0x31474b5746574b, 14, 8
 # state tuple fields of the Flink-layout checkpoint (fw_state_layout)
 FW_SF_KEY, FW_SF_F1, FW_SF_SUM, FW_SF_MIN, FW_SF_MAX, FW_SF_COUNT, FW_SF_VALUE, FW_SF_MAX_FIELDS = 1, 2, 3, 4, 5, 6, 7, 8
@@ -120,6 +120,9 @@ def declare(lib, prefix="fw"):
         "restore_kg_flink": (_i32, [_p, _i32, P(FwStateLayout), _i64, _p, _i64, _p, _i64]),
         "decode": (_i32, [_p, P(FwTupleSchema), _p, _i64, _i32, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64,
                           P(FwDecodeCounts)]),
+        "decode_begin": (_i32, [_p, P(FwTupleSchema), _p, _i64, _i32, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64,
+                                P(_i32)]),
+        "decode_end": (_i32, [_p, _i32, P(FwDecodeCounts)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}", None)

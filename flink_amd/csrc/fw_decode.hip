@@ -87,10 +87,22 @@ struct DecChunk {
 };
 // the workgroup's DEC_T chunks into LDS, each at DEC_STRIDE with its own copy of the DEC_SPILL bytes after it
 // (the next chunk's first ones), then this lane's chunk.  Global loads of 16 B, LDS stores of 4 B
-__device__ __forceinline__ void dec_put4(uint8_t* buf, int q, uint32_t w) {   // the word at group offset q
-  const int i = q / DEC_CHUNK, o = q % DEC_CHUNK;
-  if (i < DEC_T) *(uint32_t*)(buf + i * DEC_STRIDE + o) = w;
-  if (i > 0 && o < DEC_SPILL) *(uint32_t*)(buf + (i - 1) * DEC_STRIDE + DEC_CHUNK + o) = w;
+// the 16 bytes at group offset q (a multiple of 16: they lie in one chunk), and again after the previous chunk
+// when they are among the first DEC_SPILL bytes of theirs; one address per copy, four word stores
+__device__ __forceinline__ void dec_put16(uint8_t* buf, int q, const uint4& v) {
+  const int i = q >> 9, o = q & (DEC_CHUNK - 1);
+  static_assert(DEC_CHUNK == 512 && DEC_SPILL % 4 == 0, "chunk layout");
+  if (i < DEC_T) {
+    uint32_t* d = (uint32_t*)(buf + i * DEC_STRIDE + o);
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  if (i > 0 && o < DEC_SPILL) {   // (the spill copy ends at DEC_SPILL: the next chunk's copy follows it)
+    uint32_t* d = (uint32_t*)(buf + (i - 1) * DEC_STRIDE + DEC_CHUNK + o);
+    d[0] = v.x;
+    if (o + 4 < DEC_SPILL) d[1] = v.y;
+    if (o + 8 < DEC_SPILL) d[2] = v.z;
+    if (o + 12 < DEC_SPILL) d[3] = v.w;
+  }
 }
 __device__ __forceinline__ void dec_put1(uint8_t* buf, int q, uint8_t b) {
   const int i = q / DEC_CHUNK, o = q % DEC_CHUNK;
@@ -112,7 +124,7 @@ __device__ __forceinline__ DecChunk dec_stage_group(const DecSpec& d, uint8_t* b
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int i = i0 + u * DEC_TW + (int)threadIdx.x;
-        if (i < nv) { dec_put4(buf, 16 * i, v[u].x); dec_put4(buf, 16 * i + 4, v[u].y); dec_put4(buf, 16 * i + 8, v[u].z); dec_put4(buf, 16 * i + 12, v[u].w); }
+        if (i < nv) dec_put16(buf, 16 * i, v[u]);
       }
     }
     done = nv << 4;
@@ -446,13 +458,17 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_emit(DecSpec d, const int32_t* e
 
 }  // namespace fw
 
-int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_t nbytes, int32_t mem, int64_t* key,
-              int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap, int64_t* wm,
-              int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap, fw_decode_counts* out) {
+// enqueue one decode on the engine stream into scratch slot `slot`; its counts land in the slot's pinned words
+// (event `done`).  *empty: nothing was enqueued (no bytes)
+static int decode_enqueue(fw_engine* e, int slot, const fw_tuple_schema* sc, const void* bytes, int64_t nbytes,
+                          int32_t mem, int64_t* key, int32_t* key_hash, int64_t* f1, int64_t* ts, void* value,
+                          int64_t record_cap, int64_t* wm, int64_t* wm_pos, int64_t* lm, int64_t* lm_pos,
+                          int64_t marker_cap, bool* empty) {
   using namespace fw;
-  if (!e || !sc || !out || (nbytes > 0 && !bytes) || nbytes < 0) return FW_ERR_INVALID_ARG;
+  *empty = true;
+  if (!e || !sc || (nbytes > 0 && !bytes) || nbytes < 0) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
-  std::memset(out, 0, sizeof(*out));
+  fw_engine::DecSlot& ds = e->dec[slot];
   if (sc->n_fields < 1 || sc->n_fields > FW_DECODE_MAX_FIELDS || sc->key_field < 0 || sc->key_field >= sc->n_fields ||
       sc->value_field < 0 || sc->value_field >= sc->n_fields || sc->f1_field < -1 || sc->f1_field >= sc->n_fields)
     return reject(e, FW_ERR_INVALID_ARG, "bad tuple schema");
@@ -485,6 +501,13 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   d.nchunks = (nbytes + DEC_CHUNK - 1) / DEC_CHUNK;
   if (nbytes == 0) return FW_OK;
   HIPCHK(e, hipSetDevice(e->dev));
+  if (!ds.pin) {
+    if (hipHostMalloc((void**)&ds.pin, 64, hipHostMallocDefault) != hipSuccess) {
+      ds.pin = nullptr;
+      return reject(e, FW_ERR_DEVICE, "decode: pinned count words");
+    }
+    HIPCHK(e, hipEventCreateWithFlags(&ds.done, hipEventDisableTiming));
+  }
   // grow-only scratch
   auto grow = [&](void*& p, size_t& cap, size_t need) -> hipError_t {
     if (cap >= need) return hipSuccess;
@@ -497,15 +520,15 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   };
   const size_t nc = (size_t)d.nchunks;
   const size_t nblk = (nc + DEC_SCAN - 1) / DEC_SCAN;
-  HIPCHK(e, grow(e->dec_small, e->dec_small_cap, nc * (4 * DEC_W + 4 + 24 + 4 + 4 * DEC_W + 8 * DEC_S) + nblk * 24 + 256));
+  HIPCHK(e, grow(ds.small, ds.small_cap, nc * (4 * DEC_W + 4 + 24 + 4 + 4 * DEC_W + 8 * DEC_S) + nblk * 24 + 256));
   const uint8_t* src = (const uint8_t*)bytes;
   if (mem == FW_MEM_HOST) {
-    HIPCHK(e, grow(e->dec_bytes, e->dec_bytes_cap, (size_t)nbytes));
-    HIPCHK(e, hipMemcpyAsync(e->dec_bytes, bytes, (size_t)nbytes, hipMemcpyHostToDevice, e->stream));
-    src = (const uint8_t*)e->dec_bytes;
+    HIPCHK(e, grow(ds.bytes, ds.bytes_cap, (size_t)nbytes));
+    HIPCHK(e, hipMemcpyAsync(ds.bytes, bytes, (size_t)nbytes, hipMemcpyHostToDevice, e->stream));
+    src = (const uint8_t*)ds.bytes;
   }
   d.bytes = src;
-  uint8_t* sm = (uint8_t*)e->dec_small;
+  uint8_t* sm = (uint8_t*)ds.small;
   int32_t* conv = (int32_t*)sm;   // [nc][DEC_W] each wave's agreeing exit
   int32_t* entry = conv + nc * DEC_W;
   int64_t* base = (int64_t*)(((uintptr_t)(entry + nc) + 7) & ~(uintptr_t)7);
@@ -524,16 +547,72 @@ int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_
   DecOut o{key, f1, ts, (int64_t*)value, wm, wm_pos, lm, lm_pos, key_hash, record_cap, marker_cap};
   hipLaunchKernelGGL(k_dec_emit, dim3(gb), dim3(DEC_TW), 0, e->stream, d, entry, base, btot, o, err);
   HIPCHK(e, hipGetLastError());
-  int64_t tot[5];   // the totals and the error word, one read-back
-  HIPCHK(e, hipMemcpyAsync(tot, totals, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
+  // the totals and the error word, to pinned host memory behind the kernels
+  HIPCHK(e, hipMemcpyAsync(ds.pin, totals, 40, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipEventRecord(ds.done, e->stream));
+  ds.record_cap = record_cap;
+  ds.marker_cap = marker_cap;
+  *empty = false;
+  return FW_OK;
+}
+
+// wait for slot `slot`'s decode and report its counts
+static int decode_finish(fw_engine* e, int slot, fw_decode_counts* out) {
+  fw_engine::DecSlot& ds = e->dec[slot];
+  HIPCHK(e, hipSetDevice(e->dev));
+  HIPCHK(e, hipEventSynchronize(ds.done));
+  const int64_t* tot = ds.pin;
   const int32_t herr = (int32_t)(tot[4] & 0xffffffff);
   if (herr == 1) return reject(e, FW_ERR_INVALID_ARG, "corrupt stream: no element chain through the bytes");
   out->n_records = tot[0];
   out->n_watermarks = tot[1];
   out->n_latency_markers = tot[2];
   out->consumed = tot[3];
-  if (herr == 2 || tot[0] > record_cap || tot[1] > marker_cap || tot[2] > marker_cap)
+  if (herr == 2 || tot[0] > ds.record_cap || tot[1] > ds.marker_cap || tot[2] > ds.marker_cap)
     return reject(e, FW_ERR_CAPACITY, "decode output capacity exceeded");
   return FW_OK;
+}
+
+int fw_decode(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_t nbytes, int32_t mem, int64_t* key,
+              int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap, int64_t* wm,
+              int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap, fw_decode_counts* out) {
+  if (!e || !out) return FW_ERR_INVALID_ARG;
+  std::memset(out, 0, sizeof(*out));
+  int slot = -1;
+  for (int i = 0; i < fw_engine::NDEC && slot < 0; ++i) if (!e->dec[i].pending) slot = i;
+  if (slot < 0) { e->err = "fw_decode: every decode slot has a decode outstanding (fw_decode_end first)"; return FW_ERR_INVALID_ARG; }
+  bool empty = true;
+  int rc = decode_enqueue(e, slot, sc, bytes, nbytes, mem, key, key_hash, f1, ts, value, record_cap, wm, wm_pos, lm, lm_pos,
+                          marker_cap, &empty);
+  if (rc || empty) return rc;
+  return decode_finish(e, slot, out);
+}
+
+int fw_decode_begin(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, int64_t nbytes, int32_t mem, int64_t* key,
+                    int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap, int64_t* wm,
+                    int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap, int32_t* ticket) {
+  if (!e || !ticket) return FW_ERR_INVALID_ARG;
+  const int slot = (int)(e->dec_seq % fw_engine::NDEC);
+  fw_engine::DecSlot& ds = e->dec[slot];
+  if (ds.pending) { e->err = "fw_decode_begin: two decodes outstanding (fw_decode_end the older first)"; return FW_ERR_INVALID_ARG; }
+  bool empty = true;
+  int rc = decode_enqueue(e, slot, sc, bytes, nbytes, mem, key, key_hash, f1, ts, value, record_cap, wm, wm_pos, lm, lm_pos,
+                          marker_cap, &empty);
+  if (rc) return rc;
+  ds.pending = true;
+  ds.empty = empty;
+  ds.ticket = (int32_t)(e->dec_seq++ & 0x7FFFFFFF);
+  *ticket = ds.ticket;
+  return FW_OK;
+}
+
+int fw_decode_end(fw_engine* e, int32_t ticket, fw_decode_counts* out) {
+  if (!e || !out || ticket < 0) return FW_ERR_INVALID_ARG;
+  std::memset(out, 0, sizeof(*out));
+  int slot = -1;
+  for (int i = 0; i < fw_engine::NDEC; ++i) if (e->dec[i].pending && e->dec[i].ticket == ticket) slot = i;
+  if (slot < 0) { e->err = "fw_decode_end: no such decode outstanding"; return FW_ERR_INVALID_ARG; }
+  e->dec[slot].pending = false;
+  if (e->dec[slot].empty) return FW_OK;
+  return decode_finish(e, slot, out);
 }

@@ -2765,8 +2765,19 @@ struct fw_engine {
   double compact_fill = 0.5;                // FW_COMPACT_FILL
   int64_t compactions = 0;
   // fw_decode scratch (grow-only)
-  void *dec_small = nullptr, *dec_bytes = nullptr;
-  size_t dec_small_cap = 0, dec_bytes_cap = 0;
+  // fw_decode scratch: one slot per decode in flight (fw_decode_begin / fw_decode_end)
+  struct DecSlot {
+    void *small = nullptr, *bytes = nullptr;   // chunk tables; a host input's device copy
+    size_t small_cap = 0, bytes_cap = 0;
+    int64_t* pin = nullptr;                    // pinned: the totals and the error word
+    hipEvent_t done = nullptr;
+    bool pending = false, empty = false;
+    int32_t ticket = -1;
+    int64_t record_cap = 0, marker_cap = 0;
+  };
+  static constexpr int NDEC = 2;
+  DecSlot dec[NDEC];
+  int64_t dec_seq = 0;
   int agg_helpers_max = RT_MAXNB;           // FW_AGG_HELPERS (0: never split a bucket)
   int agg_split = AG_SPLIT_CHAIN;           // shares per hot bucket, at most (FW_AGG_SPLIT)
   int agg_chunk_pct = 200;                  // records per share: at least this % of the mean load (FW_AGG_CHUNK_PCT)
@@ -2860,7 +2871,11 @@ struct fw_engine {
     for (void* p : allocs) (void)hipFree(p);
     if (bload_host) (void)hipHostFree(bload_host);
     if (dir_keys_host) (void)hipHostFree(dir_keys_host);
-    for (void* p : {dec_small, dec_bytes}) if (p) (void)hipFree(p);
+    for (auto& ds : dec) {
+      for (void* p : {ds.small, ds.bytes}) if (p) (void)hipFree(p);
+      if (ds.pin) (void)hipHostFree(ds.pin);
+      if (ds.done) (void)hipEventDestroy(ds.done);
+    }
     if (h_pin) (void)hipHostFree(h_pin);
     if (dstream) { (void)hipStreamSynchronize(dstream); (void)hipStreamDestroy(dstream); }
     for (auto& d : drains) {

@@ -458,6 +458,12 @@ class WindowEngine:
         dict of numpy arrays (device=True: torch tensors on the engine's GPU, ready for push) and the counts;
         "consumed" < len(data) when the bytes end inside an element.  buffers: a previous result's "buffers" (the same
         capacities) to decode into again instead of allocating the output columns."""
+        return self.decode_end(self.decode_begin(data, fields, key, value, f1, record_cap, marker_cap, device, buffers))
+
+    def decode_begin(self, data, fields, key=0, value=None, f1=None, record_cap=None, marker_cap=1 << 16, device=False,
+                     buffers=None):
+        """fw_decode_begin: enqueue the decode and return a handle for decode_end (the same dict as decode()); the
+        next buffer's decode can be enqueued before this one's counts are read back (two outstanding at most)."""
         types = {"long": _abi.FW_FT_LONG, "double": _abi.FW_FT_DOUBLE, "int": _abi.FW_FT_INT}
         sc = _abi.FwTupleSchema()
         sc.n_fields = len(fields)
@@ -489,23 +495,40 @@ class WindowEngine:
             cols = dict(key=mk(cap), f1=mk(cap), ts=mk(cap), value=mk(cap), wm=mk(marker_cap), wm_pos=mk(marker_cap),
                         lm=mk(2 * marker_cap), lm_pos=mk(marker_cap))
             cols["key_hash"] = mk(cap, i32) if int_key else None
-        cnt = _abi.FwDecodeCounts()
         src = ctypes.c_void_p(data.data_ptr()) if dev_in else ctypes.c_void_p(data.ctypes.data)
-        self._check(self._fn("decode")(self.h, ctypes.byref(sc), src, nbytes,
-                                       _abi.FW_MEM_DEVICE if dev_in else _abi.FW_MEM_HOST,
-                                       ptr(cols["key"]), ptr(cols["key_hash"]) if int_key else None, ptr(cols["f1"]),
-                                       ptr(cols["ts"]), ptr(cols["value"]), cap, ptr(cols["wm"]),
-                                       ptr(cols["wm_pos"]), ptr(cols["lm"]), ptr(cols["lm_pos"]), marker_cap,
-                                       ctypes.byref(cnt)))
+        args = (self.h, ctypes.byref(sc), src, nbytes, _abi.FW_MEM_DEVICE if dev_in else _abi.FW_MEM_HOST,
+                ptr(cols["key"]), ptr(cols["key_hash"]) if int_key else None, ptr(cols["f1"]), ptr(cols["ts"]),
+                ptr(cols["value"]), cap, ptr(cols["wm"]), ptr(cols["wm_pos"]), ptr(cols["lm"]), ptr(cols["lm_pos"]),
+                marker_cap)
+        h = dict(cols=cols, data=data, on_gpu=on_gpu, device=device, double=fields[sc.value_field] == "double")
+        if on_gpu:
+            t = ctypes.c_int32()
+            self._check(self._fn("decode_begin")(*args, ctypes.byref(t)))
+            h["ticket"] = t.value
+        else:   # the oracle decodes synchronously
+            cnt = _abi.FwDecodeCounts()
+            self._check(self._fn("decode")(*args, ctypes.byref(cnt)))
+            h["counts"] = cnt
+        return h
+
+    def decode_end(self, h):
+        """fw_decode_end of a decode_begin handle: the decoded columns and counts (see decode())."""
+        cols = h["cols"]
+        if "ticket" in h:
+            cnt = _abi.FwDecodeCounts()
+            self._check(self._fn("decode_end")(self.h, h["ticket"], ctypes.byref(cnt)))
+        else:
+            cnt = h["counts"]
         n, nw, nl = cnt.n_records, cnt.n_watermarks, cnt.n_latency_markers
         out = {"n_records": n, "n_watermarks": nw, "n_latency_markers": nl, "consumed": cnt.consumed, "buffers": cols}
         for k in ("key", "key_hash", "f1", "ts", "value"):
             out[k] = None if cols[k] is None else cols[k][:n]
         out["wm"], out["wm_pos"] = cols["wm"][:nw], cols["wm_pos"][:nw]
         out["lm"], out["lm_pos"] = cols["lm"][:2 * nl].reshape(-1, 2), cols["lm_pos"][:nl]
-        if fields[sc.value_field] == "double":
-            out["value"] = out["value"].view(torch.float64 if on_gpu else np.float64)
-        if on_gpu and not device:
+        if h["double"]:
+            import torch
+            out["value"] = out["value"].view(torch.float64 if h["on_gpu"] else np.float64)
+        if h["on_gpu"] and not h["device"]:
             out = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in out.items() if k != "buffers"}
         return out
 

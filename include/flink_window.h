@@ -333,6 +333,15 @@ int         fw_decode(fw_engine* e, const fw_tuple_schema* schema, const void* b
                       int64_t* key, int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap,
                       int64_t* wm, int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap,
                       fw_decode_counts* out);
+/* The same in two halves, so the count read-back of one buffer overlaps the next buffer's kernels:
+ * fw_decode_begin enqueues the decode on the engine stream and returns a ticket at once; fw_decode_end(ticket)
+ * waits for it and reports its counts (the errors fw_decode reports surface there).  At most two decodes are
+ * outstanding; a host input (FW_MEM_HOST) and the output columns must stay untouched until fw_decode_end. */
+int         fw_decode_begin(fw_engine* e, const fw_tuple_schema* schema, const void* bytes, int64_t nbytes, int32_t mem,
+                            int64_t* key, int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap,
+                            int64_t* wm, int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap,
+                            int32_t* ticket);
+int         fw_decode_end(fw_engine* e, int32_t ticket, fw_decode_counts* out);
 
 /* Key-group routing for the multi-GPU keyBy exchange (enqueued on the caller stream when fw_set_stream set one)
  * (KeyGroupStreamPartitioner.selectChannels, SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:52-65;

@@ -206,3 +206,32 @@ def test_decode_then_window_end_to_end():
     ro.append(eo.collect())
     eo.close()
     assert epochs_of(out, ["sum_i64"], True) == epochs_of(ro, ["sum_i64"], True)
+
+
+@pytest.mark.gpu
+def test_gpu_decode_begin_end_pipelined():
+    """fw_decode_begin / fw_decode_end: two decodes in flight (the second enqueued before the first's counts are
+    read), each equal to the synchronous fw_decode of the same bytes; a third outstanding begin and an unknown
+    ticket are rejected."""
+    from flink_amd import _abi
+    from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, WindowEngine, make_config
+    sc = dict(fields=["long", "long", "long"], key=0, value=2, f1=1)
+    streams = [_random_stream(60_000, s, sc["fields"]) for s in (7, 8, 9)]
+    e = WindowEngine(make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", True), None, 0,
+                                 key_capacity=1 << 12, max_batch=1 << 14, out_capacity=1 << 16))
+    kw = dict(key=0, value=2, f1=1, record_cap=1 << 17, marker_cap=1 << 13)
+    want = [e.decode(d, sc["fields"], **kw) for d in streams]
+    h0 = e.decode_begin(streams[0], sc["fields"], **kw)
+    h1 = e.decode_begin(streams[1], sc["fields"], **kw)
+    with pytest.raises(_abi.FwError):
+        e.decode_begin(streams[2], sc["fields"], **kw)
+    got0 = e.decode_end(h0)
+    h2 = e.decode_begin(streams[2], sc["fields"], **kw)
+    got1, got2 = e.decode_end(h1), e.decode_end(h2)
+    with pytest.raises(_abi.FwError):
+        e.decode_end(h2)
+    for g, w in zip((got0, got1, got2), want):
+        assert g["consumed"] == w["consumed"] and g["n_records"] == w["n_records"] > 50_000
+        for k in ("key", "f1", "ts", "value", "wm", "wm_pos", "lm", "lm_pos"):
+            assert np.array_equal(g[k], w[k]), k
+    e.close()
