@@ -28,18 +28,19 @@ def per_kernel(path, counter):
 
 def main(tag):
     os.makedirs(PROF, exist_ok=True)
-    src = os.path.join(OUT, "prof_trace", "run_kernel_stats.csv")
+    pre = os.environ.get("PROF_SRC", "prof")   # gpurun_out/<pre>_trace, <pre>_fetch, <pre>_write, <pre>_md5.txt
+    src = os.path.join(OUT, f"{pre}_trace", "run_kernel_stats.csv")
     if os.path.exists(src):
         shutil.copy(src, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
     lib = os.path.join(ROOT, "flink_amd", "lib", "libflink_window.so")
     md5 = hashlib.md5(open(lib, "rb").read()).hexdigest()
-    ran = open(os.path.join(OUT, "prof_md5.txt")).read().strip()
+    ran = open(os.path.join(OUT, f"{pre}_md5.txt")).read().strip()
     if ran != md5:
         sys.exit(f"gpurun_out/prof_* was measured on library {ran}, not the in-tree {md5}: re-run the profile")
     res = {"library_md5": md5, "config": os.environ.get("PROF_CONFIG", "c1"),   # the bench config profiled
            "units": "KB per dispatch as reported by rocprofv3", "kernels": {}}
-    f = os.path.join(OUT, "prof_fetch", "run_counter_collection.csv")
-    w = os.path.join(OUT, "prof_write", "run_counter_collection.csv")
+    f = os.path.join(OUT, f"{pre}_fetch", "run_counter_collection.csv")
+    w = os.path.join(OUT, f"{pre}_write", "run_counter_collection.csv")
     if os.path.exists(f) and os.path.exists(w):
         fetch, write = per_kernel(f, "FETCH_SIZE"), per_kernel(w, "WRITE_SIZE")
         ingest_bytes = 0.0
