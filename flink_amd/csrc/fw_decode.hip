@@ -204,8 +204,10 @@ __device__ __forceinline__ int32_t dec_agree(int32_t a, int32_t x) {
 // differ) and up to DEC_SW survivors with their counts, so the true chain's counts are known once its entry is
 // (no second walk).  The workgroup's waves share a chunk's candidates (wave w takes e = w, w + DEC_W, ...; lane =
 // chunk), so DEC_W chains per chunk run at once; each wave writes its own results (no LDS beyond the chunks)
-__global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, int64_t* surv, int32_t* nsurv) {
+__global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, int64_t* surv, int32_t* nsurv,
+                                                    int32_t* err) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // (read by the kernels after this one)
   const DecChunk ch = dec_stage_group(d, buf);
   const int lane = (int)threadIdx.x & (DEC_T - 1), wv = (int)threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * DEC_T + lane;
@@ -397,7 +399,8 @@ struct DecOut {
 // in rank order, so the column stores are coalesced; markers (rare) are written by their lane
 constexpr int DEC_MAXREC = DEC_T * (DEC_CHUNK / 13 + 1);   // records of a workgroup's chunks, at most
 __global__ __launch_bounds__(DEC_TW) void k_dec_emit(DecSpec d, const int32_t* entry, const int64_t* base_in,
-                                                   const int64_t* btop, DecOut o, int32_t* err) {
+                                                   const int64_t* btop, DecOut o, int32_t* err, const int64_t* totals,
+                                                   unsigned int* done, int64_t* host_counts) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
   __shared__ uint16_t rpos[DEC_MAXREC];   // LDS position of each record's tag
   __shared__ int64_t r0_s;
@@ -454,6 +457,13 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_emit(DecSpec d, const int32_t* e
     o.f1[r] = d.f1_off < 0 ? ts : d.f1_int ? (int64_t)(int32_t)lds_be_u32(t + d.f1_off) : (int64_t)lds_be_u64(t + d.f1_off);
     o.val[r] = (int64_t)lds_be_u64(t + d.val_off);
   }
+  // the last workgroup to finish posts the totals and the error word to the host (pinned, mapped): no copy after
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(done, 1u) == gridDim.x - 1) {
+    *done = 0u;
+    for (int k = 0; k < 4; ++k) host_counts[k] = totals[k];
+    host_counts[4] = (int64_t)atomicAdd(err, 0);
+  }
 }
 
 }  // namespace fw
@@ -502,10 +512,11 @@ static int decode_enqueue(fw_engine* e, int slot, const fw_tuple_schema* sc, con
   if (nbytes == 0) return FW_OK;
   HIPCHK(e, hipSetDevice(e->dev));
   if (!ds.pin) {
-    if (hipHostMalloc((void**)&ds.pin, 64, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)&ds.pin, 64, hipHostMallocMapped) != hipSuccess) {
       ds.pin = nullptr;
       return reject(e, FW_ERR_DEVICE, "decode: pinned count words");
     }
+    HIPCHK(e, hipHostGetDevicePointer((void**)&ds.pin_dev, ds.pin, 0));
     HIPCHK(e, hipEventCreateWithFlags(&ds.done, hipEventDisableTiming));
   }
   // grow-only scratch
@@ -520,7 +531,9 @@ static int decode_enqueue(fw_engine* e, int slot, const fw_tuple_schema* sc, con
   };
   const size_t nc = (size_t)d.nchunks;
   const size_t nblk = (nc + DEC_SCAN - 1) / DEC_SCAN;
+  const void* small_was = ds.small;
   HIPCHK(e, grow(ds.small, ds.small_cap, nc * (4 * DEC_W + 4 + 24 + 4 + 4 * DEC_W + 8 * DEC_S) + nblk * 24 + 256));
+  const bool fresh = ds.small != small_was;   // (the workgroup arrival counter starts at zero)
   const uint8_t* src = (const uint8_t*)bytes;
   if (mem == FW_MEM_HOST) {
     HIPCHK(e, grow(ds.bytes, ds.bytes_cap, (size_t)nbytes));
@@ -529,7 +542,8 @@ static int decode_enqueue(fw_engine* e, int slot, const fw_tuple_schema* sc, con
   }
   d.bytes = src;
   uint8_t* sm = (uint8_t*)ds.small;
-  int32_t* conv = (int32_t*)sm;   // [nc][DEC_W] each wave's agreeing exit
+  unsigned int* done = (unsigned int*)sm;   // k_dec_emit's workgroup arrival counter (returns to 0): a fixed place
+  int32_t* conv = (int32_t*)(sm + 16);      // [nc][DEC_W] each wave's agreeing exit
   int32_t* entry = conv + nc * DEC_W;
   int64_t* base = (int64_t*)(((uintptr_t)(entry + nc) + 7) & ~(uintptr_t)7);
   int64_t* totals = base + 3 * nc;   // [4] records, watermarks, latency markers, consumed bytes; then err
@@ -538,17 +552,16 @@ static int decode_enqueue(fw_engine* e, int slot, const fw_tuple_schema* sc, con
   int32_t* cexit = (int32_t*)(btot + 3 * nblk);   // [nc] where each chunk's true chain leaves it
   int32_t* nsurv = cexit + nc;                     // [nc][DEC_W] survivors each wave found
   int64_t* surv = (int64_t*)(((uintptr_t)(nsurv + nc * DEC_W) + 7) & ~(uintptr_t)7);   // [nc][DEC_S] kept survivors
-  HIPCHK(e, hipMemsetAsync(err, 0, 4, e->stream));
+  if (fresh) HIPCHK(e, hipMemsetAsync(done, 0, 8, e->stream));
   const unsigned gb = (unsigned)((nc + DEC_T - 1) / DEC_T);
-  hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, conv, surv, nsurv);
+  hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, conv, surv, nsurv, err);
   hipLaunchKernelGGL(k_dec_bscan, dim3((unsigned)nblk), dim3(DEC_SCAN), 0, e->stream, d, conv, surv, nsurv, entry, cexit,
                      base, btot, err);
   hipLaunchKernelGGL(k_dec_top, dim3(1), dim3(DEC_SCAN), 0, e->stream, d, entry, cexit, btot, (int64_t)nblk, totals);
   DecOut o{key, f1, ts, (int64_t*)value, wm, wm_pos, lm, lm_pos, key_hash, record_cap, marker_cap};
-  hipLaunchKernelGGL(k_dec_emit, dim3(gb), dim3(DEC_TW), 0, e->stream, d, entry, base, btot, o, err);
+  hipLaunchKernelGGL(k_dec_emit, dim3(gb), dim3(DEC_TW), 0, e->stream, d, entry, base, btot, o, err, totals, done,
+                     ds.pin_dev);
   HIPCHK(e, hipGetLastError());
-  // the totals and the error word, to pinned host memory behind the kernels
-  HIPCHK(e, hipMemcpyAsync(ds.pin, totals, 40, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipEventRecord(ds.done, e->stream));
   ds.record_cap = record_cap;
   ds.marker_cap = marker_cap;

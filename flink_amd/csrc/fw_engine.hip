@@ -2769,7 +2769,8 @@ struct fw_engine {
   struct DecSlot {
     void *small = nullptr, *bytes = nullptr;   // chunk tables; a host input's device copy
     size_t small_cap = 0, bytes_cap = 0;
-    int64_t* pin = nullptr;                    // pinned: the totals and the error word
+    int64_t* pin = nullptr;                    // pinned, mapped: the totals and the error word (k_dec_emit posts them)
+    int64_t* pin_dev = nullptr;                // the same words as the device sees them
     hipEvent_t done = nullptr;
     bool pending = false, empty = false;
     int32_t ticket = -1;
