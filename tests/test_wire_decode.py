@@ -235,3 +235,4 @@ def test_gpu_decode_begin_end_pipelined():
         for k in ("key", "f1", "ts", "value", "wm", "wm_pos", "lm", "lm_pos"):
             assert np.array_equal(g[k], w[k]), k
     e.close()
+
