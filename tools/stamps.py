@@ -32,6 +32,8 @@ for j in range(6):
                      zipf=1.2 if C4 else None, ooo=300 if C4 else 0)
     torch.cuda.synchronize()
     e.push(k, t, v)
+    if os.environ.get("STAMP_WM"):   # the bench's watermark after each batch: max timestamp - lag (50 ms for c4)
+        e.advance_watermark(int(t.max().item()) - (50 if C4 else 1))
     e.sync()
     e.lib.fw_debug_stamps(e.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), buf.size)
     sk, d, span = phases(buf, B // 4096, 5)
