@@ -109,8 +109,9 @@ __device__ __forceinline__ void dec_put1(uint8_t* buf, int q, uint8_t b) {
   if (i < DEC_T) buf[i * DEC_STRIDE + o] = b;
   if (i > 0 && o < DEC_SPILL) buf[(i - 1) * DEC_STRIDE + DEC_CHUNK + o] = b;
 }
-__device__ __forceinline__ DecChunk dec_stage_group(const DecSpec& d, uint8_t* buf) {
-  const int64_t g0 = (int64_t)blockIdx.x * DEC_T * DEC_CHUNK;
+// the DEC_T chunks from chunk c0 on into LDS, then this lane's chunk
+__device__ __forceinline__ DecChunk dec_stage_at(const DecSpec& d, uint8_t* buf, int64_t c0) {
+  const int64_t g0 = c0 * DEC_CHUNK;
   const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
   const uint8_t* src = d.bytes + g0;
   int done = 0;
@@ -131,11 +132,14 @@ __device__ __forceinline__ DecChunk dec_stage_group(const DecSpec& d, uint8_t* b
   }
   for (int i = done + (int)threadIdx.x; i < len; i += DEC_TW) dec_put1(buf, i, src[i]);
   __syncthreads();
-  const int lane = (int)threadIdx.x & (DEC_T - 1);   // (only wave 0 walks)
-  const int64_t c = (int64_t)blockIdx.x * DEC_T + lane;
+  const int lane = (int)threadIdx.x & (DEC_T - 1);
+  const int64_t c = c0 + lane;
   const int64_t start = c * DEC_CHUNK;
   return {buf + lane * DEC_STRIDE, (int)max<int64_t>(0, min<int64_t>(DEC_CHUNK, d.nbytes - start)),
           (int)min<int64_t>(d.nbytes - start, (int64_t)1 << 30)};
+}
+__device__ __forceinline__ DecChunk dec_stage_group(const DecSpec& d, uint8_t* buf) {
+  return dec_stage_at(d, buf, (int64_t)blockIdx.x * DEC_T);
 }
 // the element header at LDS position p (4-byte BE length, then the tag) from two aligned word reads
 __device__ __forceinline__ void dec_header(const uint8_t* p, uint32_t& len, uint32_t& tag) {
@@ -216,8 +220,22 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, i
   int32_t agree = INT32_MIN;
   int ns = 0;
   int64_t* sv = surv + c * DEC_S + wv * DEC_SW;
-  // one step per iteration of a single loop whatever candidate it belongs to (nested loops cost ~10x the steps)
-  int e = wv, pos = wv, n0 = 0, n1 = 0, n2 = 0;
+  // first the candidates' first headers, all at once (independent reads, no divergence): most offsets are no
+  // element start and drop out here; a bit per candidate that can start a chain (or meets the stream's end)
+  uint32_t live = 0;
+  for (int i = 0, e = wv; e < lim; ++i, e += DEC_W) {
+    bool ok = e + 5 > ch.rem;
+    if (!ok) {
+      uint32_t len, tag;
+      dec_header(ch.b + e, len, tag);
+      ok = dec_kind(d, len, (uint8_t)tag) >= 0;
+    }
+    live |= (ok ? 1u : 0u) << i;
+  }
+  // then the live candidates' chains, one step per iteration of a single loop whatever candidate it belongs to
+  // (nested loops cost ~10x the steps)
+  int e = live ? wv + DEC_W * (__ffs(live) - 1) : lim, pos = e, n0 = 0, n1 = 0, n2 = 0;
+  live &= live - 1;
   while (e < lim) {
     int x = DEC_DEAD;
     bool fin = true;
@@ -246,7 +264,8 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, i
         if (ns < DEC_SW) sv[ns] = ((int64_t)e << 32) | (uint32_t)dec_cpack(x, n0, n1, n2);
         ++ns;
       }
-      e += DEC_W;
+      e = live ? wv + DEC_W * (__ffs(live) - 1) : lim;
+      live &= live - 1;
       pos = e;
       n0 = n1 = n2 = 0;
     }
@@ -397,65 +416,112 @@ struct DecOut {
 // each chunk's true chain once more: every lane lists its records' LDS positions at their rank within the
 // workgroup (its chunks' records are one contiguous run of the output), and the workgroup then decodes them
 // in rank order, so the column stores are coalesced; markers (rare) are written by their lane
-constexpr int DEC_MAXREC = DEC_T * (DEC_CHUNK / 13 + 1);   // records of a workgroup's chunks, at most
+// records of a workgroup's chunks, at most: a record element is 4 + rec_len bytes or more (the list is sized per
+// schema in dynamic LDS, so a workgroup fits four to a CU: 37 KB of chunks + ~2.3 KB for Tuple3 records)
+__host__ __device__ inline int dec_maxrec(int rec_len) { return DEC_T * (DEC_CHUNK / (4 + rec_len) + 1); }
+// the bytes of group g (DEC_T chunks + the spill after them) in registers: 16-B loads, one round; *ok false when
+// they cannot be loaded that way (an unaligned source): the group is then staged byte by byte
+constexpr int DEC_NU = (DEC_T * DEC_CHUNK + DEC_SPILL + 16 * DEC_TW - 1) / (16 * DEC_TW);
+__device__ __forceinline__ void dec_prefetch(const DecSpec& d, int64_t g, uint4 (&v)[DEC_NU]) {
+  const int64_t g0 = g * DEC_T * DEC_CHUNK;
+  const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
+  const uint4* src = (const uint4*)(d.bytes + g0);
+  const int nv = len >> 4;
+#pragma unroll
+  for (int u = 0; u < DEC_NU; ++u) {
+    const int i = u * DEC_TW + (int)threadIdx.x;
+    if (i < nv) v[u] = src[i];
+  }
+}
+// group g into LDS from the prefetched registers (+ the bytes after the last whole 16-B unit); then this lane's chunk
+__device__ __forceinline__ DecChunk dec_stage_regs(const DecSpec& d, uint8_t* buf, int64_t g, const uint4 (&v)[DEC_NU]) {
+  const int64_t g0 = g * DEC_T * DEC_CHUNK;
+  const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
+  const int nv = len >> 4;
+#pragma unroll
+  for (int u = 0; u < DEC_NU; ++u) {
+    const int i = u * DEC_TW + (int)threadIdx.x;
+    if (i < nv) dec_put16(buf, 16 * i, v[u]);
+  }
+  for (int i = (nv << 4) + (int)threadIdx.x; i < len; i += DEC_TW) dec_put1(buf, i, d.bytes[g0 + i]);
+  __syncthreads();
+  const int lane = (int)threadIdx.x & (DEC_T - 1);
+  const int64_t start = (g * DEC_T + lane) * DEC_CHUNK;
+  return {buf + lane * DEC_STRIDE, (int)max<int64_t>(0, min<int64_t>(DEC_CHUNK, d.nbytes - start)),
+          (int)min<int64_t>(d.nbytes - start, (int64_t)1 << 30)};
+}
+
+// each chunk's true chain once more: every lane lists its records' LDS positions at their rank within the
+// workgroup (its chunks' records are one contiguous run of the output), and the workgroup then decodes them
+// in rank order, so the column stores are coalesced; markers (rare) are written by their lane.  Persistent: a
+// workgroup takes groups g = blockIdx.x, + gridDim.x, ..., the next group's bytes loading into registers while
+// this one is walked and decoded (a 16-B aligned source; otherwise each group is staged as it comes)
 __global__ __launch_bounds__(DEC_TW) void k_dec_emit(DecSpec d, const int32_t* entry, const int64_t* base_in,
                                                    const int64_t* btop, DecOut o, int32_t* err, const int64_t* totals,
-                                                   unsigned int* done, int64_t* host_counts) {
+                                                   unsigned int* done, int64_t* host_counts, int64_t ngroups) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
-  __shared__ uint16_t rpos[DEC_MAXREC];   // LDS position of each record's tag
+  extern __shared__ uint16_t rpos[];       // [dec_maxrec(d.rec_len)] LDS position of each record's tag
+  const int maxrec = dec_maxrec(d.rec_len);
   __shared__ int64_t r0_s;
   __shared__ int32_t nrec_s;
-  const DecChunk ch = dec_stage_group(d, buf);
-  const int64_t c = (int64_t)blockIdx.x * DEC_T + threadIdx.x;
-  const int64_t cfirst = (int64_t)blockIdx.x * DEC_T;
-  const int64_t bfirst = cfirst / DEC_SCAN;
-  if (threadIdx.x == 0) { r0_s = btop[3 * bfirst] + base_in[3 * cfirst]; nrec_s = 0; }
-  __syncthreads();
-  const int32_t en = (threadIdx.x < DEC_T && c < d.nchunks) ? entry[c] : -1;
-  int32_t nr = 0;
-  if (en >= 0) {   // past the stream's last whole element (or corrupt: reported by k_dec_bscan) otherwise
-    const int64_t blk = c / DEC_SCAN;
-    int64_t j[3] = {btop[3 * blk] + base_in[3 * c], btop[3 * blk + 1] + base_in[3 * c + 1], btop[3 * blk + 2] + base_in[3 * c + 2]};
+  const bool aligned = ((uintptr_t)d.bytes & 15) == 0;
+  uint4 v[DEC_NU];
+  if (aligned && (int64_t)blockIdx.x < ngroups) dec_prefetch(d, blockIdx.x, v);
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    __syncthreads();   // the previous group's LDS is read
+    const DecChunk ch = aligned ? dec_stage_regs(d, buf, g, v) : dec_stage_at(d, buf, g * DEC_T);
+    if (aligned && g + gridDim.x < ngroups) dec_prefetch(d, g + gridDim.x, v);   // in flight during the work below
+    const int64_t c = g * DEC_T + threadIdx.x;
+    const int64_t cfirst = g * DEC_T;
+    const int64_t bfirst = cfirst / DEC_SCAN;
+    if (threadIdx.x == 0) { r0_s = btop[3 * bfirst] + base_in[3 * cfirst]; nrec_s = 0; }
+    __syncthreads();
+    const int32_t en = (threadIdx.x < DEC_T && c < d.nchunks) ? entry[c] : -1;
+    int32_t nr = 0;
+    if (en >= 0) {   // past the stream's last whole element (or corrupt: reported by k_dec_bscan) otherwise
+      const int64_t blk = c / DEC_SCAN;
+      int64_t j[3] = {btop[3 * blk] + base_in[3 * c], btop[3 * blk + 1] + base_in[3 * c + 1], btop[3 * blk + 2] + base_in[3 * c + 2]};
+      const int64_t r0 = r0_s;
+      (void)dec_walk(d, ch, en, [&](int pos, int k) {
+        const uint8_t* p = ch.b + pos + 4;   // the tag
+        if (k == 0) {
+          const int64_t r = j[0]++;
+          const int64_t rl = r - r0;
+          if (rl >= 0 && rl < maxrec) rpos[rl] = (uint16_t)(p - buf);
+          ++nr;
+          return;
+        }
+        const int64_t m = j[k]++;
+        if (m >= o.marker_cap) { atomicExch(err, 2); return; }
+        if (k == 1) {
+          o.wm[m] = (int64_t)lds_be_u64(p + 1);
+          o.wm_pos[m] = j[0];   // the records before it
+        } else {   // latency marker: markedTime, then vertexId << 32 | subtaskIndex
+          o.lm[2 * m] = (int64_t)lds_be_u64(p + 1);
+          o.lm[2 * m + 1] = (int64_t)(((uint64_t)lds_be_u32(p + 9) << 32) | lds_be_u32(p + 13));
+          o.lm_pos[m] = j[0];
+        }
+      });
+    }
+    if (nr) atomicAdd(&nrec_s, nr);
+    __syncthreads();
+    // the workgroup's records, in rank order
+    const int nrec = min(nrec_s, maxrec);
     const int64_t r0 = r0_s;
-    (void)dec_walk(d, ch, en, [&](int pos, int k) {
-      const uint8_t* p = ch.b + pos + 4;   // the tag
-      if (k == 0) {
-        const int64_t r = j[0]++;
-        const int64_t rl = r - r0;
-        if (rl >= 0 && rl < DEC_MAXREC) rpos[rl] = (uint16_t)(p - buf);
-        ++nr;
-        return;
-      }
-      const int64_t m = j[k]++;
-      if (m >= o.marker_cap) { atomicExch(err, 2); return; }
-      if (k == 1) {
-        o.wm[m] = (int64_t)lds_be_u64(p + 1);
-        o.wm_pos[m] = j[0];   // the records before it
-      } else {   // latency marker: markedTime, then vertexId << 32 | subtaskIndex
-        o.lm[2 * m] = (int64_t)lds_be_u64(p + 1);
-        o.lm[2 * m + 1] = (int64_t)(((uint64_t)lds_be_u32(p + 9) << 32) | lds_be_u32(p + 13));
-        o.lm_pos[m] = j[0];
-      }
-    });
-  }
-  if (nr) atomicAdd(&nrec_s, nr);
-  __syncthreads();
-  // the workgroup's records, in rank order
-  const int nrec = min(nrec_s, DEC_MAXREC);
-  const int64_t r0 = r0_s;
-  for (int rl = threadIdx.x; rl < nrec; rl += DEC_TW) {
-    const int64_t r = r0 + rl;
-    if (r >= o.record_cap) { atomicExch(err, 2); continue; }
-    const uint8_t* p = buf + rpos[rl];
-    const bool has_ts = p[0] == 0;
-    const int64_t ts = has_ts ? (int64_t)lds_be_u64(p + 1) : INT64_MIN;
-    const uint8_t* t = p + (has_ts ? 9 : 1);
-    const int64_t key = d.key_int ? (int64_t)(int32_t)lds_be_u32(t + d.key_off) : (int64_t)lds_be_u64(t + d.key_off);
-    o.key[r] = key;
-    if (o.key_hash) o.key_hash[r] = (int32_t)key;   // Integer.hashCode
-    o.ts[r] = ts;
-    o.f1[r] = d.f1_off < 0 ? ts : d.f1_int ? (int64_t)(int32_t)lds_be_u32(t + d.f1_off) : (int64_t)lds_be_u64(t + d.f1_off);
-    o.val[r] = (int64_t)lds_be_u64(t + d.val_off);
+    for (int rl = threadIdx.x; rl < nrec; rl += DEC_TW) {
+      const int64_t r = r0 + rl;
+      if (r >= o.record_cap) { atomicExch(err, 2); continue; }
+      const uint8_t* p = buf + rpos[rl];
+      const bool has_ts = p[0] == 0;
+      const int64_t ts = has_ts ? (int64_t)lds_be_u64(p + 1) : INT64_MIN;
+      const uint8_t* t = p + (has_ts ? 9 : 1);
+      const int64_t key = d.key_int ? (int64_t)(int32_t)lds_be_u32(t + d.key_off) : (int64_t)lds_be_u64(t + d.key_off);
+      o.key[r] = key;
+      if (o.key_hash) o.key_hash[r] = (int32_t)key;   // Integer.hashCode
+      o.ts[r] = ts;
+      o.f1[r] = d.f1_off < 0 ? ts : d.f1_int ? (int64_t)(int32_t)lds_be_u32(t + d.f1_off) : (int64_t)lds_be_u64(t + d.f1_off);
+      o.val[r] = (int64_t)lds_be_u64(t + d.val_off);
+    }
   }
   // the last workgroup to finish posts the totals and the error word to the host (pinned, mapped): no copy after
   __syncthreads();
@@ -559,8 +625,10 @@ static int decode_enqueue(fw_engine* e, int slot, const fw_tuple_schema* sc, con
                      base, btot, err);
   hipLaunchKernelGGL(k_dec_top, dim3(1), dim3(DEC_SCAN), 0, e->stream, d, entry, cexit, btot, (int64_t)nblk, totals);
   DecOut o{key, f1, ts, (int64_t*)value, wm, wm_pos, lm, lm_pos, key_hash, record_cap, marker_cap};
-  hipLaunchKernelGGL(k_dec_emit, dim3(gb), dim3(DEC_TW), 0, e->stream, d, entry, base, btot, o, err, totals, done,
-                     ds.pin_dev);
+  // persistent: four workgroups per CU (dynamic LDS sized to the schema), at most one per group
+  const unsigned eg = (unsigned)std::min<int64_t>((int64_t)gb, (int64_t)e->grid / 2);   // (grid = 8 per CU)
+  hipLaunchKernelGGL(k_dec_emit, dim3(eg), dim3(DEC_TW), (size_t)2 * dec_maxrec(d.rec_len), e->stream, d, entry, base,
+                     btot, o, err, totals, done, ds.pin_dev, (int64_t)gb);
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(ds.done, e->stream));
   ds.record_cap = record_cap;
