@@ -204,18 +204,58 @@ __device__ __forceinline__ int32_t dec_agree(int32_t a, int32_t x) {
   return a == INT32_MIN ? x : (x == INT32_MIN || a == x) ? a : INT32_MAX;
 }
 
+// the bytes of group g (DEC_T chunks + the spill after them) in registers: 16-B loads, one round; *ok false when
+// they cannot be loaded that way (an unaligned source): the group is then staged byte by byte
+constexpr int DEC_NU = (DEC_T * DEC_CHUNK + DEC_SPILL + 16 * DEC_TW - 1) / (16 * DEC_TW);
+__device__ __forceinline__ void dec_prefetch(const DecSpec& d, int64_t g, uint4 (&v)[DEC_NU]) {
+  const int64_t g0 = g * DEC_T * DEC_CHUNK;
+  const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
+  const uint4* src = (const uint4*)(d.bytes + g0);
+  const int nv = len >> 4;
+#pragma unroll
+  for (int u = 0; u < DEC_NU; ++u) {
+    const int i = u * DEC_TW + (int)threadIdx.x;
+    if (i < nv) v[u] = src[i];
+  }
+}
+// group g into LDS from the prefetched registers (+ the bytes after the last whole 16-B unit); then this lane's chunk
+__device__ __forceinline__ DecChunk dec_stage_regs(const DecSpec& d, uint8_t* buf, int64_t g, const uint4 (&v)[DEC_NU]) {
+  const int64_t g0 = g * DEC_T * DEC_CHUNK;
+  const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
+  const int nv = len >> 4;
+#pragma unroll
+  for (int u = 0; u < DEC_NU; ++u) {
+    const int i = u * DEC_TW + (int)threadIdx.x;
+    if (i < nv) dec_put16(buf, 16 * i, v[u]);
+  }
+  for (int i = (nv << 4) + (int)threadIdx.x; i < len; i += DEC_TW) dec_put1(buf, i, d.bytes[g0 + i]);
+  __syncthreads();
+  const int lane = (int)threadIdx.x & (DEC_T - 1);
+  const int64_t start = (g * DEC_T + lane) * DEC_CHUNK;
+  return {buf + lane * DEC_STRIDE, (int)max<int64_t>(0, min<int64_t>(DEC_CHUNK, d.nbytes - start)),
+          (int)min<int64_t>(d.nbytes - start, (int64_t)1 << 30)};
+}
+
 // per chunk and wave: the exit its surviving candidate chains agree on (INT32_MIN: none survived, INT32_MAX: they
 // differ) and up to DEC_SW survivors with their counts, so the true chain's counts are known once its entry is
 // (no second walk).  The workgroup's waves share a chunk's candidates (wave w takes e = w, w + DEC_W, ...; lane =
 // chunk), so DEC_W chains per chunk run at once; each wave writes its own results (no LDS beyond the chunks)
 __global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, int64_t* surv, int32_t* nsurv,
-                                                    int32_t* err) {
+                                                    int32_t* err, int64_t ngroups) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
   if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0;   // (read by the kernels after this one)
-  const DecChunk ch = dec_stage_group(d, buf);
+  // persistent: groups g = blockIdx.x, + gridDim.x, ..., the next group's bytes loading into registers while this
+  // one's candidates are walked (a 16-B aligned source; otherwise each group is staged as it comes)
+  const bool aligned = ((uintptr_t)d.bytes & 15) == 0;
+  uint4 v[DEC_NU];
+  if (aligned && (int64_t)blockIdx.x < ngroups) dec_prefetch(d, blockIdx.x, v);
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  __syncthreads();   // the previous group's LDS is read
+  const DecChunk ch = aligned ? dec_stage_regs(d, buf, g, v) : dec_stage_at(d, buf, g * DEC_T);
+  if (aligned && g + gridDim.x < ngroups) dec_prefetch(d, g + gridDim.x, v);
   const int lane = (int)threadIdx.x & (DEC_T - 1), wv = (int)threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * DEC_T + lane;
-  if (c >= d.nchunks) return;
+  const int64_t c = g * DEC_T + lane;
+  if (c >= d.nchunks) continue;
   const int lim = min(d.maxe, ch.clen);
   int32_t agree = INT32_MIN;
   int ns = 0;
@@ -272,6 +312,7 @@ __global__ __launch_bounds__(DEC_TW) void k_dec_scan(DecSpec d, int32_t* conv, i
   }
   conv[c * DEC_W + wv] = agree;
   nsurv[c * DEC_W + wv] = ns;
+  }
 }
 
 // chunk c's chain from pos in global memory (the rare paths): its exit or DEC_DEAD, and its counts
@@ -413,44 +454,9 @@ struct DecOut {
   int64_t record_cap, marker_cap;
 };
 
-// each chunk's true chain once more: every lane lists its records' LDS positions at their rank within the
-// workgroup (its chunks' records are one contiguous run of the output), and the workgroup then decodes them
-// in rank order, so the column stores are coalesced; markers (rare) are written by their lane
 // records of a workgroup's chunks, at most: a record element is 4 + rec_len bytes or more (the list is sized per
 // schema in dynamic LDS, so a workgroup fits four to a CU: 37 KB of chunks + ~2.3 KB for Tuple3 records)
 __host__ __device__ inline int dec_maxrec(int rec_len) { return DEC_T * (DEC_CHUNK / (4 + rec_len) + 1); }
-// the bytes of group g (DEC_T chunks + the spill after them) in registers: 16-B loads, one round; *ok false when
-// they cannot be loaded that way (an unaligned source): the group is then staged byte by byte
-constexpr int DEC_NU = (DEC_T * DEC_CHUNK + DEC_SPILL + 16 * DEC_TW - 1) / (16 * DEC_TW);
-__device__ __forceinline__ void dec_prefetch(const DecSpec& d, int64_t g, uint4 (&v)[DEC_NU]) {
-  const int64_t g0 = g * DEC_T * DEC_CHUNK;
-  const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
-  const uint4* src = (const uint4*)(d.bytes + g0);
-  const int nv = len >> 4;
-#pragma unroll
-  for (int u = 0; u < DEC_NU; ++u) {
-    const int i = u * DEC_TW + (int)threadIdx.x;
-    if (i < nv) v[u] = src[i];
-  }
-}
-// group g into LDS from the prefetched registers (+ the bytes after the last whole 16-B unit); then this lane's chunk
-__device__ __forceinline__ DecChunk dec_stage_regs(const DecSpec& d, uint8_t* buf, int64_t g, const uint4 (&v)[DEC_NU]) {
-  const int64_t g0 = g * DEC_T * DEC_CHUNK;
-  const int len = (int)min<int64_t>(DEC_T * DEC_CHUNK + DEC_SPILL, d.nbytes - g0);
-  const int nv = len >> 4;
-#pragma unroll
-  for (int u = 0; u < DEC_NU; ++u) {
-    const int i = u * DEC_TW + (int)threadIdx.x;
-    if (i < nv) dec_put16(buf, 16 * i, v[u]);
-  }
-  for (int i = (nv << 4) + (int)threadIdx.x; i < len; i += DEC_TW) dec_put1(buf, i, d.bytes[g0 + i]);
-  __syncthreads();
-  const int lane = (int)threadIdx.x & (DEC_T - 1);
-  const int64_t start = (g * DEC_T + lane) * DEC_CHUNK;
-  return {buf + lane * DEC_STRIDE, (int)max<int64_t>(0, min<int64_t>(DEC_CHUNK, d.nbytes - start)),
-          (int)min<int64_t>(d.nbytes - start, (int64_t)1 << 30)};
-}
-
 // each chunk's true chain once more: every lane lists its records' LDS positions at their rank within the
 // workgroup (its chunks' records are one contiguous run of the output), and the workgroup then decodes them
 // in rank order, so the column stores are coalesced; markers (rare) are written by their lane.  Persistent: a
@@ -620,7 +626,8 @@ static int decode_enqueue(fw_engine* e, int slot, const fw_tuple_schema* sc, con
   int64_t* surv = (int64_t*)(((uintptr_t)(nsurv + nc * DEC_W) + 7) & ~(uintptr_t)7);   // [nc][DEC_S] kept survivors
   if (fresh) HIPCHK(e, hipMemsetAsync(done, 0, 8, e->stream));
   const unsigned gb = (unsigned)((nc + DEC_T - 1) / DEC_T);
-  hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, conv, surv, nsurv, err);
+  // one workgroup per group (a persistent scan with the next group prefetched measured slower: 54 vs 47 us)
+  hipLaunchKernelGGL(k_dec_scan, dim3(gb), dim3(DEC_TW), 0, e->stream, d, conv, surv, nsurv, err, (int64_t)gb);
   hipLaunchKernelGGL(k_dec_bscan, dim3((unsigned)nblk), dim3(DEC_SCAN), 0, e->stream, d, conv, surv, nsurv, entry, cexit,
                      base, btot, err);
   hipLaunchKernelGGL(k_dec_top, dim3(1), dim3(DEC_SCAN), 0, e->stream, d, entry, cexit, btot, (int64_t)nblk, totals);
