@@ -2796,6 +2796,8 @@ struct fw_engine {
   void* list_temp = nullptr;
   size_t list_temp_bytes = 0;
   int64_t list_tmp_cap = 0;
+  int64_t* list_fire_dp = nullptr;   // list re-fires: (kid, arrival) pairs, counts, offsets (grow-only)
+  int64_t list_fire_cap = 0;
   int64_t list_out = 0;                    // results appended since the last collect
   // session windows (FW_SESSION, fw_session.hip)
   bool session = false;
@@ -2886,7 +2888,8 @@ struct fw_engine {
       if (d.staged) (void)hipEventDestroy(d.staged);
     }
     if (h_pin_cnt) (void)hipHostFree(h_pin_cnt);
-    for (void* p : {(void*)list_k1, (void*)list_k2, (void*)list_v1, (void*)list_v2, list_temp}) if (p) (void)hipFree(p);
+    for (void* p : {(void*)list_k1, (void*)list_k2, (void*)list_v1, (void*)list_v2, list_temp, (void*)list_fire_dp})
+      if (p) (void)hipFree(p);
   }
 };
 

@@ -226,7 +226,7 @@ int list_create(fw_engine* e) {
   L.cnt = e->alloc<unsigned long long>((size_t)s.P);
   L.buf = e->alloc<int64_t>((size_t)s.P * (size_t)L.cap * LST_WORDS);
   if (e->cfg.allowed_lateness > 0) {   // per-element re-fires: (kid, window, arrival) of one batch
-    L.fcap = e->cfg.max_batch;
+    L.fcap = e->cfg.max_batch * (int64_t)((s.K + s.R - 1) / s.R);   // a record re-fires each of its windows
     L.fire = e->alloc<int64_t>((size_t)L.fcap * 3);
     L.fcnt = e->alloc<unsigned long long>(1);
   }
@@ -281,8 +281,15 @@ int list_push(fw_engine* e, const BatchIn& b) {
     const int64_t Fn = (int64_t)pr.size();
     std::vector<int64_t> pairs(2 * (size_t)Fn), cnt(2 * (size_t)Fn), off((size_t)Fn);
     for (int64_t j = 0; j < Fn; ++j) { pairs[2 * (size_t)j] = pr[(size_t)j].second; pairs[2 * (size_t)j + 1] = pr[(size_t)j].first; }
-    int64_t* dp = nullptr;
-    HIPCHK(e, hipMalloc(&dp, 8 * (size_t)(5 * Fn)));
+    if (5 * Fn > e->list_fire_cap) {   // grow-only scratch (pairs, counts, offsets), freed with the engine
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      if (e->list_fire_dp) (void)hipFree(e->list_fire_dp);
+      e->list_fire_dp = nullptr;
+      e->list_fire_cap = 0;
+      HIPCHK(e, hipMalloc((void**)&e->list_fire_dp, 8 * (size_t)(10 * Fn)));
+      e->list_fire_cap = 10 * Fn;
+    }
+    int64_t* dp = e->list_fire_dp;
     HIPCHK(e, hipMemcpy(dp, pairs.data(), 16 * (size_t)Fn, hipMemcpyHostToDevice));
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((Fn + BLOCK - 1) / BLOCK, e->grid));
     hipLaunchKernelGGL(k_list_fire_count, dim3(blocks), dim3(BLOCK), 0, e->stream, e->lst, e->list_k2, e->list_v1, N, dp,
@@ -292,17 +299,13 @@ int list_push(fw_engine* e, const BatchIn& b) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     int64_t tot = 0;
     for (int64_t j = 0; j < Fn; ++j) { off[(size_t)j] = tot; tot += cnt[2 * (size_t)j + 1]; }
-    if (e->list_out + tot > e->cfg.out_capacity) {
-      (void)hipFree(dp);
-      return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded (list state)");
-    }
+    if (e->list_out + tot > e->cfg.out_capacity) return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded (list state)");
     HIPCHK(e, hipMemcpy(dp + 4 * Fn, off.data(), 8 * (size_t)Fn, hipMemcpyHostToDevice));
     const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)n * (uint64_t)e->s.slide)), e->s.size), 1);
     hipLaunchKernelGGL(k_list_fire_emit, dim3((unsigned)std::min<int64_t>(Fn, 4096)), dim3(BLOCK), 0, e->stream, e->s,
                        e->lst, e->list_v1, dp + 2 * Fn, dp + 4 * Fn, Fn, e->list_out, max_ts);
     DBGSYNC(e, "k_list_fire_emit");
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    (void)hipFree(dp);
     e->list_out += tot;
     e->late_fires_host += Fn;
   }
