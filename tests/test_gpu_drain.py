@@ -21,7 +21,8 @@ def _stream(n, keys, seed):
 
 
 def _rows(r):
-    cols = [r[c] for c in ("key", "ts", "f1", "sum_i64", "count") if r.get(c) is not None and len(r[c]) == r["n"]]
+    cols = [r[c] for c in ("key", "ts", "f1", "sum_i64", "min_i64", "max_i64", "count")
+            if r.get(c) is not None and len(r[c]) == r["n"]]
     if r.get("win_start") is not None and len(r["win_start"]) == r["n"] and r["n"]:
         cols.append(r["win_start"])
     rows = np.stack(cols, axis=1) if r["n"] else np.zeros((0, len(cols)), np.int64)
@@ -34,14 +35,17 @@ def _rows(r):
     return out
 
 
-@pytest.mark.parametrize("kind", ["tumbling", "sliding", "session"])
+@pytest.mark.parametrize("kind", ["tumbling", "sliding", "session", "tumbling_all_fields"])
 @pytest.mark.parametrize("lag", [0, 1, 2])   # drains left outstanding before the next begins (three at most at once)
 def test_async_drain_matches_collect(kind, lag):
     from flink_amd.windowing import (EventTimeSessionWindows, ReduceFunction, SlidingEventTimeWindows,
                                      TumblingEventTimeWindows, WindowEngine, make_config)
     assigner = {"tumbling": TumblingEventTimeWindows.of(100), "sliding": SlidingEventTimeWindows.of(300, 100),
-                "session": EventTimeSessionWindows.withGap(20)}[kind]
-    cfg = make_config(assigner, ReduceFunction(("sum", "count"), "i64", keep_first_f1=True), max_parallelism=128,
+                "session": EventTimeSessionWindows.withGap(20),
+                "tumbling_all_fields": TumblingEventTimeWindows.of(100)}[kind]
+    # (all fields: every output column present, so the drain's packed columns are all in play)
+    fields = ("sum", "min", "max", "count") if kind == "tumbling_all_fields" else ("sum", "count")
+    cfg = make_config(assigner, ReduceFunction(fields, "i64", keep_first_f1=True), max_parallelism=128,
                       key_capacity=1 << 12, max_batch=1 << 12, out_capacity=1 << 18)
     k, t, v = _stream(40_000, 2000, 11)
     a, b = WindowEngine(cfg), WindowEngine(cfg)
