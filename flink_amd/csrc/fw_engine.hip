@@ -3154,8 +3154,15 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   // ingest_mode 3 was the fused form (one persistent launch per batch, XCD-local hand-off of the routed records):
   // measured slower than the partitioned form in rounds 3 and 4 (23 / 14 G vs 51-56 G events/s on C1), removed
   if (c.ingest_mode == 3) return unsupported("ingest_mode 3 (fused) was removed: the partitioned form (2) is faster; DESIGN.md section 4");
-  // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys): short linear-probe sequences
-  s.D = next_pow2(std::max<int64_t>((c.key_capacity <= (1 << 20) ? 4 : 2) * c.key_capacity, 64));
+  // key directory at load factor <= 1/4 (<= 1/2 above 2^20 keys, <= 0.625 above 2^22): short linear-probe sequences.
+  // Above 2^22 keys the direct form is bound by random lines of the directory and the pane columns (D + 1 rows
+  // each), so a denser table pays: C2 (10 M keys) 16 M slots instead of 32 M, 9.3 -> 10.0 G events/s (same-box
+  // A/B).  FW_DIR_SLOTS (slots per key x 100, experiments) overrides the factor
+  {
+    int64_t f100 = c.key_capacity <= (1 << 20) ? 400 : c.key_capacity <= (1 << 22) ? 200 : 160;
+    if (const char* v = getenv("FW_DIR_SLOTS")) f100 = std::max(100, atoi(v));
+    s.D = next_pow2(std::max<int64_t>((f100 * c.key_capacity + 99) / 100, 64));
+  }
   s.dir_mask = (uint64_t)s.D - 1;
   {
     int dbits = bits_for((uint64_t)s.D) - 1;                  // D = 2^dbits
