@@ -236,3 +236,27 @@ def test_gpu_decode_begin_end_pipelined():
             assert np.array_equal(g[k], w[k]), k
     e.close()
 
+
+
+@pytest.mark.gpu
+def test_gpu_decode_all_chunks_undecided():
+    """Every record's timestamp, key, f1 and value bytes read as a record header (length 33, tag 0 / 1) at the same
+    offset of every record, so every chunk has false survivors whose exits disagree with the true one: every
+    chunk's entry comes from the walk from the nearest decided chunk (here: chunk 0).  Same columns as the oracle."""
+    from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, WindowEngine, make_config
+    from oracle.oracle import OracleEngine
+    sc = dict(fields=["long", "long", "long"], key=0, value=2, f1=1)
+    n = 12_000
+    ts, key, f1, val = 0x0000002100000000, 0x0000002101000000, 0x0000002100000005, 0x0000002100000007
+    data = b"".join(struct.pack(">ibqqqq", 33, 0, ts, key, f1, val) for _ in range(n))
+    cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum",), "i64", True), None, 0,
+                      key_capacity=1 << 12, max_batch=1 << 14, out_capacity=1 << 16)
+    res = []
+    for factory in (WindowEngine, OracleEngine):
+        e = factory(cfg)
+        res.append(e.decode(data, sc["fields"], key=0, value=2, f1=1, record_cap=1 << 15, marker_cap=1 << 10))
+        e.close()
+    g, o = res
+    assert g["n_records"] == o["n_records"] == n and g["consumed"] == o["consumed"] == len(data)
+    for k in ("key", "f1", "ts", "value"):
+        assert np.array_equal(g[k], o[k]), k
