@@ -1131,7 +1131,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   constexpr bool HELPERS_FIRST = SKEW && VT == FW_VALUE_I64 && !(AGG & (FW_AGG_MAXBY | FW_AGG_MINBY));
   const int H = HELPERS_FIRST ? r.helpers : 0;
   const int vb = (int)blockIdx.x < H ? s.nb + (int)blockIdx.x : (int)blockIdx.x - H;
-  const int owner_bkt = vb >= s.nb ? -1
+  int owner_bkt = vb >= s.nb ? -1
                         : (s.nb % 8 == 0 && !(r.dbg & 32)) ? (vb % 8) * (s.nb / 8) + vb / 8
                                                           : vb;
   const int nbq = RT_GROUPS * s.nb;
@@ -1185,6 +1185,27 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     if (threadIdx.x == 0) plan[s.nb] = 0;
     __syncthreads();
     block_scan_excl<NT, AG_MAXPER>(plan, s.nb + 1, awtot);   // plan[x] = first helper of bucket x; plan[nb] = total
+    // integer shares: owners are dispatched longest share first (owner vb takes the bucket whose share holds
+    // the vb-th most records, ties by bucket), so the workgroups that wait for a CU to free up are the
+    // shortest ones.  Every workgroup ranks the same loads: a permutation of the buckets.  (FW_DEBUG_AGG &
+    // 128: the plain order.)
+    if (HELPERS_FIRST && owner_bkt >= 0 && !(r.dbg & 128)) {   // uniform
+      for (int x = threadIdx.x; x < s.nb; x += NT)
+        step_tile[x] = (int32_t)(r.bload_prev[x] / (uint32_t)(1 + max(min(plan[x + 1], r.helpers) - plan[x], 0)));
+      __syncthreads();
+      for (int x = threadIdx.x; x < s.nb; x += NT) {
+        const int32_t wx = step_tile[x];
+        int rk = 0;
+        for (int y = 0; y < s.nb; ++y) {
+          const int32_t wy = step_tile[y];
+          rk += (wy > wx || (wy == wx && y < x)) ? 1 : 0;
+        }
+        if (rk == vb) plan[RT_MAXNB + 1] = x;
+      }
+      __syncthreads();
+      owner_bkt = plan[RT_MAXNB + 1];
+      __syncthreads();
+    }
     const int32_t h = owner_bkt < 0 ? (int32_t)vb - s.nb : -1;
     if (threadIdx.x == 0) plan[RT_MAXNB + 1] = owner_bkt < 0 ? -1 : owner_bkt;
     __syncthreads();
