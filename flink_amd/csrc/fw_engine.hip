@@ -1792,9 +1792,36 @@ __global__ __launch_bounds__(LS_CT) void k_segscan_carry(SegPart* tile_agg, int3
     run = seg_join(run, own);
   }
 }
-__global__ __launch_bounds__(LS_T) void k_segscan_apply(const SegPart* carry, const int32_t* tile_first_head, int64_t n,
+// the carries in two levels when the tiles outnumber the one workgroup's threads: each workgroup of LS_CT
+// tiles turns their aggregates into carries within the group (in place) and posts the group's aggregate;
+// k_segscan_carry then turns the groups' aggregates into their carries, and k_segscan_apply joins the two
+__global__ __launch_bounds__(LS_CT) void k_segscan_carry_grp(SegPart* tile_agg, int32_t ntiles, SegPart* grp) {
+  __shared__ __attribute__((aligned(16))) unsigned char sp_raw[LS_CT * sizeof(SegPart)];   // (LateAcc has a constructor)
+  SegPart* sp = (SegPart*)sp_raw;
+  const int t = (int)blockIdx.x * LS_CT + (int)threadIdx.x;
+  SegPart a;
+  a.empty = 1; a.head = 0; a.hp = -1;
+  if (t < ntiles) a = tile_agg[t];
+  sp[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 1; o < LS_CT; o <<= 1) {
+    SegPart y = a;
+    if ((int)threadIdx.x >= o) y = seg_join(sp[threadIdx.x - o], a);
+    __syncthreads();
+    sp[threadIdx.x] = y;
+    a = y;
+    __syncthreads();
+  }
+  if (threadIdx.x == LS_CT - 1) grp[blockIdx.x] = a;
+  SegPart ex;
+  if (threadIdx.x > 0) ex = sp[threadIdx.x - 1];
+  else { ex.empty = 1; ex.head = 0; ex.hp = -1; }
+  if (t < ntiles) tile_agg[t] = ex;
+}
+__global__ __launch_bounds__(LS_T) void k_segscan_apply(const SegPart* carry, const SegPart* grp_carry,
+                                                         const int32_t* tile_first_head, int64_t n,
                                                          LateAcc* out, int64_t* hp_out) {
-  const SegPart c = carry[blockIdx.x];
+  const SegPart c = grp_carry ? seg_join(grp_carry[blockIdx.x / LS_CT], carry[blockIdx.x]) : carry[blockIdx.x];
   if (c.empty) return;
   const int32_t lead = tile_first_head[blockIdx.x];
   const int64_t t0 = (int64_t)blockIdx.x * LS_TILE;
@@ -2735,6 +2762,7 @@ struct fw_engine {
   LateAcc *late_acc = nullptr, *late_scan = nullptr;
   int64_t *headpos = nullptr, *headpos_scan = nullptr;
   SegPart* seg_tiles = nullptr;   // the late scan's per-tile aggregates, then carries
+  SegPart* seg_groups = nullptr;  // ... and per group of LS_CT tiles (two-level carries)
   int32_t* seg_first = nullptr;   // ... and first segment head per tile
   void* temp = nullptr;
   size_t temp_bytes = 0;
@@ -3352,6 +3380,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->headpos = e->alloc<int64_t>(nb);
     e->headpos_scan = e->alloc<int64_t>(nb);
     e->seg_tiles = e->alloc<SegPart>(nb / LS_TILE + 1);
+    e->seg_groups = e->alloc<SegPart>((nb / LS_TILE + 1) / LS_CT + 2);
     e->seg_first = e->alloc<int32_t>(nb / LS_TILE + 1);
     size_t t1 = 0;
     (void)rocprim::radix_sort_keys(nullptr, t1, e->late_key, e->late_key_sorted, nb, 0, 64, e->stream);
@@ -3570,8 +3599,16 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
       const int32_t ntl = (int32_t)((n + LS_TILE - 1) / LS_TILE);
       hipLaunchKernelGGL(k_segscan_tile, dim3(ntl), dim3(LS_T), 0, e->stream, e->seg, e->late_acc, (int64_t)n,
                          e->late_scan, e->headpos_scan, e->seg_tiles, e->seg_first);
-      hipLaunchKernelGGL(k_segscan_carry, dim3(1), dim3(LS_CT), 0, e->stream, e->seg_tiles, ntl);
-      hipLaunchKernelGGL(k_segscan_apply, dim3(ntl), dim3(LS_T), 0, e->stream, e->seg_tiles, e->seg_first, (int64_t)n,
+      const SegPart* grp = nullptr;
+      if (ntl > LS_CT) {   // two levels (one workgroup's serial chunks took ~90 us at 4 K tiles)
+        const int32_t ng = (ntl + LS_CT - 1) / LS_CT;
+        hipLaunchKernelGGL(k_segscan_carry_grp, dim3(ng), dim3(LS_CT), 0, e->stream, e->seg_tiles, ntl, e->seg_groups);
+        hipLaunchKernelGGL(k_segscan_carry, dim3(1), dim3(LS_CT), 0, e->stream, e->seg_groups, ng);
+        grp = e->seg_groups;
+      } else {
+        hipLaunchKernelGGL(k_segscan_carry, dim3(1), dim3(LS_CT), 0, e->stream, e->seg_tiles, ntl);
+      }
+      hipLaunchKernelGGL(k_segscan_apply, dim3(ntl), dim3(LS_T), 0, e->stream, e->seg_tiles, grp, e->seg_first, (int64_t)n,
                          e->late_scan, e->headpos_scan);
       return FW_OK;
     };
