@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <array>
 #include <map>
+#include <mutex>
 #include <set>
 #include <cstdlib>
 #include <cstdio>
@@ -236,7 +237,7 @@ __device__ __forceinline__ int64_t dir_lookup(const Spec& s, int64_t key) {
 
 // slice number m -> slot p, claiming a FREE slot.  Returns -1 when slot p holds another live slice.
 // Out of line: one call per wave and slice change on the hot path.
-__device__ __noinline__ int32_t slice_slot_at(int64_t* slice_tag, int32_t P, int64_t m) {
+__device__ __forceinline__ int32_t slice_slot_body(int64_t* slice_tag, int32_t P, int64_t m) {
   int32_t p = (int32_t)floor_mod(m, P);
   int64_t tag = slice_tag[p];
   if (tag == m) return p;
@@ -253,6 +254,7 @@ __device__ __noinline__ int32_t slice_slot_at(int64_t* slice_tag, int32_t P, int
   if ((int64_t)now == FREE_TAG || (int64_t)now == m) return p;
   return -1;
 }
+__device__ __noinline__ int32_t slice_slot_at(int64_t* slice_tag, int32_t P, int64_t m) { return slice_slot_body(slice_tag, P, m); }
 __device__ __forceinline__ int32_t slice_slot(const Spec& s, int64_t m) { return slice_slot_at(s.slice_tag, s.P, m); }
 
 // the identity of the sum: 0, or -0.0 for doubles (x + -0.0 == x for every x, -0.0 included; +0.0 would
@@ -472,7 +474,7 @@ __device__ __forceinline__ int64_t window_start_n(const Spec& s, int64_t n) {
 // .onElement FIRE, EventTimeTrigger.java:38-40; WindowOperator.java:317-325): its slice update joins the
 // commit list (applied in arrival order by k_late_commit); for sliding windows every such window of the
 // record also gets a fire element (tumbling: the slice is the window, the commit list serves as both)
-__device__ void late_append_at(const Spec& s, const BatchIn& b, unsigned long long pos, int32_t p, int64_t kid, int64_t m,
+__device__ __forceinline__ void late_append_at(const Spec& s, const BatchIn& b, unsigned long long pos, int32_t p, int64_t kid, int64_t m,
                                int64_t i) {
   const unsigned long long pane = (unsigned long long)p * (unsigned long long)s.stride + (unsigned long long)kid;
   if ((int64_t)pos < b.late_capacity) b.late_key[pos] = (pane << b.idx_bits) | (unsigned long long)i;
@@ -654,6 +656,7 @@ constexpr int AG_THREADS = 1024;
 #endif
 constexpr int AG_WIN = FW_AG_WIN;       // k_aggregate: directory slots probed without a branch
 constexpr int AG_CHS = 1024;            // k_aggregate wave steps (64 records each) tabulated per chunk
+constexpr int AG_LOOK = 8;              // k_aggregate: segment ends a lane compares per step (independent reads)
 constexpr int AG_MAXPER = 17;           // k_aggregate segment-offset scan: ntiles + 1 <= 17 * AG_THREADS
 constexpr int AG_SPLIT_MAX = 31;        // k_aggregate: shares a hot bucket is split into, at most 
 #ifndef FW_AGG_SPLIT_INT
@@ -668,8 +671,11 @@ constexpr uint32_t NO_FIRST = 0xFFFFFFFFu;
 struct RouteBuf {
   longlong2* kv;         // [ntiles][RT_TILE] routed records (fmix64(key), value), each tile sorted by bin
   uint16_t* idx;         // [ntiles][RT_TILE] record index within its tile (first arrival)
-  uint16_t* seg;         // [ntiles][RT_GROUPS * nb + 1] start of each bin's segment in the tile; [last] = count
+  uint32_t* seg;         // [RT_GROUPS * nb][seg_stride] bucket-major: row (group, bucket), one word per tile: the
+                         // segment's start | end << 16 in the tile (written for the tile's live groups only)
+  int64_t seg_stride;    // tiles per row (max_tiles)
   int64_t* hdr;          // [ntiles][RT_Q] slice number of the tile's routed bin group q (FREE_TAG = unused)
+  uint32_t* tdir;        // [ntiles] the tile has direct-group records (its direct / fire rows are written)
   // hot buckets split over helper workgroups (k_aggregate): per-bucket routed records of the previous /
   // this / a retired batch (ring), the serialised-fold flags, the helpers launched, the batch tag
   unsigned int* bload_prev;
@@ -689,6 +695,7 @@ struct RouteBuf {
   long long* stamps;     // diagnostics (FW_DEBUG_AGG & 16): per-workgroup phase timestamps, 8 per workgroup
   int32_t ntiles;
   int32_t dbg;
+  int32_t only_direct;   // k_aggregate behind k_agg_f: takes the batch only if it has direct-group records
 };
 
 // Non-temporal access of the streamed columns, a bit mask: 1 = k_route's input loads (on: k_route 43 ->
@@ -819,7 +826,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     const uint64_t cm = __ballot(c0);
     if (cm && s.size < (1LL << 60)) {
       const int64_t ts0 = uniform64(__shfl(tt[0], __ffsll((long long)cm) - 1));
-      w0 = record_windows(s, ts0, b.wm);
+      w0 = record_windows<true>(s, ts0, b.wm);   // (inline: a call here made the whole kernel keep the calling convention)
       w0.m = uniform64(w0.m); w0.lo = uniform64(w0.lo); w0.hi = uniform64(w0.hi);
       w0.n_late = __builtin_amdgcn_readfirstlane(w0.n_late);
       w0.n_fire = __builtin_amdgcn_readfirstlane(w0.n_fire);
@@ -944,12 +951,22 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   }
   if (direct_mask != 0) *any_direct = 1;
   __syncthreads();   // every wave's slice claims are in lset, every staging read is done
-  if (threadIdx.x == 0 && *any_direct) atomicOr(r.dflag, 1u);
+  const bool tile_direct = *any_direct != 0;
+  if (threadIdx.x == 0) {
+    if (tile_direct) atomicOr(r.dflag, 1u);
+    r.tdir[blockIdx.x] = tile_direct ? 1u : 0u;
+  }
   if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
   FW_STAMP(r, 0, 2);
   block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
-  uint16_t* seg = r.seg + (int64_t)blockIdx.x * (nbq + 1);
-  for (int x = threadIdx.x; x <= nbq; x += NT) seg[x] = (uint16_t)cnt[x];
+  // the segment table, bucket-major (row (group, bucket) holds one word per tile: start | end << 16), so that the
+  // k_aggregate workgroup owning a bucket reads its rows contiguously; only the tile's live groups are written
+  // (its routed slices, and the direct / fire groups when it has direct records), k_aggregate reads no other
+  for (int x = threadIdx.x; x < nbq; x += NT) {
+    const int g = x / s.nb;
+    const bool live = g < RT_Q ? lset[g] != FREE_TAG : tile_direct;
+    if (live) r.seg[(int64_t)x * r.seg_stride + blockIdx.x] = (uint32_t)cnt[x] | ((uint32_t)cnt[x + 1] << 16);
+  }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (bin[k] >= 0) {
@@ -979,8 +996,9 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
 }
 
 template <int VT, int AGG, bool FIRST>
-__global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, RouteBuf r) {
+__global__ __launch_bounds__(RT_THREADS, 4) void k_route(const Spec* __restrict__ sd, BatchIn b, RouteBuf r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Spec& s = *sd;   // device copy (kernel arguments by value are held in scalar registers from entry)
   // every tile but the last is whole, so its 16-B loads need no bounds (uniform branch)
   route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(blockIdx.x + 1) * RT_TILE > b.n);
 }
@@ -988,8 +1006,8 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(Spec s, BatchIn b, Rout
 // the bucket's LDS directory-hash table: slot of h, inserting its key (fmix64_inv(h)) into the global
 // directory if absent (the same linear probe sequence as dir_find_or_insert).  Out of line: taken by a
 // wave only when a lane misses the probed windows.
-__device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h,
-                                                 unsigned long long* inserted) {
+__device__ __forceinline__ int32_t agg_probe_insert_body(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h,
+                                                        unsigned long long* inserted) {
   uint32_t x = (uint32_t)h & kbm;
   for (uint32_t probe = 0; probe <= kbm; ++probe) {
     const uint64_t cur = lh[x];
@@ -1006,6 +1024,10 @@ __device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys
     x = (x + 1) & kbm;
   }
   return -1;
+}
+__device__ __noinline__ int32_t agg_probe_insert(uint64_t* lh, int64_t* dir_keys, uint32_t kbm, uint64_t h,
+                                                 unsigned long long* inserted) {
+  return agg_probe_insert_body(lh, dir_keys, kbm, h, inserted);
 }
 
 // the bucket's LDS accumulators
@@ -1112,7 +1134,7 @@ __host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_
   return (size_t)8 * ((size_t)1 << kb_bits) + ((size_t)(1 << kb_bits) + 65) * (8 * nacc + (by ? 4 : 0)) +
          ((((size_t)(1 << kb_bits) + 65) + 3) & ~(size_t)3) * 4 + (size_t)(8 * RT_Q + 4 * RT_GROUPS) * ntiles +
          8 * (size_t)ntiles + 4 +
-         4 * (size_t)AG_CHS + 64 + 8 + 8 * RT_GS + 8 + 4 * (size_t)(RT_MAXNB + 4);
+         4 * (size_t)AG_CHS + 4 * (size_t)AG_LOOK + 64 + 8 + 8 * RT_GS + 8 + 4 * (size_t)(RT_MAXNB + 4);
 }
 
 // SKEW: the variant for skewed key distributions (the host launches it when the posted bucket loads ask
@@ -1134,7 +1156,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   int owner_bkt = vb >= s.nb ? -1
                         : (s.nb % 8 == 0 && !(r.dbg & 32)) ? (vb % 8) * (s.nb / 8) + vb / 8
                                                           : vb;
-  const int nbq = RT_GROUPS * s.nb;
   const int KB = 1 << s.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
   const int KA = KB + 65;                               // accumulators: KB slots, one dummy per lane, the MIN key
@@ -1151,14 +1172,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   int64_t* lhdr = (int64_t*)(lord + (BY ? ((KA + 3) & ~3) : 0)); // [ntiles][RT_Q] the tiles' routed slices
   uint32_t* lseg = (uint32_t*)(lhdr + (int64_t)r.ntiles * RT_Q);   // [ntiles][RT_GROUPS] this bucket's segment start | end << 16
   int32_t* sst = (int32_t*)(lseg + (int64_t)r.ntiles * RT_GROUPS); // [ntiles] segment start within the tile
-  int32_t* off = sst + r.ntiles;                        // [ntiles + 1] segment lengths, then their exclusive prefix
-  int32_t* step_tile = off + r.ntiles + 1;              // [AG_CHS] tile holding the first record of each step
+  int32_t* off = sst + r.ntiles;                        // [ntiles + 1] segment lengths, then their exclusive prefix;
+                                                        // then AG_LOOK entries of INT32_MAX (the step lookup's reads)
+  int32_t* step_tile = off + r.ntiles + 1 + AG_LOOK;    // [AG_CHS] tile holding the first record of each step
   int32_t* awtot = step_tile + AG_CHS;                  // [16] scan scratch
   int64_t* gsl = (int64_t*)(((uintptr_t)(awtot + 16) + 7) & ~(uintptr_t)7);   // [RT_GS] the batch's slices
   int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
   int32_t* plan = (int32_t*)(gsl + RT_GS) + 2;          // [RT_MAXNB + 1] helper prefix; then bucket, share, shares
   const int64_t SB = (int64_t)8 << 16;
-  FW_STAMP(r, SB, 0);
+  if (!(!SKEW && r.only_direct)) FW_STAMP(r, SB, 0);   // (k_agg_f stamps its own)
   // Hot buckets (skewed keys) are split over helper workgroups launched after the nb owners: bucket b
   // with L_b routed records last batch gets S_b = clamp(ceil(L_b / chunk), 1, AG_SPLIT_MAX) shares, share
   // s taking tiles [s T / S_b, (s + 1) T / S_b) (tiles are in arrival order, so share order is arrival
@@ -1228,23 +1250,37 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     for (int g = threadIdx.x; g < RT_GS; g += NT) r.fold_cnt_zero[(int64_t)bkt * RT_GS + g] = 0u;
   // does any tile hold direct-group records (the batch's flag; no: skip all direct work)
   const bool has_direct = __builtin_amdgcn_readfirstlane(*r.dflag) != 0;
+  if (!SKEW && r.only_direct && !has_direct) return;   // uniform: k_agg_f took the batch
   // every tile's header and this bucket's segment bounds in each of its bin groups, plus the bucket's
   // directory slice, into LDS: all loads independent, one round trip
+  // (the bucket's rows of the bucket-major segment table are contiguous; a row's word is read only where the tile
+  // wrote it: a live routed group, or a tile with direct records)
   for (int t = threadIdx.x; t < r.ntiles; t += NT) {
-    const uint16_t* seg = r.seg + (int64_t)t * (nbq + 1);
     int64_t h[RT_Q];
     uint32_t sg[RT_GROUPS];
+    uint32_t td = 0;
+    // every load independent (one round trip); words a tile did not write are masked after
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q) h[q] = r.hdr[(int64_t)t * RT_Q + q];
 #pragma unroll
-    for (int q = 0; q < RT_GROUPS; ++q)
-      sg[q] = q < RT_Q || has_direct ? (uint32_t)seg[q * s.nb + bkt] | ((uint32_t)seg[q * s.nb + bkt + 1] << 16) : 0u;
+    for (int q = 0; q < RT_Q; ++q) sg[q] = r.seg[(int64_t)(q * s.nb + bkt) * r.seg_stride + t];
+    if (has_direct) {   // uniform
+      td = r.tdir[t];
+#pragma unroll
+      for (int q = RT_Q; q < RT_GROUPS; ++q) sg[q] = r.seg[(int64_t)(q * s.nb + bkt) * r.seg_stride + t];
+    }
+#pragma unroll
+    for (int q = 0; q < RT_GROUPS; ++q) {
+      const bool live = q < RT_Q ? h[q] != FREE_TAG : td != 0u;
+      if (!live) sg[q] = 0u;
+    }
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q) lhdr[t * RT_Q + q] = h[q];
 #pragma unroll
     for (int q = 0; q < RT_GROUPS; ++q) lseg[t * RT_GROUPS + q] = sg[q];
   }
   for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
+  if (threadIdx.x < AG_LOOK) off[r.ntiles + 1 + threadIdx.x] = INT32_MAX;
   // claimed early (slice_slot is idempotent): the slot of tile 0's first routed slice, nearly always the
   // batch's only one
   int64_t m_pre = FREE_TAG;
@@ -1440,8 +1476,13 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
           int32_t t = 0;
           int64_t pos = 0;   // inactive lanes read tile 0's first slot
           if (ra[u]) {
-            t = step_tile[st];
-            while (off[t + 1] <= rr) ++t;
+            // the step's tiles start at t0 (wave-uniform): the segment ends at or below rr among the next
+            // AG_LOOK are counted with independent (broadcast) LDS reads, not walked one dependent read at a time
+            const int32_t t0 = step_tile[st];
+            t = t0;
+#pragma unroll
+            for (int j = 1; j <= AG_LOOK; ++j) t += off[t0 + j] <= rr ? 1 : 0;
+            while (off[t + 1] <= rr) ++t;   // a step over more than AG_LOOK segments (short or empty ones)
             pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
           }
           rv[u] = r.kv[pos];
@@ -1623,6 +1664,366 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       atomicAdd(&s.stats[ST_SHARES], 1ull);
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_agg_f: k_aggregate's fast form, for batches without direct-group records (the usual case: every record of
+// a tile in one of its RT_Q routed slices) and reduces without maxBy / minBy.  The same result as
+// k_aggregate<..., SKEW = false>; shaped for the register file: the bucket size (KBL) and the LDS layout are
+// compile-time (no scalar register per LDS array), the kernel's arguments are one small structure (the
+// engine's constants are read from a device-resident AggCold where they are used), the slice-slot claim's
+// load is issued before the main loop and consumed at the fold, and a batch with direct-group records is left
+// whole to the general kernel launched behind it (k_aggregate, only_direct).  Each lane finds its record's
+// tile with independent LDS reads.
+// ------------------------------------------------------------------------------------------------
+#ifndef AGF_OCC
+#define AGF_OCC 4
+#endif
+#ifndef AGF_EXP
+#define AGF_EXP 0
+#endif
+constexpr int AGF_MAXT = 2048;   // tiles per batch the fast form holds (8 Mi records)
+#ifndef AGF_WIN_N
+#define AGF_WIN_N 8
+#endif
+#ifndef AGF_LOOK_N
+#define AGF_LOOK_N 8
+#endif
+constexpr int AGF_WIN = AGF_WIN_N;   // directory slots compared per probe, branch-free (the full probe beyond)
+constexpr int AGF_LOOK = AGF_LOOK_N; // segment ends a lane compares per step (independent reads)
+constexpr int AGF_OFF = (AGF_MAXT + 1 + AG_LOOK + 1) & ~1;   // (AGF_LOOK <= AG_LOOK)   // k_agg_f's prefix array (even: 8-B alignment after it)
+
+struct AggCold {   // device-resident, constant per engine
+  int64_t* dir_keys;
+  int64_t* slice_tag;
+  Cols c;
+  int32_t* err;
+  unsigned long long* stats;
+  int32_t* dir_min_used;
+  unsigned int* bload;          // [4][RT_MAXNB] ring (k_aggregate's skew plan)
+  unsigned int* fold_flag;      // [5][RT_MAXNB][RT_GS]: flags, then the fold-count ring
+  unsigned int* dflags;         // [FLAG_RING]
+  unsigned int* bload_host;
+  long long* stamps;
+  int64_t stride, D;
+  int32_t P, nb, seg_stride, cmpto;
+};
+
+struct AggFast {   // by value, per batch
+  const longlong2* kv;
+  const uint16_t* idx;
+  const uint32_t* seg;
+  const int64_t* hdr;
+  const int64_t* f1col;
+  const int64_t* dir_keys;
+  unsigned int* dflags;
+  const AggCold* cold;
+  int64_t ord_base;
+  int32_t ntiles;
+  uint32_t batch;   // the engine's batch counter (rings)
+  int32_t dbg;
+  int32_t seg_stride;
+};
+
+#ifndef AGF_COLD_ATOMIC
+#define AGF_COLD_ATOMIC 0
+#endif
+template <typename T>
+__device__ __forceinline__ T cold_ld(T const* p) {   // a read of AggCold where it is used
+#if AGF_COLD_ATOMIC
+  return (T)__hip_atomic_load((const T*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void cold_cap_error(const AggCold* cold, int site) {   // cap_error of k_aggregate
+  set_error(cold_ld(&cold->err), FW_ERR_CAPACITY);
+  atomicCAS(&cold_ld(&cold->stats)[7], 0ull, (unsigned long long)site);
+}
+
+template <int AGG, int KBL>
+__host__ __device__ constexpr size_t agf_lds_bytes() {
+  constexpr size_t KB = (size_t)1 << KBL, KA = KB + 65;
+  constexpr int nacc = 1 + ((AGG & FW_AGG_MIN) ? 1 : 0) + ((AGG & FW_AGG_MAX) ? 1 : 0) + ((AGG & FW_AGG_COUNT) ? 1 : 0);
+  return 8 * KB + 8 * KA * nacc + 4 * ((KA + 3) & ~(size_t)3) + 4 * (size_t)AGF_MAXT * 4 + 4 * (size_t)AGF_OFF +
+         4 * (size_t)AG_CHS + 4 * 16 + 8 * RT_GS + 4 * RT_GS + 16;
+}
+
+template <int VT, int AGG, bool FIRST, int KBL>
+__global__ __launch_bounds__(AG_THREADS, AGF_OCC) void k_agg_f(AggFast a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NT = AG_THREADS;
+  constexpr int KB = 1 << KBL;
+  constexpr uint32_t kbm = (uint32_t)KB - 1;
+  constexpr int KA = KB + 65;   // KB slots, one dummy per lane, the Long.MIN_VALUE key (direct form only: unused)
+  constexpr bool HAS_MIN = (AGG & FW_AGG_MIN) != 0, HAS_MAX = (AGG & FW_AGG_MAX) != 0, HAS_CNT = (AGG & FW_AGG_COUNT) != 0;
+  // the layout, at compile-time offsets
+  uint64_t* lh = (uint64_t*)smem;
+  int64_t* lsum = (int64_t*)(lh + KB);
+  int64_t* lmin = lsum + KA;
+  int64_t* lmax = lmin + (HAS_MIN ? KA : 0);
+  int64_t* lcnt = lmax + (HAS_MAX ? KA : 0);
+  uint32_t* lfirst = (uint32_t*)(lcnt + (HAS_CNT ? KA : 0));
+  uint32_t* lseg0 = lfirst + ((KA + 3) & ~3);   // [AGF_MAXT] routed group 0's segment word (0 when the group is unused)
+  uint32_t* lseg1 = lseg0 + AGF_MAXT;           // ... group 1
+  uint32_t* lq = lseg1 + AGF_MAXT;              // [AGF_MAXT] round of group 0 | round of group 1 << 8 (0xFF: none)
+  int32_t* sst = (int32_t*)(lq + AGF_MAXT);     // [AGF_MAXT] this round's segment start in each tile
+  int32_t* off = sst + AGF_MAXT;                // [AGF_OFF] segment lengths, then their prefix, then INT32_MAX pads
+  int32_t* step_tile = off + AGF_OFF;
+  int32_t* awtot = step_tile + AG_CHS;
+  int64_t* gsl = (int64_t*)(awtot + 16);        // [RT_GS] the batch's routed slices (8-B aligned: AGF_OFF is even)
+  int32_t* gslot = (int32_t*)(gsl + RT_GS);     // [RT_GS] their slots
+  int32_t* nround = gslot + RT_GS;
+  const int ntiles = a.ntiles;
+  const AggCold* __restrict__ cold = a.cold;
+  const int nb = (int)gridDim.x;
+  const int vb = (int)blockIdx.x;
+  const int bkt = (nb % 8 == 0 && !(a.dbg & 32)) ? (vb % 8) * (nb / 8) + vb / 8 : vb;   // XCD-major (k_aggregate)
+  const int64_t dbase = (int64_t)bkt * KB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t slot_flag = a.batch % FLAG_RING;
+  long long* const stamps = cold_ld(&cold->stamps);
+#define AGF_STAMP(k) do { if (stamps && threadIdx.x == 0) stamps[((int64_t)8 << 16) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  AGF_STAMP(0);
+  // a batch with direct-group records goes whole to the general kernel behind this one: the flag is read with
+  // the prologue's loads (one round trip) and tested once they are issued
+  const unsigned int dflag = a.dflags[slot_flag];
+  // prologue, every load independent: two tiles per thread (headers, this bucket's words of routed groups 0 and
+  // 1), the bucket's directory slice
+  const int segrow = a.seg_stride;
+  int64_t h0[AGF_MAXT / NT], h1[AGF_MAXT / NT];
+#pragma unroll
+  for (int k = 0; k < AGF_MAXT / NT; ++k) {
+    const int t = k * NT + (int)threadIdx.x;
+    h0[k] = FREE_TAG; h1[k] = FREE_TAG;
+    if (t < ntiles) {
+      h0[k] = a.hdr[(int64_t)t * RT_Q];
+      h1[k] = a.hdr[(int64_t)t * RT_Q + 1];
+      const uint32_t s0 = a.seg[(int64_t)bkt * segrow + t], s1 = a.seg[(int64_t)(nb + bkt) * segrow + t];
+      lseg0[t] = h0[k] != FREE_TAG ? s0 : 0u;
+      lseg1[t] = h1[k] != FREE_TAG ? s1 : 0u;
+    }
+  }
+  {
+    const int64_t* dir = a.dir_keys + dbase;
+    for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)dir[x]);
+  }
+  if (__builtin_amdgcn_readfirstlane(dflag) != 0) return;   // uniform (no barrier passed yet)
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.dflags[(a.batch + FLAG_RING / 2) % FLAG_RING] = 0u;   // (the flag ring)
+  for (int x = threadIdx.x; x < KA; x += NT) {
+    lsum[x] = sum_identity(VT);
+    if (HAS_MIN) lmin[x] = INT64_MAX;
+    if (HAS_MAX) lmax[x] = INT64_MIN;
+    if (HAS_CNT) lcnt[x] = 0;
+    lfirst[x] = NO_FIRST;
+  }
+  if (threadIdx.x < AG_LOOK) off[AGF_MAXT + 1 + threadIdx.x] = INT32_MAX;
+  if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
+  if (threadIdx.x == 0) *nround = 0;
+  {
+    unsigned int* fold_flag = cold_ld(&cold->fold_flag);   // the skew variant's fold-count ring, kept consistent
+    unsigned int* fz = fold_flag + (size_t)(1 + (a.batch + 2) % 4) * RT_MAXNB * RT_GS;
+    if (threadIdx.x < RT_GS) fz[(int64_t)bkt * RT_GS + threadIdx.x] = 0u;
+  }
+  __syncthreads();
+  // the batch's routed slices (every workgroup builds the same set, in the same first-seen order; a lane whose
+  // slice equals its left neighbour's defers to it)
+#pragma unroll
+  for (int k = 0; k < AGF_MAXT / NT; ++k) {
+#pragma unroll
+    for (int q = 0; q < RT_Q; ++q) {
+      const int64_t m = q == 0 ? h0[k] : h1[k];
+      const int64_t left = __shfl_up(m, 1);
+      if (m != FREE_TAG && !(lane != 0 && left == m)) {
+        int g = 0;
+        for (; g < RT_GS; ++g) {
+          const int64_t cur = gsl[g];
+          if (cur == m) break;
+          if (cur == FREE_TAG) {
+            const unsigned long long prev = atomicCAS((unsigned long long*)&gsl[g], (unsigned long long)FREE_TAG,
+                                                      (unsigned long long)m);
+            if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) break;
+          }
+        }
+        if (g == RT_GS) cold_cap_error(cold, 6);   // more distinct slices in one batch than RT_GS
+      }
+    }
+  }
+  __syncthreads();
+  // each tile's groups -> rounds; the slots of the rounds' slices: thread 0 reads the tags now and claims at the
+  // fold (the load is in flight through the main loop)
+#pragma unroll
+  for (int k = 0; k < AGF_MAXT / NT; ++k) {
+    const int t = k * NT + (int)threadIdx.x;
+    if (t < ntiles) {
+      uint32_t r0 = 0xFF, r1 = 0xFF;
+      for (int g = 0; g < RT_GS; ++g) {
+        const int64_t m = gsl[g];
+        if (m == FREE_TAG) break;
+        if (m == h0[k]) r0 = (uint32_t)g;
+        if (m == h1[k]) r1 = (uint32_t)g;
+      }
+      lq[t] = r0 | (r1 << 8);
+    }
+  }
+  AGF_STAMP(1);
+  int64_t* const slice_tag = cold_ld(&cold->slice_tag);
+  const int32_t P = cold_ld(&cold->P);
+  const int64_t stride = cold_ld(&cold->stride);
+  const bool cmpto = cold_ld(&cold->cmpto) != 0;
+  const AggLds L{lsum, lmin, lmax, lcnt, lfirst, nullptr};
+  int32_t routed = 0;
+  for (int g = 0; g < RT_GS; ++g) {
+    const int64_t m = gsl[g];   // (uniform)
+    if (m == FREE_TAG) break;
+    int64_t tagv = FREE_TAG;
+    if (threadIdx.x == 0) tagv = slice_tag[floor_mod(m, P)];   // consumed at the fold
+    for (int t = threadIdx.x; t < ntiles; t += NT) {
+      const uint32_t qq = lq[t];
+      uint32_t sg = 0;
+      if ((qq & 0xFFu) == (uint32_t)g) sg = lseg0[t];
+      else if (((qq >> 8) & 0xFFu) == (uint32_t)g) sg = lseg1[t];
+      sst[t] = (int32_t)(sg & 0xFFFFu);
+      off[t] = (int32_t)(sg >> 16) - (int32_t)(sg & 0xFFFFu);
+    }
+    if (threadIdx.x == 0) off[ntiles] = 0;
+    __syncthreads();
+    block_scan_excl<NT, AG_MAXPER>(off, ntiles + 1, awtot);   // off[ntiles] = the bucket's records of slice m
+    // (off past ntiles: INT32_MAX for the lookup; entries between ntiles + 1 and AGF_MAXT are never read)
+    if (threadIdx.x < AG_LOOK) off[ntiles + 1 + threadIdx.x] = INT32_MAX;
+    const int32_t R = off[ntiles];
+    routed += R;
+    AGF_STAMP(2);
+    constexpr int UR = FW_AGG_UR;
+    for (int32_t cb = 0; cb < R; cb += AG_CHS * 64) {   // uniform
+      __syncthreads();
+      for (int t = threadIdx.x; t < ntiles; t += NT) {
+        const int32_t o = off[t], l = off[t + 1] - o;
+        if (l == 0) continue;
+        const int32_t s_lo = max(0, (o - cb + 63) >> 6), s_hi = min(AG_CHS, (o + l - cb + 63) >> 6);
+        for (int32_t st = s_lo; st < s_hi; ++st) step_tile[st] = t;
+      }
+      __syncthreads();
+      const int32_t nsteps = min(AG_CHS, (R - cb + 63) >> 6);
+      auto load = [&](int32_t s0, longlong2* rv, uint32_t* ri, bool* ra) {
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+          const int32_t st = s0 + u;
+          const int32_t rr = cb + 64 * st + lane;
+          ra[u] = st < nsteps && rr < R;
+          int32_t t = 0;
+          int64_t pos = 0;
+          if (ra[u]) {
+            const int32_t t0 = step_tile[st];
+            t = t0;
+#pragma unroll
+            for (int j = 1; j <= AGF_LOOK; ++j) t += off[t0 + j] <= rr ? 1 : 0;
+            while (off[t + 1] <= rr) ++t;
+            pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
+          }
+          rv[u] = a.kv[pos];
+          ri[u] = ((uint32_t)t << IDX_BITS) | (FIRST ? (uint32_t)a.idx[pos] : 0u);
+        }
+      };
+      auto process = [&](const longlong2* rv, const uint32_t* ri, const bool* ra) {
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+          const uint64_t h = (uint64_t)rv[u].x;
+          const uint32_t h0 = (uint32_t)h & kbm;
+          uint32_t kl = h0;
+          bool found = false;
+#pragma unroll
+          for (int j = AGF_WIN - 1; j >= 0; --j) {
+            const uint32_t x = (h0 + j) & kbm;
+            const bool mt = lh[x] == h;
+            kl = mt ? x : kl;
+            found |= mt;
+          }
+          bool act = ra[u];
+#if AGF_EXP & 1
+          if (false) {
+#else
+          if (__any(act && !found) && act && !found) {   // displaced beyond the window, or a new key
+#endif
+            const int32_t x = agg_probe_insert_body(lh, cold_ld(&cold->dir_keys) + dbase, kbm, h,
+                                                    cold_ld(&cold->stats) + ST_DIR_KEYS);
+            if (x < 0) { cold_cap_error(cold, 8); act = false; }
+            else kl = (uint32_t)x;
+          }
+          kl = act ? kl : (uint32_t)KB + (uint32_t)lane;
+          acc_add<VT, AGG>(L, cmpto, false, 0, kl, rv[u].y, ri[u]);
+        }
+      };
+      longlong2 rvA[UR], rvB[UR];
+      uint32_t riA[UR], riB[UR];
+      bool raA[UR], raB[UR];
+      constexpr int32_t G = (NT / 64) * UR;
+      int32_t s0 = wave * UR;
+      if (s0 < nsteps) load(s0, rvA, riA, raA);
+      while (s0 < nsteps) {   // wave-uniform
+        if (s0 + G < nsteps) load(s0 + G, rvB, riB, raB);
+        process(rvA, riA, raA);
+        s0 += G;
+        if (s0 >= nsteps) break;
+        if (s0 + G < nsteps) load(s0 + G, rvA, riA, raA);
+        process(rvB, riB, raB);
+        s0 += G;
+      }
+    }
+    // the slice's slot (authoritative here: after every earlier watermark, engine stream order)
+    if (threadIdx.x == 0) {
+      int32_t p = (int32_t)floor_mod(m, P);
+      if (tagv != m) p = slice_slot_body(slice_tag, P, m);
+      gslot[g] = p;
+      if (p < 0) cold_cap_error(cold, 9);   // slice pool exhausted
+    }
+    __syncthreads();
+    AGF_STAMP(3);
+    const int32_t p = gslot[g];
+    // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes
+    if (p >= 0) {   // uniform
+      const Cols c = {cold_ld(&cold->c.sum), HAS_MIN ? cold_ld(&cold->c.mn) : nullptr, HAS_MAX ? cold_ld(&cold->c.mx) : nullptr,
+                      HAS_CNT ? cold_ld(&cold->c.cnt) : nullptr, FIRST ? cold_ld(&cold->c.first) : nullptr,
+                      FIRST ? cold_ld(&cold->c.f1v) : nullptr, FIRST ? nullptr : cold_ld(&cold->c.present)};
+      for (int x = threadIdx.x; x < KB; x += NT) {
+        const uint32_t lf = lfirst[x];
+        if (lf == NO_FIRST) continue;
+        const int64_t idx = (int64_t)p * stride + dbase + x;
+        if (AGG & FW_AGG_SUM) {
+          if (VT == FW_VALUE_I64) c.sum[idx] = jadd(c.sum[idx], lsum[x]);
+          else c.sum[idx] = __double_as_longlong(__longlong_as_double(c.sum[idx]) + __longlong_as_double(lsum[x]));
+        }
+        if (HAS_MIN) { const int64_t o = c.mn[idx]; if (lmin[x] < o) c.mn[idx] = lmin[x]; }
+        if (HAS_MAX) { const int64_t o = c.mx[idx]; if (lmax[x] > o) c.mx[idx] = lmax[x]; }
+        if (HAS_CNT) c.cnt[idx] = jadd(c.cnt[idx], lcnt[x]);
+        if (FIRST) {
+          if (a.ord_base + (int64_t)lf < c.first[idx]) {   // the pane's earliest record of the batch, if the pane is new
+            c.first[idx] = a.ord_base + (int64_t)lf;
+            c.f1v[idx] = a.f1col[lf];
+          }
+        } else {
+          c.present[idx] = 1;
+        }
+        lsum[x] = sum_identity(VT);
+        if (HAS_MIN) lmin[x] = INT64_MAX;
+        if (HAS_MAX) lmax[x] = INT64_MIN;
+        if (HAS_CNT) lcnt[x] = 0;
+        lfirst[x] = NO_FIRST;
+      }
+    }
+    __syncthreads();
+    AGF_STAMP(4);
+  }
+  if (threadIdx.x == 0) {   // the bucket's load: the next batch's split plan (k_aggregate)
+    unsigned int* bload = cold_ld(&cold->bload);
+    atomicAdd(&bload[(a.batch % 4) * RT_MAXNB + bkt], (unsigned)routed);
+    bload[((a.batch + 2) % 4) * RT_MAXNB + bkt] = 0u;
+#if !FW_NO_HOSTLOAD
+    unsigned int* bh = cold_ld(&cold->bload_host);
+    if (bh) __hip_atomic_store(&bh[bkt], (unsigned)routed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+  }
+#undef AGF_STAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2859,6 +3260,10 @@ struct fw_engine {
   int32_t max_tiles = 0;
   size_t route_lds = 0, agg_lds = 0;
   int agg_min_lds = 81 * 1024;
+  hipError_t attr_err = hipSuccess;         // routed_attrs_t: a failed hipFuncSetAttribute
+  Spec* s_dev = nullptr;                    // routed form: device copy of s (k_route), re-uploaded when s changes
+  AggCold* cold_dev = nullptr;              // ... the engine constants k_agg_f reads
+  AggCold cold_host{};
   // partition scratch
   int64_t* new_list = nullptr;                // direct form with first arrival: panes created per batch
   unsigned long long* new_counts = nullptr;   // one list length per batch parity
@@ -2964,6 +3369,13 @@ static int fail(fw_engine* e, int code, const std::string& msg) {
   if (_r == hipSuccess) _r = hipStreamSynchronize((e)->stream); \
   if (_r != hipSuccess) return fail(e, FW_ERR_DEVICE, std::string("after ") + (what) + ": " + hipGetErrorString(_r)); } } while (0)
 
+// the engine stream orders the copy before every later kernel; the host copy is the engine's own (stable)
+static int upload_spec(fw_engine* e) {
+  if (!e->s_dev) return FW_OK;
+  HIPCHK(e, hipMemcpyAsync(e->s_dev, &e->s, sizeof(Spec), hipMemcpyHostToDevice, e->stream));
+  return FW_OK;
+}
+
 static int launch_fill(fw_engine* e, int64_t* p, int64_t v, int64_t n) {
   if (!p || n <= 0) return FW_OK;
   int blocks = (int)std::min<int64_t>((n + BLOCK - 1) / BLOCK, 4096);
@@ -2977,15 +3389,48 @@ static void launch_ingest_t(fw_engine* e, const BatchIn& b) {
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL((k_ingest_direct<VT, AGG, FIRST>), dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b);
 }
+template <int VT, int AGG, bool FIRST, int KBL>
+static hipError_t agg_f_attr() {
+  if constexpr (agf_lds_bytes<AGG, KBL>() > 160 * 1024) return hipSuccess;
+  else return hipFuncSetAttribute((const void*)k_agg_f<VT, AGG, FIRST, KBL>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+// the routed kernels use dynamic LDS only, so the whole 160 KiB is grantable: the largest any engine may ask for,
+// set once per device and instantiation (engines may be created from several threads), from fw_create, which
+// fails with the HIP error when the attribute cannot be set
+template <int VT, int AGG, bool FIRST>
+static void routed_attrs_t(fw_engine* e) {
+  static std::mutex mu;
+  static std::set<int> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count(e->dev)) return;
+  const void* fns[] = {(const void*)k_route<VT, AGG, FIRST>, (const void*)k_aggregate<VT, AGG, FIRST, false>,
+                       (const void*)k_aggregate<VT, AGG, FIRST, true>};
+  for (const void* f : fns) {
+    const hipError_t rc = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (rc != hipSuccess) { e->attr_err = rc; return; }
+  }
+  for (hipError_t rc : {agg_f_attr<VT, AGG, FIRST, 9>(), agg_f_attr<VT, AGG, FIRST, 10>(), agg_f_attr<VT, AGG, FIRST, 11>(),
+                        agg_f_attr<VT, AGG, FIRST, 12>()})
+    if (rc != hipSuccess) { e->attr_err = rc; return; }
+  done.insert(e->dev);
+}
+
+// k_agg_f for buckets of 2^KBL slots, when its LDS fits; false: the general kernel takes the batch
+template <int VT, int AGG, bool FIRST, int KBL>
+static bool launch_agg_f(fw_engine* e, const AggFast& a) {
+  if constexpr (agf_lds_bytes<AGG, KBL>() > 160 * 1024) {
+    return false;
+  } else {
+    if ((int64_t)a.ntiles > AGF_MAXT || (e->rb.dbg & 256)) return false;   // (FW_DEBUG_AGG & 256: the general kernel)
+    const size_t lds = std::max<size_t>(agf_lds_bytes<AGG, KBL>(), (size_t)e->agg_min_lds);   // one workgroup per CU
+    hipLaunchKernelGGL((k_agg_f<VT, AGG, FIRST, KBL>), dim3(e->s.nb), dim3(AG_THREADS), lds, e->stream, a);
+    return true;
+  }
+}
+
 template <int VT, int AGG, bool FIRST>
 static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col, int par) {
-  static bool attr_set = false;
-  if (!attr_set) {   // the largest any engine may ask for
-    (void)hipFuncSetAttribute((const void*)k_route<VT, AGG, FIRST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_aggregate<VT, AGG, FIRST, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;   // both kernels use dynamic LDS only, so the whole 160 KiB is grantable
-  }
   RouteBuf r = e->rbs[par];
   r.ntiles = (int32_t)((b.n + RT_TILE - 1) / RT_TILE);
   r.dflag = e->dflags + (e->batches % FLAG_RING);
@@ -3021,7 +3466,7 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, (size_t)e->agg_min_lds);
   hipStream_t rs = e->serial ? e->stream : e->rstream;
   e->phase_begin(FW_PHASE_INGEST, rs);
-  hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, rs, e->s, b, r);
+  hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, rs, e->s_dev, b, r);
   e->phase_end(b.n, rs);
   (void)hipEventRecord(e->ev_route[par], rs);
   (void)hipStreamWaitEvent(e->stream, e->ev_route[par], 0);
@@ -3029,9 +3474,31 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   if (r.helpers > 0)
     hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, true>), dim3(e->s.nb + r.helpers), dim3(AG_THREADS), agg_lds, e->stream,
                        e->s, b, r, f1col);
-  else
+  else if ((AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) || (e->rb.dbg & 256))   // (FW_DEBUG_AGG & 256: the general kernel)
     hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b,
                        r, f1col);
+  else {
+    // k_agg_f takes a batch without direct-group records; the general kernel behind it takes the others (and
+    // returns at once for the rest: on the engine stream, which waits for the next k_route anyway)
+    AggFast a;
+    a.kv = r.kv; a.idx = r.idx; a.seg = r.seg; a.hdr = r.hdr; a.f1col = f1col; a.cold = e->cold_dev;
+    a.ord_base = b.ord_base; a.ntiles = r.ntiles; a.batch = (uint32_t)e->batches; a.dbg = r.dbg;
+    a.dir_keys = e->s.dir_keys; a.dflags = e->dflags; a.seg_stride = (int32_t)r.seg_stride;
+    bool fast = false;
+    switch (e->s.kb_bits) {
+      case 9: fast = launch_agg_f<VT, AGG, FIRST, 9>(e, a); break;
+      case 10: fast = launch_agg_f<VT, AGG, FIRST, 10>(e, a); break;
+      case 11: fast = launch_agg_f<VT, AGG, FIRST, 11>(e, a); break;
+      case 12: fast = launch_agg_f<VT, AGG, FIRST, 12>(e, a); break;
+      default: break;
+    }
+    RouteBuf rd = r;
+    rd.only_direct = fast ? 1 : 0;
+    if (!(fast && (r.dbg & 512)))   // (FW_DEBUG_AGG & 512, timing only: no general kernel behind k_agg_f — wrong for a
+                                    // batch with direct-group records)
+      hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b,
+                         rd, f1col);
+  }
   e->phase_end(b.n);
   // (ev_agg[par] is recorded by fw_push_batch once the batch's extra-window list is applied too)
 }
@@ -3073,6 +3540,9 @@ static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
 }
 
 // dispatch over (value type, aggregate mask, first-arrival) — the instantiated reduce shapes
+#ifdef FW_DISPATCH_C1_ONLY   // register / spill experiments: the C1 shape only (a library that serves nothing else)
+#define FW_DISPATCH(FN, e, ...) FN<0, 1, true>(e, ##__VA_ARGS__)
+#else
 #define FW_DISPATCH(FN, e, ...)                                                                  \
   do {                                                                                           \
     const Spec& _s = (e)->s;                                                                     \
@@ -3095,6 +3565,7 @@ static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
       }                                                                                          \
     }                                                                                            \
   } while (0)
+#endif
 
 extern "C" {
 
@@ -3339,17 +3810,29 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
         r = e->rb;
         r.kv = e->alloc<longlong2>(cap);
         r.idx = e->alloc<uint16_t>(cap);
-        r.seg = e->alloc<uint16_t>((size_t)(RT_GROUPS * s.nb + 1) * max_tiles);
+        r.seg = e->alloc<uint32_t>((size_t)RT_GROUPS * s.nb * max_tiles);
+        r.seg_stride = max_tiles;
         r.hdr = e->alloc<int64_t>((size_t)max_tiles * RT_Q);
+        r.tdir = e->alloc<uint32_t>((size_t)max_tiles);
         r.dm = e->alloc<int64_t>(cap);
       }
       e->route_lds = RT_LDS;
       const char* ml = getenv("FW_AGG_MIN_LDS_KB");
       e->agg_min_lds = (ml ? atoi(ml) : 81) * 1024;
       e->agg_lds = agg_need;   // at launch: less the unused tiles, at least agg_min_lds
+      FW_DISPATCH(routed_attrs_t, e);
+      if (e->attr_err != hipSuccess) {
+        g_create_error = std::string("hipFuncSetAttribute(MaxDynamicSharedMemorySize): ") + hipGetErrorString(e->attr_err);
+        delete e;
+        return FW_ERR_DEVICE;
+      }
     }
   }
   e->wm_done = e->alloc<unsigned int>(1);
+  if (e->routed) {
+    e->s_dev = e->alloc<Spec>(1);
+    e->cold_dev = e->alloc<AggCold>(1);
+  }
   if (s.first && !e->routed) {
     e->new_list = e->alloc<int64_t>((size_t)c.max_batch);
     e->new_counts = e->alloc<unsigned long long>(2);
@@ -3432,6 +3915,15 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
   if (e->bload) HIPCHK(e, hipMemsetAsync(e->bload, 0, 4 * 4 * RT_MAXNB, e->stream));
   if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)5 * RT_MAXNB * RT_GS, e->stream));
+  if (e->routed) {   // k_route reads the Spec, k_agg_f the engine's constants, from device copies
+    AggCold& k = e->cold_host;
+    k.dir_keys = s.dir_keys; k.slice_tag = s.slice_tag; k.c = s.c; k.err = s.err; k.stats = s.stats;
+    k.dir_min_used = s.dir_min_used; k.bload = e->bload; k.fold_flag = e->fold_flag; k.dflags = e->dflags;
+    k.bload_host = e->bload_host; k.stamps = e->rb.stamps; k.stride = s.stride; k.D = s.D; k.P = s.P; k.nb = s.nb;
+    k.seg_stride = e->max_tiles; k.cmpto = s.cmpto;
+    HIPCHK(e, hipMemcpyAsync(e->cold_dev, &e->cold_host, sizeof(AggCold), hipMemcpyHostToDevice, e->stream));
+    if (int rc = upload_spec(e)) return rc;
+  }
   HIPCHK(e, hipStreamSynchronize(e->stream));
   HIPCHK(e, hipGetLastError());
   if (e->debug_sync && (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess)) {
@@ -4705,6 +5197,7 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   if (!dis_now.empty() && !e->s.disarm) {   // per-slot flags and per-pane re-arm marks, first needed here
     e->s.disarm = e->alloc<uint8_t>((size_t)s.P);
     e->s.armed = e->alloc<uint8_t>((size_t)s.P * (size_t)s.stride);
+    if (int rc = upload_spec(e)) return rc;
     if (!e->s.disarm || !e->s.armed) return reject(e, FW_ERR_DEVICE, "out of device memory");
     HIPCHK(e, hipMemset(e->s.disarm, 0, (size_t)s.P));
     HIPCHK(e, hipMemset(e->s.armed, 0, (size_t)s.P * (size_t)s.stride));
