@@ -41,7 +41,7 @@ FW_MEM_DEVICE = 1
 
 # every entry point include/flink_window.h declares
 EXPORTED_SYMBOLS = ("fw_create", "fw_push_batch", "fw_advance_watermark", "fw_sync", "fw_collect",
-                    "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_set_profiling",
+                    "fw_get_stats", "fw_last_error", "fw_destroy", "fw_partition_by_operator", "fw_partition_by_operator_last", "fw_set_profiling",
                     "fw_get_profile", "fw_debug_counters", "fw_debug_stamps", "fw_set_stream", "fw_stream_wait_input",
                     "fw_version", "fw_snapshot_kg", "fw_restore_kg", "fw_snapshot_kg_flink", "fw_restore_kg_flink", "fw_decode",
                     "fw_collect_begin", "fw_collect_end", "fw_decode_begin", "fw_decode_end")
@@ -108,6 +108,7 @@ def declare(lib, prefix="fw"):
         "last_error": (ctypes.c_char_p, [_p]),
         "destroy": (None, [_p]),
         "partition_by_operator": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p]),
+        "partition_by_operator_last": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _p, _p, _p, _p, _p, _p, _i32]),
         "version": (ctypes.c_char_p, []),
         "set_profiling": (_i32, [_p, _i32]),
         "get_profile": (_i32, [_p, P(FwProfile)]),

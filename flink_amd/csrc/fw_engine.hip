@@ -2453,7 +2453,8 @@ __global__ void k_fire_emit(Spec s, const unsigned long long* sorted_key, int64_
 // slots and records the watermark's position in the output log.
 // ------------------------------------------------------------------------------------------------
 constexpr int WM_THREADS = 1024;
-constexpr int WM_MAXT = 2048;      // windows firing at one watermark
+constexpr int WM_MAXT = MAX_P + MAX_K;   // windows firing at one watermark: every live slot's windows (a flush to
+                                         // Long.MAX_VALUE fires up to P + K - 1 of them at K slices per window)
 constexpr int WM_MAXP = MAX_P;     // slices purged at one watermark (>= P)
 constexpr int32_t PURGE_GHOST = 1 << 30;   // purge list flag: keep the panes' cleanup timers (Spec::gfirst)
 
@@ -2946,12 +2947,13 @@ __global__ __launch_bounds__(BLOCK) void k_part_count(const int64_t* key, const 
   for (int d = threadIdx.x; d < par; d += blockDim.x) block_counts[(int64_t)blockIdx.x * par + d] = cnt[d];
 }
 
-// one workgroup: per destination d (in order), an exclusive scan of the blocks' counts (column d of
-// [nblocks][par]) into per-block write offsets, after the totals of destinations 0..d-1; totals and
-// destination offsets out
+// one workgroup: per destination d (in output order), an exclusive scan of the blocks' counts (column d of
+// [nblocks][par]) into per-block write offsets, after the totals of the destinations before d; totals and
+// destination offsets out.  Output order: 0 .. par-1, or, with last >= 0, last + 1 .. par-1, 0 .. last (the
+// records of operator `last` at the end: a receiver appends what its peers send right behind its own share)
 constexpr int PART_SCAN_THREADS = 1024;
 __global__ __launch_bounds__(PART_SCAN_THREADS) void k_part_scan(int64_t* block_counts, int64_t nblocks, int32_t par,
-                                                                  int64_t* counts, int64_t* offsets) {
+                                                                  int64_t* counts, int64_t* offsets, int32_t last) {
   __shared__ int64_t wtot[PART_SCAN_THREADS / 64];
   __shared__ int64_t base;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2959,7 +2961,8 @@ __global__ __launch_bounds__(PART_SCAN_THREADS) void k_part_scan(int64_t* block_
   const int64_t b0 = (int64_t)threadIdx.x * per, b1 = min(b0 + per, nblocks);
   if (threadIdx.x == 0) base = 0;
   __syncthreads();
-  for (int32_t d = 0; d < par; ++d) {
+  for (int32_t di = 0; di < par; ++di) {
+    const int32_t d = last >= 0 ? (last + 1 + di) % par : di;
     int64_t sum = 0;
     for (int64_t b = b0; b < b1; ++b) sum += block_counts[b * par + d];
     int64_t incl = sum;
@@ -4170,6 +4173,8 @@ static int ghost_track(fw_engine* e, int64_t m) {
     if (floor_mod(o, e->s.P) == p)
       return fail(e, FW_ERR_CAPACITY, "purged windows' cleanup timers: two windows in one slice slot (raise max_open_slices)");
   e->ghost_windows.insert(m);
+  // the slot's column starts empty: a window that held slot p before left no ordinals behind to be inherited
+  if (int rc = launch_fill(e, e->s.gfirst + (size_t)p * (size_t)e->s.stride, INT64_MAX, e->s.stride)) return rc;
   return launch_fill(e, e->s.gtag + p, m, 1);
 }
 // the watermark moves from wm_old to wm_new: windows whose cleanup time it reaches drop their timers; windows it
@@ -4730,6 +4735,10 @@ int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* le
   if (!e->disarmed.empty())
     return reject(e, FW_ERR_UNSUPPORTED, "restored windows without trigger timers: only the reference layout (explicit "
                                          "timers, fw_snapshot_kg_flink) carries them");
+  if (e->s.gtag && !e->ghost_windows.empty())
+    return reject(e, FW_ERR_UNSUPPORTED, "PurgingTrigger with allowed lateness: purged windows within their lateness keep "
+                                         "cleanup timers without state, which only the reference layout "
+                                         "(fw_snapshot_kg_flink) carries");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)   // HeapInternalTimerService.restoreTimersForKeyGroup's check
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -4776,7 +4785,11 @@ int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   for (int64_t j = 0; j < n; ++j)
     if (host_key_group(e->s, ent[j * FW_SNAP_ENTRY_WORDS + 1]) != kg)
       return reject(e, FW_ERR_KEY_GROUP, "snapshot entry key outside its key group");
-  return restore_entries(e, h[4], ent, n);
+  if (int rc = restore_entries(e, h[4], ent, n)) return rc;
+  // PurgingTrigger + allowed lateness: the windows within their lateness at the restored watermark are tracked
+  // for their cleanup timers as after any watermark (fw_snapshot_kg took none with such timers pending)
+  if (e->s.gtag) return ghost_advance(e, INT64_MIN, e->cur_wm);
+  return FW_OK;
 }
 
 // load n validated snapshot entries (FW_SNAP_ENTRY_WORDS each) and set the watermark
@@ -5238,8 +5251,18 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
                              const int64_t* ts, const void* value, int64_t n, int32_t max_parallelism,
                              int32_t parallelism, int64_t* out_key, int32_t* out_key_hash, int64_t* out_f1,
                              int64_t* out_ts, void* out_value, int64_t* counts, int64_t* offsets) {
+  return fw_partition_by_operator_last(e, key, key_hash, f1, ts, value, n, max_parallelism, parallelism, out_key,
+                                       out_key_hash, out_f1, out_ts, out_value, counts, offsets, -1);
+}
+
+int fw_partition_by_operator_last(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1,
+                                  const int64_t* ts, const void* value, int64_t n, int32_t max_parallelism,
+                                  int32_t parallelism, int64_t* out_key, int32_t* out_key_hash, int64_t* out_f1,
+                                  int64_t* out_ts, void* out_value, int64_t* counts, int64_t* offsets,
+                                  int32_t last_operator) {
   if (!e) return FW_ERR_INVALID_ARG;
   if (parallelism <= 0 || parallelism > PART_MAX || max_parallelism < parallelism) return fail(e, FW_ERR_INVALID_ARG, "bad parallelism");
+  if (last_operator >= parallelism) return fail(e, FW_ERR_INVALID_ARG, "last_operator >= parallelism");
   HIPCHK(e, hipSetDevice(e->dev));
   int64_t nblocks = std::max<int64_t>((n + PART_CHUNK - 1) / PART_CHUNK, 1);
   if (nblocks * parallelism > e->part_blocks_cap) {
@@ -5252,7 +5275,8 @@ int fw_partition_by_operator(fw_engine* e, const int64_t* key, const int32_t* ke
   hipStream_t ps = e->has_client ? (hipStream_t)e->client : e->stream;
   hipLaunchKernelGGL(k_part_count, dim3((unsigned)nblocks), dim3(BLOCK), 0, ps, key, key_hash, n, max_parallelism,
                      parallelism, e->part_block_counts);
-  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PART_SCAN_THREADS), 0, ps, e->part_block_counts, nblocks, parallelism, counts, offsets);
+  hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PART_SCAN_THREADS), 0, ps, e->part_block_counts, nblocks, parallelism, counts, offsets,
+                     last_operator < 0 ? -1 : last_operator);
   hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblocks), dim3(BLOCK), 0, ps, key, key_hash, f1, ts,
                      (const int64_t*)value, n, max_parallelism, parallelism, e->part_block_counts, out_key, out_key_hash,
                      out_f1, out_ts, (int64_t*)out_value);

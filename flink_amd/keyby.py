@@ -7,11 +7,13 @@ Mirrors the reference's hash edge between source and window operator:
   watermark RecordWriterOutput.emitWatermark -> broadcastEmit (RecordWriterOutput.java:80-84, RecordWriter.java:92-95);
             the receiver keeps one watermark per input channel, raised only when a larger one arrives, and
             forwards min over channels only when that minimum increases  SJ/runtime/io/StreamInputProcessor.java:147-161
-MI355X form: the HIP partition kernel (fw_partition_by_operator) counting-sorts a batch by destination
-in HBM; one all-to-all of per-destination counts, one MIN all-reduce of the channels' watermarks, and
-the routed records: a rank's own share is pushed straight from the partition buffers (a local channel:
-no copy), the other shares move as one group of point-to-point sends/receives over xGMI (RCCL via
-torch.distributed backend "nccl": one group call for the three columns of every peer).
+MI355X form: the HIP partition kernel (fw_partition_by_operator_last) counting-sorts a batch by
+destination in HBM with the rank's own share last; one all-to-all of per-destination counts, one MIN
+all-reduce of the channels' watermarks, and the routed records: the other shares move as one group of
+point-to-point sends/receives over xGMI (RCCL via torch.distributed backend "nccl": one group call for the
+three columns of every peer), received into the same columns right behind the own share (a local channel:
+never copied), and the whole goes to the engine in ONE push per step (a push carries a fixed device cost,
+~15-20 us).
 
 Every rank is both a source subtask (its own watermark = one input channel of every window subtask)
 and a window subtask.  Because every watermark is broadcast, all window subtasks see the same channel
@@ -83,6 +85,7 @@ class KeyByExchange:
         self.cuda = self.device.type == "cuda"
         self.pipelined = self.cuda if pipelined is None else bool(pipelined)
         assert self.pipelined or not self.cuda, "the GPU path is pipelined"
+        self.pushes = 0                 # engine pushes made (one per step; more only for a share above max_batch)
         self.local_wm = LONG_MIN        # this source's channel watermark, only raised
         self.last_emitted = LONG_MIN    # last watermark forwarded to the window subtask
         self.emitted = []               # the forwarded watermarks, in order (tests)
@@ -94,7 +97,11 @@ class KeyByExchange:
             self.depth = depth
             S = self.depth + 1          # send sets: partition of batch j must not overwrite batch j - depth's
             z = lambda n, dt=torch.int64: torch.empty(n, dtype=dt, device=self.device)
-            self.send = [(z(batch), z(batch), z(batch)) for _ in range(S)]
+            # a send set holds the batch sorted by destination with the own share last, then what the peers send
+            # (received right behind it): batch + room for about a batch received; more (skew) regrows the set
+            self.batch = batch
+            cap = self._set_cap(batch)
+            self.send = [(z(cap), z(cap), z(cap)) for _ in range(S)]
             # per send set: [send counts | received counts | aligned watermark] in one device tensor, read
             # back by one copy
             self.meta = [torch.zeros(2 * world + 1, dtype=torch.int64, device=self.device) for _ in range(S)]
@@ -105,39 +112,44 @@ class KeyByExchange:
             self.ready = [torch.cuda.Event() if self.cuda else _HostEvent() for _ in range(S)]
             self.pending = deque()      # (set, batch size) staged, not yet finished
             self.staged = 0
-            self.send_pushed_at = [None] * S   # engine push index that last read each send set (own share)
-            # receive column sets: before a set is rewritten, torch's stream waits on the device for the
-            # engine to have read it (fw_stream_wait_input), no host synchronisation
-            self.RING = 3
-            self.ring = [None] * self.RING
-            self.pushed_at = [None] * self.RING   # engine push index that last read each set
+            # engine push index that last read each send set: before a set is rewritten, torch's stream waits on
+            # the device for the engine to have read it (fw_stream_wait_input), no host synchronisation
+            self.send_pushed_at = [None] * S
             self.finished = self.pushes = 0
             # the engine enqueues its partition on torch's stream, so the exchange below is ordered after it
             if self.cuda:
                 self.eng.use_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     # ------------------------------------------------------------------ routing
+    @staticmethod
+    def _set_cap(batch):
+        return int(2.25 * batch) + 64
+
+    def _dest_order(self):
+        """Destinations in the order the partition writes them: the own share last."""
+        return [(self.rank + 1 + i) % self.world for i in range(self.world)]
+
     def _route_cuda(self, k, t, v, si):
         n = k.numel()
-        if n > self.send[si][0].numel():
-            raise ValueError(f"batch of {n} records exceeds the exchange's batch capacity {self.send[si][0].numel()}")
+        if n > self.batch:
+            raise ValueError(f"batch of {n} records exceeds the exchange's batch capacity {self.batch}")
         P = lambda x: ctypes.c_void_p(x.data_ptr())
         sk, st, sv = self.send[si]
-        rc = self.eng.lib.fw_partition_by_operator(self.eng.h, P(k), None, None, P(t), P(v), n, self.mp, self.world,
-                                                   P(sk), None, None, P(st), P(sv), P(self.meta[si]),
-                                                   P(self.offsets[si]))
+        rc = self.eng.lib.fw_partition_by_operator_last(self.eng.h, P(k), None, None, P(t), P(v), n, self.mp, self.world,
+                                                        P(sk), None, None, P(st), P(sv), P(self.meta[si]),
+                                                        P(self.offsets[si]), self.rank)
         if rc != 0:
-            raise RuntimeError(f"fw_partition_by_operator failed: {rc}")
+            raise RuntimeError(f"fw_partition_by_operator_last failed: {rc}")
 
     def _route_into(self, k, t, v, si):
-        """Partition a source batch into send set si and its send counts (meta[si][:world])."""
+        """Partition a source batch into send set si (own share last) and its send counts (meta[si][:world])."""
         if self.cuda:
             self._route_cuda(k, t, v, si)
             return
         n = k.numel()
-        if n > self.send[si][0].numel():
-            raise ValueError(f"batch of {n} records exceeds the exchange's batch capacity {self.send[si][0].numel()}")
-        rk, rt, rv, counts = self._route_host(k, t, v)
+        if n > self.batch:
+            raise ValueError(f"batch of {n} records exceeds the exchange's batch capacity {self.batch}")
+        rk, rt, rv, counts = self._route_host(k, t, v, own_last=True)
         sk, st, sv = self.send[si]
         sk[:n].copy_(rk)
         st[:n].copy_(rt)
@@ -170,20 +182,25 @@ class KeyByExchange:
             self.pushes += 1
         return self.pushes - 1
 
-    def _route_host(self, k, t, v):
+    def _route_host(self, k, t, v, own_last=False):
         dest = operator_index_np(k.numpy(), self.mp, self.world)
-        order = np.argsort(dest, kind="stable")
+        # stable by destination; with own_last in the partition kernel's order (the own share at the end)
+        order = np.argsort((dest - self.rank - 1) % self.world if own_last else dest, kind="stable")
         counts = torch.from_numpy(np.bincount(dest, minlength=self.world).astype(np.int64))
         idx = torch.from_numpy(order)
         return k[idx], t[idx], v[idx], counts
 
-    def _transfer(self, send, send_splits, recv_splits, recv):
-        """The routed records between the ranks: `send` = (key, ts, value) sorted by destination with
-        send_splits per rank; the other ranks' shares land in `recv` (concatenated in rank order) through one
-        group of point-to-point sends / receives.  Returns this rank's own share: views of `send` (a local
-        channel, never copied).  Used by the GPU path (RCCL) and the CPU path (gloo) alike."""
+    def _transfer(self, send, send_splits, recv_splits, recv, order=None):
+        """The routed records between the ranks: `send` = (key, ts, value) sorted by destination (in `order`,
+        default rank order) with send_splits per rank; the other ranks' shares land in `recv` (concatenated in
+        rank order) through one group of point-to-point sends / receives.  Returns this rank's own share: views
+        of `send` (a local channel, never copied).  Used by the GPU path (RCCL) and the CPU path (gloo) alike."""
         me, w = self.rank, self.world
-        soff = np.concatenate([[0], np.cumsum(send_splits)]).astype(np.int64).tolist()
+        soff, o = [0] * (w + 1), 0
+        for d in (order or range(w)):
+            soff[d] = o
+            o += send_splits[d]
+        soff = {d: (soff[d], soff[d] + send_splits[d]) for d in range(w)}
         ops, roff = [], 0
         for p in range(w):
             if p == me:
@@ -193,11 +210,11 @@ class KeyByExchange:
                 ops += [dist.P2POp(dist.irecv, x[roff:roff + c], p) for x in recv]
                 roff += c
             if send_splits[p]:
-                ops += [dist.P2POp(dist.isend, x[soff[p]:soff[p + 1]], p) for x in send]
+                ops += [dist.P2POp(dist.isend, x[soff[p][0]:soff[p][1]], p) for x in send]
         if ops:
             for req in dist.batch_isend_irecv(ops):   # one group; on RCCL wait() orders torch's stream after it
                 req.wait()
-        return tuple(x[soff[me]:soff[me + 1]] for x in send)
+        return tuple(x[soff[me][0]:soff[me][1]] for x in send)
 
     def exchange(self, k, t, v):
         """CPU (gloo) path: route a source batch to the key-group owners; returns this rank's shares:
@@ -234,9 +251,12 @@ class KeyByExchange:
     def step(self, k, t, v, wm_local):
         """Source batch (k, t, v) followed by this source's watermark wm_local."""
         if not self.pipelined:
-            for rk, rt, rv in self.exchange(k, t, v):   # both shares between the same watermarks
-                if rk.numel():
-                    self.eng.push(rk.numpy(), rt.numpy(), rv.numpy())
+            # both shares between the same watermarks: one push, as the pipelined path
+            own, recv = self.exchange(k, t, v)
+            rk, rt, rv = (torch.cat([a, b]) for a, b in zip(own, recv))
+            if rk.numel():
+                self.eng.push(rk.numpy(), rt.numpy(), rv.numpy())
+                self.pushes += 1
             self._forward(self.align_watermark(wm_local))
             return
         # finish the oldest batch first: its push then waits (device-side) for the partitions enqueued so far
@@ -274,22 +294,23 @@ class KeyByExchange:
             send_splits, recv_splits, aligned = h[:1], h[:1], self.local_wm_at[si]
         me = self.rank
         m = sum(recv_splits) - recv_splits[me]   # received from the other ranks
-        slot = self.finished % self.RING
+        own_n = send_splits[me]
         self.finished += 1
-        cols = self.ring[slot]
-        if cols is None or cols[0].numel() < m:
-            if cols is not None:
-                self.eng.sync()   # growing: the old set is dropped only once nothing reads it
-            cap = max(m, int(1.25 * n))
-            cols = self.ring[slot] = [torch.empty(cap, dtype=torch.int64, device=self.device) for _ in range(3)]
-        else:
-            self._wait_read(self.pushed_at[slot])
-        rk, rt, rv = (x[:m] for x in cols)
         sk, st, sv = self.send[si]
-        own = self._transfer((sk[:n], st[:n], sv[:n]), send_splits, recv_splits, (rk, rt, rv))
-        # both shares lie between the same watermarks; a share above max_batch (skew) goes in pieces
-        if send_splits[me]:
-            self.send_pushed_at[si] = self._push_share(own, send_splits[me])
-        if m:
-            self.pushed_at[slot] = self._push_share((rk, rt, rv), m)
+        if n + m > sk.numel():   # skew: more received than the set has room for behind the batch
+            self.eng.sync()      # (nothing reads the old set once the engine is idle)
+            cap = self._set_cap(n + m)
+            grown = [torch.empty(cap, dtype=torch.int64, device=self.device) for _ in range(3)]
+            for g, x in zip(grown, (sk, st, sv)):
+                g[:n].copy_(x[:n])
+            self.send[si] = tuple(grown)
+            sk, st, sv = self.send[si]
+        # the peers' shares land right behind the own share (the last destination of the partition's order)
+        recv = (sk[n:n + m], st[n:n + m], sv[n:n + m])
+        self._transfer((sk[:n], st[:n], sv[:n]), send_splits, recv_splits, recv, order=self._dest_order())
+        # own share and received shares lie between the same watermarks: one push (a run above max_batch, under
+        # skew, goes in pieces)
+        if own_n + m:
+            self.send_pushed_at[si] = self._push_share((sk[n - own_n:n + m], st[n - own_n:n + m], sv[n - own_n:n + m]),
+                                                       own_n + m)
         self._forward(aligned)

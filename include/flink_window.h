@@ -353,6 +353,16 @@ int         fw_partition_by_operator(fw_engine* e, const int64_t* key, const int
                                      int32_t max_parallelism, int32_t parallelism,
                                      int64_t* out_key, int32_t* out_key_hash, int64_t* out_f1,
                                      int64_t* out_ts, void* out_value, int64_t* counts, int64_t* offsets);
+/* The same with operator `last_operator`'s records placed after every other operator's (output order
+ * last+1 .. parallelism-1, 0 .. last; counts stay indexed by operator, offsets[d] is operator d's start): a
+ * receiving subtask lands its peers' records right behind its own share in the same columns and pushes the
+ * whole in one fw_push_batch.  last_operator < 0: operator order, as fw_partition_by_operator. */
+int         fw_partition_by_operator_last(fw_engine* e, const int64_t* key, const int32_t* key_hash,
+                                          const int64_t* f1, const int64_t* ts, const void* value, int64_t n,
+                                          int32_t max_parallelism, int32_t parallelism,
+                                          int64_t* out_key, int32_t* out_key_hash, int64_t* out_f1,
+                                          int64_t* out_ts, void* out_value, int64_t* counts, int64_t* offsets,
+                                          int32_t last_operator);
 
 /* Device-time accounting (HIP events around each kernel, on the stream it runs on), for the roofline
  * figures of bench.py.  Off by default; enabling it adds timed event records between kernels, which

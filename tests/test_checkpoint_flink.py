@@ -523,3 +523,60 @@ def test_sliding_lateness_checkpoint(mode):
         e.restore_kg_flink(kg, layout, *blobs["o"][kg], LONG_MIN)
     assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
     e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_native_snapshot_purging_lateness(mode):
+    """PurgingTrigger + allowed lateness through the engine's own blob (fw_snapshot_kg): refused while a purged window
+    is within its lateness (its keys' cleanup timers have no place in that format, only in the reference layout);
+    taken between two such periods, restored, and continued — late records, per-element fires and purges, windows
+    reusing slice slots — the engine's results and reference-layout sections (purged windows' cleanup timers
+    included) equal an oracle that ran through without the checkpoint.  (a slot's purged-window
+    ordinals were inherited by the next window claiming the slot, and a native round trip lost the tracking.)"""
+    from flink_amd import _abi
+    from flink_amd.windowing import (EventTimeTrigger, PurgingTrigger, ReduceFunction, TumblingEventTimeWindows,
+                                     WindowEngine, make_config)
+    from harness import drive, gen_stream
+    from oracle.oracle import OracleEngine
+    keys, ts, vals = gen_stream(64_000, 2000, rate=1 << 13, zipf=1.1, ooo=300)   # ~7.8 s of event time
+    f1 = np.arange(len(keys), dtype=np.int64) * 3 + 1
+    cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "max"), "i64", True),
+                      PurgingTrigger.of(EventTimeTrigger.create()), 400, max_parallelism=128, key_capacity=1 << 13,
+                      max_batch=1 << 13, out_capacity=1 << 20, max_open_slices=4, ingest_mode=mode)
+    layout = ("f1", "key", "max", "sum")
+    B = 2048
+    wm_after = lambda n: int(ts[:n].max()) - 120   # drive()'s watermark after the batch ending at n
+    cuts = [n for n in range(B * 4, B * 20, B)]
+    inside = next(n for n in cuts if 0 <= wm_after(n) % 1000 < 380)     # a fired window within its lateness
+    between = next(n for n in cuts if 420 <= wm_after(n) % 1000 < 990)  # none: cleanup passed, next not fired
+    e = WindowEngine(cfg)
+    drive(e, keys[:inside], ts[:inside], vals[:inside], B, 120, None, f1=f1[:inside])
+    with pytest.raises(_abi.FwError) as ei:
+        e.snapshot_kg(0)
+    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+    e.close()
+    n = between
+    # the engine up to the cut, its own blobs, a fresh engine restored from them
+    e = WindowEngine(cfg)
+    drive(e, keys[:n], ts[:n], vals[:n], B, 120, None, f1=f1[:n])
+    blobs = {kg: e.snapshot_kg(kg) for kg in range(128)}
+    e.close()
+    g = WindowEngine(cfg)
+    for kg, blob in blobs.items():
+        g.restore_kg(kg, blob)
+    o = OracleEngine(cfg)
+    drive(o, keys[:n], ts[:n], vals[:n], B, 120, None, f1=f1[:n])
+    m = len(keys) - 3 * B   # continue up to a point with purged windows within their lateness, then compare
+    outs = {}
+    for name, eng in (("g", g), ("o", o)):
+        outs[name] = _canon(epochs_of(drive(eng, keys[n:m], ts[n:m], vals[n:m], B, 120, None, f1=f1[n:m]),
+                                      ["sum_i64", "max_i64"], True))
+    assert outs["g"] == outs["o"]
+    assert any(r[1] < w for w, recs in outs["o"] if w != "tail" for r in recs), "per-element fires after the restore"
+    sg = {kg: g.snapshot_kg_flink(kg, layout) for kg in range(128)}
+    so = {kg: o.snapshot_kg_flink(kg, layout) for kg in range(128)}
+    assert _diff(sg, so) is None, _diff(sg, so)
+    assert any(tm != b"\x00\x00\x00\x00" and len(tm) > 4 for _, tm in so.values())
+    g.close()
+    o.close()

@@ -8,7 +8,8 @@ The window subtasks here are oracle engines (no GPU); on GPUs the same class dri
 and the HIP partition kernel over RCCL.  `pipelined` runs the GPUs' own step()/_finish() code (the
 depth-2 software pipeline, count all-to-all and MIN all-reduce in one meta tensor, the receive ring) on
 CPU tensors; the Zipf(1.2) case makes one rank receive several times its engine's max_batch, which the
-exchange pushes in pieces (the hot keys' key groups meet on one operator at p = 8).
+exchange pushes in pieces (the hot keys' key groups meet on one operator at p = 8).  Without
+skew every rank makes exactly one engine push per step (own and received shares in one run of records).
 """
 import os
 import socket
@@ -95,7 +96,7 @@ def _worker(rank, world, port, q, pipelined=False, zipf=None):
     results.append(eng.collect())
     eng.advance_watermark(LONG_MAX)
     results.append(eng.collect())
-    pushes = ex.pushes if pipelined else None
+    pushes = ex.pushes
     q.put((rank, epochs_of(results, ["sum_i64", "count"]), ex.emitted, pushes))
     dist.destroy_process_group()
 
@@ -121,8 +122,10 @@ def test_keyby_exchange_two_ranks(world, pipelined, zipf):
     exp = expected_forwarded(world, STEPS, BATCH, zipf)
     if world == 2:
         assert any(e is None for e in exp), "the stream must exercise non-increasing aligned watermarks"
-    if zipf:   # some rank received more than max_batch = BATCH per step: more pushes than 2 per step
-        assert max(pushes.values()) > 2 * STEPS
+    if zipf:   # some rank received more than max_batch = BATCH per step: its run goes in pieces
+        assert max(pushes.values()) > STEPS
+    else:      # own share and received shares between two watermarks: ONE engine push per step
+        assert all(pushes[r] == STEPS for r in range(world)), pushes
     forwarded = [e for e in exp if e is not None]
     # every window subtask forwards exactly the valve's watermarks (positions included)
     for r in range(world):
