@@ -958,11 +958,17 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   }
   if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
   FW_STAMP(r, 0, 2);
-  block_scan_excl<NT>(cnt, nbq + 1, wtot);   // cnt[nbq] = routed records of the tile
+  // bins past the tile's last live group hold nothing, so the scan covers the live groups only (an in-order stream:
+  // one group of nb bins); the tile's routed slices claimed lset's entries in order (a prefix)
+  int nlive = tile_direct ? RT_GROUPS : 0;
+  if (!tile_direct)
+    for (int q = 0; q < RT_Q; ++q) nlive = lset[q] != FREE_TAG ? q + 1 : nlive;
+  const int nlb = nlive * s.nb;
+  block_scan_excl<NT>(cnt, nlb + 1, wtot);   // cnt[nlb] = routed records of the tile
   // the segment table, bucket-major (row (group, bucket) holds one word per tile: start | end << 16), so that the
   // k_aggregate workgroup owning a bucket reads its rows contiguously; only the tile's live groups are written
   // (its routed slices, and the direct / fire groups when it has direct records), k_aggregate reads no other
-  for (int x = threadIdx.x; x < nbq; x += NT) {
+  for (int x = threadIdx.x; x < nlb; x += NT) {
     const int g = x / s.nb;
     const bool live = g < RT_Q ? lset[g] != FREE_TAG : tile_direct;
     if (live) r.seg[(int64_t)x * r.seg_stride + blockIdx.x] = (uint32_t)cnt[x] | ((uint32_t)cnt[x + 1] << 16);
@@ -978,7 +984,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   }
   __syncthreads();
   FW_STAMP(r, 0, 3);
-  const int32_t total = cnt[nbq];
+  const int32_t total = cnt[nlb];
 #pragma unroll 2
   for (int k = 0; k < PER; ++k) {
     const int32_t pos = k * NT + (int)threadIdx.x;
