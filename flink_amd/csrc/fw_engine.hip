@@ -695,7 +695,6 @@ struct RouteBuf {
   long long* stamps;     // diagnostics (FW_DEBUG_AGG & 16): per-workgroup phase timestamps, 8 per workgroup
   int32_t ntiles;
   int32_t dbg;
-  int32_t only_direct;   // k_aggregate behind k_agg_f: takes the batch only if it has direct-group records
 };
 
 // Non-temporal access of the streamed columns, a bit mask: 1 = k_route's input loads (on: k_route 43 ->
@@ -705,6 +704,7 @@ struct RouteBuf {
 #define FW_ROUTE_NT 1
 #endif
 #define FW_STAMP(r, base, k) do { if ((r).stamps && threadIdx.x == 0) (r).stamps[(base) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RT_STAMP(k) do { if (r.stamps && threadIdx.x == 0) r.stamps[(int64_t)tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 // tile-local slice set in LDS (RT_Q entries): index of slice m, inserting it if new; -1 when full
 __device__ __forceinline__ int32_t tile_slice(int64_t* lset, int64_t m) {
@@ -759,7 +759,7 @@ constexpr size_t RT_LDS = (size_t)RT_TILE * (16 + 2) + 4 * (size_t)(RT_GROUPS * 
 
 template <int VT, int AGG, bool FIRST>
 __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, const RouteBuf& r, unsigned char* smem,
-                                           const bool tail) {
+                                           const bool tail, const int tile) {
   constexpr int NT = RT_THREADS;
   constexpr int PER = RT_TILE / NT;     // records per thread
   constexpr int V = PER / 2;            // 16-B vectors per column per thread
@@ -771,8 +771,8 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   int64_t* lset = (int64_t*)(wtot + 16);           // [RT_Q] the tile's routed slices
   int32_t* any_direct = (int32_t*)(lset + RT_Q);   // the tile has direct-group records
   int32_t* lhash = (int32_t*)smem;                 // Java key hashes (optional column)
-  const int64_t base = (int64_t)blockIdx.x * RT_TILE;
-  FW_STAMP(r, 0, 0);
+  const int64_t base = (int64_t)tile * RT_TILE;
+  RT_STAMP(0);
   for (int x = threadIdx.x; x <= nbq; x += NT) cnt[x] = 0;
   if (threadIdx.x < RT_Q) lset[threadIdx.x] = FREE_TAG;
   if (threadIdx.x == 0) *any_direct = 0;
@@ -810,7 +810,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     }
   }
   __syncthreads();   // cnt and lset initialised
-  FW_STAMP(r, 0, 1);
+  RT_STAMP(1);
   // phase B1: per record operator work (timestamp, key group, windows, lateness) — pure ALU; the slice
   // number replaces the timestamp in tt[]
   unsigned long long late_pairs = 0;
@@ -954,10 +954,10 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   const bool tile_direct = *any_direct != 0;
   if (threadIdx.x == 0) {
     if (tile_direct) atomicOr(r.dflag, 1u);
-    r.tdir[blockIdx.x] = tile_direct ? 1u : 0u;
+    r.tdir[tile] = tile_direct ? 1u : 0u;
   }
-  if (threadIdx.x < RT_Q) r.hdr[(int64_t)blockIdx.x * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
-  FW_STAMP(r, 0, 2);
+  if (threadIdx.x < RT_Q) r.hdr[(int64_t)tile * RT_Q + threadIdx.x] = lset[threadIdx.x];   // routed slices
+  RT_STAMP(2);
   // bins past the tile's last live group hold nothing, so the scan covers the live groups only (an in-order stream:
   // one group of nb bins); the tile's routed slices claimed lset's entries in order (a prefix)
   int nlive = tile_direct ? RT_GROUPS : 0;
@@ -971,7 +971,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   for (int x = threadIdx.x; x < nlb; x += NT) {
     const int g = x / s.nb;
     const bool live = g < RT_Q ? lset[g] != FREE_TAG : tile_direct;
-    if (live) r.seg[(int64_t)x * r.seg_stride + blockIdx.x] = (uint32_t)cnt[x] | ((uint32_t)cnt[x + 1] << 16);
+    if (live) r.seg[(int64_t)x * r.seg_stride + tile] = (uint32_t)cnt[x] | ((uint32_t)cnt[x + 1] << 16);
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -983,7 +983,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     }
   }
   __syncthreads();
-  FW_STAMP(r, 0, 3);
+  RT_STAMP(3);
   const int32_t total = cnt[nlb];
 #pragma unroll 2
   for (int k = 0; k < PER; ++k) {
@@ -998,7 +998,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
       if (pos < total) *(uint32_t*)(r.idx + base + pos) = *(const uint32_t*)(st_idx + pos);
     }
   }
-  FW_STAMP(r, 0, 4);
+  RT_STAMP(4);
 }
 
 template <int VT, int AGG, bool FIRST>
@@ -1006,7 +1006,11 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(const Spec* __restrict_
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Spec& s = *sd;   // device copy (kernel arguments by value are held in scalar registers from entry)
   // every tile but the last is whole, so its 16-B loads need no bounds (uniform branch)
-  route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(blockIdx.x + 1) * RT_TILE > b.n);
+  // one tile per workgroup (a persistent form, two workgroups per CU looping over the tiles with the second half
+  // started late so that one's compute phase falls beside the other's memory phases, measured no faster and
+  // spilled: round 5)
+  const int tile = (int)blockIdx.x;
+  route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(tile + 1) * RT_TILE > b.n, tile);
 }
 
 // the bucket's LDS directory-hash table: slot of h, inserting its key (fmix64_inv(h)) into the global
@@ -1147,8 +1151,9 @@ __host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_
 // for helpers): hot buckets split over helper workgroups, and the in-wave hot-key combine.  The uniform
 // variant carries neither (registers: the 1024-thread workgroup has 128 VGPRs per lane)
 template <int VT, int AGG, bool FIRST, bool SKEW>
-__global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, RouteBuf r, const int64_t* f1col) {
+__global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict__ sd, BatchIn b, RouteBuf r, const int64_t* f1col) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Spec& s = *sd;   // device copy (kernel arguments by value are held in scalar registers from entry)
   constexpr int NT = AG_THREADS;
   // XCD-aware bucket order: workgroups are dealt to the 8 XCDs round-robin, so XCD x runs the
   // contiguous bucket range [x * nb/8, (x + 1) * nb/8).  Neighbouring buckets' segments share the
@@ -1186,7 +1191,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
   int32_t* plan = (int32_t*)(gsl + RT_GS) + 2;          // [RT_MAXNB + 1] helper prefix; then bucket, share, shares
   const int64_t SB = (int64_t)8 << 16;
-  if (!(!SKEW && r.only_direct)) FW_STAMP(r, SB, 0);   // (k_agg_f stamps its own)
+  FW_STAMP(r, SB, 0);
   // Hot buckets (skewed keys) are split over helper workgroups launched after the nb owners: bucket b
   // with L_b routed records last batch gets S_b = clamp(ceil(L_b / chunk), 1, AG_SPLIT_MAX) shares, share
   // s taking tiles [s T / S_b, (s + 1) T / S_b) (tiles are in arrival order, so share order is arrival
@@ -1256,7 +1261,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     for (int g = threadIdx.x; g < RT_GS; g += NT) r.fold_cnt_zero[(int64_t)bkt * RT_GS + g] = 0u;
   // does any tile hold direct-group records (the batch's flag; no: skip all direct work)
   const bool has_direct = __builtin_amdgcn_readfirstlane(*r.dflag) != 0;
-  if (!SKEW && r.only_direct && !has_direct) return;   // uniform: k_agg_f took the batch
   // every tile's header and this bucket's segment bounds in each of its bin groups, plus the bucket's
   // directory slice, into LDS: all loads independent, one round trip
   // (the bucket's rows of the bucket-major segment table are contiguous; a row's word is read only where the tile
@@ -1287,14 +1291,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
   }
   for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
   if (threadIdx.x < AG_LOOK) off[r.ntiles + 1 + threadIdx.x] = INT32_MAX;
-  // claimed early (slice_slot is idempotent): the slot of tile 0's first routed slice, nearly always the
-  // batch's only one
-  int64_t m_pre = FREE_TAG;
-  int32_t pre_p = -1;
-  if (threadIdx.x == 0 && r.ntiles > 0) {
-    m_pre = r.hdr[0];
-    if (m_pre != FREE_TAG) pre_p = slice_slot(s, m_pre);
-  }
   for (int x = threadIdx.x; x < KA; x += NT) {
     lsum[x] = sum_identity(VT);
     if (HAS_MIN) lmin[x] = INT64_MAX;
@@ -1358,11 +1354,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
         const uint64_t h = (uint64_t)r.kv[pos].x;
         const int64_t m = r.dm[pos];
-        int32_t p = slice_slot(s, m);
+        int32_t p = slice_slot_body(s.slice_tag, s.P, m);
         int64_t kid = s.D;
-        if (h == EMPTY_H) (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
-        else {
-          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
+        if (h == EMPTY_H) {   // marks the Long.MIN_VALUE key's column in use
+          if (s.dir_min_used[0] == 0) s.dir_min_used[0] = 1;
+        } else {
+          const int32_t x2 = agg_probe_insert_body(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
           kid = x2 < 0 ? -1 : dbase + x2;
         }
         if (p < 0 || kid < 0) { cap_error(s, 7); p = 0; kid = 0; }   // (a failed batch: a harmless entry keeps the slot)
@@ -1417,7 +1414,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       }
       const bool miss2 = miss && !found2;
       if (__any(miss2) && miss2) {
-        const int32_t x = agg_probe_insert(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
+        const int32_t x = agg_probe_insert_body(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
         if (x < 0) { cap_error(s, 8); act = false; }
         else kl = (uint32_t)x;
       }
@@ -1430,12 +1427,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     const int64_t m = gsl[g];
     if (m == FREE_TAG) break;                            // uniform
     // pane-slot claim: authoritative here, after every earlier watermark (engine stream order); slot
-    // p = floor_mod(m, P) is claimed by whichever workgroup comes first, the rest find it taken by m
-    __syncthreads();   // every thread has read the previous round's lclaim
-    if (threadIdx.x == 0) lclaim = (pre_p >= 0 && m == m_pre) ? pre_p : slice_slot(s, m);
-    __syncthreads();
-    const int32_t p = lclaim;
-    if (p < 0) { if (threadIdx.x == 0) cap_error(s, 9); continue; }   // slice pool exhausted
+    // p = floor_mod(m, P) is claimed by whichever workgroup comes first, the rest find it taken by m.  The
+    // slot's tag is read now, its value used (and the slot claimed if free) at the fold: the load's latency
+    // lies under the main loop instead of in front of it
+    int64_t tagv = FREE_TAG;
+    if (threadIdx.x == 0) tagv = s.slice_tag[floor_mod(m, s.P)];
     for (int t = threadIdx.x; t < r.ntiles; t += NT) {
       int32_t a0 = 0, a1 = 0;
 #pragma unroll
@@ -1535,9 +1531,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
         const longlong2 rec = r.kv[pos];
         uint32_t kl = KMIN;
         if ((uint64_t)rec.x == EMPTY_H) {
-          (void)dir_lookup(s, EMPTY_KEY);   // marks the Long.MIN_VALUE key's column in use
+          if (s.dir_min_used[0] == 0) s.dir_min_used[0] = 1;   // marks the Long.MIN_VALUE key's column in use
         } else {
-          const int32_t x2 = agg_probe_insert(lh, s.dir_keys + dbase, kbm, (uint64_t)rec.x, s.stats + ST_DIR_KEYS);
+          const int32_t x2 = agg_probe_insert_body(lh, s.dir_keys + dbase, kbm, (uint64_t)rec.x, s.stats + ST_DIR_KEYS);
           if (x2 < 0) { cap_error(s, 10); continue; }
           kl = (uint32_t)x2;
         }
@@ -1547,6 +1543,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
     __syncthreads();
     }   // passes
     FW_STAMP(r, SB, 3 + 3 * min(g, 1));
+    if (threadIdx.x == 0) lclaim = tagv == m ? (int32_t)floor_mod(m, s.P) : slice_slot_body(s.slice_tag, s.P, m);
+    __syncthreads();
+    const int32_t p = lclaim;
+    __syncthreads();   // every thread has read lclaim (the next round rewrites it)
+    if (p < 0) { if (threadIdx.x == 0) cap_error(s, 9); continue; }   // slice pool exhausted (uniform)
     unsigned int* flag = r.fold_flag + (int64_t)bkt * RT_GS + g;
     // integer shares of a split bucket fold concurrently with device atomics (sum / count / min / max
     // are exact in any order, and the first arrival is the least batch index over the shares: the last
@@ -1670,366 +1671,6 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(Spec s, BatchIn b, Rou
       atomicAdd(&s.stats[ST_SHARES], 1ull);
     }
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_agg_f: k_aggregate's fast form, for batches without direct-group records (the usual case: every record of
-// a tile in one of its RT_Q routed slices) and reduces without maxBy / minBy.  The same result as
-// k_aggregate<..., SKEW = false>; shaped for the register file: the bucket size (KBL) and the LDS layout are
-// compile-time (no scalar register per LDS array), the kernel's arguments are one small structure (the
-// engine's constants are read from a device-resident AggCold where they are used), the slice-slot claim's
-// load is issued before the main loop and consumed at the fold, and a batch with direct-group records is left
-// whole to the general kernel launched behind it (k_aggregate, only_direct).  Each lane finds its record's
-// tile with independent LDS reads.
-// ------------------------------------------------------------------------------------------------
-#ifndef AGF_OCC
-#define AGF_OCC 4
-#endif
-#ifndef AGF_EXP
-#define AGF_EXP 0
-#endif
-constexpr int AGF_MAXT = 2048;   // tiles per batch the fast form holds (8 Mi records)
-#ifndef AGF_WIN_N
-#define AGF_WIN_N 8
-#endif
-#ifndef AGF_LOOK_N
-#define AGF_LOOK_N 8
-#endif
-constexpr int AGF_WIN = AGF_WIN_N;   // directory slots compared per probe, branch-free (the full probe beyond)
-constexpr int AGF_LOOK = AGF_LOOK_N; // segment ends a lane compares per step (independent reads)
-constexpr int AGF_OFF = (AGF_MAXT + 1 + AG_LOOK + 1) & ~1;   // (AGF_LOOK <= AG_LOOK)   // k_agg_f's prefix array (even: 8-B alignment after it)
-
-struct AggCold {   // device-resident, constant per engine
-  int64_t* dir_keys;
-  int64_t* slice_tag;
-  Cols c;
-  int32_t* err;
-  unsigned long long* stats;
-  int32_t* dir_min_used;
-  unsigned int* bload;          // [4][RT_MAXNB] ring (k_aggregate's skew plan)
-  unsigned int* fold_flag;      // [5][RT_MAXNB][RT_GS]: flags, then the fold-count ring
-  unsigned int* dflags;         // [FLAG_RING]
-  unsigned int* bload_host;
-  long long* stamps;
-  int64_t stride, D;
-  int32_t P, nb, seg_stride, cmpto;
-};
-
-struct AggFast {   // by value, per batch
-  const longlong2* kv;
-  const uint16_t* idx;
-  const uint32_t* seg;
-  const int64_t* hdr;
-  const int64_t* f1col;
-  const int64_t* dir_keys;
-  unsigned int* dflags;
-  const AggCold* cold;
-  int64_t ord_base;
-  int32_t ntiles;
-  uint32_t batch;   // the engine's batch counter (rings)
-  int32_t dbg;
-  int32_t seg_stride;
-};
-
-#ifndef AGF_COLD_ATOMIC
-#define AGF_COLD_ATOMIC 0
-#endif
-template <typename T>
-__device__ __forceinline__ T cold_ld(T const* p) {   // a read of AggCold where it is used
-#if AGF_COLD_ATOMIC
-  return (T)__hip_atomic_load((const T*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  return *p;
-#endif
-}
-__device__ __forceinline__ void cold_cap_error(const AggCold* cold, int site) {   // cap_error of k_aggregate
-  set_error(cold_ld(&cold->err), FW_ERR_CAPACITY);
-  atomicCAS(&cold_ld(&cold->stats)[7], 0ull, (unsigned long long)site);
-}
-
-template <int AGG, int KBL>
-__host__ __device__ constexpr size_t agf_lds_bytes() {
-  constexpr size_t KB = (size_t)1 << KBL, KA = KB + 65;
-  constexpr int nacc = 1 + ((AGG & FW_AGG_MIN) ? 1 : 0) + ((AGG & FW_AGG_MAX) ? 1 : 0) + ((AGG & FW_AGG_COUNT) ? 1 : 0);
-  return 8 * KB + 8 * KA * nacc + 4 * ((KA + 3) & ~(size_t)3) + 4 * (size_t)AGF_MAXT * 4 + 4 * (size_t)AGF_OFF +
-         4 * (size_t)AG_CHS + 4 * 16 + 8 * RT_GS + 4 * RT_GS + 16;
-}
-
-template <int VT, int AGG, bool FIRST, int KBL>
-__global__ __launch_bounds__(AG_THREADS, AGF_OCC) void k_agg_f(AggFast a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NT = AG_THREADS;
-  constexpr int KB = 1 << KBL;
-  constexpr uint32_t kbm = (uint32_t)KB - 1;
-  constexpr int KA = KB + 65;   // KB slots, one dummy per lane, the Long.MIN_VALUE key (direct form only: unused)
-  constexpr bool HAS_MIN = (AGG & FW_AGG_MIN) != 0, HAS_MAX = (AGG & FW_AGG_MAX) != 0, HAS_CNT = (AGG & FW_AGG_COUNT) != 0;
-  // the layout, at compile-time offsets
-  uint64_t* lh = (uint64_t*)smem;
-  int64_t* lsum = (int64_t*)(lh + KB);
-  int64_t* lmin = lsum + KA;
-  int64_t* lmax = lmin + (HAS_MIN ? KA : 0);
-  int64_t* lcnt = lmax + (HAS_MAX ? KA : 0);
-  uint32_t* lfirst = (uint32_t*)(lcnt + (HAS_CNT ? KA : 0));
-  uint32_t* lseg0 = lfirst + ((KA + 3) & ~3);   // [AGF_MAXT] routed group 0's segment word (0 when the group is unused)
-  uint32_t* lseg1 = lseg0 + AGF_MAXT;           // ... group 1
-  uint32_t* lq = lseg1 + AGF_MAXT;              // [AGF_MAXT] round of group 0 | round of group 1 << 8 (0xFF: none)
-  int32_t* sst = (int32_t*)(lq + AGF_MAXT);     // [AGF_MAXT] this round's segment start in each tile
-  int32_t* off = sst + AGF_MAXT;                // [AGF_OFF] segment lengths, then their prefix, then INT32_MAX pads
-  int32_t* step_tile = off + AGF_OFF;
-  int32_t* awtot = step_tile + AG_CHS;
-  int64_t* gsl = (int64_t*)(awtot + 16);        // [RT_GS] the batch's routed slices (8-B aligned: AGF_OFF is even)
-  int32_t* gslot = (int32_t*)(gsl + RT_GS);     // [RT_GS] their slots
-  int32_t* nround = gslot + RT_GS;
-  const int ntiles = a.ntiles;
-  const AggCold* __restrict__ cold = a.cold;
-  const int nb = (int)gridDim.x;
-  const int vb = (int)blockIdx.x;
-  const int bkt = (nb % 8 == 0 && !(a.dbg & 32)) ? (vb % 8) * (nb / 8) + vb / 8 : vb;   // XCD-major (k_aggregate)
-  const int64_t dbase = (int64_t)bkt * KB;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t slot_flag = a.batch % FLAG_RING;
-  long long* const stamps = cold_ld(&cold->stamps);
-#define AGF_STAMP(k) do { if (stamps && threadIdx.x == 0) stamps[((int64_t)8 << 16) + (int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-  AGF_STAMP(0);
-  // a batch with direct-group records goes whole to the general kernel behind this one: the flag is read with
-  // the prologue's loads (one round trip) and tested once they are issued
-  const unsigned int dflag = a.dflags[slot_flag];
-  // prologue, every load independent: two tiles per thread (headers, this bucket's words of routed groups 0 and
-  // 1), the bucket's directory slice
-  const int segrow = a.seg_stride;
-  int64_t h0[AGF_MAXT / NT], h1[AGF_MAXT / NT];
-#pragma unroll
-  for (int k = 0; k < AGF_MAXT / NT; ++k) {
-    const int t = k * NT + (int)threadIdx.x;
-    h0[k] = FREE_TAG; h1[k] = FREE_TAG;
-    if (t < ntiles) {
-      h0[k] = a.hdr[(int64_t)t * RT_Q];
-      h1[k] = a.hdr[(int64_t)t * RT_Q + 1];
-      const uint32_t s0 = a.seg[(int64_t)bkt * segrow + t], s1 = a.seg[(int64_t)(nb + bkt) * segrow + t];
-      lseg0[t] = h0[k] != FREE_TAG ? s0 : 0u;
-      lseg1[t] = h1[k] != FREE_TAG ? s1 : 0u;
-    }
-  }
-  {
-    const int64_t* dir = a.dir_keys + dbase;
-    for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)dir[x]);
-  }
-  if (__builtin_amdgcn_readfirstlane(dflag) != 0) return;   // uniform (no barrier passed yet)
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.dflags[(a.batch + FLAG_RING / 2) % FLAG_RING] = 0u;   // (the flag ring)
-  for (int x = threadIdx.x; x < KA; x += NT) {
-    lsum[x] = sum_identity(VT);
-    if (HAS_MIN) lmin[x] = INT64_MAX;
-    if (HAS_MAX) lmax[x] = INT64_MIN;
-    if (HAS_CNT) lcnt[x] = 0;
-    lfirst[x] = NO_FIRST;
-  }
-  if (threadIdx.x < AG_LOOK) off[AGF_MAXT + 1 + threadIdx.x] = INT32_MAX;
-  if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
-  if (threadIdx.x == 0) *nround = 0;
-  {
-    unsigned int* fold_flag = cold_ld(&cold->fold_flag);   // the skew variant's fold-count ring, kept consistent
-    unsigned int* fz = fold_flag + (size_t)(1 + (a.batch + 2) % 4) * RT_MAXNB * RT_GS;
-    if (threadIdx.x < RT_GS) fz[(int64_t)bkt * RT_GS + threadIdx.x] = 0u;
-  }
-  __syncthreads();
-  // the batch's routed slices (every workgroup builds the same set, in the same first-seen order; a lane whose
-  // slice equals its left neighbour's defers to it)
-#pragma unroll
-  for (int k = 0; k < AGF_MAXT / NT; ++k) {
-#pragma unroll
-    for (int q = 0; q < RT_Q; ++q) {
-      const int64_t m = q == 0 ? h0[k] : h1[k];
-      const int64_t left = __shfl_up(m, 1);
-      if (m != FREE_TAG && !(lane != 0 && left == m)) {
-        int g = 0;
-        for (; g < RT_GS; ++g) {
-          const int64_t cur = gsl[g];
-          if (cur == m) break;
-          if (cur == FREE_TAG) {
-            const unsigned long long prev = atomicCAS((unsigned long long*)&gsl[g], (unsigned long long)FREE_TAG,
-                                                      (unsigned long long)m);
-            if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) break;
-          }
-        }
-        if (g == RT_GS) cold_cap_error(cold, 6);   // more distinct slices in one batch than RT_GS
-      }
-    }
-  }
-  __syncthreads();
-  // each tile's groups -> rounds; the slots of the rounds' slices: thread 0 reads the tags now and claims at the
-  // fold (the load is in flight through the main loop)
-#pragma unroll
-  for (int k = 0; k < AGF_MAXT / NT; ++k) {
-    const int t = k * NT + (int)threadIdx.x;
-    if (t < ntiles) {
-      uint32_t r0 = 0xFF, r1 = 0xFF;
-      for (int g = 0; g < RT_GS; ++g) {
-        const int64_t m = gsl[g];
-        if (m == FREE_TAG) break;
-        if (m == h0[k]) r0 = (uint32_t)g;
-        if (m == h1[k]) r1 = (uint32_t)g;
-      }
-      lq[t] = r0 | (r1 << 8);
-    }
-  }
-  AGF_STAMP(1);
-  int64_t* const slice_tag = cold_ld(&cold->slice_tag);
-  const int32_t P = cold_ld(&cold->P);
-  const int64_t stride = cold_ld(&cold->stride);
-  const bool cmpto = cold_ld(&cold->cmpto) != 0;
-  const AggLds L{lsum, lmin, lmax, lcnt, lfirst, nullptr};
-  int32_t routed = 0;
-  for (int g = 0; g < RT_GS; ++g) {
-    const int64_t m = gsl[g];   // (uniform)
-    if (m == FREE_TAG) break;
-    int64_t tagv = FREE_TAG;
-    if (threadIdx.x == 0) tagv = slice_tag[floor_mod(m, P)];   // consumed at the fold
-    for (int t = threadIdx.x; t < ntiles; t += NT) {
-      const uint32_t qq = lq[t];
-      uint32_t sg = 0;
-      if ((qq & 0xFFu) == (uint32_t)g) sg = lseg0[t];
-      else if (((qq >> 8) & 0xFFu) == (uint32_t)g) sg = lseg1[t];
-      sst[t] = (int32_t)(sg & 0xFFFFu);
-      off[t] = (int32_t)(sg >> 16) - (int32_t)(sg & 0xFFFFu);
-    }
-    if (threadIdx.x == 0) off[ntiles] = 0;
-    __syncthreads();
-    block_scan_excl<NT, AG_MAXPER>(off, ntiles + 1, awtot);   // off[ntiles] = the bucket's records of slice m
-    // (off past ntiles: INT32_MAX for the lookup; entries between ntiles + 1 and AGF_MAXT are never read)
-    if (threadIdx.x < AG_LOOK) off[ntiles + 1 + threadIdx.x] = INT32_MAX;
-    const int32_t R = off[ntiles];
-    routed += R;
-    AGF_STAMP(2);
-    constexpr int UR = FW_AGG_UR;
-    for (int32_t cb = 0; cb < R; cb += AG_CHS * 64) {   // uniform
-      __syncthreads();
-      for (int t = threadIdx.x; t < ntiles; t += NT) {
-        const int32_t o = off[t], l = off[t + 1] - o;
-        if (l == 0) continue;
-        const int32_t s_lo = max(0, (o - cb + 63) >> 6), s_hi = min(AG_CHS, (o + l - cb + 63) >> 6);
-        for (int32_t st = s_lo; st < s_hi; ++st) step_tile[st] = t;
-      }
-      __syncthreads();
-      const int32_t nsteps = min(AG_CHS, (R - cb + 63) >> 6);
-      auto load = [&](int32_t s0, longlong2* rv, uint32_t* ri, bool* ra) {
-#pragma unroll
-        for (int u = 0; u < UR; ++u) {
-          const int32_t st = s0 + u;
-          const int32_t rr = cb + 64 * st + lane;
-          ra[u] = st < nsteps && rr < R;
-          int32_t t = 0;
-          int64_t pos = 0;
-          if (ra[u]) {
-            const int32_t t0 = step_tile[st];
-            t = t0;
-#pragma unroll
-            for (int j = 1; j <= AGF_LOOK; ++j) t += off[t0 + j] <= rr ? 1 : 0;
-            while (off[t + 1] <= rr) ++t;
-            pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
-          }
-          rv[u] = a.kv[pos];
-          ri[u] = ((uint32_t)t << IDX_BITS) | (FIRST ? (uint32_t)a.idx[pos] : 0u);
-        }
-      };
-      auto process = [&](const longlong2* rv, const uint32_t* ri, const bool* ra) {
-#pragma unroll
-        for (int u = 0; u < UR; ++u) {
-          const uint64_t h = (uint64_t)rv[u].x;
-          const uint32_t h0 = (uint32_t)h & kbm;
-          uint32_t kl = h0;
-          bool found = false;
-#pragma unroll
-          for (int j = AGF_WIN - 1; j >= 0; --j) {
-            const uint32_t x = (h0 + j) & kbm;
-            const bool mt = lh[x] == h;
-            kl = mt ? x : kl;
-            found |= mt;
-          }
-          bool act = ra[u];
-#if AGF_EXP & 1
-          if (false) {
-#else
-          if (__any(act && !found) && act && !found) {   // displaced beyond the window, or a new key
-#endif
-            const int32_t x = agg_probe_insert_body(lh, cold_ld(&cold->dir_keys) + dbase, kbm, h,
-                                                    cold_ld(&cold->stats) + ST_DIR_KEYS);
-            if (x < 0) { cold_cap_error(cold, 8); act = false; }
-            else kl = (uint32_t)x;
-          }
-          kl = act ? kl : (uint32_t)KB + (uint32_t)lane;
-          acc_add<VT, AGG>(L, cmpto, false, 0, kl, rv[u].y, ri[u]);
-        }
-      };
-      longlong2 rvA[UR], rvB[UR];
-      uint32_t riA[UR], riB[UR];
-      bool raA[UR], raB[UR];
-      constexpr int32_t G = (NT / 64) * UR;
-      int32_t s0 = wave * UR;
-      if (s0 < nsteps) load(s0, rvA, riA, raA);
-      while (s0 < nsteps) {   // wave-uniform
-        if (s0 + G < nsteps) load(s0 + G, rvB, riB, raB);
-        process(rvA, riA, raA);
-        s0 += G;
-        if (s0 >= nsteps) break;
-        if (s0 + G < nsteps) load(s0 + G, rvA, riA, raA);
-        process(rvB, riB, raB);
-        s0 += G;
-      }
-    }
-    // the slice's slot (authoritative here: after every earlier watermark, engine stream order)
-    if (threadIdx.x == 0) {
-      int32_t p = (int32_t)floor_mod(m, P);
-      if (tagv != m) p = slice_slot_body(slice_tag, P, m);
-      gslot[g] = p;
-      if (p < 0) cold_cap_error(cold, 9);   // slice pool exhausted
-    }
-    __syncthreads();
-    AGF_STAMP(3);
-    const int32_t p = gslot[g];
-    // fold into the dense columns: this workgroup is the only writer of (p, bucket) panes
-    if (p >= 0) {   // uniform
-      const Cols c = {cold_ld(&cold->c.sum), HAS_MIN ? cold_ld(&cold->c.mn) : nullptr, HAS_MAX ? cold_ld(&cold->c.mx) : nullptr,
-                      HAS_CNT ? cold_ld(&cold->c.cnt) : nullptr, FIRST ? cold_ld(&cold->c.first) : nullptr,
-                      FIRST ? cold_ld(&cold->c.f1v) : nullptr, FIRST ? nullptr : cold_ld(&cold->c.present)};
-      for (int x = threadIdx.x; x < KB; x += NT) {
-        const uint32_t lf = lfirst[x];
-        if (lf == NO_FIRST) continue;
-        const int64_t idx = (int64_t)p * stride + dbase + x;
-        if (AGG & FW_AGG_SUM) {
-          if (VT == FW_VALUE_I64) c.sum[idx] = jadd(c.sum[idx], lsum[x]);
-          else c.sum[idx] = __double_as_longlong(__longlong_as_double(c.sum[idx]) + __longlong_as_double(lsum[x]));
-        }
-        if (HAS_MIN) { const int64_t o = c.mn[idx]; if (lmin[x] < o) c.mn[idx] = lmin[x]; }
-        if (HAS_MAX) { const int64_t o = c.mx[idx]; if (lmax[x] > o) c.mx[idx] = lmax[x]; }
-        if (HAS_CNT) c.cnt[idx] = jadd(c.cnt[idx], lcnt[x]);
-        if (FIRST) {
-          if (a.ord_base + (int64_t)lf < c.first[idx]) {   // the pane's earliest record of the batch, if the pane is new
-            c.first[idx] = a.ord_base + (int64_t)lf;
-            c.f1v[idx] = a.f1col[lf];
-          }
-        } else {
-          c.present[idx] = 1;
-        }
-        lsum[x] = sum_identity(VT);
-        if (HAS_MIN) lmin[x] = INT64_MAX;
-        if (HAS_MAX) lmax[x] = INT64_MIN;
-        if (HAS_CNT) lcnt[x] = 0;
-        lfirst[x] = NO_FIRST;
-      }
-    }
-    __syncthreads();
-    AGF_STAMP(4);
-  }
-  if (threadIdx.x == 0) {   // the bucket's load: the next batch's split plan (k_aggregate)
-    unsigned int* bload = cold_ld(&cold->bload);
-    atomicAdd(&bload[(a.batch % 4) * RT_MAXNB + bkt], (unsigned)routed);
-    bload[((a.batch + 2) % 4) * RT_MAXNB + bkt] = 0u;
-#if !FW_NO_HOSTLOAD
-    unsigned int* bh = cold_ld(&cold->bload_host);
-    if (bh) __hip_atomic_store(&bh[bkt], (unsigned)routed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
-  }
-#undef AGF_STAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3271,8 +2912,6 @@ struct fw_engine {
   int agg_min_lds = 81 * 1024;
   hipError_t attr_err = hipSuccess;         // routed_attrs_t: a failed hipFuncSetAttribute
   Spec* s_dev = nullptr;                    // routed form: device copy of s (k_route), re-uploaded when s changes
-  AggCold* cold_dev = nullptr;              // ... the engine constants k_agg_f reads
-  AggCold cold_host{};
   // partition scratch
   int64_t* new_list = nullptr;                // direct form with first arrival: panes created per batch
   unsigned long long* new_counts = nullptr;   // one list length per batch parity
@@ -3398,12 +3037,6 @@ static void launch_ingest_t(fw_engine* e, const BatchIn& b) {
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL((k_ingest_direct<VT, AGG, FIRST>), dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, b);
 }
-template <int VT, int AGG, bool FIRST, int KBL>
-static hipError_t agg_f_attr() {
-  if constexpr (agf_lds_bytes<AGG, KBL>() > 160 * 1024) return hipSuccess;
-  else return hipFuncSetAttribute((const void*)k_agg_f<VT, AGG, FIRST, KBL>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-}
-
 // the routed kernels use dynamic LDS only, so the whole 160 KiB is grantable: the largest any engine may ask for,
 // set once per device and instantiation (engines may be created from several threads), from fw_create, which
 // fails with the HIP error when the attribute cannot be set
@@ -3419,23 +3052,7 @@ static void routed_attrs_t(fw_engine* e) {
     const hipError_t rc = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (rc != hipSuccess) { e->attr_err = rc; return; }
   }
-  for (hipError_t rc : {agg_f_attr<VT, AGG, FIRST, 9>(), agg_f_attr<VT, AGG, FIRST, 10>(), agg_f_attr<VT, AGG, FIRST, 11>(),
-                        agg_f_attr<VT, AGG, FIRST, 12>()})
-    if (rc != hipSuccess) { e->attr_err = rc; return; }
   done.insert(e->dev);
-}
-
-// k_agg_f for buckets of 2^KBL slots, when its LDS fits; false: the general kernel takes the batch
-template <int VT, int AGG, bool FIRST, int KBL>
-static bool launch_agg_f(fw_engine* e, const AggFast& a) {
-  if constexpr (agf_lds_bytes<AGG, KBL>() > 160 * 1024) {
-    return false;
-  } else {
-    if ((int64_t)a.ntiles > AGF_MAXT || (e->rb.dbg & 256)) return false;   // (FW_DEBUG_AGG & 256: the general kernel)
-    const size_t lds = std::max<size_t>(agf_lds_bytes<AGG, KBL>(), (size_t)e->agg_min_lds);   // one workgroup per CU
-    hipLaunchKernelGGL((k_agg_f<VT, AGG, FIRST, KBL>), dim3(e->s.nb), dim3(AG_THREADS), lds, e->stream, a);
-    return true;
-  }
 }
 
 template <int VT, int AGG, bool FIRST>
@@ -3482,32 +3099,10 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   e->phase_begin(FW_PHASE_AGGREGATE);
   if (r.helpers > 0)
     hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, true>), dim3(e->s.nb + r.helpers), dim3(AG_THREADS), agg_lds, e->stream,
-                       e->s, b, r, f1col);
-  else if ((AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) || (e->rb.dbg & 256))   // (FW_DEBUG_AGG & 256: the general kernel)
-    hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b,
-                       r, f1col);
-  else {
-    // k_agg_f takes a batch without direct-group records; the general kernel behind it takes the others (and
-    // returns at once for the rest: on the engine stream, which waits for the next k_route anyway)
-    AggFast a;
-    a.kv = r.kv; a.idx = r.idx; a.seg = r.seg; a.hdr = r.hdr; a.f1col = f1col; a.cold = e->cold_dev;
-    a.ord_base = b.ord_base; a.ntiles = r.ntiles; a.batch = (uint32_t)e->batches; a.dbg = r.dbg;
-    a.dir_keys = e->s.dir_keys; a.dflags = e->dflags; a.seg_stride = (int32_t)r.seg_stride;
-    bool fast = false;
-    switch (e->s.kb_bits) {
-      case 9: fast = launch_agg_f<VT, AGG, FIRST, 9>(e, a); break;
-      case 10: fast = launch_agg_f<VT, AGG, FIRST, 10>(e, a); break;
-      case 11: fast = launch_agg_f<VT, AGG, FIRST, 11>(e, a); break;
-      case 12: fast = launch_agg_f<VT, AGG, FIRST, 12>(e, a); break;
-      default: break;
-    }
-    RouteBuf rd = r;
-    rd.only_direct = fast ? 1 : 0;
-    if (!(fast && (r.dbg & 512)))   // (FW_DEBUG_AGG & 512, timing only: no general kernel behind k_agg_f — wrong for a
-                                    // batch with direct-group records)
-      hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s, b,
-                         rd, f1col);
-  }
+                       e->s_dev, b, r, f1col);
+  else
+    hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s_dev, b, r,
+                       f1col);
   e->phase_end(b.n);
   // (ev_agg[par] is recorded by fw_push_batch once the batch's extra-window list is applied too)
 }
@@ -3838,10 +3433,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     }
   }
   e->wm_done = e->alloc<unsigned int>(1);
-  if (e->routed) {
-    e->s_dev = e->alloc<Spec>(1);
-    e->cold_dev = e->alloc<AggCold>(1);
-  }
+  if (e->routed) e->s_dev = e->alloc<Spec>(1);
   if (s.first && !e->routed) {
     e->new_list = e->alloc<int64_t>((size_t)c.max_batch);
     e->new_counts = e->alloc<unsigned long long>(2);
@@ -3924,13 +3516,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if (e->dflags) HIPCHK(e, hipMemsetAsync(e->dflags, 0, 4 * FLAG_RING, e->stream));
   if (e->bload) HIPCHK(e, hipMemsetAsync(e->bload, 0, 4 * 4 * RT_MAXNB, e->stream));
   if (e->fold_flag) HIPCHK(e, hipMemsetAsync(e->fold_flag, 0, 4 * (size_t)5 * RT_MAXNB * RT_GS, e->stream));
-  if (e->routed) {   // k_route reads the Spec, k_agg_f the engine's constants, from device copies
-    AggCold& k = e->cold_host;
-    k.dir_keys = s.dir_keys; k.slice_tag = s.slice_tag; k.c = s.c; k.err = s.err; k.stats = s.stats;
-    k.dir_min_used = s.dir_min_used; k.bload = e->bload; k.fold_flag = e->fold_flag; k.dflags = e->dflags;
-    k.bload_host = e->bload_host; k.stamps = e->rb.stamps; k.stride = s.stride; k.D = s.D; k.P = s.P; k.nb = s.nb;
-    k.seg_stride = e->max_tiles; k.cmpto = s.cmpto;
-    HIPCHK(e, hipMemcpyAsync(e->cold_dev, &e->cold_host, sizeof(AggCold), hipMemcpyHostToDevice, e->stream));
+  if (e->routed) {   // k_route reads the Spec from a device copy
     if (int rc = upload_spec(e)) return rc;
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
