@@ -264,14 +264,16 @@ __host__ __device__ __forceinline__ int64_t sum_identity(int32_t vt) { return vt
 // orderable codes of a value for the min / max columns: int64 values as they are; doubles in Math.min /
 // Math.max order, or Double.compareTo order for ComparableAggregator (.min/.max with FW_AGGF_COMPARABLE,
 // and always for maxBy/minBy)
-__device__ __forceinline__ int64_t min_code(int32_t vt, bool cmpto, int64_t v) {
+__host__ __device__ __forceinline__ int64_t min_code(int32_t vt, bool cmpto, int64_t v) {
   if (vt == FW_VALUE_I64) return v;
-  const double d = __longlong_as_double(v);
+  double d;
+  memcpy(&d, &v, 8);
   return cmpto ? f64_cmp_code(d) : f64_min_code(d);
 }
-__device__ __forceinline__ int64_t max_code(int32_t vt, bool cmpto, int64_t v) {
+__host__ __device__ __forceinline__ int64_t max_code(int32_t vt, bool cmpto, int64_t v) {
   if (vt == FW_VALUE_I64) return v;
-  const double d = __longlong_as_double(v);
+  double d;
+  memcpy(&d, &v, 8);
   return cmpto ? f64_cmp_code(d) : f64_max_code(d);
 }
 
@@ -2105,20 +2107,315 @@ constexpr int WM_MAXT = MAX_P + MAX_K;   // windows firing at one watermark: eve
 constexpr int WM_MAXP = MAX_P;     // slices purged at one watermark (>= P)
 constexpr int32_t PURGE_GHOST = 1 << 30;   // purge list flag: keep the panes' cleanup timers (Spec::gfirst)
 
+constexpr int WM_C = 8;                    // slices whose panes one thread loads at once (one round trip each)
+
+// a pane's state for the fire pass: the columns the reduce shape keeps (AGG 15: the runtime set)
+template <int VT, int AGG>
+__device__ __forceinline__ LateAcc wm_load(const Spec& s, int64_t idx) {
+  constexpr bool BY = (AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;   // maxBy / minBy come alone (fw_create)
+  LateAcc a;
+  a.vt = VT;
+  if (AGG == 15) {   // the runtime column set, never maxBy / minBy
+    if (s.c.sum) a.sum = s.c.sum[idx];
+    if (s.c.mn) a.mn = s.c.mn[idx];
+    if (s.c.mx) a.mx = s.c.mx[idx];
+    if (s.c.cnt) a.cnt = s.c.cnt[idx];
+    return a;
+  }
+  if (BY) {   // the extremal record: its code, its ordinal (count column) and its f1
+    a.by = s.by | (s.by_last ? 1 : 0);
+    if (AGG & FW_AGG_MAXBY) a.mx = s.c.mx[idx]; else a.mn = s.c.mn[idx];
+    a.ord = s.c.cnt[idx];
+    a.f1 = s.c.f1v[idx];
+    return a;
+  }
+  if (AGG & FW_AGG_SUM) a.sum = s.c.sum[idx];
+  if (AGG & FW_AGG_MIN) a.mn = s.c.mn[idx];
+  if (AGG & FW_AGG_MAX) a.mx = s.c.mx[idx];
+  if (AGG & FW_AGG_COUNT) a.cnt = s.c.cnt[idx];
+  return a;
+}
+template <int VT, int AGG>
+__device__ __forceinline__ LateAcc wm_combine(const LateAcc& a, const LateAcc& b) {
+  if (AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) return by_select(a, b);
+  LateAcc r = a;   // (absent columns hold their identities on both sides)
+  if (AGG & FW_AGG_SUM)
+    r.sum = VT == FW_VALUE_I64 ? jadd(a.sum, b.sum)
+                               : __double_as_longlong(__longlong_as_double(a.sum) + __longlong_as_double(b.sum));
+  if (AGG & FW_AGG_MIN) r.mn = a.mn < b.mn ? a.mn : b.mn;
+  if (AGG & FW_AGG_MAX) r.mx = a.mx > b.mx ? a.mx : b.mx;
+  if (AGG & FW_AGG_COUNT) r.cnt = jadd(a.cnt, b.cnt);
+  return r;
+}
+// a slice pane back to the empty state (WindowOperator.clearAllState -> windowState.clear())
+__device__ __forceinline__ void pane_clear(const Spec& s, int64_t idx) {
+  if (s.c.sum) s.c.sum[idx] = sum_identity(s.vt);
+  if (s.c.mn) s.c.mn[idx] = INT64_MAX;
+  if (s.c.mx) s.c.mx[idx] = INT64_MIN;
+  if (s.c.cnt) s.c.cnt[idx] = 0;
+  if (s.first) s.c.first[idx] = INT64_MAX; else s.c.present[idx] = 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-element fires of tumbling windows in one pass (WindowOperator.processElement :317-325 for each late
+// record in arrival order, EventTimeTrigger.onElement FIRE): over the (pane, arrival)-sorted late list, an
+// ordered segmented scan whose segment head folds in the pane's state before the batch, so every record's
+// result is its running window content; each record emits it, each segment tail writes the pane back.
+// Tiles take tickets in launch order and chain their carries by decoupled look-back (a tile holding a
+// segment head publishes its inclusive carry at once), so the list is read once and the pane state
+// columns once per segment.  Replaces prepare / tile scan / carries / apply / emit / commit (six kernels
+// and ~270 B of accumulator traffic per record).
+// ------------------------------------------------------------------------------------------------
+constexpr int LF_T = 256;                   // records per tile, one per thread
+struct LfPart {
+  LateAcc v;        // the segment's running content (its head folded in the pane's state before the batch)
+  int64_t sf1;      // the segment's first-arrival f1 (the pane's, else its head record's)
+  int64_t sfirst;   // the head record's arrival ordinal
+  int32_t head;     // a segment starts inside
+  int32_t bpres;    // the pane existed before the batch (of the last head inside)
+  int32_t empty;
+};
+template <int VT, int AGG>
+__device__ __forceinline__ LfPart lf_join(const LfPart& x, const LfPart& y) {
+  if (y.empty) return x;
+  if (x.empty) return y;
+  LfPart r = y;
+  if (!y.head) {   // y continues x's segment
+    r.v = wm_combine<VT, AGG>(x.v, y.v);
+    r.sf1 = x.sf1; r.sfirst = x.sfirst; r.bpres = x.bpres;
+    r.head = x.head;
+  }
+  return r;
+}
+__device__ __forceinline__ LfPart lf_shfl(const LfPart& v, int src) {
+  static_assert(sizeof(LfPart) % 4 == 0, "LfPart moves in dwords");
+  LfPart r;
+  const int* a = (const int*)&v;
+  int* b = (int*)&r;
+#pragma unroll
+  for (int w = 0; w < (int)(sizeof(LfPart) / 4); ++w) b[w] = __shfl(a[w], src);
+  return r;
+}
+// a tile's carry crosses XCDs: written and read with agent-scope atomics (they bypass the XCD's L2), the
+// writer waiting for its stores before it raises the flag — no release fence, whose L2 write-back cost
+// ~20-50 us per tile behind the batch's output stores
+__device__ __forceinline__ void lf_put(LfPart* dst, const LfPart& v) {
+  static_assert(sizeof(LfPart) % 8 == 0, "LfPart moves in qwords");
+  const unsigned long long* a = (const unsigned long long*)&v;
+  unsigned long long* b = (unsigned long long*)dst;
+#pragma unroll
+  for (int w = 0; w < (int)(sizeof(LfPart) / 8); ++w) __hip_atomic_store(b + w, a[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ LfPart lf_get(const LfPart* src) {
+  LfPart r;
+  unsigned long long* b = (unsigned long long*)&r;
+  const unsigned long long* a = (const unsigned long long*)src;
+#pragma unroll
+  for (int w = 0; w < (int)(sizeof(LfPart) / 8); ++w)
+    b[w] = __hip_atomic_load((unsigned long long*)(a + w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return r;
+}
+__device__ __forceinline__ void lf_raise(unsigned int* flag, unsigned int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the data's stores acknowledged first
+  __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct LfLink {            // one tile's published carry: epoch << 2 | 1 (tile aggregate), | 2 (inclusive prefix)
+  unsigned int* flag;
+  LfPart* agg;
+  LfPart* incl;
+  unsigned long long* base;   // [0] the launch's first output slot, [1] its epoch
+  unsigned int* ticket;
+  unsigned int ticket0, epoch;
+};
+
+template <int VT, int AGG, bool FIRST>
+__global__ __launch_bounds__(LF_T) void k_late_fused(Spec s, const unsigned long long* __restrict__ sorted_key, int64_t nl,
+                                                     int32_t idx_bits, const int64_t* __restrict__ val,
+                                                     const int64_t* __restrict__ f1col, int64_t ord_base, LfLink L) {
+  __shared__ __attribute__((aligned(16))) unsigned char sp_raw[LF_T * sizeof(LfPart)];
+  LfPart* sp = (LfPart*)sp_raw;
+  __shared__ __attribute__((aligned(16))) unsigned char carry_raw[sizeof(LfPart)];
+  LfPart& carry_s = *(LfPart*)carry_raw;
+  __shared__ unsigned int tile_s;
+  __shared__ unsigned long long base_s;
+  constexpr bool BY = (AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;
+  const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
+  if (threadIdx.x == 0) tile_s = atomicAdd(L.ticket, 1u) - L.ticket0;
+  __syncthreads();
+  const int64_t tile = tile_s;
+  const int64_t j = tile * LF_T + threadIdx.x;
+  const unsigned long long imask = (1ull << idx_bits) - 1;
+  // this record: its pane, its accumulator; a segment head folds in the pane's state before the batch
+  LfPart a;
+  a.empty = 1; a.head = 0; a.bpres = 0; a.sf1 = 0; a.sfirst = 0;
+  unsigned long long pane = 0;
+  int64_t i_self = 0;
+  bool tail = false;
+  if (j < nl) {
+    const unsigned long long k = sorted_key[j];
+    pane = k >> idx_bits;
+    i_self = (int64_t)(k & imask);
+    const bool head = j == 0 || (sorted_key[j - 1] >> idx_bits) != pane;
+    tail = j == nl - 1 || (sorted_key[j + 1] >> idx_bits) != pane;
+    const int64_t v = val[i_self];
+    a.v.vt = VT;
+    a.v.sum = v;
+    a.v.mn = min_code(VT, s.cmpto, v);
+    a.v.mx = max_code(VT, s.cmpto, v);
+    a.v.cnt = 1;
+    if (BY) { a.v.by = s.by | (s.by_last ? 1 : 0); a.v.ord = ord_base + i_self; a.v.f1 = f1col[i_self]; }
+    a.empty = 0;
+    a.head = head;
+    a.sfirst = ord_base + i_self;
+    if (FIRST && !BY) a.sf1 = f1col[i_self];
+    if (head) {
+      const int64_t idx = (int64_t)pane;
+      const bool pres = pane_present(s, idx);
+      a.bpres = pres;
+      if (pres) {
+        a.v = wm_combine<VT, AGG>(wm_load<VT, AGG>(s, idx), a.v);
+        if (FIRST && !BY) a.sf1 = s.c.f1v[idx];
+      }
+    }
+  }
+  // inclusive segmented scan over the tile (Hillis-Steele in LDS)
+  sp[threadIdx.x] = a;
+  __syncthreads();
+  LfPart x = a;
+  for (int o = 1; o < LF_T; o <<= 1) {
+    LfPart y = x;
+    if ((int)threadIdx.x >= o) y = lf_join<VT, AGG>(sp[threadIdx.x - o], x);
+    __syncthreads();
+    sp[threadIdx.x] = y;
+    x = y;
+    __syncthreads();
+  }
+  // the tile's carry from its predecessors (decoupled look-back), and the launch's output base
+  if (threadIdx.x < 64) {   // wave 0
+    const int lane = threadIdx.x;
+    const LfPart agg = sp[LF_T - 1];
+    const unsigned int ep = L.epoch << 2;
+    if (lane == 0) {
+      if (tile == 0) {
+        __hip_atomic_store(&L.base[0], atomicAdd(s.o.count, (unsigned long long)nl), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&L.base[1], (unsigned long long)L.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (agg.head || tile == 0) {   // the inclusive prefix needs nothing before the tile's last head
+        lf_put(&L.incl[tile], agg);
+        lf_raise(&L.flag[tile], ep | 2u);
+      } else {
+        lf_put(&L.agg[tile], agg);
+        lf_raise(&L.flag[tile], ep | 1u);
+      }
+    }
+    LfPart c;
+    c.empty = 1; c.head = 0; c.bpres = 0; c.sf1 = 0; c.sfirst = 0;
+    // look back 64 tiles a step, one per lane, to the nearest inclusive prefix or segment head (none needed
+    // when the tile's first record starts a segment)
+    if (tile > 0 && !sp[0].head) {
+      int64_t hi = tile - 1;
+      while (true) {
+        const int64_t t = hi - lane;
+        LfPart e;
+        e.empty = 1; e.head = 0; e.bpres = 0; e.sf1 = 0; e.sfirst = 0;
+        bool stop = false;
+        if (t >= 0) {
+          unsigned int f;
+          do { f = __hip_atomic_load(&L.flag[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); } while ((f & ~3u) != ep || (f & 3u) == 0);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          e = lf_get((f & 2u) ? L.incl + t : L.agg + t);
+          stop = (f & 2u) || e.head;
+        }
+        const uint64_t sb = __ballot(stop);
+        const int first_stop = sb ? __builtin_ctzll(sb) : 64;
+        if (lane > first_stop) e.empty = 1;
+        for (int off = 1; off < 64; off <<= 1) {   // lane 0: the lanes' parts joined, farthest first
+          const LfPart o = lf_shfl(e, lane + off < 64 ? lane + off : lane);
+          if (lane + off < 64) e = lf_join<VT, AGG>(o, e);
+        }
+        c = lf_join<VT, AGG>(lf_shfl(e, 0), c);
+        if (sb || hi < 64) break;
+        hi -= 64;
+      }
+    }
+    if (lane == 0) {
+      if (tile > 0 && !agg.head) {
+        lf_put(&L.incl[tile], lf_join<VT, AGG>(c, agg));
+        lf_raise(&L.flag[tile], ep | 2u);
+      }
+      while (__hip_atomic_load(&L.base[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned long long)L.epoch) {
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      base_s = __hip_atomic_load(&L.base[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      carry_s = c;
+    }
+  }
+  __syncthreads();
+  if (j >= nl) return;
+  const LfPart r = lf_join<VT, AGG>(carry_s, x);   // the record's running window content
+  // PurgingTrigger: every fire purged the pane, so a record's result is itself (its segment's head: with the
+  // pane's state before the batch; its f1 the pane's, else its own, as a.sf1 holds)
+  const LateAcc out = purging ? a.v : r.v;
+  const int64_t idx = (int64_t)pane;
+  const int32_t p = (int32_t)(pane / (unsigned long long)s.stride);
+  const int64_t kid = (int64_t)(pane % (unsigned long long)s.stride);
+  int64_t f1 = 0;
+  if (BY) f1 = out.f1;
+  else if (FIRST) f1 = purging ? a.sf1 : r.sf1;
+  emit_record(s, base_s + (unsigned long long)j, kid_key(s, kid), f1, slot_max_ts(s, p), out);
+  if (!tail) return;
+  // segment tail: the pane after the batch's per-element fires
+  if (purging) {   // FIRE_AND_PURGE after the last element: the pane cleared, its cleanup timer kept (s.gfirst)
+    if (s.gfirst) {
+      int64_t o = s.first ? r.sfirst : 0;
+      if (s.first && s.c.first[idx] < o) o = s.c.first[idx];
+      if (o < s.gfirst[idx]) s.gfirst[idx] = o;
+    }
+    pane_clear(s, idx);
+    return;
+  }
+  if (s.c.sum) s.c.sum[idx] = r.v.sum;
+  if (s.c.mn) s.c.mn[idx] = r.v.mn;
+  if (s.c.mx) s.c.mx[idx] = r.v.mx;
+  if (s.c.cnt) s.c.cnt[idx] = BY ? r.v.ord : r.v.cnt;
+  if (BY) s.c.f1v[idx] = r.v.f1;
+  if (!r.bpres) {
+    if (s.first) { s.c.first[idx] = r.sfirst; if (!BY) s.c.f1v[idx] = r.sf1; }
+    else s.c.present[idx] = 1;
+  }
+}
+
+// k_watermark's LDS, sized per engine (a small plan leaves the CU's LDS to the route and aggregate
+// workgroups it runs beside): windows firing at one watermark are those holding a live slice (each slice
+// lies in ceil(K / R) windows) or a window pane, at most WM_MAXT
+__host__ __device__ inline int32_t wm_max_tasks(int32_t P, int32_t K, int32_t R, int32_t W) {
+  const int64_t t = (int64_t)P * ((K + R - 1) / R) + W;
+  return (int32_t)(t < WM_MAXT ? t : WM_MAXT);
+}
+__host__ __device__ inline size_t wm_lds_bytes(int32_t P, int32_t K, int32_t R, int32_t W) {
+  return 8 * ((size_t)wm_max_tasks(P, K, R, W) + P) + 4 * ((size_t)P + K + (W > 0 ? W : 1)) + 16;
+}
+
 template <int VT, int AGG, bool FIRST>
 __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old, int64_t wm_new, unsigned int* done) {
-  __shared__ int64_t task_n[WM_MAXT];
-  __shared__ int32_t purge[WM_MAXP];
-  __shared__ int32_t slots[MAX_K];
-  __shared__ int32_t wpurge[WM_MAXP];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int32_t maxt = wm_max_tasks(s.P, s.K, s.R, s.W);
+  int64_t* task_n = (int64_t*)smem;                // [maxt]
+  int64_t* tags = task_n + maxt;                   // [P] the slice tags, read once
+  int32_t* purge = (int32_t*)(tags + s.P);         // [P]
+  int32_t* slots = purge + s.P;                    // [K]
+  int32_t* wpurge = slots + s.K;                   // [max(W, 1)]
   __shared__ int32_t n_tasks, n_purge, n_wpurge, wslot_t, last;
   __shared__ int32_t wtot[WM_THREADS / 64];
   __shared__ unsigned long long base;
   __shared__ unsigned long long fired;
   if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; n_wpurge = 0; last = 0; fired = 0; }
+  for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) tags[p] = s.slice_tag[p];
   __syncthreads();
   for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) {
-    const int64_t m = s.slice_tag[p];
+    const int64_t m = tags[p];
     if (m == FREE_TAG) continue;
     const int64_t n_hi = floor_div(m, s.R);
     const int64_t n_lo = floor_div(m - s.K, s.R) + 1;
@@ -2130,11 +2427,11 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) purge_now = fire_purge = true;   // the slice is the window
       bool owner = true;                                                    // first live slice of window n
       for (int64_t mm = n * s.R; mm < m; ++mm) {
-        if (s.slice_tag[floor_mod(mm, s.P)] == mm) { owner = false; break; }
+        if (tags[floor_mod(mm, s.P)] == mm) { owner = false; break; }
       }
       if (!owner) continue;
       const int32_t t = atomicAdd(&n_tasks, 1);
-      if (t < WM_MAXT) task_n[t] = n;
+      if (t < maxt) task_n[t] = n;
       else cap_error(s, 12);
     }
     const int64_t ct = cleanup_time(jsub(jadd(window_start_n(s, n_hi), s.size), 1), s.lateness);
@@ -2142,7 +2439,8 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     if (purge_now) {
       const int32_t q = atomicAdd(&n_purge, 1);
       // a fire's purge keeps the panes' cleanup timers (as ghost ordinals) until the cleanup time
-      if (q < WM_MAXP) purge[q] = p | ((s.gfirst && fire_purge && ct > wm_new) ? PURGE_GHOST : 0);
+      const bool ghost = s.gfirst && fire_purge && ct > wm_new;
+      if (q < s.P) purge[q] = p | (ghost ? PURGE_GHOST : 0);
     }
   }
   // window panes (sliding: the assigner's extra windows): a firing window without any live slice is a task
@@ -2153,29 +2451,31 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
     if (max_ts > wm_old && max_ts <= wm_new) {
       bool slice_live = false;
-      for (int64_t mm = n * s.R; mm < n * s.R + s.K && !slice_live; ++mm) slice_live = s.slice_tag[floor_mod(mm, s.P)] == mm;
+      for (int64_t mm = n * s.R; mm < n * s.R + s.K && !slice_live; ++mm) slice_live = tags[floor_mod(mm, s.P)] == mm;
       if (!slice_live) {
         const int32_t t = atomicAdd(&n_tasks, 1);
-        if (t < WM_MAXT) task_n[t] = n;
+        if (t < maxt) task_n[t] = n;
         else cap_error(s, 12);
       }
     }
     if (cleanup_time(max_ts, s.lateness) <= wm_new) {
       const int32_t q = atomicAdd(&n_wpurge, 1);
-      if (q < WM_MAXP) wpurge[q] = w;
+      if (q < s.W) wpurge[q] = w;
     }
   }
   __syncthreads();
-  const int32_t nt = min(n_tasks, WM_MAXT), np = min(n_purge, WM_MAXP), nwp = min(n_wpurge, WM_MAXP);
+  const int32_t nt = min(n_tasks, maxt), np = min(n_purge, s.P), nwp = min(n_wpurge, s.W);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t gstride = (int64_t)gridDim.x * WM_THREADS;
-  LateCombine op;
+  // windows of many slices: a key id without a key holds no pane, so its key is read first and gates the
+  // slice loads (a quarter of the directory is live at the default load)
+  const bool gate = s.K > 2;
   for (int32_t t = 0; t < nt; ++t) {
     const int64_t n = task_n[t];
     if (threadIdx.x < s.K) {
       const int64_t mm = n * s.R + threadIdx.x;
       const int32_t pp = (int32_t)floor_mod(mm, s.P);
-      slots[threadIdx.x] = s.slice_tag[pp] == mm ? pp : -1;
+      slots[threadIdx.x] = tags[pp] == mm ? pp : -1;
     }
     if (threadIdx.x == 0) wslot_t = wpane_slot(s, n);
     __syncthreads();
@@ -2188,24 +2488,41 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       LateAcc a;
       a.vt = VT;
       int64_t best_ord = INT64_MAX, f1 = 0;
-      if (kid < s.stride) {
-        for (int k = 0; k < s.K; ++k) {
-          const int32_t p = slots[k];
-          if (p < 0) continue;
-          const int64_t idx = (int64_t)p * s.stride + kid;
-          bool pres;
-          if (FIRST) {
-            const int64_t o = s.c.first[idx];
-            pres = o != INT64_MAX;
-            if (pres && o < best_ord) { best_ord = o; f1 = s.c.f1v[idx]; }
-          } else {
-            pres = s.c.present[idx] != 0;
+      const int64_t key = kid < s.stride ? kid_key(s, kid) : EMPTY_KEY;
+      const bool live = kid < s.stride && !(gate && kid != s.D && key == EMPTY_KEY);
+      if (live) {
+        for (int kb = 0; kb < s.K; kb += WM_C) {
+          // the chunk's presence words in one round trip, then the present panes' columns in one more
+          int64_t fo[WM_C];
+#pragma unroll
+          for (int j = 0; j < WM_C; ++j) {
+            const int32_t v = kb + j < s.K ? slots[kb + j] : -1;
+            fo[j] = INT64_MAX;
+            if (v >= 0) {
+              const int64_t idx = (int64_t)v * s.stride + kid;
+              fo[j] = FIRST ? s.c.first[idx] : (s.c.present[idx] ? 0 : INT64_MAX);
+            }
           }
-          if (!pres) continue;
-          if (p_dis >= 0 && !s.armed[idx]) continue;
-          const LateAcc b = pane_load(s, idx);
-          a = any ? op(a, b) : b;
-          any = true;
+          if (FIRST) {
+            int jb = -1;
+#pragma unroll
+            for (int j = 0; j < WM_C; ++j) if (fo[j] < best_ord) { best_ord = fo[j]; jb = j; }
+            if (jb >= 0) f1 = s.c.f1v[(int64_t)slots[kb + jb] * s.stride + kid];
+          }
+          LateAcc b[WM_C];
+#pragma unroll
+          for (int j = 0; j < WM_C; ++j) {
+            if (fo[j] == INT64_MAX) continue;
+            b[j] = wm_load<VT, AGG>(s, (int64_t)slots[kb + j] * s.stride + kid);
+          }
+#pragma unroll
+          for (int j = 0; j < WM_C; ++j) {
+            if (fo[j] == INT64_MAX) continue;
+            if (p_dis < 0 || s.armed[(int64_t)slots[kb + j] * s.stride + kid]) {
+              a = any ? wm_combine<VT, AGG>(a, b[j]) : b[j];
+              any = true;
+            }
+          }
         }
         if (wslot_t >= 0) {   // the window's own pane
           const int64_t idx = (int64_t)wslot_t * s.stride + kid;
@@ -2215,7 +2532,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
               if (o < best_ord) { best_ord = o; f1 = s.wc.f1v[idx]; }
             }
             const LateAcc b = cols_load(s, s.wc, idx);
-            a = any ? op(a, b) : b;
+            a = any ? LateCombine()(a, b) : b;
             any = true;
           }
         }
@@ -2229,25 +2546,23 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       for (int w = 0; w < WM_THREADS / 64; ++w) { const int32_t c = wtot[w]; off += w < wave ? c : 0; tot += c; }
       if (threadIdx.x == 0 && tot > 0) { base = atomicAdd(s.o.count, (unsigned long long)tot); fired += tot; }
       __syncthreads();
-      if (any) emit_record(s, base + off + rank, kid_key(s, kid), s.by ? a.f1 : f1, max_ts, a);
+      if (any) emit_record(s, base + off + rank, key, s.by ? a.f1 : f1, max_ts, a);
     }
     __syncthreads();
   }
-  // purge this workgroup's share of the expired slices (it fired that share above)
+  // purge this workgroup's share of the expired slices (it fired that share above; clearing each pane as the
+  // fire reads it writes partial column lines and measured slower beside the next batch's kernels)
   for (int32_t q = 0; q < np; ++q) {
     const bool ghost = (purge[q] & PURGE_GHOST) != 0;
-    const int64_t pbase = (int64_t)(purge[q] & ~PURGE_GHOST) * s.stride;
+    const int32_t p = purge[q] & ~PURGE_GHOST;
+    const int64_t pbase = (int64_t)p * s.stride;
     for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < s.stride; kid += gstride) {
       const int64_t idx = pbase + kid;
       if (ghost) {
         const int64_t o = s.first ? s.c.first[idx] : (s.c.present[idx] ? 0 : INT64_MAX);
         if (o < s.gfirst[idx]) s.gfirst[idx] = o;
       }
-      if (s.c.sum) s.c.sum[idx] = sum_identity(s.vt);
-      if (s.c.mn) s.c.mn[idx] = INT64_MAX;
-      if (s.c.mx) s.c.mx[idx] = INT64_MIN;
-      if (s.c.cnt) s.c.cnt[idx] = 0;
-      if (s.first) s.c.first[idx] = INT64_MAX; else s.c.present[idx] = 0;
+      pane_clear(s, idx);
     }
   }
   for (int32_t q = 0; q < nwp; ++q) {
@@ -2422,6 +2737,7 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
 // their window fires (a record whose extra window had already fired is rejected at ingest).
 __global__ __launch_bounds__(1024) void k_quirk_apply(Spec s, int64_t* list, unsigned long long* count, int64_t cap) {
   const int64_t n = min((int64_t)*count, cap);
+  if (n == 0) return;   // the usual batch (timestamps past the offset by a slide have no extra window)
   for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
     int64_t* q = list + e * QK_WORDS;
     const int64_t kid = dir_lookup(s, q[0]);
@@ -2815,6 +3131,13 @@ struct fw_engine {
   SegPart* seg_tiles = nullptr;   // the late scan's per-tile aggregates, then carries
   SegPart* seg_groups = nullptr;  // ... and per group of LS_CT tiles (two-level carries)
   int32_t* seg_first = nullptr;   // ... and first segment head per tile
+  // tumbling per-element fires in one pass (k_late_fused): per-tile look-back links, launch epochs, tickets
+  bool late_fused = true;
+  unsigned int* lf_flag = nullptr;
+  LfPart *lf_agg = nullptr, *lf_incl = nullptr;
+  unsigned long long* lf_base = nullptr;
+  unsigned int* lf_ticket = nullptr;
+  unsigned int lf_ticket0 = 0, lf_epoch = 0;
   void* temp = nullptr;
   size_t temp_bytes = 0;
   int32_t idx_bits = 0;
@@ -3055,6 +3378,20 @@ static void routed_attrs_t(fw_engine* e) {
   done.insert(e->dev);
 }
 
+// k_watermark's plan grows to ~112 KiB of LDS at the largest P and K (dynamic LDS past 64 KiB needs the attribute)
+template <int VT, int AGG, bool FIRST>
+static void wm_attrs_t(fw_engine* e) {
+  static std::mutex mu;
+  static std::set<int> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count(e->dev)) return;
+  const hipError_t rc = hipFuncSetAttribute((const void*)k_watermark<VT, AGG, FIRST>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)wm_lds_bytes(MAX_P, MAX_K, 1, MAX_P));
+  if (rc != hipSuccess) { e->attr_err = rc; return; }
+  done.insert(e->dev);
+}
+
 template <int VT, int AGG, bool FIRST>
 static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col, int par) {
   RouteBuf r = e->rbs[par];
@@ -3138,9 +3475,21 @@ static bool fires_possible(const Spec& s, int64_t wm) {
 }
 
 template <int VT, int AGG, bool FIRST>
+static void launch_late_fused_t(fw_engine* e, int64_t nl, const int64_t* dv, const int64_t* df1) {
+  const unsigned int ntiles = (unsigned int)((nl + LF_T - 1) / LF_T);
+  const LfLink L{e->lf_flag, e->lf_agg, e->lf_incl, e->lf_base, e->lf_ticket, e->lf_ticket0, ++e->lf_epoch};
+  hipLaunchKernelGGL((k_late_fused<VT, AGG, FIRST>), dim3(ntiles), dim3(LF_T), 0, e->stream, e->s, e->late_key_sorted, nl,
+                     e->idx_bits, dv, df1, e->ordinal, L);
+  e->lf_ticket0 += ntiles;   // (the ticket counter wraps with it)
+}
+
+template <int VT, int AGG, bool FIRST>
 static void launch_watermark_t(fw_engine* e, int64_t wm_old, int64_t wm_new) {
+  // (one workgroup per CU: a 257th for the null key's id D = 2^k measured ~4 us slower per fire than workgroup 0
+  // taking that id's chunk too)
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + WM_THREADS - 1) / WM_THREADS, e->grid / 8));
-  hipLaunchKernelGGL((k_watermark<VT, AGG, FIRST>), dim3(blocks), dim3(WM_THREADS), 0, e->stream, e->s, wm_old, wm_new, e->wm_done);
+  hipLaunchKernelGGL((k_watermark<VT, AGG, FIRST>), dim3(blocks), dim3(WM_THREADS),
+                     wm_lds_bytes(e->s.P, e->s.K, e->s.R, e->s.W), e->stream, e->s, wm_old, wm_new, e->wm_done);
 }
 
 // dispatch over (value type, aggregate mask, first-arrival) — the instantiated reduce shapes
@@ -3273,7 +3622,9 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   s.cmpto = by || (c.agg_flags & FW_AGGF_COMPARABLE) ? 1 : 0;
   s.fold = (c.agg_flags & FW_AGGF_FOLD) ? 1 : 0;
   s.fold_init = c.fold_initial;
-  s.first = c.keep_first_f1 || by ? 1 : 0;   // maxBy/minBy: the pane's presence and the extremal f1
+  // maxBy/minBy: the pane's presence and the extremal f1; fold: first arrivals order the reference layout's
+  // entries (HashMap chains in insertion order) though no f1 is kept
+  s.first = c.keep_first_f1 || by || (c.agg_flags & FW_AGGF_FOLD) ? 1 : 0;
 
   // ingest_mode 3 was the fused form (one persistent launch per batch, XCD-local hand-off of the routed records):
   // measured slower than the partitioned form in rounds 3 and 4 (23 / 14 G vs 51-56 G events/s on C1), removed
@@ -3340,7 +3691,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   OutLog& o = s.o;
   o.capacity = c.out_capacity;
   o.key = e->alloc<int64_t>((size_t)o.capacity);
-  o.f1 = s.first ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
+  o.f1 = c.keep_first_f1 || s.by ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
   o.ts = e->alloc<int64_t>((size_t)o.capacity);
   o.sum = (s.agg & FW_AGG_SUM) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
   o.mn = (s.agg & (FW_AGG_MIN | FW_AGG_MINBY)) ? e->alloc<int64_t>((size_t)o.capacity) : nullptr;
@@ -3432,6 +3783,14 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       }
     }
   }
+  if (wm_lds_bytes(s.P, s.K, s.R, s.W) > 64 * 1024) {
+    FW_DISPATCH(wm_attrs_t, e);
+    if (e->attr_err != hipSuccess) {
+      g_create_error = std::string("hipFuncSetAttribute(MaxDynamicSharedMemorySize): ") + hipGetErrorString(e->attr_err);
+      delete e;
+      return FW_ERR_DEVICE;
+    }
+  }
   e->wm_done = e->alloc<unsigned int>(1);
   if (e->routed) e->s_dev = e->alloc<Spec>(1);
   if (s.first && !e->routed) {
@@ -3466,6 +3825,21 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     e->seg_tiles = e->alloc<SegPart>(nb / LS_TILE + 1);
     e->seg_groups = e->alloc<SegPart>((nb / LS_TILE + 1) / LS_CT + 2);
     e->seg_first = e->alloc<int32_t>(nb / LS_TILE + 1);
+    if (c.assigner != FW_SLIDING) {
+      const char* lf = getenv("FW_LATE_FUSED");   // 0: the six-kernel scan (A/B)
+      e->late_fused = !(lf && atoi(lf) == 0);
+      const size_t nt = (size_t)c.max_batch / LF_T + 1;
+      e->lf_flag = e->alloc<unsigned int>(nt);
+      e->lf_agg = e->alloc<LfPart>(nt);
+      e->lf_incl = e->alloc<LfPart>(nt);
+      e->lf_base = e->alloc<unsigned long long>(2);
+      e->lf_ticket = e->alloc<unsigned int>(1);
+      if (!e->lf_flag || !e->lf_base || !e->lf_ticket || hipMemset(e->lf_flag, 0, 4 * nt) != hipSuccess ||
+          hipMemset(e->lf_base, 0, 16) != hipSuccess || hipMemset(e->lf_ticket, 0, 4) != hipSuccess) {
+        delete e;
+        return FW_ERR_DEVICE;
+      }
+    }
     size_t t1 = 0;
     (void)rocprim::radix_sort_keys(nullptr, t1, e->late_key, e->late_key_sorted, nb, 0, 64, e->stream);
     e->temp_bytes = t1;
@@ -3707,7 +4081,13 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
       e->late_fires_host += (int64_t)nf;
       HIPCHK(e, hipMemsetAsync(e->fire_count, 0, 8, e->stream));
     }
-    if (nl > 0) {
+    if (nl > 0 && !sliding && e->late_fused) {
+      size_t tb = e->temp_bytes;
+      HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, e->late_key, e->late_key_sorted, (size_t)nl, 0, key_bits, e->stream));
+      FW_DISPATCH(launch_late_fused_t, e, (int64_t)nl, dv, df1);
+      e->late_fires_host += (int64_t)nl;
+      HIPCHK(e, hipMemsetAsync(e->late_count, 0, 8, e->stream));
+    } else if (nl > 0) {
       if (int rc = sorted_scan(e->late_key, nl, sliding ? 0 : (int64_t)nl)) return rc;
       const int blocks = (int)((nl + BLOCK - 1) / BLOCK);
       if (!sliding) {
@@ -4322,7 +4702,6 @@ int fw_snapshot_kg(fw_engine* e, int32_t kg, void* buf, int64_t cap, int64_t* le
   if (!e || !len) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
   if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
-  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (window_panes_used(e)) return reject(e, FW_ERR_UNSUPPORTED, "sliding windows: records below offset - slide put state in window panes, which no checkpoint layout carries");
   if (!e->disarmed.empty())
     return reject(e, FW_ERR_UNSUPPORTED, "restored windows without trigger timers: only the reference layout (explicit "
@@ -4355,7 +4734,6 @@ int fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len) {
   if (!e || !buf) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
   if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
-  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
   if (len < 8 * FW_SNAP_HEADER_WORDS) return reject(e, FW_ERR_INVALID_ARG, "snapshot blob too short");
@@ -4430,7 +4808,7 @@ static int check_state_layout(fw_engine* e, const fw_state_layout* L) {
   }
   const fw_config& c = e->cfg;
   const bool by = e->s.by;
-  const int want[FW_SF_VALUE + 1] = {0, -1, e->s.first ? 1 : 0, !by && (c.agg_mask & FW_AGG_SUM) ? 1 : 0,
+  const int want[FW_SF_VALUE + 1] = {0, -1, c.keep_first_f1 || by ? 1 : 0, !by && (c.agg_mask & FW_AGG_SUM) ? 1 : 0,
                                      !by && (c.agg_mask & FW_AGG_MIN) ? 1 : 0, !by && (c.agg_mask & FW_AGG_MAX) ? 1 : 0,
                                      !by && (c.agg_mask & FW_AGG_COUNT) ? 1 : 0, by ? 1 : 0};
   if (seen[FW_SF_KEY] > 1) return reject(e, FW_ERR_INVALID_ARG, "state layout names the key twice");
@@ -4445,8 +4823,31 @@ static int64_t host_window_start(const fw_config& c, int64_t n) {
   return fw::jadd(c.offset, (int64_t)((uint64_t)n * (uint64_t)(c.assigner == FW_TUMBLING ? c.size : c.slide)));
 }
 
+// HeapFoldingState holds the accumulator: the fold's initial value folded with the pane (as emit_record
+// applies it), and back (sum and count subtract it: exact for Long, to the last bit for doubles only when
+// the initial value is 0; min and max hold it already: the accumulator is at or beyond it)
+static KgPane fold_pane(const fw_engine* e, KgPane p) {
+  const fw::Spec& s = e->s;
+  const int64_t x = s.fold_init;
+  if (s.vt == FW_VALUE_I64) p.sum = fw::jadd(x, p.sum);
+  else { double a, b; memcpy(&a, &x, 8); memcpy(&b, &p.sum, 8); b = a + b; memcpy(&p.sum, &b, 8); }
+  p.mn = std::min(p.mn, fw::min_code(s.vt, s.cmpto, x));
+  p.mx = std::max(p.mx, fw::max_code(s.vt, s.cmpto, x));
+  p.cnt = fw::jadd(x, p.cnt);
+  return p;
+}
+static KgPane unfold_pane(const fw_engine* e, KgPane p) {
+  const fw::Spec& s = e->s;
+  const int64_t x = s.fold_init;
+  if (s.vt == FW_VALUE_I64) p.sum = fw::jsub(p.sum, x);
+  else { double a, b; memcpy(&a, &x, 8); memcpy(&b, &p.sum, 8); b = b - a; memcpy(&p.sum, &b, 8); }
+  p.cnt = fw::jsub(p.cnt, x);
+  return p;
+}
+
 // the pane value of field f, written as the field's Java type
-static void put_field(const fw_engine* e, fwkg::BeOut& o, int f, const KgPane& p) {
+static void put_field(const fw_engine* e, fwkg::BeOut& o, int f, const KgPane& p_in) {
+  const KgPane p = e->s.fold ? fold_pane(e, p_in) : p_in;
   const bool f64 = e->s.vt == FW_VALUE_F64;
   auto val = [&](int64_t bits) { if (f64) { double d; memcpy(&d, &bits, 8); o.f64(d); } else o.i64(bits); };
   auto code = [&](int64_t c) { if (f64) o.f64(fw::f64_from_code(c)); else o.i64(c); };
@@ -4550,7 +4951,6 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   if (!e || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
   if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
-  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -4672,7 +5072,6 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   if (!e || (!state && state_len) || !timers || state_len < 0) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
   if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
-  if (e->s.fold) return reject(e, FW_ERR_UNSUPPORTED, "fold: the folded accumulator has no checkpoint layout here");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
   if (kg < e->s.kg_start || kg > e->s.kg_end)
@@ -4725,6 +5124,7 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
           }
         }
         if (!in.ok) break;
+        if (s.fold) p = unfold_pane(e, p);
         if (host_key_group(s, p.key) != kg) return reject(e, FW_ERR_KEY_GROUP, "state entry key outside its key group");
         if (!seen.insert({m, p.key}).second) return reject(e, FW_ERR_INVALID_ARG, "duplicate (window, key) entry");
         panes.push_back(p);

@@ -943,7 +943,6 @@ int fwo_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layou
   if (!e || !layout || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
   if (kg < e->op.cfg.kg_start || kg > e->op.cfg.kg_end) return FW_ERR_INVALID_ARG;
   if (e->op.cfg.assigner == FW_SESSION) { e->op.err = "session windows: no checkpoint layout"; return FW_ERR_UNSUPPORTED; }
-  if (e->op.cfg.agg_flags & FW_AGGF_FOLD) { e->op.err = "fold: no checkpoint layout"; return FW_ERR_UNSUPPORTED; }
   JavaOut st, tm;
   snapshotKeyGroup(e->op, kg, *layout, st, tm);
   *state_len = (int64_t)st.b.size();

@@ -580,3 +580,79 @@ def test_native_snapshot_purging_lateness(mode):
     assert any(tm != b"\x00\x00\x00\x00" and len(tm) > 4 for _, tm in so.values())
     g.close()
     o.close()
+
+
+FOLD_CASES = [("sum", 123456789, "i64", "tumbling"), ("count", -7, "i64", "sliding"), ("max", 1 << 62, "i64", "tumbling"),
+              ("min", 0.25, "f64", "sliding"), ("sum", 2.5, "f64", "tumbling")]
+
+
+def _fold_run(factory, kind, initial, vt, assigner, mode, restore=None):
+    """Drive 2/3 of a Zipf stream through a fold engine and snapshot every key group in the reference layout
+    (the key and the accumulator: HeapFoldingState's value); or restore such snapshots at their watermark and
+    drive the rest to a final MAX_WATERMARK."""
+    from flink_amd.windowing import FoldFunction, SlidingEventTimeWindows, TumblingEventTimeWindows, make_config
+    from harness import drive, gen_stream
+    a = TumblingEventTimeWindows.of(1000) if assigner == "tumbling" else SlidingEventTimeWindows.of(3000, 1000)
+    keys, ts, vals = gen_stream(40_000, 2000, rate=1 << 14, zipf=1.1, ooo=300, value_type=vt)
+    cfg = make_config(a, FoldFunction(kind, initial, vt), None, 0, max_parallelism=128, key_capacity=1 << 13,
+                      max_batch=1 << 14, out_capacity=1 << 20, ingest_mode=mode)
+    layout = ("key", kind)
+    n = len(keys) * 2 // 3
+    wm = int(ts[:n].max()) - 120
+    e = factory(cfg)
+    if restore is None:
+        drive(e, keys[:n], ts[:n], vals[:n], 4096, 120, None)
+        snaps = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        e.close()
+        return snaps, wm
+    for kg, (st, tm) in restore.items():
+        e.restore_kg_flink(kg, layout, st, tm, wm)
+    back = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+    out = drive(e, keys[n:], ts[n:], vals[n:], 4096, 120, LONG_MAX)
+    e.close()
+    return back, out
+
+
+@pytest.mark.parametrize("kind,initial,vt,assigner", FOLD_CASES)
+def test_oracle_fold_checkpoint_round_trip(kind, initial, vt, assigner):
+    """The oracle's HeapFoldingState sections restore and snapshot back byte for byte."""
+    from oracle.oracle import OracleEngine
+    snaps, _ = _fold_run(OracleEngine, kind, initial, vt, assigner, 0)
+    assert sum(len(s) for s, _ in snaps.values()) > 128 * 8
+    back, _ = _fold_run(OracleEngine, kind, initial, vt, assigner, 0, restore=snaps)
+    assert _diff(back, snaps) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("kind,initial,vt,assigner", FOLD_CASES)
+def test_fold_checkpoint(mode, kind, initial, vt, assigner):
+    """fold in the reference layout (WindowOperator's window-contents as HeapFoldingState: the initial value
+    folded with the window's records).  The engine's sections are byte-identical to the oracle's, it restores
+    the oracle's sections (subtracting a sum or count's initial value back out), snapshots them back unchanged
+    and continues like the oracle restored from the same bytes — exactly, but for a double sum with a
+    non-zero initial value (relative 1e-12: the engine adds the initial value once, at the fire)."""
+    from flink_amd.windowing import WindowEngine
+    from oracle.oracle import OracleEngine
+    g, _ = _fold_run(WindowEngine, kind, initial, vt, assigner, mode)
+    o, _ = _fold_run(OracleEngine, kind, initial, vt, assigner, 0)
+    # a double sum is associated differently (slices, then the initial value): same layout, values to 1e-12
+    exact = not (vt == "f64" and kind == "sum")
+    if exact:
+        assert _diff(g, o) is None, _diff(g, o)
+    else:
+        assert {kg: (len(a), b) for kg, (a, b) in g.items()} == {kg: (len(a), b) for kg, (a, b) in o.items()}
+    back, out_g = _fold_run(WindowEngine, kind, initial, vt, assigner, mode, restore=o)
+    _, out_o = _fold_run(OracleEngine, kind, initial, vt, assigner, 0, restore=o)
+    if exact:
+        assert _diff(back, o) is None
+    field = "count" if kind == "count" else f"{kind}_{vt}"
+    from harness import epochs_of
+    eg, eo = epochs_of(out_g, [field]), epochs_of(out_o, [field])
+    assert [w for w, _ in eg] == [w for w, _ in eo] and sum(len(r) for _, r in eo) > 1000
+    for (w, rg), (_, ro) in zip(eg, eo):
+        if exact:
+            assert rg == ro, w
+        else:
+            assert len(rg) == len(ro) and all(x[:2] == y[:2] and abs(x[2] - y[2]) <= 1e-12 * max(1.0, abs(y[2]))
+                                              for x, y in zip(rg, ro)), w

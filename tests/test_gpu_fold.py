@@ -64,13 +64,20 @@ def test_fold_parity(hip, oracle_engine, mode, kind, initial, vt, assigner):
             assert rg == ro, wg
 
 
-def test_fold_rejections(hip):
+def test_fold_rejections_and_native_checkpoint(hip):
     from flink_amd import _abi
     from flink_amd.windowing import EventTimeSessionWindows, FoldFunction, TumblingEventTimeWindows, make_config
     with pytest.raises(_abi.FwError):   # WindowedStream.java:466-467
         hip(make_config(EventTimeSessionWindows.withGap(10), FoldFunction("sum", 0)))
+    # the native layout carries fold engines as it does reduces (raw panes; the initial value joins at the fire)
     e = hip(make_config(TumblingEventTimeWindows.of(1000), FoldFunction("sum", 5)))
     e.push(np.array([1], np.int64), np.array([5], np.int64), np.array([1], np.int64))
-    with pytest.raises(_abi.FwError, match="fold"):
-        e.snapshot_kg(0)
+    blobs = {kg: e.snapshot_kg(kg) for kg in range(128)}
+    e.close()
+    e = hip(make_config(TumblingEventTimeWindows.of(1000), FoldFunction("sum", 5)))
+    for kg, blob in blobs.items():
+        e.restore_kg(kg, blob)
+    e.advance_watermark(LONG_MAX)
+    r = e.collect()
+    assert r["n"] == 1 and int(r["sum_i64"][0]) == 6
     e.close()

@@ -629,14 +629,21 @@ int main(int argc, char** argv) {
     for (int j = 0; j < 48; ++j) k_agg<1024, 2><<<NBK, 1024, ag_lds()>>>(ain_of(c, j), c.rb[j % 2], c.pane);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
     printf("aggregate alone, 1024 thr UR2                  %7.2f us/batch\n", ms / 48 * 1e3);
+    CK(hipFuncSetAttribute((const void*)k_agg<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    CK(hipEventRecord(a));
+    for (int j = 0; j < 48; ++j) k_agg<1024, 2><<<NBK, 1024, 81 * 1024>>>(ain_of(c, j), c.rb[j % 2], c.pane);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
+    printf("aggregate alone, 1024 thr UR2, 81 KB LDS       %7.2f us/batch\n", ms / 48 * 1e3);
     fflush(stdout);
     CK(hipMalloc(&g_stamps, 8 * 8 * NBK)); CK(hipMalloc(&g_hdr, 16 * NTILE));
     k_fill<<<64, 256>>>(g_hdr, 0, 2 * NTILE);
-    for (int mode : {0, 1, 2, 4, 6}) {
+    CK(hipFuncSetAttribute((const void*)k_agg<1024, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    for (int mode : {0, 2, 4, 6, 8}) {
       g_mode = mode;
+      const size_t lds = (mode & 8) ? 81 * 1024 : ag_lds();   // 8: one workgroup per CU as the engine forces
       for (int rep = 0; rep < 3; ++rep) {
         k_route<false><<<NTILE, RT_NT, RT_LDS>>>(rin_of(c, rep), c.rb[0], c.other);
-        k_agg<1024, 2><<<NBK, 1024, ag_lds()>>>(ain_of(c, rep), c.rb[0], c.pane);
+        k_agg<1024, 2><<<NBK, 1024, lds>>>(ain_of(c, rep), c.rb[0], c.pane);
       }
       CK(hipDeviceSynchronize());
       std::vector<long long> h(8 * NBK);
