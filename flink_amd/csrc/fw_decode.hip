@@ -680,9 +680,10 @@ int fw_decode_begin(fw_engine* e, const fw_tuple_schema* sc, const void* bytes, 
                     int32_t* key_hash, int64_t* f1, int64_t* ts, void* value, int64_t record_cap, int64_t* wm,
                     int64_t* wm_pos, int64_t* lm, int64_t* lm_pos, int64_t marker_cap, int32_t* ticket) {
   if (!e || !ticket) return FW_ERR_INVALID_ARG;
-  const int slot = (int)(e->dec_seq % fw_engine::NDEC);
+  int slot = -1;   // the first free slot (decodes may end in any order)
+  for (int i = 0; i < fw_engine::NDEC && slot < 0; ++i) if (!e->dec[i].pending) slot = i;
+  if (slot < 0) { e->err = "fw_decode_begin: two decodes outstanding (fw_decode_end one first)"; return FW_ERR_INVALID_ARG; }
   fw_engine::DecSlot& ds = e->dec[slot];
-  if (ds.pending) { e->err = "fw_decode_begin: two decodes outstanding (fw_decode_end the older first)"; return FW_ERR_INVALID_ARG; }
   bool empty = true;
   int rc = decode_enqueue(e, slot, sc, bytes, nbytes, mem, key, key_hash, f1, ts, value, record_cap, wm, wm_pos, lm, lm_pos,
                           marker_cap, &empty);

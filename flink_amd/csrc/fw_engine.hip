@@ -602,10 +602,24 @@ __global__ __launch_bounds__(BLOCK) void k_fix_first_f1(Spec s, const int64_t* l
 // after a batch's ingest, while restored windows are disarmed and ahead of the watermark: each record of such a
 // window re-arms its pane's trigger timer (EventTimeTrigger.onElement registers maxTimestamp while the
 // watermark is below it; the window then fires at its maxTimestamp with everything the pane holds)
+// (sliding: each of the record's windows whose own pane is disarmed, by window-pane slot)
 __global__ __launch_bounds__(BLOCK) void k_arm(Spec s, BatchIn b) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ts = b.ts[i];
     if (ts == INT64_MIN) continue;
+    if (s.assigner == FW_SLIDING) {
+      const int64_t m = record_windows(s, ts, b.wm).m;
+      const int64_t n_hi = floor_div(m, s.R), n_lo = floor_div(m - s.K, s.R) + 1;
+      int64_t kid = -2;
+      for (int64_t n = n_lo; n <= n_hi; ++n) {
+        const int32_t w = (int32_t)floor_mod(n, s.W);
+        if (!s.disarm[w] || s.wtag[w] != n) continue;
+        if (jsub(jadd(window_start_n(s, n), s.size), 1) <= b.wm) continue;
+        if (kid == -2) kid = dir_lookup(s, b.key[i]);
+        if (kid >= 0) s.armed[(int64_t)w * s.stride + kid] = 1;
+      }
+      continue;
+    }
     const int64_t m = floor_div(jsub(ts, s.offset), s.size);   // tumbling: the slice is the window
     const int32_t p = (int32_t)floor_mod(m, s.P);
     if (!s.disarm[p] || s.slice_tag[p] != m) continue;
@@ -2481,7 +2495,10 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     __syncthreads();
     const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
     // a restored window whose trigger timers fired before the checkpoint: only re-armed panes fire
-    const int32_t p_dis = (s.disarm && s.K == 1 && slots[0] >= 0 && s.disarm[slots[0]]) ? slots[0] : -1;
+    const int32_t p_dis =
+        (s.disarm && s.assigner != FW_SLIDING && s.K == 1 && slots[0] >= 0 && s.disarm[slots[0]]) ? slots[0] : -1;
+    // (sliding: a restored window's own pane disarmed — the window fires only for the keys re-armed since)
+    const int32_t w_dis = (s.disarm && s.assigner == FW_SLIDING && wslot_t >= 0 && s.disarm[wslot_t]) ? wslot_t : -1;
     for (int64_t k0 = (int64_t)blockIdx.x * WM_THREADS; k0 < s.stride; k0 += gstride) {
       const int64_t kid = k0 + threadIdx.x;
       bool any = false;
@@ -2489,7 +2506,8 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       a.vt = VT;
       int64_t best_ord = INT64_MAX, f1 = 0;
       const int64_t key = kid < s.stride ? kid_key(s, kid) : EMPTY_KEY;
-      const bool live = kid < s.stride && !(gate && kid != s.D && key == EMPTY_KEY);
+      const bool live = kid < s.stride && !(gate && kid != s.D && key == EMPTY_KEY) &&
+                        (w_dis < 0 || s.armed[(int64_t)w_dis * s.stride + kid]);
       if (live) {
         for (int kb = 0; kb < s.K; kb += WM_C) {
           // the chunk's presence words in one round trip, then the present panes' columns in one more
@@ -3931,6 +3949,8 @@ static int device_error(fw_engine* e, int32_t derr) {
   return e->sticky;
 }
 
+static int64_t host_window_start(const fw_config& c, int64_t n);   // (below, with the checkpoint code)
+
 int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1, const int64_t* ts,
                   const void* value, int64_t n, int32_t mem) {
   if (!e) return FW_ERR_INVALID_ARG;
@@ -4019,8 +4039,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
                        e->cfg.max_batch);
   e->batches++;
   HIPCHK(e, hipGetLastError());
-  if (!e->disarmed.empty() &&
-      jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)*e->disarmed.rbegin() * (uint64_t)e->s.size)), e->s.size), 1) > e->cur_wm)
+  if (!e->disarmed.empty() && jsub(jadd(host_window_start(e->cfg, *e->disarmed.rbegin()), e->s.size), 1) > e->cur_wm)
     hipLaunchKernelGGL(k_arm, dim3(std::min<int64_t>((n + BLOCK - 1) / BLOCK, e->grid)), dim3(BLOCK), 0, e->stream, e->s, b);
   // (the direct form's record-indexed list of f1 fix-ups; the partitioned form sets f1 in k_aggregate, and session /
   // list state keep theirs themselves — new_list holds nothing of theirs)
@@ -4212,8 +4231,8 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   // restored disarmed windows whose maxTimestamp the watermark passed: their re-armed panes fired above; the
   // rest never fires again (cleanup at the cleanup time, as any window)
   for (auto it = e->disarmed.begin(); it != e->disarmed.end();) {
-    const int64_t m = *it;
-    const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)m * (uint64_t)e->s.size)), e->s.size), 1);
+    const int64_t m = *it;   // (tumbling: a slice number; sliding: a window number, its own pane's slot)
+    const int64_t max_ts = jsub(jadd(host_window_start(e->cfg, m), e->s.size), 1);
     if (max_ts > wm) { ++it; continue; }
     const int32_t p = (int32_t)floor_mod(m, e->s.P);
     HIPCHK(e, hipMemsetAsync(e->s.disarm + p, 0, 1, e->stream));
@@ -4626,7 +4645,7 @@ static int build_snapshot(fw_engine* e) {
       HIPCHK(e, hipMemcpy(present.data(), s.c.present + off, st, hipMemcpyDeviceToHost));
     }
     std::vector<uint8_t> armed;
-    const bool dis = e->disarmed.count(m) != 0;
+    const bool dis = s.assigner != FW_SLIDING && e->disarmed.count(m) != 0;
     if (dis) {
       armed.resize(st);
       HIPCHK(e, hipMemcpy(armed.data(), s.armed + off, st, hipMemcpyDeviceToHost));
@@ -4667,6 +4686,12 @@ static int build_snapshot(fw_engine* e) {
       } else {
         present.resize(st);
         HIPCHK(e, hipMemcpy(present.data(), s.wc.present + off, st, hipMemcpyDeviceToHost));
+      }
+      if (e->disarmed.count(n)) {   // a restored window that fired before: the keys no record re-armed since
+        std::vector<uint8_t> armed(st);
+        HIPCHK(e, hipMemcpy(armed.data(), s.armed + off, st, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < st; ++k)
+          if (!armed[k] && kid_kg[k] >= 0) e->snap_unarmed.insert({n, (int64_t)k == s.D ? fw::EMPTY_KEY : keys[k]});
       }
       for (size_t k = 0; k < st; ++k) {
         const bool pres = s.first ? first[k] != INT64_MAX : present[k] != 0;
@@ -4943,7 +4968,10 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
       if (s.first && b.first < a.first) { a.first = b.first; a.f1 = b.f1; }
     }
   }
-  for (auto& kv : win) out.push_back(kv.second);
+  for (auto& kv : win) {   // (sliding: a window restored disarmed and not re-armed for the key)
+    kv.second.unarmed = e->snap_unarmed.count({kv.first.first, kv.first.second}) != 0;
+    out.push_back(kv.second);
+  }
 }
 
 int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, void* state, int64_t state_cap,
@@ -5165,9 +5193,6 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   for (int64_t m : dis_now)
     if (armed_now.count(m) || e->armed_windows.count(m) || c.allowed_lateness == 0)
       return reject(e, FW_ERR_UNSUPPORTED, "a window with and without trigger timers (not an aligned checkpoint)");
-  if (sliding && !dis_now.empty())   // (disarmed windows are slice slots: tumbling only)
-    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows that fired before the checkpoint, restored below their "
-                                         "maxTimestamp (restore at the checkpoint's watermark)");
   for (int64_t m : armed_now)
     if (e->disarmed.count(m)) return reject(e, FW_ERR_UNSUPPORTED, "a window with and without trigger timers (not an aligned checkpoint)");
   for (size_t i = 0; i < panes.size(); ++i) {

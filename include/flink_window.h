@@ -206,7 +206,10 @@ int         fw_collect(fw_engine* e, fw_out* out, int32_t mem);
  * buffers, in turn) and restarts the log; it returns at once with a ticket.  fw_collect_end(ticket) waits for
  * that copy and fills `out` (FW_MEM_HOST layout) with columns valid until the next fw_collect_begin after it.  At
  * most three drains are outstanding; one holds at most min(out_capacity, 2^25) results (more: FW_ERR_CAPACITY at
- * fw_collect_end).  Device errors surface at fw_collect_end. */
+ * fw_collect_end).  Device errors surface at fw_collect_end.  Footprint: each drain's staging is allocated at its
+ * first use, sized by capacity, not by results: 3 x (columns x min(out_capacity, 2^25) x 8 B) of
+ * pinned host memory plus as much HBM (all 8 columns at out_capacity >= 2^25: 6 GiB pinned + 6 GiB device) —
+ * size out_capacity to the results a watermark can fire. */
 int         fw_collect_begin(fw_engine* e, int32_t* ticket);
 int         fw_collect_end(fw_engine* e, int32_t ticket, fw_out* out);
 int         fw_get_stats(fw_engine* e, fw_stats* st);

@@ -484,9 +484,8 @@ def test_sliding_lateness_checkpoint(mode):
     """SlidingEventTimeWindows.of(3 s, 1 s) with allowed lateness 1.5 s, checkpointed while fired windows are kept
     for their lateness: the engine's sections equal the oracle's, restore (at the checkpoint's watermark) writes them
     back — each window's state in its own window pane — and the restored engine's per-element fires and watermark
-    fires continue as the restored oracle's.  Restored at Long.MIN_VALUE, a window that fired before the checkpoint
-    would need a disarmed window pane: rejected."""
-    from flink_amd import _abi
+    fires continue as the restored oracle's, restored at the checkpoint's watermark or at Long.MIN_VALUE (windows
+    that fired before the checkpoint: disarmed window panes, re-armed per key by later records)."""
     from flink_amd.windowing import ReduceFunction, SlidingEventTimeWindows, WindowEngine, make_config
     from harness import drive, gen_stream
     from oracle.oracle import OracleEngine
@@ -517,12 +516,26 @@ def test_sliding_lateness_checkpoint(mode):
     assert outs["g"] == outs["o"]
     late = [r for w, recs in outs["o"] if w != "tail" for r in recs if r[1] < wm_cut]
     assert late, "windows kept for their lateness fired again after the restore"
-    e = WindowEngine(cfg)
-    kg = max(blobs["o"], key=lambda k: len(blobs["o"][k][1]))
-    with pytest.raises(_abi.FwError) as ei:
-        e.restore_kg_flink(kg, layout, *blobs["o"][kg], LONG_MIN)
-    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
-    e.close()
+    # restored at Long.MIN_VALUE: a window that fired before the checkpoint (its panes carry only cleanup timers)
+    # is restored with its own pane disarmed — it fires at its maxTimestamp only for the keys a later record
+    # re-armed (EventTimeTrigger.onElement), the others wait for their cleanup — as the oracle restored alike
+    outs = {}
+    for name, factory in (("g", WindowEngine), ("o", OracleEngine)):
+        e = factory(cfg)
+        for kg, (st, tm) in blobs["o"].items():
+            e.restore_kg_flink(kg, layout, st, tm, LONG_MIN)
+        back = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        assert _diff(back, blobs["o"]) is None, _diff(back, blobs["o"])
+        res = drive(e, keys[n:], ts[n:], vals[n:], 2048, 120, None, f1=f1[n:])
+        mid = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        e.advance_watermark(LONG_MAX)
+        res.append(e.collect())
+        outs[name] = (_canon(epochs_of(res, ["sum_i64", "count"], True)), mid)
+        e.close()
+    assert outs["g"][0] == outs["o"][0]
+    assert _diff(outs["g"][1], outs["o"][1]) is None, _diff(outs["g"][1], outs["o"][1])
+    refired = [r for w, recs in outs["o"][0] if w != "tail" for r in recs if r[1] < wm_cut]
+    assert refired, "a window that fired before the checkpoint fired again for re-armed keys"
 
 
 @pytest.mark.gpu

@@ -211,8 +211,8 @@ def test_decode_then_window_end_to_end():
 @pytest.mark.gpu
 def test_gpu_decode_begin_end_pipelined():
     """fw_decode_begin / fw_decode_end: two decodes in flight (the second enqueued before the first's counts are
-    read), each equal to the synchronous fw_decode of the same bytes; a third outstanding begin and an unknown
-    ticket are rejected."""
+    read), each equal to the synchronous fw_decode of the same bytes, ended in any order; a third outstanding
+    begin and an unknown ticket are rejected."""
     from flink_amd import _abi
     from flink_amd.windowing import ReduceFunction, TumblingEventTimeWindows, WindowEngine, make_config
     sc = dict(fields=["long", "long", "long"], key=0, value=2, f1=1)
@@ -227,10 +227,12 @@ def test_gpu_decode_begin_end_pipelined():
         e.decode_begin(streams[2], sc["fields"], **kw)
     got0 = e.decode_end(h0)
     h2 = e.decode_begin(streams[2], sc["fields"], **kw)
-    got1, got2 = e.decode_end(h1), e.decode_end(h2)
+    got2 = e.decode_end(h2)   # ends in any order: the newer first, then a begin takes the slot it freed
+    h3 = e.decode_begin(streams[0], sc["fields"], **kw)
+    got1, got3 = e.decode_end(h1), e.decode_end(h3)
     with pytest.raises(_abi.FwError):
         e.decode_end(h2)
-    for g, w in zip((got0, got1, got2), want):
+    for g, w in zip((got0, got1, got2, got3), want + want[:1]):
         assert g["consumed"] == w["consumed"] and g["n_records"] == w["n_records"] > 50_000
         for k in ("key", "f1", "ts", "value", "wm", "wm_pos", "lm", "lm_pos"):
             assert np.array_equal(g[k], w[k]), k

@@ -8,9 +8,11 @@ run() {   # name, env...
   env "$@" timeout -k 10 120 python3 bench.py --config c4 --steps 64 --drain-steps 0 --decode-steps 0 --h2d-steps 0 --cpu-sample 0 --no-check > gpurun_out/ab_c4_$n.json 2>/dev/null
   python3 -c "import json; l=json.loads(open('gpurun_out/ab_c4_$n.json').read().strip().splitlines()[-1]); k=l['roofline']['kernels']; print('$n', round(l['value']/1e9,2), round(l['ms_per_step']*1e3,1), {a:round(b['ms']*1e3,1) for a,b in k.items()})"
 }
+# longest-share-first owner order (default) against the plain order, interleaved A-B-A-B
 run lpt FW_DEBUG_AGG=0
-run lpt250 FW_DEBUG_AGG=0 FW_AGG_CHUNK_PCT=250
-run lpt300 FW_DEBUG_AGG=0 FW_AGG_CHUNK_PCT=300
-run lpt175 FW_DEBUG_AGG=0 FW_AGG_CHUNK_PCT=175
+run plain FW_DEBUG_AGG=128
 run lpt_b FW_DEBUG_AGG=0
-run lpt250_b FW_DEBUG_AGG=0 FW_AGG_CHUNK_PCT=250
+run plain_b FW_DEBUG_AGG=128
+# share size
+run lpt250 FW_DEBUG_AGG=0 FW_AGG_CHUNK_PCT=250
+run lpt175 FW_DEBUG_AGG=0 FW_AGG_CHUNK_PCT=175
