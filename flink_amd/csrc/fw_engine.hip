@@ -3036,6 +3036,7 @@ struct DevBuf {
 };
 
 // list state (fw_list.hip): per pane slice slot a buffer of elements (kid, ordinal, value, f1)
+constexpr int LST_WORDS = 4;   // a buffered list element: kid, arrival ordinal, value, f1
 struct ListDev {
   int64_t cap;                  // elements per slice slot
   unsigned long long* cnt;      // [P] elements buffered
@@ -3125,6 +3126,8 @@ struct fw_engine {
   std::vector<std::vector<int64_t>> snap_kg;
   std::vector<std::vector<int64_t>> snap_wkg;   // sliding: the windows' own panes (entry word 0 = window number)
   std::vector<uint8_t> snap_has_key;   // per key group: a key of it is in the directory (it held window state)
+  // list state (tumbling): each (window, key)'s elements as (arrival ordinal, value bits, f1), in arrival order
+  std::map<std::pair<int64_t, int64_t>, std::vector<std::array<int64_t, 3>>> snap_list;
   bool snap_any_key = false;
   std::vector<uint8_t> kg_touched;     // per key group: restored with present = 1 (fw_restore_kg_flink)
   int64_t restore_ord = -((int64_t)1 << 62);   // arrival ordinals of restored panes, in blob order
@@ -4621,6 +4624,38 @@ static int build_snapshot(fw_engine* e) {
     HIPCHK(e, hipMemcpy(ev.data(), e->kg_evicted, (size_t)mp, hipMemcpyDeviceToHost));
     for (int32_t k = 0; k < mp; ++k) if (ev[(size_t)k]) { e->snap_has_key[(size_t)k] = 1; e->snap_any_key = true; }
   }
+  if (e->list) {   // list state (tumbling): the slices' element buffers, grouped by (window, key) in arrival order
+    e->snap_list.clear();
+    std::vector<unsigned long long> lc((size_t)s.P);
+    HIPCHK(e, hipMemcpy(lc.data(), e->lst.cnt, 8 * (size_t)s.P, hipMemcpyDeviceToHost));
+    std::vector<int64_t> rows;
+    for (int32_t p = 0; p < s.P; ++p) {
+      const int64_t m = tags[(size_t)p];
+      if (m == fw::FREE_TAG) continue;
+      const int64_t ne = std::min<int64_t>((int64_t)lc[(size_t)p], e->lst.cap);
+      rows.resize((size_t)ne * LST_WORDS);
+      if (ne > 0)
+        HIPCHK(e, hipMemcpy(rows.data(), e->lst.buf + (size_t)p * (size_t)e->lst.cap * LST_WORDS, 8 * rows.size(),
+                            hipMemcpyDeviceToHost));
+      for (int64_t j = 0; j < ne; ++j) {
+        const int64_t* x = &rows[(size_t)j * LST_WORDS];   // kid, ordinal, value, f1
+        if (x[0] < 0 || x[0] >= s.stride || kid_kg[(size_t)x[0]] < 0) continue;
+        const int64_t key = x[0] == s.D ? fw::EMPTY_KEY : keys[(size_t)x[0]];
+        e->snap_list[{m, key}].push_back({x[1], x[2], x[3]});
+      }
+    }
+    for (auto& kv : e->snap_list) {
+      std::sort(kv.second.begin(), kv.second.end());
+      const int64_t key = kv.first.second;
+      const int64_t ent[FW_SNAP_ENTRY_WORDS] = {kv.first.first, key, 0, INT64_MAX, INT64_MIN, 0,
+                                                kv.second[0][0] - e->ordinal, 0};
+      auto& v = e->snap_kg[(size_t)host_key_group(s, key)];
+      v.insert(v.end(), ent, ent + FW_SNAP_ENTRY_WORDS);
+    }
+    e->snap_gkg.assign((size_t)mp, {});
+    e->snap_epoch = e->state_epoch;
+    return FW_OK;
+  }
   const size_t st = (size_t)s.stride;
   std::vector<int64_t> sum(st), mn, mx, cnt, first, f1v;
   std::vector<uint8_t> present;
@@ -4820,6 +4855,7 @@ struct KgPane {
   int64_t first;    // first-arrival ordinal (0 when the config does not track first arrival)
   int64_t f1;
   bool unarmed;     // a restored window's pane whose trigger timer fired before the checkpoint (none pending)
+  int64_t m = 0;    // tumbling: the slice (= window) number
 };
 
 static int check_state_layout(fw_engine* e, const fw_state_layout* L) {
@@ -4833,6 +4869,13 @@ static int check_state_layout(fw_engine* e, const fw_state_layout* L) {
   }
   const fw_config& c = e->cfg;
   const bool by = e->s.by;
+  if (e->list) {   // ListSerializer's element: the window's input tuple — its key, f1 and value fields, in order
+    if (seen[FW_SF_KEY] > 1 || seen[FW_SF_F1] > 1 || seen[FW_SF_VALUE] != 1 || seen[FW_SF_SUM] || seen[FW_SF_MIN] ||
+        seen[FW_SF_MAX] || seen[FW_SF_COUNT])
+      return reject(e, FW_ERR_INVALID_ARG, "list state layout: the element tuple's fields, FW_SF_VALUE once and "
+                                           "FW_SF_KEY / FW_SF_F1 at most once");
+    return FW_OK;
+  }
   const int want[FW_SF_VALUE + 1] = {0, -1, c.keep_first_f1 || by ? 1 : 0, !by && (c.agg_mask & FW_AGG_SUM) ? 1 : 0,
                                      !by && (c.agg_mask & FW_AGG_MIN) ? 1 : 0, !by && (c.agg_mask & FW_AGG_MAX) ? 1 : 0,
                                      !by && (c.agg_mask & FW_AGG_COUNT) ? 1 : 0, by ? 1 : 0};
@@ -4906,6 +4949,7 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
     p.first = s.first ? x[6] : 0;
     p.f1 = x[7];
     p.unarmed = e->snap_unarmed.count({x[0], x[1]}) != 0 && tumbling;
+    p.m = x[0];
     return p;
   };
   out.clear();
@@ -4978,7 +5022,9 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
                          int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
   if (!e || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
-  if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
+  if (e->list && e->cfg.assigner != FW_TUMBLING)
+    return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows: a record is in several windows' lists, which "
+                                         "the engine's slices hold once");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -5032,6 +5078,19 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
         st.i32((int32_t)ent.size());
         for (size_t i : ent) {
           st.i64(panes[i].key);
+          if (e->list) {   // ListSerializer.serialize: int size, then every element in insertion order
+            const auto& el = e->snap_list.at({panes[i].m, panes[i].key});
+            st.i32((int32_t)el.size());
+            for (const auto& x : el)
+              for (int f = 0; f < layout->n_fields; ++f) {
+                const int fld = layout->field[f];
+                if (fld == FW_SF_KEY) st.i64(panes[i].key);
+                else if (fld == FW_SF_F1) st.i64(x[2]);
+                else if (e->s.vt == FW_VALUE_F64) { double d; memcpy(&d, &x[1], 8); st.f64(d); }
+                else st.i64(x[1]);
+              }
+            continue;
+          }
           for (int f = 0; f < layout->n_fields; ++f) put_field(e, st, layout->field[f], panes[i]);
         }
       }
@@ -5095,11 +5154,46 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   return FW_OK;
 }
 
+// list state (tumbling): the restored entries' elements appended to their slices' buffers (the directory and
+// the slots were set by restore_entries), each with its ordinal in blob order
+static int restore_list_elements(fw_engine* e, const std::vector<KgPane>& panes, const std::vector<int64_t>& slice_of,
+                                 const std::vector<std::vector<std::array<int64_t, 2>>>& lists,
+                                 const std::vector<int64_t>& ord0) {
+  const fw::Spec& s = e->s;
+  std::vector<int64_t> keys((size_t)s.D);
+  HIPCHK(e, hipMemcpy(keys.data(), s.dir_keys, 8 * (size_t)s.D, hipMemcpyDeviceToHost));
+  std::unordered_map<int64_t, int64_t> kid_of;
+  for (int64_t k = 0; k < s.D; ++k) if (keys[(size_t)k] != fw::EMPTY_KEY) kid_of[keys[(size_t)k]] = k;
+  std::vector<unsigned long long> lc((size_t)s.P);
+  HIPCHK(e, hipMemcpy(lc.data(), e->lst.cnt, 8 * (size_t)s.P, hipMemcpyDeviceToHost));
+  std::map<int32_t, std::vector<int64_t>> rows;   // slot -> elements (kid, ordinal, value, f1)
+  for (size_t i = 0; i < panes.size(); ++i) {
+    const int64_t kid = panes[i].key == fw::EMPTY_KEY ? s.D : (kid_of.count(panes[i].key) ? kid_of[panes[i].key] : -1);
+    if (kid < 0) return reject(e, FW_ERR_CAPACITY, "restored key not in the key directory");
+    auto& r = rows[(int32_t)fw::floor_mod(slice_of[i], s.P)];
+    for (size_t q = 0; q < lists[i].size(); ++q) r.insert(r.end(), {kid, ord0[i] + (int64_t)q, lists[i][q][0], lists[i][q][1]});
+  }
+  for (auto& kv : rows) {
+    const int32_t p = kv.first;
+    const int64_t n = (int64_t)(kv.second.size() / LST_WORDS);
+    if ((int64_t)lc[(size_t)p] + n > e->lst.cap)
+      return reject(e, FW_ERR_CAPACITY, "restored list state exceeds list_capacity for its slice");
+    HIPCHK(e, hipMemcpy(e->lst.buf + ((size_t)p * (size_t)e->lst.cap + lc[(size_t)p]) * LST_WORDS, kv.second.data(),
+                        8 * kv.second.size(), hipMemcpyHostToDevice));
+    lc[(size_t)p] += (unsigned long long)n;
+  }
+  HIPCHK(e, hipMemcpy(e->lst.cnt, lc.data(), 8 * (size_t)s.P, hipMemcpyHostToDevice));
+  e->state_epoch++;
+  return FW_OK;
+}
+
 int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
                         const void* state, int64_t state_len, const void* timers, int64_t timers_len) {
   if (!e || (!state && state_len) || !timers || state_len < 0) return FW_ERR_INVALID_ARG;
   if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
-  if (e->list) return reject(e, FW_ERR_UNSUPPORTED, "list state: buffered elements have no checkpoint layout here");
+  if (e->list && e->cfg.assigner != FW_TUMBLING)
+    return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows: a record is in several windows' lists, which "
+                                         "the engine's slices hold once");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
   if (kg < e->s.kg_start || kg > e->s.kg_end)
@@ -5114,6 +5208,7 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   const bool f64 = s.vt == FW_VALUE_F64;
   std::vector<KgPane> panes;
   std::vector<int64_t> slice_of;
+  std::vector<std::vector<std::array<int64_t, 2>>> lists;   // list state: each entry's elements (value bits, f1)
   bool present = false;
   if (state_len > 0) {
     fwkg::BeIn in(state, state_len);
@@ -5135,7 +5230,26 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
       if (ne < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
       for (int32_t j = 0; j < ne && in.ok; ++j) {
         KgPane p{start, end, in.i64(), 0, INT64_MAX, INT64_MIN, 0, 0, 0, false};
-        for (int f = 0; f < layout->n_fields; ++f) {
+        if (e->list) {   // ListSerializer.deserialize: int size, then the elements
+          const int32_t nel = in.i32();
+          if (nel < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt list state");
+          std::vector<std::array<int64_t, 2>> el;
+          for (int32_t q = 0; q < nel && in.ok; ++q) {
+            std::array<int64_t, 2> x{0, 0};
+            for (int f = 0; f < layout->n_fields; ++f) {
+              const int64_t v = in.i64();
+              if (layout->field[f] == FW_SF_KEY && in.ok && v != p.key)
+                return reject(e, FW_ERR_UNSUPPORTED, "element key field differs from the key");
+              if (layout->field[f] == FW_SF_F1) x[1] = v;
+              if (layout->field[f] == FW_SF_VALUE) x[0] = v;
+            }
+            el.push_back(x);
+          }
+          if (!in.ok) break;
+          if (el.empty()) return reject(e, FW_ERR_INVALID_ARG, "empty list state entry");
+          lists.push_back(std::move(el));
+        }
+        for (int f = 0; f < layout->n_fields && !e->list; ++f) {
           const int64_t x = in.i64();
           double d;
           memcpy(&d, &x, 8);
@@ -5224,6 +5338,9 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   } else if (got != want) {
     return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
   }
+  if (e->list && !dis_now.empty())
+    return reject(e, FW_ERR_UNSUPPORTED, "list state: windows that fired before the checkpoint, restored below their "
+                                         "maxTimestamp (restore at the checkpoint's watermark)");
   if (!dis_now.empty() && !e->s.disarm) {   // per-slot flags and per-pane re-arm marks, first needed here
     e->s.disarm = e->alloc<uint8_t>((size_t)s.P);
     e->s.armed = e->alloc<uint8_t>((size_t)s.P * (size_t)s.stride);
@@ -5241,9 +5358,12 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   // arrival ordinals in blob order: restored panes precede every later record, and keep the blob's
   // (HashMap iteration) order as their insertion order, as readStateTableForKeyGroup's puts do
   std::vector<int64_t> ent(panes.size() * FW_SNAP_ENTRY_WORDS);
+  std::vector<int64_t> list_ord(panes.size());
   for (size_t i = 0; i < panes.size(); ++i) {
     const KgPane& p = panes[i];
-    const int64_t ord = e->restore_ord++;
+    const int64_t ord = e->restore_ord;
+    e->restore_ord += e->list ? (int64_t)lists[i].size() : 1;   // list state: one ordinal per element
+    list_ord[i] = ord;
     const int64_t w[FW_SNAP_ENTRY_WORDS] = {slice_of[i], p.key, p.sum, p.mn, p.mx, s.by ? ord : p.cnt, ord, p.f1};
     memcpy(&ent[i * FW_SNAP_ENTRY_WORDS], w, sizeof(w));
   }
@@ -5251,7 +5371,9 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(s.kg_end - s.kg_start + 1), 0);
   if (present) e->kg_touched[(size_t)(kg - s.kg_start)] = 1;
   rc = restore_entries(e, watermark, ent.data(), (int64_t)panes.size(), sliding ? 1 : 0);
-  if (rc || !s.gtag) return rc;
+  if (rc) return rc;
+  if (e->list) return restore_list_elements(e, panes, slice_of, lists, list_ord);
+  if (!s.gtag) return rc;
   // windows within their lateness at the restore watermark (later per-element fires purge them again), and the
   // restored cleanup timers without state, each with its arrival ordinal (after the panes', in blob order)
   rc = ghost_advance(e, INT64_MIN, watermark);

@@ -19,7 +19,6 @@
 
 namespace fw {
 
-constexpr int LST_WORDS = 4;   // kid, ordinal, value, f1
 // k_list_plan output: [0] windows firing, [1] slots purged, then WM_MAXT (window, elements) pairs, then
 // WM_MAXP purged slots
 constexpr int LPLAN_WORDS = 2 + 2 * WM_MAXT + WM_MAXP;

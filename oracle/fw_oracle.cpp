@@ -740,6 +740,15 @@ void readField(const fw_config& c, JavaIn& in, int f, Acc& a) {
   (void)c;
 }
 
+// a list-state element (the window's input record: key, f1, value fields in the element tuple's order)
+void writeListField(const fw_config& c, JavaOut& o, int f, int64_t key, const ListElem& x) {
+  switch (f) {
+    case FW_SF_KEY: o.writeLong(key); break;
+    case FW_SF_F1: o.writeLong(x.f1); break;
+    case FW_SF_VALUE: if (c.value_type == FW_VALUE_F64) o.writeDouble(x.vd); else o.writeLong(x.vi); break;
+  }
+}
+
 struct NsRef { TimeWindow w; int64_t seq; const std::unordered_map<int64_t, Acc>* entries; };
 struct EntRef { int64_t key; const Acc* acc; };
 struct TimerRef { InternalTimer t; int64_t seq; };
@@ -775,6 +784,12 @@ void snapshotKeyGroup(const Operator& op, int32_t kg, const fw_state_layout& L, 
         st.writeInt((int32_t)ent.size());
         for (const EntRef& x : ent) {
           st.writeLong(x.key);     // LongSerializer (Tuple1<Long>: TupleSerializer over it, the same 8 bytes)
+          if (op.cfg.agg_mask == FW_AGG_LIST) {   // ListSerializer.serialize: int size, then every element
+            st.writeInt((int32_t)x.acc->list->size());
+            for (const ListElem& el : *x.acc->list)
+              for (int f = 0; f < L.n_fields; ++f) writeListField(op.cfg, st, L.field[f], x.key, el);
+            continue;
+          }
           for (int f = 0; f < L.n_fields; ++f) writeField(op.cfg, st, L.field[f], *x.acc);
         }
       }
@@ -825,7 +840,22 @@ int restoreKeyGroup(Operator& op, int32_t kg, const fw_state_layout& L, int64_t 
           Acc a{};
           a.key = in.readLong();
           const int64_t mapKey = a.key;
-          for (int f = 0; f < L.n_fields; ++f) readField(op.cfg, in, L.field[f], a);
+          if (op.cfg.agg_mask == FW_AGG_LIST) {   // ListSerializer.deserialize
+            const int32_t ne = in.readInt();
+            if (ne < 0) { op.err = "corrupt list state"; return FW_ERR_INVALID_ARG; }
+            a.list = std::make_shared<std::vector<ListElem>>();
+            for (int32_t q = 0; q < ne && !in.eof; ++q) {
+              ListElem el{0, 0.0, 0};
+              for (int f = 0; f < L.n_fields; ++f) {
+                const int64_t x = in.readLong();
+                if (L.field[f] == FW_SF_F1) el.f1 = x;
+                if (L.field[f] == FW_SF_VALUE) { el.vi = x; std::memcpy(&el.vd, &x, 8); }
+              }
+              a.list->push_back(el);
+            }
+          } else {
+            for (int f = 0; f < L.n_fields; ++f) readField(op.cfg, in, L.field[f], a);
+          }
           a.seq = ++op.seqCounter;
           entries[mapKey] = a;
         }

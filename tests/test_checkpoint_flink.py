@@ -669,3 +669,74 @@ def test_fold_checkpoint(mode, kind, initial, vt, assigner):
         else:
             assert len(rg) == len(ro) and all(x[:2] == y[:2] and abs(x[2] - y[2]) <= 1e-12 * max(1.0, abs(y[2]))
                                               for x, y in zip(rg, ro)), w
+
+
+def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "value")):
+    """Tumbling list state (WindowedStream.apply: HeapListState "window-contents" of the input tuples): drive 2/3
+    of a Zipf stream, snapshot every key group in the reference layout; or restore such sections at their
+    watermark and drive the rest to a final MAX_WATERMARK."""
+    from flink_amd.windowing import ListStateDescriptor, TumblingEventTimeWindows, make_config
+    from harness import drive, gen_stream
+    keys, ts, vals = gen_stream(24_000, 1200, rate=1 << 13, zipf=1.1, ooo=300, value_type=vt)
+    f1 = np.arange(len(keys), dtype=np.int64) * 7 + 3
+    cfg = make_config(TumblingEventTimeWindows.of(1000), ListStateDescriptor(vt), None, lateness, max_parallelism=128,
+                      key_capacity=1 << 12, max_batch=1 << 12, out_capacity=1 << 20, ingest_mode=mode)
+    n = len(keys) * 2 // 3
+    wm = int(ts[:n].max()) - 100
+    e = factory(cfg)
+    if restore is None:
+        drive(e, keys[:n], ts[:n], vals[:n], 2048, 100, None, f1=f1[:n])
+        snaps = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+        e.close()
+        return snaps
+    for kg, (st, tm) in restore.items():
+        e.restore_kg_flink(kg, layout, st, tm, wm)
+    back = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
+    out = drive(e, keys[n:], ts[n:], vals[n:], 2048, 100, LONG_MAX, f1=f1[n:])
+    e.close()
+    return back, out
+
+
+@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 400)])
+def test_oracle_list_checkpoint_round_trip(vt, lateness):
+    """The oracle's HeapListState sections (ListSerializer: int size, then the elements) restore and snapshot
+    back byte for byte."""
+    from oracle.oracle import OracleEngine
+    snaps = _list_run(OracleEngine, vt, lateness, 0)
+    assert sum(len(s) for s, _ in snaps.values()) > 128 * 8
+    back, _ = _list_run(OracleEngine, vt, lateness, 0, restore=snaps)
+    assert _diff(back, snaps) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 400)])
+def test_list_checkpoint(mode, vt, lateness):
+    """List state of tumbling windows in the reference layout: the engine's sections (its slices' element
+    buffers grouped per window and key in arrival order) are byte-identical to the oracle's; the engine
+    restores the oracle's sections (elements back into the slices, ahead of every later arrival), writes them
+    back unchanged, and its fires — watermark fires and, under allowed lateness, per-element re-fires — continue
+    exactly as the oracle restored from the same bytes."""
+    from flink_amd.windowing import WindowEngine
+    from harness import epochs_of
+    from oracle.oracle import OracleEngine
+    g = _list_run(WindowEngine, vt, lateness, mode)
+    o = _list_run(OracleEngine, vt, lateness, 0)
+    assert _diff(g, o) is None, _diff(g, o)
+    back, out_g = _list_run(WindowEngine, vt, lateness, mode, restore=o)
+    _, out_o = _list_run(OracleEngine, vt, lateness, 0, restore=o)
+    assert _diff(back, o) is None, _diff(back, o)
+    field = f"sum_{vt}"
+    eg, eo = _canon(epochs_of(out_g, [field], True)), _canon(epochs_of(out_o, [field], True))
+    assert eg == eo and sum(len(r) for _, r in eo) > 1000
+
+
+@pytest.mark.gpu
+def test_list_checkpoint_rejections():
+    from flink_amd import _abi
+    from flink_amd.windowing import ListStateDescriptor, SlidingEventTimeWindows, WindowEngine, make_config
+    e = WindowEngine(make_config(SlidingEventTimeWindows.of(2000, 1000), ListStateDescriptor()))
+    with pytest.raises(_abi.FwError) as ei:
+        e.snapshot_kg_flink(0, ("key", "f1", "value"))
+    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+    e.close()
