@@ -2281,7 +2281,9 @@ __global__ __launch_bounds__(LF_T) void k_late_fused(Spec s, const unsigned long
     a.empty = 0;
     a.head = head;
     a.sfirst = ord_base + i_self;
-    if (FIRST && !BY) a.sf1 = f1col[i_self];
+    // f1 by batch index (a random line per record): a segment takes its head's, so only heads need it, and
+    // under PurgingTrigger, where every record's result carries its own
+    if (FIRST && !BY && (head || purging)) a.sf1 = f1col[i_self];
     if (head) {
       const int64_t idx = (int64_t)pane;
       const bool pres = pane_present(s, idx);
@@ -2422,17 +2424,22 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   int32_t* slots = purge + s.P;                    // [K]
   int32_t* wpurge = slots + s.K;                   // [max(W, 1)]
   __shared__ int32_t n_tasks, n_purge, n_wpurge, wslot_t, last;
+  __shared__ int64_t nkid_s;
   __shared__ int32_t wtot[WM_THREADS / 64];
   __shared__ unsigned long long base;
   __shared__ unsigned long long fired;
   if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; n_wpurge = 0; last = 0; fired = 0; }
   for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) tags[p] = s.slice_tag[p];
+  // key ids scanned: the null key's id D only while it is in use (D = 2^k ids fill 2^k / 1024 workgroups
+  // exactly; id D would give workgroup 0 a second round of loads, ~4 us per fire)
+  if (threadIdx.x == 0) nkid_s = s.dir_min_used[0] ? s.stride : s.D;
   __syncthreads();
+  const int64_t nkid = nkid_s;
   for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) {
     const int64_t m = tags[p];
     if (m == FREE_TAG) continue;
-    const int64_t n_hi = floor_div(m, s.R);
-    const int64_t n_lo = floor_div(m - s.K, s.R) + 1;
+    const int64_t n_hi = s.R == 1 ? m : floor_div(m, s.R);   // (64-bit divides: ~100 instructions each)
+    const int64_t n_lo = s.R == 1 ? m - s.K + 1 : floor_div(m - s.K, s.R) + 1;
     bool purge_now = false, fire_purge = false;
     for (int64_t n = n_lo; n <= n_hi; ++n) {
       const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
@@ -2440,8 +2447,10 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
       if (!fires) continue;
       if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) purge_now = fire_purge = true;   // the slice is the window
       bool owner = true;                                                    // first live slice of window n
+      int32_t pp = (int32_t)floor_mod(n * s.R, s.P);
       for (int64_t mm = n * s.R; mm < m; ++mm) {
-        if (tags[floor_mod(mm, s.P)] == mm) { owner = false; break; }
+        if (tags[pp] == mm) { owner = false; break; }
+        pp = pp + 1 == s.P ? 0 : pp + 1;
       }
       if (!owner) continue;
       const int32_t t = atomicAdd(&n_tasks, 1);
@@ -2499,14 +2508,14 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
         (s.disarm && s.assigner != FW_SLIDING && s.K == 1 && slots[0] >= 0 && s.disarm[slots[0]]) ? slots[0] : -1;
     // (sliding: a restored window's own pane disarmed — the window fires only for the keys re-armed since)
     const int32_t w_dis = (s.disarm && s.assigner == FW_SLIDING && wslot_t >= 0 && s.disarm[wslot_t]) ? wslot_t : -1;
-    for (int64_t k0 = (int64_t)blockIdx.x * WM_THREADS; k0 < s.stride; k0 += gstride) {
+    for (int64_t k0 = (int64_t)blockIdx.x * WM_THREADS; k0 < nkid; k0 += gstride) {
       const int64_t kid = k0 + threadIdx.x;
       bool any = false;
       LateAcc a;
       a.vt = VT;
       int64_t best_ord = INT64_MAX, f1 = 0;
-      const int64_t key = kid < s.stride ? kid_key(s, kid) : EMPTY_KEY;
-      const bool live = kid < s.stride && !(gate && kid != s.D && key == EMPTY_KEY) &&
+      const int64_t key = kid < nkid ? kid_key(s, kid) : EMPTY_KEY;
+      const bool live = kid < nkid && !(gate && kid != s.D && key == EMPTY_KEY) &&
                         (w_dis < 0 || s.armed[(int64_t)w_dis * s.stride + kid]);
       if (live) {
         for (int kb = 0; kb < s.K; kb += WM_C) {
@@ -2574,7 +2583,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     const bool ghost = (purge[q] & PURGE_GHOST) != 0;
     const int32_t p = purge[q] & ~PURGE_GHOST;
     const int64_t pbase = (int64_t)p * s.stride;
-    for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < s.stride; kid += gstride) {
+    for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < nkid; kid += gstride) {
       const int64_t idx = pbase + kid;
       if (ghost) {
         const int64_t o = s.first ? s.c.first[idx] : (s.c.present[idx] ? 0 : INT64_MAX);
@@ -2585,7 +2594,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   }
   for (int32_t q = 0; q < nwp; ++q) {
     const int64_t pbase = (int64_t)wpurge[q] * s.stride;
-    for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < s.stride; kid += gstride) {
+    for (int64_t kid = (int64_t)blockIdx.x * WM_THREADS + threadIdx.x; kid < nkid; kid += gstride) {
       const int64_t idx = pbase + kid;
       if (s.wc.sum) s.wc.sum[idx] = sum_identity(s.vt);
       if (s.wc.mn) s.wc.mn[idx] = INT64_MAX;
@@ -4037,7 +4046,11 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     FW_DISPATCH(launch_ingest_t, e, b);
     e->phase_end(n);
   }
-  if (e->s.W > 0)   // sliding: this batch's extra-window records into the window panes
+  // sliding: this batch's extra-window records into the window panes.  A record gets an extra window only
+  // when ts < offset - slide, and every window of such a record ends before offset + size: once the watermark
+  // is past that plus the allowed lateness, they are all late and none is listed, so nothing is launched
+  // (C3: ~5 us per push on the engine stream)
+  if (e->s.W > 0 && (__int128)e->cur_wm < (__int128)e->s.offset + e->s.size + e->s.slide + e->s.lateness)
     hipLaunchKernelGGL(k_quirk_apply, dim3(1), dim3(1024), 0, e->stream, e->s, e->quirk_list[par], e->quirk_count + par,
                        e->cfg.max_batch);
   e->batches++;
