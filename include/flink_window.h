@@ -264,7 +264,12 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * The state tuple is the ReduceFunction's value type: layout->field[0..n_fields) in tuple order, each an
  * 8-byte LongSerializer / DoubleSerializer field (TupleSerializer.serialize :120-129).  The layout must
  * name every aggregate the config computes (FW_SF_VALUE for maxBy/minBy), FW_SF_F1 iff keep_first_f1,
- * FW_SF_KEY at most once.  Namespaces, entries and timers come in java.util.HashMap iteration order for
+ * FW_SF_KEY at most once.  Fold (FW_AGGF_FOLD): the state is HeapFoldingState's accumulator, the initial value
+ * folded with the pane (the layout names the one aggregate).  List state (FW_AGG_LIST, tumbling windows only):
+ * the state is ListSerializer's `int size | element * size`, each element the window's input tuple with the
+ * fields the layout names — FW_SF_VALUE once, FW_SF_KEY and FW_SF_F1 at most once each — in arrival order.
+ * Session windows: FW_ERR_UNSUPPORTED (their "merging-window-set" state is not written).
+ * Namespaces, entries and timers come in java.util.HashMap iteration order for
  * tables sized by their current size (when a JVM table iterates differently).
  * A buffer argument NULL (or too small: FW_ERR_CAPACITY) stores the required lengths only.
  * *state_len == 0: no keyed state at all yet (no record accepted, nothing restored), for which
@@ -279,7 +284,8 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * with one exception the reference's own checkpoints produce: a tumbling window ahead of `watermark` whose
  * panes carry no trigger timer (it fired before the checkpoint and is kept for its allowed lateness) is
  * restored disarmed — it fires again only for keys whose records re-arm it before the watermark passes its
- * maxTimestamp (EventTimeTrigger.onElement), otherwise it waits for its cleanup time.  Every restored key
+ * maxTimestamp (EventTimeTrigger.onElement), otherwise it waits for its cleanup time; a sliding window likewise,
+ * through its own pane (tumbling list state: not restorable below such a window's maxTimestamp).  Every restored key
  * group must use the same `watermark`. */
 #define FW_SF_KEY    1   /* the key (the tuple's key field, e.g. f0)                          */
 #define FW_SF_F1     2   /* the pass-through field of the first arrival (maxBy/minBy: of the extremal record) */
