@@ -2201,15 +2201,6 @@ __device__ __forceinline__ LfPart lf_join(const LfPart& x, const LfPart& y) {
   }
   return r;
 }
-__device__ __forceinline__ LfPart lf_shfl(const LfPart& v, int src) {
-  static_assert(sizeof(LfPart) % 4 == 0, "LfPart moves in dwords");
-  LfPart r;
-  const int* a = (const int*)&v;
-  int* b = (int*)&r;
-#pragma unroll
-  for (int w = 0; w < (int)(sizeof(LfPart) / 4); ++w) b[w] = __shfl(a[w], src);
-  return r;
-}
 // a tile's carry crosses XCDs: written and read with agent-scope atomics (they bypass the XCD's L2), the
 // writer waiting for its stores before it raises the flag — no release fence, whose L2 write-back cost
 // ~20-50 us per tile behind the batch's output stores
@@ -2232,6 +2223,41 @@ __device__ __forceinline__ LfPart lf_get(const LfPart* src) {
 __device__ __forceinline__ void lf_raise(unsigned int* flag, unsigned int v) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the data's stores acknowledged first
   __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the scan's LDS traffic and shuffles carry only the accumulator fields the reduce shape keeps (a whole LfPart
+// per step held ~150 VGPRs: three tiles per CU)
+template <int AGG>
+__device__ __forceinline__ void lf_fields(LfPart& d, const LfPart& x) {
+  constexpr bool BY = (AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;
+  if (AGG & FW_AGG_SUM) d.v.sum = x.v.sum;
+  if (AGG & (FW_AGG_MIN | FW_AGG_MINBY)) d.v.mn = x.v.mn;
+  if (AGG & (FW_AGG_MAX | FW_AGG_MAXBY)) d.v.mx = x.v.mx;
+  if (AGG & FW_AGG_COUNT) d.v.cnt = x.v.cnt;
+  if (BY) { d.v.ord = x.v.ord; d.v.f1 = x.v.f1; d.v.by = x.v.by; }
+  d.sf1 = x.sf1; d.sfirst = x.sfirst; d.head = x.head; d.bpres = x.bpres; d.empty = x.empty;
+}
+template <int VT, int AGG>
+__device__ __forceinline__ LfPart lf_ld(const LfPart* p) {
+  LfPart r;
+  r.v.vt = VT;
+  lf_fields<AGG>(r, *p);
+  return r;
+}
+template <int AGG>
+__device__ __forceinline__ void lf_st(LfPart* p, const LfPart& x) { lf_fields<AGG>(*p, x); }
+template <int VT, int AGG>
+__device__ __forceinline__ LfPart lf_shfl_t(const LfPart& x, int src) {
+  constexpr bool BY = (AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;
+  LfPart r;
+  r.v.vt = VT;
+  if (AGG & FW_AGG_SUM) r.v.sum = __shfl(x.v.sum, src);
+  if (AGG & (FW_AGG_MIN | FW_AGG_MINBY)) r.v.mn = __shfl(x.v.mn, src);
+  if (AGG & (FW_AGG_MAX | FW_AGG_MAXBY)) r.v.mx = __shfl(x.v.mx, src);
+  if (AGG & FW_AGG_COUNT) r.v.cnt = __shfl(x.v.cnt, src);
+  if (BY) { r.v.ord = __shfl(x.v.ord, src); r.v.f1 = __shfl(x.v.f1, src); r.v.by = __shfl(x.v.by, src); }
+  r.sf1 = __shfl(x.sf1, src); r.sfirst = __shfl(x.sfirst, src);
+  r.head = __shfl(x.head, src); r.bpres = __shfl(x.bpres, src); r.empty = __shfl(x.empty, src);
+  return r;
 }
 struct LfLink {            // one tile's published carry: epoch << 2 | 1 (tile aggregate), | 2 (inclusive prefix)
   unsigned int* flag;
@@ -2295,21 +2321,21 @@ __global__ __launch_bounds__(LF_T) void k_late_fused(Spec s, const unsigned long
     }
   }
   // inclusive segmented scan over the tile (Hillis-Steele in LDS)
-  sp[threadIdx.x] = a;
+  lf_st<AGG>(&sp[threadIdx.x], a);
   __syncthreads();
   LfPart x = a;
   for (int o = 1; o < LF_T; o <<= 1) {
     LfPart y = x;
-    if ((int)threadIdx.x >= o) y = lf_join<VT, AGG>(sp[threadIdx.x - o], x);
+    if ((int)threadIdx.x >= o) y = lf_join<VT, AGG>(lf_ld<VT, AGG>(&sp[threadIdx.x - o]), x);
     __syncthreads();
-    sp[threadIdx.x] = y;
+    lf_st<AGG>(&sp[threadIdx.x], y);
     x = y;
     __syncthreads();
   }
   // the tile's carry from its predecessors (decoupled look-back), and the launch's output base
   if (threadIdx.x < 64) {   // wave 0
     const int lane = threadIdx.x;
-    const LfPart agg = sp[LF_T - 1];
+    const LfPart agg = lf_ld<VT, AGG>(&sp[LF_T - 1]);
     const unsigned int ep = L.epoch << 2;
     if (lane == 0) {
       if (tile == 0) {
@@ -2348,10 +2374,10 @@ __global__ __launch_bounds__(LF_T) void k_late_fused(Spec s, const unsigned long
         const int first_stop = sb ? __builtin_ctzll(sb) : 64;
         if (lane > first_stop) e.empty = 1;
         for (int off = 1; off < 64; off <<= 1) {   // lane 0: the lanes' parts joined, farthest first
-          const LfPart o = lf_shfl(e, lane + off < 64 ? lane + off : lane);
+          const LfPart o = lf_shfl_t<VT, AGG>(e, lane + off < 64 ? lane + off : lane);
           if (lane + off < 64) e = lf_join<VT, AGG>(o, e);
         }
-        c = lf_join<VT, AGG>(lf_shfl(e, 0), c);
+        c = lf_join<VT, AGG>(lf_shfl_t<VT, AGG>(e, 0), c);
         if (sb || hi < 64) break;
         hi -= 64;
       }
