@@ -697,7 +697,7 @@ def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "v
     return back, out
 
 
-@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 400)])
+@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 400), ("i64", 900)])
 def test_oracle_list_checkpoint_round_trip(vt, lateness):
     """The oracle's HeapListState sections (ListSerializer: int size, then the elements) restore and snapshot
     back byte for byte."""
@@ -710,7 +710,7 @@ def test_oracle_list_checkpoint_round_trip(vt, lateness):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 400)])
+@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 400), ("i64", 900)])
 def test_list_checkpoint(mode, vt, lateness):
     """List state of tumbling windows in the reference layout: the engine's sections (its slices' element
     buffers grouped per window and key in arrival order) are byte-identical to the oracle's; the engine
@@ -733,10 +733,26 @@ def test_list_checkpoint(mode, vt, lateness):
 
 @pytest.mark.gpu
 def test_list_checkpoint_rejections():
+    """Sliding-window list state takes no reference-layout checkpoint; tumbling list state restored below the
+    maxTimestamp of a window that fired before the checkpoint (Long.MIN_VALUE) is refused, not mis-fired."""
     from flink_amd import _abi
     from flink_amd.windowing import ListStateDescriptor, SlidingEventTimeWindows, WindowEngine, make_config
+    from oracle.oracle import OracleEngine
     e = WindowEngine(make_config(SlidingEventTimeWindows.of(2000, 1000), ListStateDescriptor()))
     with pytest.raises(_abi.FwError) as ei:
         e.snapshot_kg_flink(0, ("key", "f1", "value"))
     assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+    e.close()
+    o = _list_run(OracleEngine, "i64", 900, 0)   # window [0, 1000) fired and kept for its lateness at the checkpoint
+    from flink_amd.windowing import TumblingEventTimeWindows, make_config as mk
+    e = WindowEngine(mk(TumblingEventTimeWindows.of(1000), ListStateDescriptor("i64"), None, 900, max_parallelism=128,
+                        key_capacity=1 << 12, max_batch=1 << 12, out_capacity=1 << 20))
+    codes = []
+    for kg, (st, tm) in o.items():
+        try:
+            e.restore_kg_flink(kg, ("key", "f1", "value"), st, tm, LONG_MIN)
+        except _abi.FwError as err:
+            codes.append(err.code)
+            break
+    assert codes == [_abi.FW_ERR_UNSUPPORTED]
     e.close()
