@@ -4243,6 +4243,21 @@ static int ghost_advance(fw_engine* e, int64_t wm_old, int64_t wm_new) {
   return FW_OK;
 }
 
+// restored disarmed windows whose maxTimestamp the watermark passed: their re-armed panes (list state: keys)
+// fired with it; the rest never fires again (cleanup at the cleanup time, as any window)
+static int disarm_advance(fw_engine* e, int64_t wm) {
+  for (auto it = e->disarmed.begin(); it != e->disarmed.end();) {
+    const int64_t m = *it;   // (tumbling: a slice number; sliding: a window number, its own pane's slot)
+    const int64_t max_ts = jsub(jadd(host_window_start(e->cfg, m), e->s.size), 1);
+    if (max_ts > wm) { ++it; continue; }
+    const int32_t p = (int32_t)floor_mod(m, e->s.P);
+    HIPCHK(e, hipMemsetAsync(e->s.disarm + p, 0, 1, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->s.armed + (size_t)p * (size_t)e->s.stride, 0, (size_t)e->s.stride, e->stream));
+    it = e->disarmed.erase(it);
+  }
+  return FW_OK;
+}
+
 int fw_advance_watermark(fw_engine* e, int64_t wm) {
   if (!e) return FW_ERR_INVALID_ARG;
   if (e->sticky) return e->sticky;
@@ -4270,17 +4285,7 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   FW_DISPATCH(launch_watermark_t, e, e->cur_wm, wm);
   e->phase_end(e->s.stride);
   HIPCHK(e, hipGetLastError());
-  // restored disarmed windows whose maxTimestamp the watermark passed: their re-armed panes fired above; the
-  // rest never fires again (cleanup at the cleanup time, as any window)
-  for (auto it = e->disarmed.begin(); it != e->disarmed.end();) {
-    const int64_t m = *it;   // (tumbling: a slice number; sliding: a window number, its own pane's slot)
-    const int64_t max_ts = jsub(jadd(host_window_start(e->cfg, m), e->s.size), 1);
-    if (max_ts > wm) { ++it; continue; }
-    const int32_t p = (int32_t)floor_mod(m, e->s.P);
-    HIPCHK(e, hipMemsetAsync(e->s.disarm + p, 0, 1, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->s.armed + (size_t)p * (size_t)e->s.stride, 0, (size_t)e->s.stride, e->stream));
-    it = e->disarmed.erase(it);
-  }
+  if (int rc = disarm_advance(e, wm)) return rc;
   e->hmarks.push_back({wm, e->dev_marks++, true});
   e->out_dirty = false;
   e->cur_wm = wm;
@@ -4676,11 +4681,17 @@ static int build_snapshot(fw_engine* e) {
       if (ne > 0)
         HIPCHK(e, hipMemcpy(rows.data(), e->lst.buf + (size_t)p * (size_t)e->lst.cap * LST_WORDS, 8 * rows.size(),
                             hipMemcpyDeviceToHost));
+      std::vector<uint8_t> armed;
+      if (e->disarmed.count(m)) {   // a restored window that fired before: the keys no record re-armed since
+        armed.resize((size_t)s.stride);
+        HIPCHK(e, hipMemcpy(armed.data(), s.armed + (size_t)p * (size_t)s.stride, (size_t)s.stride, hipMemcpyDeviceToHost));
+      }
       for (int64_t j = 0; j < ne; ++j) {
         const int64_t* x = &rows[(size_t)j * LST_WORDS];   // kid, ordinal, value, f1
         if (x[0] < 0 || x[0] >= s.stride || kid_kg[(size_t)x[0]] < 0) continue;
         const int64_t key = x[0] == s.D ? fw::EMPTY_KEY : keys[(size_t)x[0]];
         e->snap_list[{m, key}].push_back({x[1], x[2], x[3]});
+        if (!armed.empty() && !armed[(size_t)x[0]]) e->snap_unarmed.insert({m, key});
       }
     }
     for (auto& kv : e->snap_list) {
@@ -5377,9 +5388,6 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   } else if (got != want) {
     return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
   }
-  if (e->list && !dis_now.empty())
-    return reject(e, FW_ERR_UNSUPPORTED, "list state: windows that fired before the checkpoint, restored below their "
-                                         "maxTimestamp (restore at the checkpoint's watermark)");
   if (!dis_now.empty() && !e->s.disarm) {   // per-slot flags and per-pane re-arm marks, first needed here
     e->s.disarm = e->alloc<uint8_t>((size_t)s.P);
     e->s.armed = e->alloc<uint8_t>((size_t)s.P * (size_t)s.stride);

@@ -376,10 +376,29 @@ int list_watermark(fw_engine* e, int64_t wm) {
   HIPCHK(e, hipStreamSynchronize(e->stream));
   const int64_t nt = e->list_plan_h[0];
   for (int64_t t = 0; t < nt; ++t) {
-    const int64_t n = e->list_plan_h[2 + 2 * t], N = e->list_plan_h[3 + 2 * t];
+    const int64_t n = e->list_plan_h[2 + 2 * t];
+    int64_t N = e->list_plan_h[3 + 2 * t];
     if (N == 0) continue;
     if (e->list_out + N > e->cfg.out_capacity) return fail(e, FW_ERR_CAPACITY, "output log capacity exceeded (list state)");
     if (int rc = list_sort_window(e, n, N)) return rc;
+    if (e->disarmed.count(n)) {   // a restored window that fired before the checkpoint: only the re-armed keys fire
+      std::vector<int64_t> pos((size_t)N);
+      std::vector<unsigned long long> kids((size_t)N);
+      std::vector<uint8_t> armed((size_t)e->s.stride);
+      const int32_t p = (int32_t)floor_mod(n, e->s.P);
+      HIPCHK(e, hipMemcpyAsync(pos.data(), e->list_v1, 8 * (size_t)N, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipMemcpyAsync(kids.data(), e->list_k2, 8 * (size_t)N, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipMemcpyAsync(armed.data(), e->s.armed + (size_t)p * (size_t)e->s.stride, (size_t)e->s.stride,
+                               hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      int64_t keep = 0;
+      for (int64_t x = 0; x < N; ++x)
+        if (armed[(size_t)kids[(size_t)x]]) pos[(size_t)keep++] = pos[(size_t)x];
+      N = keep;
+      if (N == 0) continue;
+      HIPCHK(e, hipMemcpyAsync(e->list_v1, pos.data(), 8 * (size_t)N, hipMemcpyHostToDevice, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((N + BLOCK - 1) / BLOCK, e->grid));
     const int64_t max_ts = jsub(jadd(jadd(e->s.offset, (int64_t)((uint64_t)n * (uint64_t)e->s.slide)), e->s.size), 1);
     hipLaunchKernelGGL(k_list_emit, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->lst, e->list_v1, N, e->list_out, max_ts);
@@ -387,6 +406,7 @@ int list_watermark(fw_engine* e, int64_t wm) {
     e->list_out += N;
   }
   hipLaunchKernelGGL(k_list_finish, dim3(1), dim3(1024), 0, e->stream, e->s, e->lst, e->list_plan, e->list_out);
+  if (int rc = disarm_advance(e, wm)) return rc;
   DBGSYNC(e, "k_list_finish");
   hipLaunchKernelGGL(k_mark_only, dim3(1), dim3(1), 0, e->stream, e->s, wm);
   e->phase_end(e->s.stride);

@@ -671,7 +671,7 @@ def test_fold_checkpoint(mode, kind, initial, vt, assigner):
                                               for x, y in zip(rg, ro)), w
 
 
-def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "value")):
+def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "value"), restore_wm=None, pre=None):
     """Tumbling list state (WindowedStream.apply: HeapListState "window-contents" of the input tuples): drive 2/3
     of a Zipf stream, snapshot every key group in the reference layout; or restore such sections at their
     watermark and drive the rest to a final MAX_WATERMARK."""
@@ -690,9 +690,14 @@ def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "v
         e.close()
         return snaps
     for kg, (st, tm) in restore.items():
-        e.restore_kg_flink(kg, layout, st, tm, wm)
+        e.restore_kg_flink(kg, layout, st, tm, wm if restore_wm is None else restore_wm)
     back = {kg: e.snapshot_kg_flink(kg, layout) for kg in range(128)}
-    out = drive(e, keys[n:], ts[n:], vals[n:], 2048, 100, LONG_MAX, f1=f1[n:])
+    first = []
+    if pre is not None:   # records pushed right after the restore, before any watermark
+        sel = np.arange(pre)
+        e.push(keys[sel].copy(), 600 + sel.astype(np.int64), vals[sel].copy(), f1=90_000 + sel.astype(np.int64))
+        first = [e.collect()]
+    out = first + drive(e, keys[n:], ts[n:], vals[n:], 2048, 100, LONG_MAX, f1=f1[n:])
     e.close()
     return back, out
 
@@ -733,26 +738,32 @@ def test_list_checkpoint(mode, vt, lateness):
 
 @pytest.mark.gpu
 def test_list_checkpoint_rejections():
-    """Sliding-window list state takes no reference-layout checkpoint; tumbling list state restored below the
-    maxTimestamp of a window that fired before the checkpoint (Long.MIN_VALUE) is refused, not mis-fired."""
+    """Sliding-window list state takes no reference-layout checkpoint."""
     from flink_amd import _abi
     from flink_amd.windowing import ListStateDescriptor, SlidingEventTimeWindows, WindowEngine, make_config
-    from oracle.oracle import OracleEngine
     e = WindowEngine(make_config(SlidingEventTimeWindows.of(2000, 1000), ListStateDescriptor()))
     with pytest.raises(_abi.FwError) as ei:
         e.snapshot_kg_flink(0, ("key", "f1", "value"))
     assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
     e.close()
-    o = _list_run(OracleEngine, "i64", 900, 0)   # window [0, 1000) fired and kept for its lateness at the checkpoint
-    from flink_amd.windowing import TumblingEventTimeWindows, make_config as mk
-    e = WindowEngine(mk(TumblingEventTimeWindows.of(1000), ListStateDescriptor("i64"), None, 900, max_parallelism=128,
-                        key_capacity=1 << 12, max_batch=1 << 12, out_capacity=1 << 20))
-    codes = []
-    for kg, (st, tm) in o.items():
-        try:
-            e.restore_kg_flink(kg, ("key", "f1", "value"), st, tm, LONG_MIN)
-        except _abi.FwError as err:
-            codes.append(err.code)
-            break
-    assert codes == [_abi.FW_ERR_UNSUPPORTED]
-    e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_list_restore_at_long_min(mode):
+    """Tumbling list state restored at Long.MIN_VALUE while window [0, 1000) had fired and was kept for its lateness
+    (its entries carry only cleanup timers): restored disarmed, it fires again at its maxTimestamp only for the keys a
+    later record re-armed, with every element so far (EventTimeTrigger.onElement), the others wait for their cleanup —
+    as the oracle restored from the same bytes; the sections are written back unchanged."""
+    from harness import epochs_of
+    from flink_amd.windowing import WindowEngine
+    from oracle.oracle import OracleEngine
+    o = _list_run(OracleEngine, "i64", 900, 0)
+    outs = {}
+    for name, factory, md in (("g", WindowEngine, mode), ("o", OracleEngine, 0)):
+        back, out = _list_run(factory, "i64", 900, md, restore=o, restore_wm=LONG_MIN, pre=40)
+        assert _diff(back, o) is None, (name, _diff(back, o))
+        outs[name] = _canon(epochs_of(out, ["sum_i64"], True))
+    assert outs["g"] == outs["o"]
+    refired = [r for w, recs in outs["o"] if w != "tail" for r in recs if r[1] < 1000]
+    assert refired, "the window that fired before the checkpoint fired again for re-armed keys"
