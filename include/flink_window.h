@@ -285,7 +285,7 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * panes carry no trigger timer (it fired before the checkpoint and is kept for its allowed lateness) is
  * restored disarmed — it fires again only for keys whose records re-arm it before the watermark passes its
  * maxTimestamp (EventTimeTrigger.onElement), otherwise it waits for its cleanup time; a sliding window likewise,
- * through its own pane (tumbling list state: not restorable below such a window's maxTimestamp).  Every restored key
+ * through its own pane, and tumbling list state through its slice.  Every restored key
  * group must use the same `watermark`. */
 #define FW_SF_KEY    1   /* the key (the tuple's key field, e.g. f0)                          */
 #define FW_SF_F1     2   /* the pass-through field of the first arrival (maxBy/minBy: of the extremal record) */
