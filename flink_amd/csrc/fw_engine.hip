@@ -50,7 +50,7 @@
 #define FW_AGG_PRECHECK 0
 #endif
 #ifndef FW_AGG_UR
-#define FW_AGG_UR 2   // k_aggregate: wave steps whose loads are in flight together (two sets: 2 x UR)
+#define FW_AGG_UR 1   // k_aggregate: wave steps whose loads are in flight together (two sets: 2 x UR; 1 measured faster than 2 in round 6)
 #endif
 
 namespace fw {
@@ -146,10 +146,28 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   int64_t* gfirst;
 };
 
+// the Spec fields k_route's per-record work reads, passed by value (kernel arguments, in SGPRs from the wave's start;
+// read through the device Spec pointer they were scalar loads issued and waited on in the middle of each tile's
+// record pass, round 6).  Field names as in Spec, so the window assignment takes either
+struct RouteSpec {
+  int32_t assigner, K, R, mp, kg_start, kg_end, mp_mask, kb_bits, nb;
+  int64_t size, slide, offset, lateness, g;
+  double inv_size, inv_g;
+  uint64_t dir_mask;
+  int32_t* err;
+  unsigned long long* stats;
+};
+
 __device__ __forceinline__ void set_error(int32_t* err, int32_t code) { atomicCAS(err, 0, code); }
 // a capacity error, with the id of the site that raised it first (fw_debug_counters word 7: diagnostics)
 #define cap_error(s, site) do { set_error((s).err, FW_ERR_CAPACITY); \
     atomicCAS(&(s).stats[7], 0ull, (unsigned long long)(site)); } while (0)
+
+// a pointer the compiler cannot see is global (loaded from the device-resident Spec) is accessed as flat: every
+// flat access waits on LDS and global traffic alike (s_waitcnt vmcnt(0) lgkmcnt(0)), which serialised k_aggregate's
+// fold and prologue loads (round 6).  G() states the address space where it matters
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* G(T* p) { return (__attribute__((address_space(1))) T*)p; }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {  // MurmurHash3 finaliser: directory hash
   k ^= k >> 33;
@@ -350,8 +368,8 @@ __device__ __noinline__ RecWin record_windows_sliding(SlideSpec s, int64_t ts, i
 }
 
 
-template <bool INL = false>
-__device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int64_t wm) {
+template <bool INL = false, class SP = Spec>
+__device__ __forceinline__ RecWin record_windows(const SP& s, int64_t ts, int64_t wm) {
   if (s.assigner != FW_TUMBLING) {
     const SlideSpec ss{s.offset, s.size, s.slide, s.g, s.lateness, s.inv_g, s.K, s.R};
     return INL ? record_windows_sliding_body<true>(ss, ts, wm) : record_windows_sliding(ss, ts, wm);
@@ -383,7 +401,8 @@ __device__ __forceinline__ RecWin record_windows(const Spec& s, int64_t ts, int6
 
 // key group of a record (KeyGroupRangeAssignment.assignToKeyGroup :51-64); murmurHash is >= 0, so for
 // the usual power-of-two maxParallelism the remainder is a mask
-__device__ __forceinline__ int32_t record_key_group(const Spec& s, int32_t key_hash) {
+template <class SP>
+__device__ __forceinline__ int32_t record_key_group(const SP& s, int32_t key_hash) {
   return s.mp_mask ? (murmur_hash(key_hash) & s.mp_mask) : key_group_for_hash(key_hash, s.mp);
 }
 
@@ -655,6 +674,9 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 // 12-B records measured slower: the per-record probe of the global directory cost k_route more than the
 // 6 B/event it saved)
 // ------------------------------------------------------------------------------------------------
+#ifndef FW_AGG_UNCOND
+#define FW_AGG_UNCOND 1   // k_aggregate: the next group's loads issued without a branch (A/B switch)
+#endif
 #ifndef FW_RT_TILE_LOG
 #define FW_RT_TILE_LOG 12
 #endif
@@ -773,13 +795,17 @@ __device__ __forceinline__ void block_scan_excl(int32_t* a, int n, int32_t* wtot
 // slice set.
 constexpr size_t RT_LDS = (size_t)RT_TILE * (16 + 2) + 4 * (size_t)(RT_GROUPS * RT_MAXNB + 8) + 4 * 16 + 8 * RT_Q + 8;
 
-template <int VT, int AGG, bool FIRST>
-__device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, const RouteBuf& r, unsigned char* smem,
-                                           const bool tail, const int tile) {
+// TAIL: the batch's last, partial tile.  A separate instantiation (round 6): with one code path for both, the whole
+// tiles' 16-B loads followed a join with the tail's loads, and the compiler's waits for the join made each whole tile
+// wait for its first loads before issuing the rest
+template <int VT, int AGG, bool FIRST, bool TAIL>
+__device__ __forceinline__ void route_tile(const Spec& s, const RouteSpec& rq, const BatchIn& b, const RouteBuf& r,
+                                           unsigned char* smem, const int tile) {
+  constexpr bool tail = TAIL;
   constexpr int NT = RT_THREADS;
   constexpr int PER = RT_TILE / NT;     // records per thread
   constexpr int V = PER / 2;            // 16-B vectors per column per thread
-  const int nbq = RT_GROUPS * s.nb;
+  const int nbq = RT_GROUPS * rq.nb;
   longlong2* st_kv = (longlong2*)smem;
   uint16_t* st_idx = (uint16_t*)(st_kv + RT_TILE);
   int32_t* cnt = (int32_t*)(st_idx + RT_TILE);     // [nbq + 1]
@@ -794,11 +820,13 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   if (threadIdx.x == 0) *any_direct = 0;
   // phase A: every load of the tile in flight before any dependent work; record (j, e) of this thread
   // is tile index 2 * (j * NT + tid) + e
+  // (the tail test is hoisted out of the loads and the optional key-hash column is loaded after them: a branch
+  // between two vectors' loads made the compiler wait for most earlier loads before issuing the next, round 6)
   int64_t kk[PER], tt[PER], vv[PER];
+  if (!tail) {   // uniform
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
-    const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
-    if (!tail) {
+    for (int j = 0; j < V; ++j) {
+      const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
 #if FW_ROUTE_NT & 1
       // streamed once per batch: non-temporal, so the routed intermediate k_aggregate reads next keeps the cache
       typedef long long v2i64 __attribute__((ext_vector_type(2)));
@@ -813,16 +841,27 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
       kk[2 * j] = a.x; kk[2 * j + 1] = a.y;
       tt[2 * j] = c.x; tt[2 * j + 1] = c.y;
       vv[2 * j] = d.x; vv[2 * j + 1] = d.y;
-      if (b.key_hash) *(int2*)(lhash + (i - base)) = *(const int2*)(b.key_hash + i);
-    } else {
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int64_t ie = min(i + e, b.n - 1);
         kk[2 * j + e] = b.key[ie];
         tt[2 * j + e] = b.ts[ie];
         vv[2 * j + e] = b.val[ie];
-        if (b.key_hash) lhash[i + e - base] = b.key_hash[ie];
       }
+    }
+  }
+  if (b.key_hash) {   // uniform: the Java key hashes (optional column)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int64_t i = base + 2 * (j * NT + (int)threadIdx.x);
+      if (!tail) *(int2*)(lhash + (i - base)) = *(const int2*)(b.key_hash + i);
+      else
+        for (int e = 0; e < 2; ++e) lhash[i + e - base] = b.key_hash[min(i + e, b.n - 1)];
     }
   }
   __syncthreads();   // cnt and lset initialised
@@ -834,35 +873,37 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   // the wave's reference slice: assignment of its first record, valid for every record whose timestamp
   // lies in the same slice (a wave of an in-order stream nearly always does); the others take the
   // full per-record path.  Bounded away from the int64 edges so no wrap happens inside the range.
+  // a subtask owning every key group cannot see a foreign key: skip the murmur range check
+  const bool all_kg = rq.kg_start == 0 && rq.kg_end == rq.mp - 1;
+  uint32_t slow_mask = 0;   // records outside the wave's reference slice
+  bool e_ts = false, e_kg = false;   // errors, reported once after the loop (no atomics inside it)
+  {
   RecWin w0;
   w0.m = 0; w0.n_late = 0; w0.n_fire = 0; w0.n_windows = 0; w0.quirk = false; w0.lo = 1; w0.hi = 0;
   {
     const int64_t i0 = base + 2 * (int)threadIdx.x;
     const bool c0 = (!tail || i0 < b.n) && tt[0] > -(1LL << 61) && tt[0] < (1LL << 61);
     const uint64_t cm = __ballot(c0);
-    if (cm && s.size < (1LL << 60)) {
+    if (cm && rq.size < (1LL << 60)) {
       const int64_t ts0 = uniform64(__shfl(tt[0], __ffsll((long long)cm) - 1));
-      w0 = record_windows<true>(s, ts0, b.wm);   // (inline: a call here made the whole kernel keep the calling convention)
+      w0 = record_windows<true>(rq, ts0, b.wm);   // (inline: a call here made the whole kernel keep the calling convention)
       w0.m = uniform64(w0.m); w0.lo = uniform64(w0.lo); w0.hi = uniform64(w0.hi);
       w0.n_late = __builtin_amdgcn_readfirstlane(w0.n_late);
       w0.n_fire = __builtin_amdgcn_readfirstlane(w0.n_fire);
       w0.n_windows = __builtin_amdgcn_readfirstlane(w0.n_windows);
     }
   }
-  // a subtask owning every key group cannot see a foreign key: skip the murmur range check
-  const bool all_kg = s.kg_start == 0 && s.kg_end == s.mp - 1;
-  uint32_t slow_mask = 0;   // records outside the wave's reference slice
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int64_t i = base + 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
     const bool valid = !tail || i < b.n;
     const int64_t key = kk[k], ts = tt[k];
     bool ok = valid;
-    if (ok && ts == INT64_MIN) { set_error(s.err, FW_ERR_NO_TIMESTAMP); ok = false; }
+    if (ok && ts == INT64_MIN) { e_ts = true; ok = false; }
     if (ok && !all_kg) {
       const int32_t h = b.key_hash ? lhash[i - base] : long_hash_code(key);
-      const int32_t kg = record_key_group(s, h);   // AbstractKeyedStateBackend.setCurrentKey :167-170
-      if (kg < s.kg_start || kg > s.kg_end) { set_error(s.err, FW_ERR_KEY_GROUP); ok = false; }
+      const int32_t kg = record_key_group(rq, h);   // AbstractKeyedStateBackend.setCurrentKey :167-170
+      if (kg < rq.kg_start || kg > rq.kg_end) { e_kg = true; ok = false; }
     }
     const bool fast = ok && ts >= w0.lo && ts <= w0.hi;
     slow_mask |= (ok && !fast ? 1u : 0u) << k;
@@ -876,8 +917,14 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
     fire_mask |= (late_fire ? 1u : 0u) << k;
     tt[k] = w0.m;
   }
+  }
+  if (__any(e_ts || e_kg)) {
+    if (e_ts) set_error(rq.err, FW_ERR_NO_TIMESTAMP);
+    if (e_kg) set_error(rq.err, FW_ERR_KEY_GROUP);
+  }
   // the full assignment for the rest: one call-free copy of the code (a call would make the register
   // allocator spill the tile around it), timestamps re-read from the input, results through LDS
+  RT_STAMP(5);
   if (__any(slow_mask != 0)) {
     int64_t* sm = (int64_t*)(smem + (size_t)RT_TILE * 4);        // [RT_TILE] slice numbers
     int32_t* sf = (int32_t*)(smem + (size_t)RT_TILE * 12);       // [RT_TILE] flags: live | late_fire << 1 | n_late << 2
@@ -886,7 +933,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
       if ((slow_mask >> k) & 1u) {
         const int32_t t = 2 * ((k >> 1) * NT + (int)threadIdx.x) + (k & 1);
         const int64_t ts = b.ts[base + t];
-        const RecWin w = record_windows<true>(s, ts, b.wm);
+        const RecWin w = record_windows<true>(rq, ts, b.wm);
         if (w.quirk) quirk_record(s, b, kk[k], base + t, w.qn, w.q_late, w.q_fire);
         const bool live = (w.n_windows - w.n_late) > 0;
         const int32_t f = (live ? 1 : 0) | (live && w.n_fire > 0 ? 2 : 0) | (w.n_late << 2);
@@ -914,6 +961,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   // counting-sort rank.  The rest (rare: per-element fires, slices beyond the tile's RT_Q, the
   // Long.MIN_VALUE key, bucket 0) take the bucket's direct or fire bin group, which the k_aggregate
   // workgroup owning the bucket applies.
+  RT_STAMP(6);
   int64_t m_ref = INT64_MIN;
   {
     const uint64_t lm = __ballot(route_mask != 0);
@@ -954,16 +1002,17 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
       // Long.MIN_VALUE key's, which lives in bucket 0)
       const bool kmin = kk[k] == EMPTY_KEY;
       const uint64_t hk = fmix64((uint64_t)kk[k]);
-      const int32_t bkt = kmin ? 0 : (int32_t)((hk & s.dir_mask) >> s.kb_bits);
+      const int32_t bkt = kmin ? 0 : (int32_t)((hk & rq.dir_mask) >> rq.kb_bits);
       const int32_t g = q >= 0 ? q : RT_Q + (int32_t)((fire_mask >> k) & 1u);
-      bin[k] = g * s.nb + bkt;
+      bin[k] = g * rq.nb + bkt;
       rank[k] = atomicAdd(&cnt[bin[k]], 1);
       kk[k] = (int64_t)hk;
     }
   }
+  RT_STAMP(7);
   if (__any(late_pairs != 0)) {
     for (int off = 32; off > 0; off >>= 1) late_pairs += __shfl_xor(late_pairs, off);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&s.stats[ST_LATE], late_pairs);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&rq.stats[ST_LATE], late_pairs);
   }
   if (direct_mask != 0) *any_direct = 1;
   __syncthreads();   // every wave's slice claims are in lset, every staging read is done
@@ -979,13 +1028,13 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
   int nlive = tile_direct ? RT_GROUPS : 0;
   if (!tile_direct)
     for (int q = 0; q < RT_Q; ++q) nlive = lset[q] != FREE_TAG ? q + 1 : nlive;
-  const int nlb = nlive * s.nb;
+  const int nlb = nlive * rq.nb;
   block_scan_excl<NT>(cnt, nlb + 1, wtot);   // cnt[nlb] = routed records of the tile
   // the segment table, bucket-major (row (group, bucket) holds one word per tile: start | end << 16), so that the
   // k_aggregate workgroup owning a bucket reads its rows contiguously; only the tile's live groups are written
   // (its routed slices, and the direct / fire groups when it has direct records), k_aggregate reads no other
   for (int x = threadIdx.x; x < nlb; x += NT) {
-    const int g = x / s.nb;
+    const int g = x / rq.nb;
     const bool live = g < RT_Q ? lset[g] != FREE_TAG : tile_direct;
     if (live) r.seg[(int64_t)x * r.seg_stride + tile] = (uint32_t)cnt[x] | ((uint32_t)cnt[x + 1] << 16);
   }
@@ -1018,7 +1067,7 @@ __device__ __forceinline__ void route_tile(const Spec& s, const BatchIn& b, cons
 }
 
 template <int VT, int AGG, bool FIRST>
-__global__ __launch_bounds__(RT_THREADS, 4) void k_route(const Spec* __restrict__ sd, BatchIn b, RouteBuf r) {
+__global__ __launch_bounds__(RT_THREADS, 4) void k_route(const Spec* __restrict__ sd, RouteSpec rq, BatchIn b, RouteBuf r) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Spec& s = *sd;   // device copy (kernel arguments by value are held in scalar registers from entry)
   // every tile but the last is whole, so its 16-B loads need no bounds (uniform branch)
@@ -1026,7 +1075,8 @@ __global__ __launch_bounds__(RT_THREADS, 4) void k_route(const Spec* __restrict_
   // started late so that one's compute phase falls beside the other's memory phases, measured no faster and
   // spilled: round 5)
   const int tile = (int)blockIdx.x;
-  route_tile<VT, AGG, FIRST>(s, b, r, smem, (int64_t)(tile + 1) * RT_TILE > b.n, tile);
+  if ((int64_t)(tile + 1) * RT_TILE > b.n) route_tile<VT, AGG, FIRST, true>(s, rq, b, r, smem, tile);   // uniform
+  else route_tile<VT, AGG, FIRST, false>(s, rq, b, r, smem, tile);
 }
 
 // the bucket's LDS directory-hash table: slot of h, inserting its key (fmix64_inv(h)) into the global
@@ -1203,7 +1253,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
                                                         // then AG_LOOK entries of INT32_MAX (the step lookup's reads)
   int32_t* step_tile = off + r.ntiles + 1 + AG_LOOK;    // [AG_CHS] tile holding the first record of each step
   int32_t* awtot = step_tile + AG_CHS;                  // [16] scan scratch
-  int64_t* gsl = (int64_t*)(((uintptr_t)(awtot + 16) + 7) & ~(uintptr_t)7);   // [RT_GS] the batch's slices
+  // (aligned by an offset from smem, not through an integer: a pointer rebuilt from an integer loses the LDS
+  // address space, and every access through it became a flat access that waited on all outstanding global loads)
+  int64_t* gsl = (int64_t*)(smem + ((((unsigned char*)(awtot + 16) - smem) + 7) & ~(ptrdiff_t)7));   // [RT_GS] the batch's slices
   int32_t& lclaim = *(int32_t*)(gsl + RT_GS);
   int32_t* plan = (int32_t*)(gsl + RT_GS) + 2;          // [RT_MAXNB + 1] helper prefix; then bucket, share, shares
   const int64_t SB = (int64_t)8 << 16;
@@ -1275,37 +1327,68 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
   const int64_t dbase = (int64_t)bkt * KB;
   if (share == 0 && r.fold_cnt_zero)
     for (int g = threadIdx.x; g < RT_GS; g += NT) r.fold_cnt_zero[(int64_t)bkt * RT_GS + g] = 0u;
-  // does any tile hold direct-group records (the batch's flag; no: skip all direct work)
-  const bool has_direct = __builtin_amdgcn_readfirstlane(*r.dflag) != 0;
-  // every tile's header and this bucket's segment bounds in each of its bin groups, plus the bucket's
-  // directory slice, into LDS: all loads independent, one round trip
-  // (the bucket's rows of the bucket-major segment table are contiguous; a row's word is read only where the tile
-  // wrote it: a live routed group, or a tile with direct records)
+  // the bucket's directory slice, every tile's header and this bucket's segment bounds in each of its routed bin
+  // groups, the tiles' direct marks and the batch's direct flag: all loads independent, issued before any is
+  // used (one round trip; the flag read first and waited on cost a round trip of its own, round 6).  The
+  // bucket's rows of the bucket-major segment table are contiguous; a row's word is used only where the tile
+  // wrote it (a live routed group; the direct / fire groups of a tile with direct records, read in a second
+  // round trip by those tiles only)
+  const int64_t dk0 = (int)threadIdx.x < KB ? G(s.dir_keys)[dbase + threadIdx.x] : EMPTY_KEY;
+  const unsigned int dfl = *r.dflag;
+  // one-slice batches (the usual in-order batch: every tile routed one slice, the same, into group 0, and no tile
+  // has direct records) need no slice set and no separate segment scan: with at most one tile per thread, each
+  // thread keeps its tile's group-0 segment, the waves scan their lengths and post their slice here, and the
+  // checks after the first barrier decide (every thread alike) whether the batch is such a batch
+  const bool one_pass = !SKEW && r.ntiles <= NT;   // uniform
+  int64_t my_m = FREE_TAG;
+  bool my_ok = true;
+  int32_t my_len = 0, my_st = 0;
   for (int t = threadIdx.x; t < r.ntiles; t += NT) {
     int64_t h[RT_Q];
     uint32_t sg[RT_GROUPS];
-    uint32_t td = 0;
-    // every load independent (one round trip); words a tile did not write are masked after
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q) h[q] = r.hdr[(int64_t)t * RT_Q + q];
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q) sg[q] = r.seg[(int64_t)(q * s.nb + bkt) * r.seg_stride + t];
-    if (has_direct) {   // uniform
-      td = r.tdir[t];
+    const uint32_t td = r.tdir[t];
+#pragma unroll
+    for (int q = RT_Q; q < RT_GROUPS; ++q) sg[q] = 0u;
+    if (td != 0u) {
 #pragma unroll
       for (int q = RT_Q; q < RT_GROUPS; ++q) sg[q] = r.seg[(int64_t)(q * s.nb + bkt) * r.seg_stride + t];
     }
 #pragma unroll
-    for (int q = 0; q < RT_GROUPS; ++q) {
-      const bool live = q < RT_Q ? h[q] != FREE_TAG : td != 0u;
-      if (!live) sg[q] = 0u;
-    }
+    for (int q = 0; q < RT_Q; ++q)
+      if (h[q] == FREE_TAG) sg[q] = 0u;
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q) lhdr[t * RT_Q + q] = h[q];
 #pragma unroll
     for (int q = 0; q < RT_GROUPS; ++q) lseg[t * RT_GROUPS + q] = sg[q];
+    my_m = h[0];
+    my_ok = h[1] == FREE_TAG;
+    my_st = (int32_t)(sg[0] & 0xFFFFu);
+    my_len = (int32_t)(sg[0] >> 16) - my_st;
   }
-  for (int x = threadIdx.x; x < KB; x += NT) lh[x] = fmix64((uint64_t)s.dir_keys[dbase + x]);
+  // does any tile hold direct-group records (the batch's flag; no: skip all direct work)
+  const bool has_direct = __builtin_amdgcn_readfirstlane(dfl) != 0;
+  int64_t* wsl = (int64_t*)plan;                  // [NT / 64] one-slice check: each wave's slice (plan is SKEW's)
+  int32_t* wok = (int32_t*)(wsl + NT / 64);       // [NT / 64] ... and whether its tiles agree
+  int32_t my_incl = 0;
+  if (one_pass) {   // uniform
+    const uint64_t lm = __ballot(my_m != FREE_TAG);
+    const int64_t wm = lm ? __shfl(my_m, __ffsll((long long)lm) - 1) : FREE_TAG;
+    const bool ok = __all(my_ok && (my_m == FREE_TAG || my_m == wm));
+    my_incl = my_len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(my_incl, o);
+      if ((threadIdx.x & 63) >= (unsigned)o) my_incl += y;
+    }
+    if ((threadIdx.x & 63) == 63) awtot[threadIdx.x >> 6] = my_incl;
+    if ((threadIdx.x & 63) == 0) { wsl[threadIdx.x >> 6] = wm; wok[threadIdx.x >> 6] = ok ? 1 : 0; }
+  }
+  if ((int)threadIdx.x < KB) lh[threadIdx.x] = fmix64((uint64_t)dk0);
+  for (int x = threadIdx.x + NT; x < KB; x += NT) lh[x] = fmix64((uint64_t)G(s.dir_keys)[dbase + x]);
   if (threadIdx.x < AG_LOOK) off[r.ntiles + 1 + threadIdx.x] = INT32_MAX;
   for (int x = threadIdx.x; x < KA; x += NT) {
     lsum[x] = sum_identity(VT);
@@ -1322,6 +1405,38 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
   FW_STAMP(r, SB, 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t ord_base = b.ord_base;
+  // a one-slice batch: the slice set is {m0} and this bucket's segment offsets are the waves' scans (every thread
+  // reads the same NT / 64 posts, so `uni` is uniform)
+  bool uni = false;
+  if (one_pass && !has_direct) {   // uniform
+    // lane w < NT / 64 reads wave w's post (one LDS read per lane, no loop of dependent reads and branches)
+    constexpr int NW = NT / 64;
+    const bool in = lane < NW;
+    const int64_t x = in ? wsl[lane] : FREE_TAG;
+    const bool okw = !in || wok[lane] != 0;
+    const int32_t c = in ? awtot[lane] : 0;
+    const uint64_t nz = __ballot(x != FREE_TAG);
+    const int64_t m0 = nz ? __shfl(x, __ffsll((long long)nz) - 1) : FREE_TAG;
+    const bool ok = __all(okw && (x == FREE_TAG || x == m0));
+    int32_t total = c, before = lane < wave ? c : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {   // (over the whole wave: every lane needs the sums)
+      total += __shfl_xor(total, o);
+      before += __shfl_xor(before, o);
+    }
+    uni = ok;
+    FW_STAMP(r, SB, 5);
+    if (uni) {
+      if ((int)threadIdx.x < r.ntiles) {
+        sst[threadIdx.x] = my_st;
+        off[threadIdx.x] = before + my_incl - my_len;
+      }
+      if (threadIdx.x == 0) {
+        off[r.ntiles] = total;
+        gsl[0] = m0;   // (FREE_TAG: nothing routed)
+      }
+    }
+  }
   auto gsl_insert = [&](int64_t m) {
     int g = 0;
     for (; g < RT_GS; ++g) {
@@ -1386,7 +1501,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
   // the batch's routed slices: distinct entries of the tile headers (every workgroup builds the same
   // set).  A lane whose slice equals its left neighbour's leaves the insert to it, so a wave of an
   // in-order stream inserts once, not 64 times (same-address LDS atomics serialise)
-  for (int t0 = 0; t0 < r.ntiles; t0 += NT) {   // uniform
+  for (int t0 = 0; !uni && t0 < r.ntiles; t0 += NT) {   // uniform
     const int t = t0 + (int)threadIdx.x;
     for (int q = 0; q < RT_Q; ++q) {
       const int64_t m = t < r.ntiles ? lhdr[t * RT_Q + q] : FREE_TAG;
@@ -1396,11 +1511,14 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
     }
   }
   __syncthreads();
-  if (SKEW && threadIdx.x == 0) {   // ascending: every share of a bucket takes the slices in the same rounds
-    for (int i = 1; i < RT_GS && gsl[i] != FREE_TAG; ++i)
-      for (int j = i; j > 0 && gsl[j - 1] > gsl[j]; --j) { const int64_t t = gsl[j]; gsl[j] = gsl[j - 1]; gsl[j - 1] = t; }
+  FW_STAMP(r, SB, 6);
+  if (SKEW) {   // uniform
+    if (threadIdx.x == 0) {   // ascending: every share of a bucket takes the slices in the same rounds
+      for (int i = 1; i < RT_GS && gsl[i] != FREE_TAG; ++i)
+        for (int j = i; j > 0 && gsl[j - 1] > gsl[j]; --j) { const int64_t t = gsl[j]; gsl[j] = gsl[j - 1]; gsl[j - 1] = t; }
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   // directory hash -> slot in this bucket.  Linear probing keeps a key within the run that starts at
   // its home slot, so the first AG_WIN slots are compared without branching (the directory's load factor
@@ -1447,8 +1565,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
     // slot's tag is read now, its value used (and the slot claimed if free) at the fold: the load's latency
     // lies under the main loop instead of in front of it
     int64_t tagv = FREE_TAG;
-    if (threadIdx.x == 0) tagv = s.slice_tag[floor_mod(m, s.P)];
-    for (int t = threadIdx.x; t < r.ntiles; t += NT) {
+    if (threadIdx.x == 0) tagv = G(s.slice_tag)[floor_mod(m, s.P)];
+    if (g == 0) FW_STAMP(r, SB, 7);
+    for (int t = threadIdx.x; !uni && t < r.ntiles; t += NT) {   // (uni: offsets already in place)
       int32_t a0 = 0, a1 = 0;
 #pragma unroll
       for (int q = 0; q < RT_Q; ++q) {
@@ -1461,9 +1580,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
       sst[t] = a0;
       off[t] = a1 - a0;
     }
-    if (threadIdx.x == 0) off[r.ntiles] = 0;
-    __syncthreads();
-    block_scan_excl<NT, AG_MAXPER>(off, r.ntiles + 1, awtot);   // off[ntiles] = the bucket's records of slice m
+    if (!uni) {   // uniform
+      if (threadIdx.x == 0) off[r.ntiles] = 0;
+      __syncthreads();
+      block_scan_excl<NT, AG_MAXPER>(off, r.ntiles + 1, awtot);   // off[ntiles] = the bucket's records of slice m
+    }
     const int32_t R = off[r.ntiles];
     routed += R;
     FW_STAMP(r, SB, 2 + 3 * min(g, 1));
@@ -1485,7 +1606,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
       __syncthreads();
       const int32_t nsteps = min(AG_CHS, (R - cb + 63) >> 6);
       // one group = UR steps of this wave: addresses from the step table, loads issued, nothing waited on
-      auto load_group = [&](int32_t s0, longlong2* rv, uint32_t* ri, bool* ra) {
+      // (the record's tile and its in-tile index stay apart until the group is processed: OR-ing the loaded index in
+      // here made every group wait for its own loads at once, so no loads were in flight across a group, round 6)
+      auto load_group = [&](int32_t s0, longlong2* rv, uint32_t* ri, uint16_t* rx, bool* ra) {
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
           const int32_t st = s0 + u;
@@ -1504,34 +1627,40 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
             pos = (int64_t)t * RT_TILE + sst[t] + (rr - off[t]);
           }
           rv[u] = r.kv[pos];
-          ri[u] = ((uint32_t)t << IDX_BITS) | (FIRST ? (uint32_t)r.idx[pos] : 0u);
+          ri[u] = (uint32_t)t << IDX_BITS;
+          rx[u] = FIRST ? r.idx[pos] : (uint16_t)0;
         }
       };
-      auto process_group = [&](const longlong2* rv, const uint32_t* ri, const bool* ra) {
+      auto process_group = [&](const longlong2* rv, const uint32_t* ri, const uint16_t* rx, const bool* ra) {
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
           bool act = ra[u];
           uint32_t kl = probe(act, (uint64_t)rv[u].x);
-          if (SKEW && !BY) act = hot_combine<VT, AGG>(L, cmpto, act, kl, rv[u].y, ri[u], lane);
+          const uint32_t oi = ri[u] | (uint32_t)rx[u];
+          if (SKEW && !BY) act = hot_combine<VT, AGG>(L, cmpto, act, kl, rv[u].y, oi, lane);
           kl = act ? kl : (uint32_t)KB + (uint32_t)lane;   // inactive lanes update a private dummy slot
-          acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, rv[u].y, ri[u]);
+          acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, rv[u].y, oi);
         }
       };
       // software pipelined: the next group's loads are in flight while this group updates LDS (two
       // register sets, the loop unrolled by two so that both stay in registers)
       longlong2 rvA[UR], rvB[UR];
       uint32_t riA[UR], riB[UR];
+      uint16_t rxA[UR], rxB[UR];
       bool raA[UR], raB[UR];
       constexpr int32_t G = (NT / 64) * UR;
       int32_t s0 = wave * UR;
-      if (s0 < nsteps) load_group(s0, rvA, riA, raA);
+      if (s0 < nsteps) load_group(s0, rvA, riA, rxA, raA);
+      // (the next group's loads are issued unconditionally — past the end a group's lanes are inactive and read tile
+      // 0's first slot — so no branch joins paths with different loads in flight: at such a join the compiler waited
+      // for every load, the next group's included, round 6)
       while (s0 < nsteps) {   // wave-uniform
-        if (s0 + G < nsteps) load_group(s0 + G, rvB, riB, raB);
-        process_group(rvA, riA, raA);
+        if (FW_AGG_UNCOND || s0 + G < nsteps) load_group(s0 + G, rvB, riB, rxB, raB);
+        process_group(rvA, riA, rxA, raA);
         s0 += G;
         if (s0 >= nsteps) break;
-        if (s0 + G < nsteps) load_group(s0 + G, rvA, riA, raA);
-        process_group(rvB, riB, raB);
+        if (FW_AGG_UNCOND || s0 + G < nsteps) load_group(s0 + G, rvA, riA, rxA, raA);
+        process_group(rvB, riB, rxB, raB);
         s0 += G;
       }
       __syncthreads();   // the next chunk rewrites step_tile
@@ -1597,37 +1726,55 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
         if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&s.c.cnt[idx], (unsigned long long)lcnt[xl]);
         if (FIRST) atomicMin((long long*)&s.c.first[idx], (long long)(ord_base + (int64_t)lf));
         else s.c.present[idx] = 1;
+      } else if (!BY) {
+      // every column of the pane (and the f1 of the batch's earliest record, used if the pane is new) loaded
+      // before any store: one round trip (as far as the compiler knows the columns may alias, so a store between
+      // two loads made the second wait for it: three round trips per pane, round 6)
+      const int64_t o_sum = (AGG & FW_AGG_SUM) ? G(s.c.sum)[idx] : 0;
+      const int64_t o_mn = (AGG & FW_AGG_MIN) ? G(s.c.mn)[idx] : 0;
+      const int64_t o_mx = (AGG & FW_AGG_MAX) ? G(s.c.mx)[idx] : 0;
+      const int64_t o_cnt = (AGG & FW_AGG_COUNT) ? G(s.c.cnt)[idx] : 0;
+      const int64_t o_first = FIRST ? G(s.c.first)[idx] : 0;
+      const int64_t f1n = FIRST ? f1col[lf] : 0;
+      if (AGG & FW_AGG_SUM) {
+        if (VT == FW_VALUE_I64) G(s.c.sum)[idx] = jadd(o_sum, lsum[xl]);
+        else G(s.c.sum)[idx] = __double_as_longlong(__longlong_as_double(o_sum) + __longlong_as_double(lsum[xl]));
+      }
+      if (AGG & FW_AGG_MIN) { if (lmin[xl] < o_mn) G(s.c.mn)[idx] = lmin[xl]; }
+      if (AGG & FW_AGG_MAX) { if (lmax[xl] > o_mx) G(s.c.mx)[idx] = lmax[xl]; }
+      if (AGG & FW_AGG_COUNT) G(s.c.cnt)[idx] = jadd(o_cnt, lcnt[xl]);
+      if (FIRST) {
+        // first arrival: the pane's earliest record of the batch, if the pane is new
+        if (ord_base + (int64_t)lf < o_first) {
+          G(s.c.first)[idx] = ord_base + (int64_t)lf;
+          G(s.c.f1v)[idx] = f1n;
+        }
+      } else {
+        G(s.c.present)[idx] = 1;
+      }
       } else {
       if (AGG & FW_AGG_SUM) {
-        if (VT == FW_VALUE_I64) s.c.sum[idx] = jadd(s.c.sum[idx], lsum[xl]);
-        else s.c.sum[idx] = __double_as_longlong(__longlong_as_double(s.c.sum[idx]) + __longlong_as_double(lsum[xl]));
+        if (VT == FW_VALUE_I64) G(s.c.sum)[idx] = jadd(G(s.c.sum)[idx], lsum[xl]);
+        else G(s.c.sum)[idx] = __double_as_longlong(__longlong_as_double(G(s.c.sum)[idx]) + __longlong_as_double(lsum[xl]));
       }
-      if (AGG & FW_AGG_MIN) { const int64_t o = s.c.mn[idx]; if (lmin[xl] < o) s.c.mn[idx] = lmin[xl]; }
-      if (AGG & FW_AGG_MAX) { const int64_t o = s.c.mx[idx]; if (lmax[xl] > o) s.c.mx[idx] = lmax[xl]; }
-      if (AGG & FW_AGG_COUNT) s.c.cnt[idx] = jadd(s.c.cnt[idx], lcnt[xl]);
-      if (BY) {
+      if (AGG & FW_AGG_MIN) { const int64_t o = G(s.c.mn)[idx]; if (lmin[xl] < o) G(s.c.mn)[idx] = lmin[xl]; }
+      if (AGG & FW_AGG_MAX) { const int64_t o = G(s.c.mx)[idx]; if (lmax[xl] > o) G(s.c.mx)[idx] = lmax[xl]; }
+      if (AGG & FW_AGG_COUNT) G(s.c.cnt)[idx] = jadd(G(s.c.cnt)[idx], lcnt[xl]);
+      {   // BY
         // the batch's extremal record against the pane's (an earlier arrival: a tie keeps it under
         // "first", takes the batch's under "last"); its ordinal in the count column, its f1 in f1v
-        int64_t* col = MAXBY ? s.c.mx : s.c.mn;
+        auto col = G(MAXBY ? s.c.mx : s.c.mn);
         const int64_t code = MAXBY ? lmax[xl] : lmin[xl];
         const uint32_t lo = lord[xl];
         const int64_t cur = col[idx];
-        const bool present = s.c.first[idx] != INT64_MAX;
+        const bool present = G(s.c.first)[idx] != INT64_MAX;
         if (!present || (MAXBY ? code > cur : code < cur) || (code == cur && by_last)) {
           col[idx] = code;
-          s.c.cnt[idx] = ord_base + (int64_t)lo;
-          s.c.f1v[idx] = f1col[lo];
+          G(s.c.cnt)[idx] = ord_base + (int64_t)lo;
+          G(s.c.f1v)[idx] = f1col[lo];
         }
-        if (ord_base + (int64_t)lf < s.c.first[idx]) s.c.first[idx] = ord_base + (int64_t)lf;
+        if (ord_base + (int64_t)lf < G(s.c.first)[idx]) G(s.c.first)[idx] = ord_base + (int64_t)lf;
         lord[xl] = by_last ? 0u : NO_FIRST;
-      } else if (FIRST) {
-        // first arrival: the pane's earliest record of the batch, if the pane is new
-        if (ord_base + (int64_t)lf < s.c.first[idx]) {
-          s.c.first[idx] = ord_base + (int64_t)lf;
-          s.c.f1v[idx] = f1col[lf];
-        }
-      } else {
-        s.c.present[idx] = 1;
       }
       }   // !afold
       // cleared for the next round (untouched entries still are; the per-lane dummies are never read)
@@ -2764,6 +2911,17 @@ __global__ __launch_bounds__(CP_THREADS) void k_compact(Spec s, unsigned char* k
       for (int y = threadIdx.x; y < KB; y += CP_THREADS) c[y] = inv[y] >= 0 ? tmp[inv[y]] : INT64_MAX;
       __syncthreads();
     }
+  // re-arm marks of restored disarmed windows (tumbling: by slice slot, sliding: by window-pane slot; W = P): a
+  // key's mark moves with its key id, or the window would fire for whichever key took the old id
+  if (s.armed && s.disarm)
+    for (int p = 0; p < s.P; ++p) {   // uniform
+      if (!s.disarm[p]) continue;
+      uint8_t* c = s.armed + (int64_t)p * s.stride + dbase;
+      for (int x = threadIdx.x; x < KB; x += CP_THREADS) tmp[x] = c[x];
+      __syncthreads();
+      for (int y = threadIdx.x; y < KB; y += CP_THREADS) c[y] = inv[y] >= 0 ? (uint8_t)tmp[inv[y]] : 0;
+      __syncthreads();
+    }
   if (s.c.sum) move(s.c.sum, sum_identity(s.vt));
   if (s.c.mn) move(s.c.mn, INT64_MAX);
   if (s.c.mx) move(s.c.mx, INT64_MIN);
@@ -3485,7 +3643,10 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, (size_t)e->agg_min_lds);
   hipStream_t rs = e->serial ? e->stream : e->rstream;
   e->phase_begin(FW_PHASE_INGEST, rs);
-  hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, rs, e->s_dev, b, r);
+  const Spec& sp = e->s;
+  const RouteSpec q{sp.assigner, sp.K, sp.R, sp.mp, sp.kg_start, sp.kg_end, sp.mp_mask, sp.kb_bits, sp.nb,
+                    sp.size, sp.slide, sp.offset, sp.lateness, sp.g, sp.inv_size, sp.inv_g, sp.dir_mask, sp.err, sp.stats};
+  hipLaunchKernelGGL((k_route<VT, AGG, FIRST>), dim3(r.ntiles), dim3(RT_THREADS), e->route_lds, rs, e->s_dev, q, b, r);
   e->phase_end(b.n, rs);
   (void)hipEventRecord(e->ev_route[par], rs);
   (void)hipStreamWaitEvent(e->stream, e->ev_route[par], 0);

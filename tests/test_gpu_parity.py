@@ -436,6 +436,43 @@ def test_partition_by_operator_matches_key_group_routing(hip):
     e.close()
 
 
+@pytest.mark.parametrize("last", range(8))
+def test_partition_by_operator_last_rotated_order(hip, last):
+    """fw_partition_by_operator_last at parallelism 8 (the keyBy exchange's form, keyby.py): destinations in the
+    rotated order last+1 .. 7, 0 .. last (keyby.py _dest_order), each stable, counts indexed by operator and
+    offsets[d] the start of operator d's run; keys routed by KeyGroupStreamPartitioner (maxParallelism 128)."""
+    import ctypes
+    import torch
+    from flink_amd.keygroups import operator_index_np
+    from flink_amd.windowing import TumblingEventTimeWindows
+    e = hip(_cfg(TumblingEventTimeWindows.of(1000)))
+    keys, ts, vals = gen_stream(70_001 + 37 * last, 1 << 20, rate=1 << 14, seed=3 + last)
+    d = {n: torch.from_numpy(a).cuda() for n, a in (("k", keys), ("t", ts), ("v", vals))}
+    ok, ot, ov = (torch.empty_like(d["k"]) for _ in range(3))
+    counts = torch.zeros(8, dtype=torch.int64, device="cuda")
+    offs = torch.zeros(8, dtype=torch.int64, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    rc = e.lib.fw_partition_by_operator_last(e.h, P(d["k"]), None, None, P(d["t"]), P(d["v"]), len(keys), 128, 8,
+                                             P(ok), None, None, P(ot), P(ov), P(counts), P(offs), last)
+    assert rc == 0
+    e.sync()
+    dest = operator_index_np(keys, 128, 8)
+    rank = (dest - (last + 1)) % 8            # position of each destination in the rotated order
+    order = np.argsort(rank, kind="stable")
+    assert np.array_equal(ok.cpu().numpy(), keys[order])
+    assert np.array_equal(ot.cpu().numpy(), ts[order])
+    assert np.array_equal(ov.cpu().numpy(), vals[order])
+    cnt = np.bincount(dest, minlength=8)
+    assert np.array_equal(counts.cpu().numpy(), cnt)
+    rot = [(last + 1 + i) % 8 for i in range(8)]
+    start, want = 0, np.zeros(8, np.int64)
+    for dd in rot:
+        want[dd] = start
+        start += cnt[dd]
+    assert np.array_equal(offs.cpu().numpy(), want)
+    e.close()
+
+
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
 def test_host_buffers_reusable_after_push(hip, oracle_engine, mode, pinned):

@@ -38,6 +38,10 @@ for j in range(6):
     e.lib.fw_debug_stamps(e.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), buf.size)
     sk, d, span = phases(buf, B // 4096, 5)
     print(f"batch {j} route: start-skew {sk:.0f} ns, load {d[0]:.0f} phaseB {d[1]:.0f} scan {d[2]:.0f} write {d[3]:.0f} | span {span:.0f} ns")
+    rs = buf[: (B // 4096) * 8].reshape(-1, 8).astype(np.float64)
+    if rs[:, 5].any():   # inside phase B (ns from stamp 1): per-record pass, slow path, bins + ranks
+        print("      phaseB split: records %.0f slow %.0f bins %.0f rest %.0f" % tuple(
+            (np.diff(rs[:, [1, 5, 6, 7, 2]], axis=1) * 10.0).mean(axis=0)))
     nagg = 256
     if os.environ.get("STAMP_HELPERS"):   # owners + helper shares (blocks past 256 that ran)
         a = buf[8 << 16:].reshape(-1, 8)
@@ -49,6 +53,10 @@ for j in range(6):
         t0 = a[:nagg, 0][a[:nagg, 0] > 0].min()
         for b in top[:4]:   # every stamp of the block, ns from the kernel's first stamp (0 = not reached)
             print(f"        block {int(b)}:", [int((x - t0) * 10) if x else 0 for x in a[b]])
+    ag = buf[8 << 16:][: nagg * 8].reshape(-1, 8).astype(np.float64)
+    if ag[:, 5].any() and ag[:, 7].any():   # inside the segment-table phase (ns from stamp 1)
+        print("      segtab split: decide %.0f gsl+barrier %.0f g0 %.0f rest %.0f" % tuple(
+            (np.diff(ag[:, [1, 5, 6, 7, 2]], axis=1) * 10.0).mean(axis=0)))
     sk, d, span = phases(buf[8 << 16:], nagg, 5)
     print(f"        aggregate: start-skew {sk:.0f} ns, ldir {d[0]:.0f} segtab {d[1]:.0f} main {d[2]:.0f} fold {d[3]:.0f} | span {span:.0f} ns")
     e.advance_watermark(int(t.max().item()) - (50 if C4 else 1))
