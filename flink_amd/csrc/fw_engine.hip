@@ -674,6 +674,9 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 // 12-B records measured slower: the per-record probe of the global directory cost k_route more than the
 // 6 B/event it saved)
 // ------------------------------------------------------------------------------------------------
+#ifndef FW_NBUF
+#define FW_NBUF 3   // routed-batch buffer sets (fw_engine::NBUF)
+#endif
 #ifndef FW_AGG_UNCOND
 #define FW_AGG_UNCOND 1   // k_aggregate: the next group's loads issued without a branch (A/B switch)
 #endif
@@ -3298,7 +3301,7 @@ struct fw_engine {
   // routed batches rotate over NBUF buffer sets: k_route of batch j waits only for k_aggregate of batch
   // j - NBUF, long finished, so neither stream waits on the other's latest kernel (a cross-stream wait costs
   // ~13 us of signal latency on MI355X, measured: profiles/r02_v13_timeline.txt)
-  static constexpr int NBUF = 3;
+  static constexpr int NBUF = FW_NBUF;
   hipEvent_t ev_route[NBUF] = {};     // k_route of the batch using that buffer set done
   hipEvent_t ev_agg[NBUF] = {};       // k_aggregate of the batch using that buffer set done
   Spec s{};

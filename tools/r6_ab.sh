@@ -5,8 +5,10 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp; mkdir -p gpurun_out
 CFG=${CFG:-c1}
 for rep in ${REPS:-1 2 3}; do
   for v in ${LIBS:-main base}; do
-    [ "$v" = main ] && path=flink_amd/lib/libflink_window.so || path=flink_amd/lib/$v/libflink_window.so
-    FW_LIBRARY=$PWD/$path timeout -k 10 180 python3 bench.py --config $CFG --steps ${STEPS:-20} --warmup 5 --cpu-sample 0 --decode-steps 0 --drain-steps 0 --h2d-steps 0 > gpurun_out/ab_${v}_$rep.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/ab_${v}_$rep.log; exit 1; }
+    lib=${v%%:*}; envs=""; [ "$lib" != "$v" ] && envs=${v#*:}   # "lib:VAR=value" runs lib with that variable set
+    [ "$lib" = main ] && path=flink_amd/lib/libflink_window.so || path=flink_amd/lib/$lib/libflink_window.so
+    v=$(echo "$v" | tr ':=/' '___')
+    env $envs FW_LIBRARY=$PWD/$path timeout -k 10 180 python3 bench.py --config $CFG --steps ${STEPS:-20} --warmup 5 --cpu-sample 0 --decode-steps 0 --drain-steps 0 --h2d-steps 0 > gpurun_out/ab_${v}_$rep.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/ab_${v}_$rep.log; exit 1; }
     python3 - gpurun_out/ab_${v}_$rep.log $v <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
