@@ -144,6 +144,7 @@ struct Spec {  // window specification + reduce + subtask, passed by value
   // (0 without first-arrival tracking), INT64_MAX = none; the timers' only trace, written to checkpoints.  Null else
   int64_t* gtag;
   int64_t* gfirst;
+  long long* wm_stamps;   // diagnostics (FW_DEBUG_AGG & 16): k_watermark phase timestamps, 8 per workgroup; null else
 };
 
 // the Spec fields k_route's per-record work reads, passed by value (kernel arguments, in SGPRs from the wave's start;
@@ -2604,6 +2605,8 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   __shared__ int32_t wtot[WM_THREADS / 64];
   __shared__ unsigned long long base;
   __shared__ unsigned long long fired;
+#define WM_STAMP(k) do { if (s.wm_stamps && threadIdx.x == 0) s.wm_stamps[(int64_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  WM_STAMP(0);
   if (threadIdx.x == 0) { n_tasks = 0; n_purge = 0; n_wpurge = 0; last = 0; fired = 0; }
   for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) tags[p] = s.slice_tag[p];
   // key ids scanned: the null key's id D only while it is in use (D = 2^k ids fill 2^k / 1024 workgroups
@@ -2611,27 +2614,45 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
   if (threadIdx.x == 0) nkid_s = s.dir_min_used[0] ? s.stride : s.D;
   __syncthreads();
   const int64_t nkid = nkid_s;
-  for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) {
+  // one thread per (slot, window of its slice) pair, not one per slot looping over its windows (a serial chain of
+  // K windows x up to K owner checks per thread: the plan took 7-8 us per fire at C3's K = 10, round 6)
+  // (tumbling, K = 1: a slot's one window in the purge loop below, no pair loop)
+  const int32_t nw = (s.K + s.R - 1) / s.R + 1;   // windows of one slice, at most
+  for (int32_t x = threadIdx.x; s.K > 1 && x < s.P * nw; x += WM_THREADS) {
+    const int32_t p = x / nw, j = x - p * nw;
     const int64_t m = tags[p];
     if (m == FREE_TAG) continue;
     const int64_t n_hi = s.R == 1 ? m : floor_div(m, s.R);   // (64-bit divides: ~100 instructions each)
     const int64_t n_lo = s.R == 1 ? m - s.K + 1 : floor_div(m - s.K, s.R) + 1;
+    const int64_t n = n_hi - j;
+    if (n < n_lo) continue;
+    const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
+    const bool fires = max_ts > wm_old && max_ts <= wm_new;
+    if (!fires) continue;
+    bool owner = true;                                                    // first live slice of window n
+    int32_t pp = (int32_t)floor_mod(n * s.R, s.P);
+    for (int64_t mm = n * s.R; mm < m; ++mm) {
+      if (tags[pp] == mm) { owner = false; break; }
+      pp = pp + 1 == s.P ? 0 : pp + 1;
+    }
+    if (!owner) continue;
+    const int32_t t = atomicAdd(&n_tasks, 1);
+    if (t < maxt) task_n[t] = n;
+    else cap_error(s, 12);
+  }
+  for (int32_t p = threadIdx.x; p < s.P; p += WM_THREADS) {
+    const int64_t m = tags[p];
+    if (m == FREE_TAG) continue;
+    const int64_t n_hi = s.R == 1 ? m : floor_div(m, s.R);
     bool purge_now = false, fire_purge = false;
-    for (int64_t n = n_lo; n <= n_hi; ++n) {
-      const int64_t max_ts = jsub(jadd(window_start_n(s, n), s.size), 1);
-      const bool fires = max_ts > wm_old && max_ts <= wm_new;
-      if (!fires) continue;
-      if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) purge_now = fire_purge = true;   // the slice is the window
-      bool owner = true;                                                    // first live slice of window n
-      int32_t pp = (int32_t)floor_mod(n * s.R, s.P);
-      for (int64_t mm = n * s.R; mm < m; ++mm) {
-        if (tags[pp] == mm) { owner = false; break; }
-        pp = pp + 1 == s.P ? 0 : pp + 1;
+    if (s.K == 1 && n_hi * s.R == m) {   // tumbling (and K = 1 sliding): the slice is the window, its task here
+      const int64_t max_ts = jsub(jadd(window_start_n(s, n_hi), s.size), 1);
+      if (max_ts > wm_old && max_ts <= wm_new) {
+        if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) purge_now = fire_purge = true;
+        const int32_t t = atomicAdd(&n_tasks, 1);
+        if (t < maxt) task_n[t] = n_hi;
+        else cap_error(s, 12);
       }
-      if (!owner) continue;
-      const int32_t t = atomicAdd(&n_tasks, 1);
-      if (t < maxt) task_n[t] = n;
-      else cap_error(s, 12);
     }
     const int64_t ct = cleanup_time(jsub(jadd(window_start_n(s, n_hi), s.size), 1), s.lateness);
     if (ct <= wm_new) purge_now = true;
@@ -2663,6 +2684,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     }
   }
   __syncthreads();
+  WM_STAMP(1);
   const int32_t nt = min(n_tasks, maxt), np = min(n_purge, s.P), nwp = min(n_wpurge, s.W);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t gstride = (int64_t)gridDim.x * WM_THREADS;
@@ -2753,6 +2775,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     }
     __syncthreads();
   }
+  WM_STAMP(2);
   // purge this workgroup's share of the expired slices (it fired that share above; clearing each pane as the
   // fire reads it writes partial column lines and measured slower beside the next batch's kernels)
   for (int32_t q = 0; q < np; ++q) {
@@ -2780,6 +2803,7 @@ __global__ __launch_bounds__(WM_THREADS) void k_watermark(Spec s, int64_t wm_old
     }
   }
   __syncthreads();
+  WM_STAMP(3);
   if (threadIdx.x == 0) {
     if (fired) atomicAdd(&s.stats[ST_FIRED], fired);
     last = atomicAdd(done, 1u) == gridDim.x - 1;   // issued after this workgroup's appends returned
@@ -3966,6 +3990,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
       const char* dbg = getenv("FW_DEBUG_AGG");
       e->rb.dbg = dbg ? atoi(dbg) : 0;
       e->rb.stamps = (e->rb.dbg & 16) ? e->alloc<long long>((size_t)16 << 16) : nullptr;
+      e->s.wm_stamps = e->rb.stamps ? e->rb.stamps + ((size_t)12 << 16) : nullptr;
       e->dflags = e->alloc<unsigned int>(FLAG_RING);
       e->bload = e->alloc<unsigned int>(4 * RT_MAXNB);
       e->fold_flag = e->alloc<unsigned int>((size_t)5 * RT_MAXNB * RT_GS);   // flags, then the 4-entry count ring
