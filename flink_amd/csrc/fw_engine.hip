@@ -2371,6 +2371,13 @@ __device__ __forceinline__ LfPart lf_get(const LfPart* src) {
     b[w] = __hip_atomic_load((unsigned long long*)(a + w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return r;
 }
+// Ordering of the carries (target-dependent, gfx94x / gfx950 only): a tile's data is written with
+// agent-scope relaxed atomic stores (write-through past the XCD's non-coherent L2), lf_raise waits for their
+// acknowledgement (s_waitcnt vmcnt(0)) before the agent-scope flag store, and a reader issues its agent-scope
+// relaxed atomic data loads only after its flag load returned the new value (control dependency, loads issued in
+// order and served at the coherence point).  The C++ model would want acquire on the flag load; on these targets an
+// agent-scope acquire adds a cache invalidate per look-back step and buys nothing the atomics do not already give.
+// Porting this kernel to another target means making the flag load an acquire.
 __device__ __forceinline__ void lf_raise(unsigned int* flag, unsigned int v) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the data's stores acknowledged first
   __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -298,12 +298,23 @@ class KeyByExchange:
         self.finished += 1
         sk, st, sv = self.send[si]
         if n + m > sk.numel():   # skew: more received than the set has room for behind the batch
-            self.eng.sync()      # (nothing reads the old set once the engine is idle)
+            self.eng.sync()      # (nothing reads the old sets once the engine is idle)
+            if self.cuda:        # (the partitions of the staged batches ran on this stream)
+                torch.cuda.current_stream(self.device).synchronize()
+            # every set grows to the new capacity at once: one engine sync per growth event, not one per
+            # set as each meets the skew in turn; a set keeps the partitioned batch still staged in it
             cap = self._set_cap(n + m)
-            grown = [torch.empty(cap, dtype=torch.int64, device=self.device) for _ in range(3)]
-            for g, x in zip(grown, (sk, st, sv)):
-                g[:n].copy_(x[:n])
-            self.send[si] = tuple(grown)
+            staged = {sj: nj for sj, nj in self.pending}
+            staged[si] = n
+            for sj in range(len(self.send)):
+                old = self.send[sj]
+                if old[0].numel() >= cap:
+                    continue
+                grown = [torch.empty(cap, dtype=torch.int64, device=self.device) for _ in range(3)]
+                keep = staged.get(sj, 0)
+                for g, x in zip(grown, old):
+                    g[:keep].copy_(x[:keep])
+                self.send[sj] = tuple(grown)
             sk, st, sv = self.send[si]
         # the peers' shares land right behind the own share (the last destination of the partition's order)
         recv = (sk[n:n + m], st[n:n + m], sv[n:n + m])
