@@ -159,6 +159,19 @@ struct RouteSpec {
   unsigned long long* stats;
 };
 
+// the Spec fields k_aggregate reads, by value (kernel arguments: in SGPRs from the wave's start, where the
+// device Spec's fields were scalar loads waited on at the prologue and at each slice's claim, round 6)
+struct AggSpec {
+  int32_t nb, kb_bits, P, by_last, cmpto;
+  int64_t stride, D;
+  int64_t* dir_keys;
+  int64_t* slice_tag;
+  int32_t* dir_min_used;
+  int32_t* err;
+  unsigned long long* stats;
+  Cols c;
+};
+
 __device__ __forceinline__ void set_error(int32_t* err, int32_t code) { atomicCAS(err, 0, code); }
 // a capacity error, with the id of the site that raised it first (fw_debug_counters word 7: diagnostics)
 #define cap_error(s, site) do { set_error((s).err, FW_ERR_CAPACITY); \
@@ -1221,7 +1234,7 @@ __host__ __device__ constexpr size_t agg_lds_bytes(int kb_bits, int nacc, int64_
 // for helpers): hot buckets split over helper workgroups, and the in-wave hot-key combine.  The uniform
 // variant carries neither (registers: the 1024-thread workgroup has 128 VGPRs per lane)
 template <int VT, int AGG, bool FIRST, bool SKEW>
-__global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict__ sd, BatchIn b, RouteBuf r, const int64_t* f1col) {
+__global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict__ sd, AggSpec sa, BatchIn b, RouteBuf r, const int64_t* f1col) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Spec& s = *sd;   // device copy (kernel arguments by value are held in scalar registers from entry)
   constexpr int NT = AG_THREADS;
@@ -1233,11 +1246,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
   // of waiting for an owner's CU; vb is the block's index in the owners-then-helpers numbering
   constexpr bool HELPERS_FIRST = SKEW && VT == FW_VALUE_I64 && !(AGG & (FW_AGG_MAXBY | FW_AGG_MINBY));
   const int H = HELPERS_FIRST ? r.helpers : 0;
-  const int vb = (int)blockIdx.x < H ? s.nb + (int)blockIdx.x : (int)blockIdx.x - H;
-  int owner_bkt = vb >= s.nb ? -1
-                        : (s.nb % 8 == 0 && !(r.dbg & 32)) ? (vb % 8) * (s.nb / 8) + vb / 8
+  const int vb = (int)blockIdx.x < H ? sa.nb + (int)blockIdx.x : (int)blockIdx.x - H;
+  int owner_bkt = vb >= sa.nb ? -1
+                        : (sa.nb % 8 == 0 && !(r.dbg & 32)) ? (vb % 8) * (sa.nb / 8) + vb / 8
                                                           : vb;
-  const int KB = 1 << s.kb_bits;
+  const int KB = 1 << sa.kb_bits;
   const uint32_t kbm = (uint32_t)KB - 1;
   const int KA = KB + 65;                               // accumulators: KB slots, one dummy per lane, the MIN key
   const uint32_t KMIN = (uint32_t)KB + 64;              // slot of the Long.MIN_VALUE key (kid D, bucket 0)
@@ -1274,7 +1287,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
   int bkt = owner_bkt, share = 0, nshare = 1;
   if (SKEW && r.helpers > 0) {   // uniform
     uint32_t tot = 0;
-    for (int x = threadIdx.x; x < s.nb; x += NT) tot += r.bload_prev[x];
+    for (int x = threadIdx.x; x < sa.nb; x += NT) tot += r.bload_prev[x];
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     if ((threadIdx.x & 63) == 0) awtot[threadIdx.x >> 6] = (int32_t)tot;
     __syncthreads();
@@ -1282,26 +1295,26 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
     for (int w = 0; w < NT / 64; ++w) all += (uint32_t)awtot[w];
     // (FW_DEBUG_AGG & 64: a share of 256 records, so that tests split buckets at small sizes)
     const uint32_t chunk = max((r.dbg & 64) ? 256u : AG_SPLIT_MIN,
-                               (uint32_t)(((uint64_t)(all / (uint32_t)s.nb + 1u) * (uint32_t)r.chunk_pct) / 100u));
-    for (int x = threadIdx.x; x < s.nb; x += NT) {
+                               (uint32_t)(((uint64_t)(all / (uint32_t)sa.nb + 1u) * (uint32_t)r.chunk_pct) / 100u));
+    for (int x = threadIdx.x; x < sa.nb; x += NT) {
       const uint32_t sh = min((r.bload_prev[x] + chunk - 1) / chunk, (uint32_t)r.split_max);
       plan[x] = sh > 1 ? (int32_t)sh - 1 : 0;    // helpers bucket x asks for
     }
-    if (threadIdx.x == 0) plan[s.nb] = 0;
+    if (threadIdx.x == 0) plan[sa.nb] = 0;
     __syncthreads();
-    block_scan_excl<NT, AG_MAXPER>(plan, s.nb + 1, awtot);   // plan[x] = first helper of bucket x; plan[nb] = total
+    block_scan_excl<NT, AG_MAXPER>(plan, sa.nb + 1, awtot);   // plan[x] = first helper of bucket x; plan[nb] = total
     // integer shares: owners are dispatched longest share first (owner vb takes the bucket whose share holds
     // the vb-th most records, ties by bucket), so the workgroups that wait for a CU to free up are the
     // shortest ones.  Every workgroup ranks the same loads: a permutation of the buckets.  (FW_DEBUG_AGG &
     // 128: the plain order.)
     if (HELPERS_FIRST && owner_bkt >= 0 && !(r.dbg & 128)) {   // uniform
-      for (int x = threadIdx.x; x < s.nb; x += NT)
+      for (int x = threadIdx.x; x < sa.nb; x += NT)
         step_tile[x] = (int32_t)(r.bload_prev[x] / (uint32_t)(1 + max(min(plan[x + 1], r.helpers) - plan[x], 0)));
       __syncthreads();
-      for (int x = threadIdx.x; x < s.nb; x += NT) {
+      for (int x = threadIdx.x; x < sa.nb; x += NT) {
         const int32_t wx = step_tile[x];
         int rk = 0;
-        for (int y = 0; y < s.nb; ++y) {
+        for (int y = 0; y < sa.nb; ++y) {
           const int32_t wy = step_tile[y];
           rk += (wy > wx || (wy == wx && y < x)) ? 1 : 0;
         }
@@ -1311,10 +1324,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
       owner_bkt = plan[RT_MAXNB + 1];
       __syncthreads();
     }
-    const int32_t h = owner_bkt < 0 ? (int32_t)vb - s.nb : -1;
+    const int32_t h = owner_bkt < 0 ? (int32_t)vb - sa.nb : -1;
     if (threadIdx.x == 0) plan[RT_MAXNB + 1] = owner_bkt < 0 ? -1 : owner_bkt;
     __syncthreads();
-    for (int x = threadIdx.x; x < s.nb; x += NT) {
+    for (int x = threadIdx.x; x < sa.nb; x += NT) {
       const int32_t lo = plan[x], n = max(min(plan[x + 1], r.helpers) - lo, 0);   // helpers bucket x gets
       if (h >= lo && h < lo + n) { plan[RT_MAXNB + 1] = x; plan[RT_MAXNB + 2] = h - lo + 1; plan[RT_MAXNB + 3] = 1 + n; }
       if (x == owner_bkt) { plan[RT_MAXNB + 2] = 0; plan[RT_MAXNB + 3] = 1 + n; }
@@ -1337,7 +1350,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
   // bucket's rows of the bucket-major segment table are contiguous; a row's word is used only where the tile
   // wrote it (a live routed group; the direct / fire groups of a tile with direct records, read in a second
   // round trip by those tiles only)
-  const int64_t dk0 = (int)threadIdx.x < KB ? G(s.dir_keys)[dbase + threadIdx.x] : EMPTY_KEY;
+  const int64_t dk0 = (int)threadIdx.x < KB ? G(sa.dir_keys)[dbase + threadIdx.x] : EMPTY_KEY;
   const unsigned int dfl = *r.dflag;
   // one-slice batches (the usual in-order batch: every tile routed one slice, the same, into group 0, and no tile
   // has direct records) need no slice set and no separate segment scan: with at most one tile per thread, each
@@ -1353,13 +1366,13 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q) h[q] = r.hdr[(int64_t)t * RT_Q + q];
 #pragma unroll
-    for (int q = 0; q < RT_Q; ++q) sg[q] = r.seg[(int64_t)(q * s.nb + bkt) * r.seg_stride + t];
+    for (int q = 0; q < RT_Q; ++q) sg[q] = r.seg[(int64_t)(q * sa.nb + bkt) * r.seg_stride + t];
     const uint32_t td = r.tdir[t];
 #pragma unroll
     for (int q = RT_Q; q < RT_GROUPS; ++q) sg[q] = 0u;
     if (td != 0u) {
 #pragma unroll
-      for (int q = RT_Q; q < RT_GROUPS; ++q) sg[q] = r.seg[(int64_t)(q * s.nb + bkt) * r.seg_stride + t];
+      for (int q = RT_Q; q < RT_GROUPS; ++q) sg[q] = r.seg[(int64_t)(q * sa.nb + bkt) * r.seg_stride + t];
     }
 #pragma unroll
     for (int q = 0; q < RT_Q; ++q)
@@ -1392,7 +1405,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
     if ((threadIdx.x & 63) == 0) { wsl[threadIdx.x >> 6] = wm; wok[threadIdx.x >> 6] = ok ? 1 : 0; }
   }
   if ((int)threadIdx.x < KB) lh[threadIdx.x] = fmix64((uint64_t)dk0);
-  for (int x = threadIdx.x + NT; x < KB; x += NT) lh[x] = fmix64((uint64_t)G(s.dir_keys)[dbase + x]);
+  for (int x = threadIdx.x + NT; x < KB; x += NT) lh[x] = fmix64((uint64_t)G(sa.dir_keys)[dbase + x]);
   if (threadIdx.x < AG_LOOK) off[r.ntiles + 1 + threadIdx.x] = INT32_MAX;
   for (int x = threadIdx.x; x < KA; x += NT) {
     lsum[x] = sum_identity(VT);
@@ -1400,10 +1413,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
     if (HAS_MAX) lmax[x] = INT64_MIN;
     if (AGG & FW_AGG_COUNT) lcnt[x] = 0;
     lfirst[x] = NO_FIRST;
-    if (BY) lord[x] = s.by_last ? 0u : NO_FIRST;
+    if (BY) lord[x] = sa.by_last ? 0u : NO_FIRST;
   }
   const AggLds L{lsum, lmin, lmax, lcnt, lfirst, lord};
-  const bool cmpto = s.cmpto != 0, by_last = s.by_last != 0;
+  const bool cmpto = sa.cmpto != 0, by_last = sa.by_last != 0;
   if (threadIdx.x < RT_GS) gsl[threadIdx.x] = FREE_TAG;
   __syncthreads();
   FW_STAMP(r, SB, 1);
@@ -1451,7 +1464,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
         if ((int64_t)prev == FREE_TAG || (int64_t)prev == m) break;
       }
     }
-    if (g == RT_GS) cap_error(s, 6);   // more distinct slices in one batch than RT_GS
+    if (g == RT_GS) cap_error(sa, 6);   // more distinct slices in one batch than RT_GS
   };
   // this bucket's direct-group records (one tile per thread): per-element fires join the late list
   // (k_late_* apply them after this kernel, in arrival order); the others are added in the round of
@@ -1489,15 +1502,15 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
         const int64_t i = (int64_t)t * RT_TILE + r.idx[pos];
         const uint64_t h = (uint64_t)r.kv[pos].x;
         const int64_t m = r.dm[pos];
-        int32_t p = slice_slot_body(s.slice_tag, s.P, m);
-        int64_t kid = s.D;
+        int32_t p = slice_slot_body(sa.slice_tag, sa.P, m);
+        int64_t kid = sa.D;
         if (h == EMPTY_H) {   // marks the Long.MIN_VALUE key's column in use
-          if (s.dir_min_used[0] == 0) s.dir_min_used[0] = 1;
+          if (sa.dir_min_used[0] == 0) sa.dir_min_used[0] = 1;
         } else {
-          const int32_t x2 = agg_probe_insert_body(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
+          const int32_t x2 = agg_probe_insert_body(lh, sa.dir_keys + dbase, kbm, h, sa.stats + ST_DIR_KEYS);
           kid = x2 < 0 ? -1 : dbase + x2;
         }
-        if (p < 0 || kid < 0) { cap_error(s, 7); p = 0; kid = 0; }   // (a failed batch: a harmless entry keeps the slot)
+        if (p < 0 || kid < 0) { cap_error(sa, 7); p = 0; kid = 0; }   // (a failed batch: a harmless entry keeps the slot)
         late_append_at(s, b, lbase + (unsigned long long)j, p, kid, m, i);
       }
     }
@@ -1552,8 +1565,8 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
       }
       const bool miss2 = miss && !found2;
       if (__any(miss2) && miss2) {
-        const int32_t x = agg_probe_insert_body(lh, s.dir_keys + dbase, kbm, h, s.stats + ST_DIR_KEYS);
-        if (x < 0) { cap_error(s, 8); act = false; }
+        const int32_t x = agg_probe_insert_body(lh, sa.dir_keys + dbase, kbm, h, sa.stats + ST_DIR_KEYS);
+        if (x < 0) { cap_error(sa, 8); act = false; }
         else kl = (uint32_t)x;
       }
     }
@@ -1569,7 +1582,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
     // slot's tag is read now, its value used (and the slot claimed if free) at the fold: the load's latency
     // lies under the main loop instead of in front of it
     int64_t tagv = FREE_TAG;
-    if (threadIdx.x == 0) tagv = G(s.slice_tag)[floor_mod(m, s.P)];
+    if (threadIdx.x == 0) tagv = G(sa.slice_tag)[floor_mod(m, sa.P)];
     if (g == 0) FW_STAMP(r, SB, 7);
     for (int t = threadIdx.x; !uni && t < r.ntiles; t += NT) {   // (uni: offsets already in place)
       int32_t a0 = 0, a1 = 0;
@@ -1680,10 +1693,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
         const longlong2 rec = r.kv[pos];
         uint32_t kl = KMIN;
         if ((uint64_t)rec.x == EMPTY_H) {
-          if (s.dir_min_used[0] == 0) s.dir_min_used[0] = 1;   // marks the Long.MIN_VALUE key's column in use
+          if (sa.dir_min_used[0] == 0) sa.dir_min_used[0] = 1;   // marks the Long.MIN_VALUE key's column in use
         } else {
-          const int32_t x2 = agg_probe_insert_body(lh, s.dir_keys + dbase, kbm, (uint64_t)rec.x, s.stats + ST_DIR_KEYS);
-          if (x2 < 0) { cap_error(s, 10); continue; }
+          const int32_t x2 = agg_probe_insert_body(lh, sa.dir_keys + dbase, kbm, (uint64_t)rec.x, sa.stats + ST_DIR_KEYS);
+          if (x2 < 0) { cap_error(sa, 10); continue; }
           kl = (uint32_t)x2;
         }
         acc_add<VT, AGG>(L, cmpto, by_last, pass, kl, rec.y, (uint32_t)i);
@@ -1692,11 +1705,11 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
     __syncthreads();
     }   // passes
     FW_STAMP(r, SB, 3 + 3 * min(g, 1));
-    if (threadIdx.x == 0) lclaim = tagv == m ? (int32_t)floor_mod(m, s.P) : slice_slot_body(s.slice_tag, s.P, m);
+    if (threadIdx.x == 0) lclaim = tagv == m ? (int32_t)floor_mod(m, sa.P) : slice_slot_body(sa.slice_tag, sa.P, m);
     __syncthreads();
     const int32_t p = lclaim;
     __syncthreads();   // every thread has read lclaim (the next round rewrites it)
-    if (p < 0) { if (threadIdx.x == 0) cap_error(s, 9); continue; }   // slice pool exhausted (uniform)
+    if (p < 0) { if (threadIdx.x == 0) cap_error(sa, 9); continue; }   // slice pool exhausted (uniform)
     unsigned int* flag = r.fold_flag + (int64_t)bkt * RT_GS + g;
     // integer shares of a split bucket fold concurrently with device atomics (sum / count / min / max
     // are exact in any order, and the first arrival is the least batch index over the shares: the last
@@ -1709,7 +1722,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
         int64_t spins = 0;
         while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
           __builtin_amdgcn_s_sleep(8);
-          if (++spins > ((int64_t)1 << 21)) { cap_error(s, 16); break; }   // never hang: report and go on
+          if (++spins > ((int64_t)1 << 21)) { cap_error(sa, 16); break; }   // never hang: report and go on
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 invalidated once, for the workgroup
       }
@@ -1722,62 +1735,62 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
       const uint32_t xl = x < KB ? (uint32_t)x : KMIN;
       const uint32_t lf = lfirst[xl];
       if (lf == NO_FIRST) continue;
-      const int64_t idx = (int64_t)p * s.stride + (x < KB ? dbase + x : s.D);
+      const int64_t idx = (int64_t)p * sa.stride + (x < KB ? dbase + x : sa.D);
       if (AFOLD && afold) {
-        if (AGG & FW_AGG_SUM) atomicAdd((unsigned long long*)&s.c.sum[idx], (unsigned long long)lsum[xl]);
-        if (AGG & FW_AGG_MIN) atomicMin((long long*)&s.c.mn[idx], (long long)lmin[xl]);
-        if (AGG & FW_AGG_MAX) atomicMax((long long*)&s.c.mx[idx], (long long)lmax[xl]);
-        if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&s.c.cnt[idx], (unsigned long long)lcnt[xl]);
-        if (FIRST) atomicMin((long long*)&s.c.first[idx], (long long)(ord_base + (int64_t)lf));
-        else s.c.present[idx] = 1;
+        if (AGG & FW_AGG_SUM) atomicAdd((unsigned long long*)&sa.c.sum[idx], (unsigned long long)lsum[xl]);
+        if (AGG & FW_AGG_MIN) atomicMin((long long*)&sa.c.mn[idx], (long long)lmin[xl]);
+        if (AGG & FW_AGG_MAX) atomicMax((long long*)&sa.c.mx[idx], (long long)lmax[xl]);
+        if (AGG & FW_AGG_COUNT) atomicAdd((unsigned long long*)&sa.c.cnt[idx], (unsigned long long)lcnt[xl]);
+        if (FIRST) atomicMin((long long*)&sa.c.first[idx], (long long)(ord_base + (int64_t)lf));
+        else sa.c.present[idx] = 1;
       } else if (!BY) {
       // every column of the pane (and the f1 of the batch's earliest record, used if the pane is new) loaded
       // before any store: one round trip (as far as the compiler knows the columns may alias, so a store between
       // two loads made the second wait for it: three round trips per pane, round 6)
-      const int64_t o_sum = (AGG & FW_AGG_SUM) ? G(s.c.sum)[idx] : 0;
-      const int64_t o_mn = (AGG & FW_AGG_MIN) ? G(s.c.mn)[idx] : 0;
-      const int64_t o_mx = (AGG & FW_AGG_MAX) ? G(s.c.mx)[idx] : 0;
-      const int64_t o_cnt = (AGG & FW_AGG_COUNT) ? G(s.c.cnt)[idx] : 0;
-      const int64_t o_first = FIRST ? G(s.c.first)[idx] : 0;
+      const int64_t o_sum = (AGG & FW_AGG_SUM) ? G(sa.c.sum)[idx] : 0;
+      const int64_t o_mn = (AGG & FW_AGG_MIN) ? G(sa.c.mn)[idx] : 0;
+      const int64_t o_mx = (AGG & FW_AGG_MAX) ? G(sa.c.mx)[idx] : 0;
+      const int64_t o_cnt = (AGG & FW_AGG_COUNT) ? G(sa.c.cnt)[idx] : 0;
+      const int64_t o_first = FIRST ? G(sa.c.first)[idx] : 0;
       const int64_t f1n = FIRST ? f1col[lf] : 0;
       if (AGG & FW_AGG_SUM) {
-        if (VT == FW_VALUE_I64) G(s.c.sum)[idx] = jadd(o_sum, lsum[xl]);
-        else G(s.c.sum)[idx] = __double_as_longlong(__longlong_as_double(o_sum) + __longlong_as_double(lsum[xl]));
+        if (VT == FW_VALUE_I64) G(sa.c.sum)[idx] = jadd(o_sum, lsum[xl]);
+        else G(sa.c.sum)[idx] = __double_as_longlong(__longlong_as_double(o_sum) + __longlong_as_double(lsum[xl]));
       }
-      if (AGG & FW_AGG_MIN) { if (lmin[xl] < o_mn) G(s.c.mn)[idx] = lmin[xl]; }
-      if (AGG & FW_AGG_MAX) { if (lmax[xl] > o_mx) G(s.c.mx)[idx] = lmax[xl]; }
-      if (AGG & FW_AGG_COUNT) G(s.c.cnt)[idx] = jadd(o_cnt, lcnt[xl]);
+      if (AGG & FW_AGG_MIN) { if (lmin[xl] < o_mn) G(sa.c.mn)[idx] = lmin[xl]; }
+      if (AGG & FW_AGG_MAX) { if (lmax[xl] > o_mx) G(sa.c.mx)[idx] = lmax[xl]; }
+      if (AGG & FW_AGG_COUNT) G(sa.c.cnt)[idx] = jadd(o_cnt, lcnt[xl]);
       if (FIRST) {
         // first arrival: the pane's earliest record of the batch, if the pane is new
         if (ord_base + (int64_t)lf < o_first) {
-          G(s.c.first)[idx] = ord_base + (int64_t)lf;
-          G(s.c.f1v)[idx] = f1n;
+          G(sa.c.first)[idx] = ord_base + (int64_t)lf;
+          G(sa.c.f1v)[idx] = f1n;
         }
       } else {
-        G(s.c.present)[idx] = 1;
+        G(sa.c.present)[idx] = 1;
       }
       } else {
       if (AGG & FW_AGG_SUM) {
-        if (VT == FW_VALUE_I64) G(s.c.sum)[idx] = jadd(G(s.c.sum)[idx], lsum[xl]);
-        else G(s.c.sum)[idx] = __double_as_longlong(__longlong_as_double(G(s.c.sum)[idx]) + __longlong_as_double(lsum[xl]));
+        if (VT == FW_VALUE_I64) G(sa.c.sum)[idx] = jadd(G(sa.c.sum)[idx], lsum[xl]);
+        else G(sa.c.sum)[idx] = __double_as_longlong(__longlong_as_double(G(sa.c.sum)[idx]) + __longlong_as_double(lsum[xl]));
       }
-      if (AGG & FW_AGG_MIN) { const int64_t o = G(s.c.mn)[idx]; if (lmin[xl] < o) G(s.c.mn)[idx] = lmin[xl]; }
-      if (AGG & FW_AGG_MAX) { const int64_t o = G(s.c.mx)[idx]; if (lmax[xl] > o) G(s.c.mx)[idx] = lmax[xl]; }
-      if (AGG & FW_AGG_COUNT) G(s.c.cnt)[idx] = jadd(G(s.c.cnt)[idx], lcnt[xl]);
+      if (AGG & FW_AGG_MIN) { const int64_t o = G(sa.c.mn)[idx]; if (lmin[xl] < o) G(sa.c.mn)[idx] = lmin[xl]; }
+      if (AGG & FW_AGG_MAX) { const int64_t o = G(sa.c.mx)[idx]; if (lmax[xl] > o) G(sa.c.mx)[idx] = lmax[xl]; }
+      if (AGG & FW_AGG_COUNT) G(sa.c.cnt)[idx] = jadd(G(sa.c.cnt)[idx], lcnt[xl]);
       {   // BY
         // the batch's extremal record against the pane's (an earlier arrival: a tie keeps it under
         // "first", takes the batch's under "last"); its ordinal in the count column, its f1 in f1v
-        auto col = G(MAXBY ? s.c.mx : s.c.mn);
+        auto col = G(MAXBY ? sa.c.mx : sa.c.mn);
         const int64_t code = MAXBY ? lmax[xl] : lmin[xl];
         const uint32_t lo = lord[xl];
         const int64_t cur = col[idx];
-        const bool present = G(s.c.first)[idx] != INT64_MAX;
+        const bool present = G(sa.c.first)[idx] != INT64_MAX;
         if (!present || (MAXBY ? code > cur : code < cur) || (code == cur && by_last)) {
           col[idx] = code;
-          G(s.c.cnt)[idx] = ord_base + (int64_t)lo;
-          G(s.c.f1v)[idx] = f1col[lo];
+          G(sa.c.cnt)[idx] = ord_base + (int64_t)lo;
+          G(sa.c.f1v)[idx] = f1col[lo];
         }
-        if (ord_base + (int64_t)lf < G(s.c.first)[idx]) G(s.c.first)[idx] = ord_base + (int64_t)lf;
+        if (ord_base + (int64_t)lf < G(sa.c.first)[idx]) G(sa.c.first)[idx] = ord_base + (int64_t)lf;
         lord[xl] = by_last ? 0u : NO_FIRST;
       }
       }   // !afold
@@ -1804,10 +1817,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
       if (FIRST && lclaim) {   // uniform
         for (int x = threadIdx.x; x <= KB; x += NT) {
           if (x == KB && bkt != 0) continue;
-          const int64_t idx = (int64_t)p * s.stride + (x < KB ? dbase + x : s.D);
-          const int64_t f = (int64_t)__hip_atomic_fetch_add((unsigned long long*)&s.c.first[idx], 0ull,
+          const int64_t idx = (int64_t)p * sa.stride + (x < KB ? dbase + x : sa.D);
+          const int64_t f = (int64_t)__hip_atomic_fetch_add((unsigned long long*)&sa.c.first[idx], 0ull,
                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (f >= ord_base && f != INT64_MAX) s.c.f1v[idx] = f1col[f - ord_base];
+          if (f >= ord_base && f != INT64_MAX) sa.c.f1v[idx] = f1col[f - ord_base];
         }
       }
     } else {
@@ -1835,7 +1848,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_aggregate(const Spec* __restrict
                            __HIP_MEMORY_SCOPE_SYSTEM);
 #endif
     } else {
-      atomicAdd(&s.stats[ST_SHARES], 1ull);
+      atomicAdd(&sa.stats[ST_SHARES], 1ull);
     }
   }
 }
@@ -3676,6 +3689,8 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   // of the nb = CU-count workgroups on one CU and leave another idle)
   const size_t agg_lds = std::max<size_t>(e->agg_lds - (size_t)(e->max_tiles - r.ntiles) * 8, (size_t)e->agg_min_lds);
   hipStream_t rs = e->serial ? e->stream : e->rstream;
+  const AggSpec sa{e->s.nb, e->s.kb_bits, e->s.P, e->s.by_last, e->s.cmpto, e->s.stride, e->s.D, e->s.dir_keys, e->s.slice_tag,
+                   e->s.dir_min_used, e->s.err, e->s.stats, e->s.c};
   e->phase_begin(FW_PHASE_INGEST, rs);
   const Spec& sp = e->s;
   const RouteSpec q{sp.assigner, sp.K, sp.R, sp.mp, sp.kg_start, sp.kg_end, sp.mp_mask, sp.kb_bits, sp.nb,
@@ -3687,9 +3702,10 @@ static void launch_routed_t(fw_engine* e, const BatchIn& b, const int64_t* f1col
   e->phase_begin(FW_PHASE_AGGREGATE);
   if (r.helpers > 0)
     hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, true>), dim3(e->s.nb + r.helpers), dim3(AG_THREADS), agg_lds, e->stream,
-                       e->s_dev, b, r, f1col);
+                       e->s_dev, sa, b, r, f1col);
   else
-    hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream, e->s_dev, b, r,
+    hipLaunchKernelGGL((k_aggregate<VT, AGG, FIRST, false>), dim3(e->s.nb), dim3(AG_THREADS), agg_lds, e->stream,
+                       e->s_dev, sa, b, r,
                        f1col);
   e->phase_end(b.n);
   // (ev_agg[par] is recorded by fw_push_batch once the batch's extra-window list is applied too)
