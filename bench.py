@@ -251,12 +251,19 @@ def main():
         if exch is not None:
             exch.flush()   # the pipelined exchange's outstanding batches
 
+    # the warm-up's results are collected to the host before its last step, so the timed region does not start
+    # from a device left idle through that copy (the device clocks down while idle: a 20-step region lost ~10 us
+    # per step to its first steps, round 6)
+    collected = []
     for j in range(args.warmup):
+        if j == args.warmup - 1:
+            drain()
+            eng.sync()
+            collected.append(eng.collect())
         step(j, *cols[j])
     drain()
     eng.sync()
     torch.cuda.synchronize()
-    collected = [eng.collect()]
     st0 = eng.stats()
     barrier(world)
     torch.cuda.synchronize()
