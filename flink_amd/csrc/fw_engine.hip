@@ -3342,6 +3342,7 @@ struct fw_engine {
   // packet the command processor handles between the engine stream's kernels
   bool track_consumed = false;
   hipEvent_t ev_now = nullptr;
+  hipEvent_t ev_hcopy = nullptr;      // host-column copies of a push done (system-scope fence kept)
   // routed batches rotate over NBUF buffer sets: k_route of batch j waits only for k_aggregate of batch
   // j - NBUF, long finished, so neither stream waits on the other's latest kernel (a cross-stream wait costs
   // ~13 us of signal latency on MI355X, measured: profiles/r02_v13_timeline.txt)
@@ -3555,6 +3556,7 @@ struct fw_engine {
     for (int q = 0; q < NBUF; ++q) for (hipEvent_t ev : {ev_route[q], ev_agg[q]}) if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : ev_consumed) if (ev) (void)hipEventDestroy(ev);
     if (ev_now) (void)hipEventDestroy(ev_now);
+    if (ev_hcopy) (void)hipEventDestroy(ev_hcopy);
     for (auto& t : timed) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto ev : event_pool) (void)hipEventDestroy(ev);
     for (void* p : allocs) (void)hipFree(p);
@@ -3853,9 +3855,13 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
   for (auto& ev : e->ev_consumed) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   HIPCHK(e, hipEventCreateWithFlags(&e->ev_now, hipEventDisableTiming));
+  HIPCHK(e, hipEventCreateWithFlags(&e->ev_hcopy, hipEventDisableTiming));
+  // ev_route / ev_agg order two device streams of one GPU: no system-scope fence needed (FW_EVENT_FENCE=1: with)
+  const unsigned pf = hipEventDisableTiming |
+      ((getenv("FW_EVENT_FENCE") && atoi(getenv("FW_EVENT_FENCE")) != 0) ? 0u : (unsigned)hipEventDisableSystemFence);
   for (int q = 0; q < fw_engine::NBUF; ++q) {
-    HIPCHK(e, hipEventCreateWithFlags(&e->ev_route[q], hipEventDisableTiming));
-    HIPCHK(e, hipEventCreateWithFlags(&e->ev_agg[q], hipEventDisableTiming));
+    HIPCHK(e, hipEventCreateWithFlags(&e->ev_route[q], pf));
+    HIPCHK(e, hipEventCreateWithFlags(&e->ev_agg[q], pf));
   }
   hipDeviceProp_t prop;
   HIPCHK(e, hipGetDeviceProperties(&prop, c.device));
@@ -4242,9 +4248,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     // the caller may reuse its arrays once fw_push_batch returns (flink_window.h): wait for the copies here
     // (pinned host memory would otherwise still be read by the DMA engine afterwards); the earlier batches'
     // kernels keep running on the engine stream meanwhile
-    HIPCHK(e, hipEventRecord(e->ev_route[par], in_stream));
-    HIPCHK(e, hipEventSynchronize(e->ev_route[par]));
-    if (in_stream != e->stream && !e->routed) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_route[par], 0));
+    HIPCHK(e, hipEventRecord(e->ev_hcopy, in_stream));
+    HIPCHK(e, hipEventSynchronize(e->ev_hcopy));
+    if (in_stream != e->stream && !e->routed) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_hcopy, 0));
   }
   if (e->routed && mem == FW_MEM_DEVICE) {
     // k_route streams the columns with 16-B loads (key hashes with 8-B loads): realign odd pointers
