@@ -254,12 +254,25 @@ struct Operator {
   // session windows: per key the in-flight windows -> their state window (MergingWindowSet.windows, a
   // HashMap<W, W>; ordered here by (start, end), which mergeWindows' stable sort by start makes equivalent)
   std::unordered_map<int64_t, std::map<TimeWindow, TimeWindow>> mergingWindowsByKey;
+  // checkpoint bookkeeping of session windows (WindowOperator.java:445-460 getMergingWindowSet, :724-736
+  // snapshotState; MergingWindowSet.java:77-95): when each in-flight window was last put into its key's
+  // MergingWindowSet.windows (a HashMap: remove + put moves it to the end of its bucket), when each key's set
+  // entered mergingWindowsByKey, and the "merging-window-set" list state (VoidNamespace) per key group: an
+  // entry per key written by a snapshot or read by a restore, cleared when the key's set is first fetched
+  std::unordered_map<int64_t, std::map<TimeWindow, int64_t>> putSeq;
+  std::unordered_map<int64_t, int64_t> mwsSeq;
+  struct MwsEntry { int64_t seq; std::vector<std::pair<TimeWindow, TimeWindow>> list; };
+  std::vector<std::unordered_map<int64_t, MwsEntry>> mwsHeap;
+  std::vector<uint8_t> mwsKgCreated;
+  bool mwsTable = false;   // the "merging-window-set" state table exists (first getMergingWindowSet or a restore)
   std::vector<double> c_sum_d, c_min_d, c_max_d;
 
   explicit Operator(const fw_config& c) : cfg(c) {
     state.resize((size_t)(cfg.kg_end - cfg.kg_start + 1));
     nsSeq.resize(state.size());
     kgCreated.assign(state.size(), 0);
+    mwsHeap.resize(state.size());
+    mwsKgCreated.assign(state.size(), 0);
   }
 
   // ---- WindowAssigner.assignWindows ----
@@ -467,9 +480,9 @@ struct Operator {
       std::vector<TimeWindow> mergedStateWindows;
       for (const TimeWindow& m : merged) {
         auto f = windows.find(m);
-        if (f != windows.end()) { mergedStateWindows.push_back(f->second); windows.erase(f); }
+        if (f != windows.end()) { mergedStateWindows.push_back(f->second); mwsErase(windows, f->first); }
       }
-      windows[mergeResult] = mergedStateWindow;
+      mwsPut(windows, mergeResult, mergedStateWindow);
       {
         auto f = std::find(mergedStateWindows.begin(), mergedStateWindows.end(), mergedStateWindow);
         if (f != mergedStateWindows.end()) mergedStateWindows.erase(f);
@@ -520,16 +533,45 @@ struct Operator {
         }
       }
     }
-    if (resultWindow == newWindow && !anyMerge) windows[resultWindow] = resultWindow;
+    if (resultWindow == newWindow && !anyMerge) mwsPut(windows, resultWindow, resultWindow);
     return resultWindow;
+  }
+  // MergingWindowSet.windows.put / remove, with the put's position in the HashMap's insertion order
+  void mwsPut(std::map<TimeWindow, TimeWindow>& windows, const TimeWindow& w, const TimeWindow& sw) {
+    windows.erase(w);
+    windows[w] = sw;
+    putSeq[curKey][w] = ++seqCounter;
+  }
+  void mwsErase(std::map<TimeWindow, TimeWindow>& windows, const TimeWindow w) {
+    windows.erase(w);
+    auto it = putSeq.find(curKey);
+    if (it != putSeq.end()) it->second.erase(w);
+  }
+  // WindowOperator.getMergingWindowSet (:445-460): the key's set, created on first use from its
+  // "merging-window-set" list state (puts in list order), which is then cleared
+  std::map<TimeWindow, TimeWindow>& getMergingWindowSet() {
+    auto it = mergingWindowsByKey.find(curKey);
+    if (it != mergingWindowsByKey.end()) return it->second;
+    mwsTable = true;
+    auto& windows = mergingWindowsByKey[curKey];
+    mwsSeq[curKey] = ++seqCounter;
+    if (curKeyGroup >= cfg.kg_start && curKeyGroup <= cfg.kg_end) {
+      auto& heap = mwsHeap[(size_t)(curKeyGroup - cfg.kg_start)];
+      auto h = heap.find(curKey);
+      if (h != heap.end()) {
+        for (const auto& p : h->second.list) mwsPut(windows, p.first, p.second);
+        heap.erase(h);
+      }
+    }
+    return windows;
   }
 
   int processElementMerging(const Acc& value, int64_t ts) {  // WindowOperator.java:228-301
     const TimeWindow window{ts, jlong_add(ts, cfg.size)};   // EventTimeSessionWindows.assignWindows :53-56
-    auto& windows = mergingWindowsByKey[curKey];
+    auto& windows = getMergingWindowSet();
     const TimeWindow actualWindow = addWindow(windows, window);
     if (isLate(actualWindow)) {   // :265-269
-      windows.erase(actualWindow);
+      mwsErase(windows, actualWindow);
       stats.records_late++;
       return FW_OK;
     }
@@ -553,7 +595,7 @@ struct Operator {
   }
   void cleanupMerging(const TimeWindow& w, const TimeWindow& stateWindow, std::map<TimeWindow, TimeWindow>& windows) {
     stateClear(stateWindow);   // :420-428
-    windows.erase(w);          // MergingWindowSet.retireWindow
+    mwsErase(windows, w);      // MergingWindowSet.retireWindow
     triggerClear(w);
   }
 
@@ -609,17 +651,16 @@ struct Operator {
     curKey = timer.key;
     const TimeWindow& window = timer.ns;
     if (cfg.assigner == FW_SESSION) {   // :344-353: the state lives in the window's state window
-      auto kit = mergingWindowsByKey.find(curKey);
-      if (kit == mergingWindowsByKey.end()) return;
-      auto sw = kit->second.find(window);
-      if (sw == kit->second.end()) return;   // already purged: a leftover cleanup timer
+      auto& windows = getMergingWindowSet();
+      auto sw = windows.find(window);
+      if (sw == windows.end()) return;   // already purged: a leftover cleanup timer
       const TimeWindow stateWindow = sw->second;
       const Acc* c = stateGet(stateWindow);
       if (c == nullptr) return;
       Acc contents = *c;
       TriggerResult triggerResult = triggerOnEventTime(window, timer.timestamp);
       if (isFire(triggerResult)) fire(window, contents);
-      if (isPurge(triggerResult) || isCleanupTime(window, timer.timestamp)) cleanupMerging(window, stateWindow, kit->second);
+      if (isPurge(triggerResult) || isCleanupTime(window, timer.timestamp)) cleanupMerging(window, stateWindow, windows);
       return;
     }
     const Acc* c = stateGet(window);
@@ -759,13 +800,80 @@ int64_t entSeqOf(const EntRef& r) { return r.acc->seq; }
 int32_t tmHash(const TimerRef& r) { return timerHashCode(r.t); }
 int64_t tmSeqOf(const TimerRef& r) { return r.seq; }
 
-// HeapKeyedStateBackend.snapshot's key-group section (:196-212) + writeStateTableForKeyGroup (:217-248), and
-// HeapInternalTimerService.snapshotTimersForKeyGroup (:285-310) after its serializer records
-void snapshotKeyGroup(const Operator& op, int32_t kg, const fw_state_layout& L, JavaOut& st, JavaOut& tm) {
+// WindowOperator.snapshotState (:724-736) for the keys of key group kg: in mergingWindowsByKey's iteration
+// order (a HashMap<K, MergingWindowSet>), each key's "merging-window-set" entry cleared and rewritten by
+// MergingWindowSet.persist (:91-95: the windows HashMap's entries in its iteration order; an empty set
+// writes none)
+void persistMergingWindows(Operator& op, int32_t kg) {
   const size_t kgi = (size_t)(kg - op.cfg.kg_start);
+  std::vector<int64_t> keys;
+  for (const auto& kv : op.mergingWindowsByKey) keys.push_back(kv.first);
+  const uint32_t gmask = hmCapacity(keys.size()) - 1;
+  std::sort(keys.begin(), keys.end(), [&](int64_t a, int64_t b) {
+    const uint32_t ia = (uint32_t)hmHash(longHashCode(a)) & gmask, ib = (uint32_t)hmHash(longHashCode(b)) & gmask;
+    return ia != ib ? ia < ib : op.mwsSeq.at(a) < op.mwsSeq.at(b);
+  });
+  auto& heap = op.mwsHeap[kgi];
+  for (int64_t k : keys) {
+    if (computeKeyGroupForKeyHash(op.keyHashOf(k), op.cfg.max_parallelism) != kg) continue;
+    heap.erase(k);   // mergeState.clear()
+    const auto& windows = op.mergingWindowsByKey.at(k);
+    if (windows.empty()) continue;
+    const auto& ps = op.putSeq.at(k);
+    std::vector<std::pair<TimeWindow, TimeWindow>> v(windows.begin(), windows.end());
+    const uint32_t wmask = hmCapacity(v.size()) - 1;
+    std::sort(v.begin(), v.end(), [&](const auto& a, const auto& b) {
+      const uint32_t ia = (uint32_t)hmHash(timeWindowHashCode(a.first)) & wmask;
+      const uint32_t ib = (uint32_t)hmHash(timeWindowHashCode(b.first)) & wmask;
+      return ia != ib ? ia < ib : ps.at(a.first) < ps.at(b.first);
+    });
+    heap[k] = Operator::MwsEntry{++op.seqCounter, v};   // mergeState.add per entry (HeapListState.add)
+    op.mwsKgCreated[kgi] = 1;
+  }
+}
+
+// the "merging-window-set" table of key group kg: ListState<Tuple2<W, W>> in VoidNamespace
+// (writeStateTableForKeyGroup; VoidNamespaceSerializer: one byte; ArrayListSerializer: int size, then the
+// elements; TupleSerializer of two TimeWindow.Serializer: start, end of the window, then of its state window)
+void writeMergingWindowTable(const Operator& op, size_t kgi, JavaOut& st) {
+  if (!op.mwsKgCreated[kgi]) { st.writeByte(0); return; }
+  st.writeByte(1);
+  const auto& heap = op.mwsHeap[kgi];
+  st.writeInt(heap.empty() ? 0 : 1);
+  if (heap.empty()) return;
+  st.writeByte(0);
+  std::vector<std::pair<int64_t, const Operator::MwsEntry*>> ent;
+  for (const auto& kv : heap) ent.push_back({kv.first, &kv.second});
+  const uint32_t mask = hmCapacity(ent.size()) - 1;
+  std::sort(ent.begin(), ent.end(), [&](const auto& a, const auto& b) {
+    const uint32_t ia = (uint32_t)hmHash(longHashCode(a.first)) & mask, ib = (uint32_t)hmHash(longHashCode(b.first)) & mask;
+    return ia != ib ? ia < ib : a.second->seq < b.second->seq;
+  });
+  st.writeInt((int32_t)ent.size());
+  for (const auto& x : ent) {
+    st.writeLong(x.first);
+    st.writeInt((int32_t)x.second->list.size());
+    for (const auto& w : x.second->list) {
+      st.writeLong(w.first.start);
+      st.writeLong(w.first.end);
+      st.writeLong(w.second.start);
+      st.writeLong(w.second.end);
+    }
+  }
+}
+
+// HeapKeyedStateBackend.snapshot's key-group section (:196-212) + writeStateTableForKeyGroup (:217-248), and
+// HeapInternalTimerService.snapshotTimersForKeyGroup (:285-310) after its serializer records.  The state
+// tables in stateTables' HashMap order: "window-contents" (bucket 12 of 16), then session windows'
+// "merging-window-set" (bucket 15); each key group lists every table, under its kVStateToId
+void snapshotKeyGroup(Operator& op, int32_t kg, const fw_state_layout& L, JavaOut& st, JavaOut& tm) {
+  const size_t kgi = (size_t)(kg - op.cfg.kg_start);
+  const bool session = op.cfg.assigner == FW_SESSION;
+  if (session) persistMergingWindows(op, kg);
+  if (op.anyState || (session && op.mwsTable)) st.writeInt(kg);
+  int nextId = 0;
   if (op.anyState) {
-    st.writeInt(kg);
-    st.writeShort(0);   // kVStateToId of "window-contents", the only state table
+    st.writeShort(nextId++);   // kVStateToId of "window-contents"
     if (!op.kgCreated[kgi]) {
       st.writeByte(0);
     } else {
@@ -795,6 +903,10 @@ void snapshotKeyGroup(const Operator& op, int32_t kg, const fw_state_layout& L, 
       }
     }
   }
+  if (session && op.mwsTable) {
+    st.writeShort(nextId++);
+    writeMergingWindowTable(op, kgi, st);
+  }
   std::vector<TimerRef> ts;
   for (const auto& kv : op.timerSeq)
     if (computeKeyGroupForKeyHash(op.keyHashOf(kv.first.key), op.cfg.max_parallelism) == kg) ts.push_back({kv.first, kv.second});
@@ -820,10 +932,40 @@ int restoreKeyGroup(Operator& op, int32_t kg, const fw_state_layout& L, int64_t 
   const size_t kgi = (size_t)(kg - op.cfg.kg_start);
   if (sn > 0) {
     JavaIn in{st, sn};
+    const bool session = op.cfg.assigner == FW_SESSION;
     const int32_t written = in.readInt();
+    if (written != kg) { op.err = "bad key-group section"; return FW_ERR_INVALID_ARG; }
+    for (int table = 0; !in.eof && in.pos < sn; ++table) {
     const int stateId = in.readShort();
     const int present = in.readByte();
-    if (written != kg || stateId != 0) { op.err = "bad key-group section"; return FW_ERR_INVALID_ARG; }
+    if (stateId != table || table > (session ? 1 : 0)) { op.err = "bad key-group section"; return FW_ERR_INVALID_ARG; }
+    if (table == 1) {   // session windows' "merging-window-set": per key its (window, state window) list
+      op.mwsTable = true;
+      if (!present) continue;
+      op.mwsKgCreated[kgi] = 1;
+      const int32_t nns = in.readInt();
+      if (nns < 0 || nns > 1) { op.err = "bad merging-window-set section"; return FW_ERR_INVALID_ARG; }
+      if (nns == 0) continue;
+      if (in.readByte() != 0) { op.err = "bad merging-window-set namespace"; return FW_ERR_INVALID_ARG; }
+      const int32_t ne = in.readInt();
+      for (int32_t j = 0; j < ne && !in.eof; ++j) {
+        const int64_t key = in.readLong();
+        const int32_t m = in.readInt();
+        if (m < 0) { op.err = "corrupt merging-window-set entry"; return FW_ERR_INVALID_ARG; }
+        Operator::MwsEntry me{++op.seqCounter, {}};
+        for (int32_t q = 0; q < m && !in.eof; ++q) {
+          TimeWindow w, sw;
+          w.start = in.readLong();
+          w.end = in.readLong();
+          sw.start = in.readLong();
+          sw.end = in.readLong();
+          me.list.push_back({w, sw});
+        }
+        op.mwsHeap[kgi][key] = me;
+      }
+      continue;
+    }
+    if (session) op.anyState = true;   // (the table exists: a session checkpoint lists both)
     if (present) {
       op.kgCreated[kgi] = 1;
       op.anyState = true;
@@ -860,6 +1002,7 @@ int restoreKeyGroup(Operator& op, int32_t kg, const fw_state_layout& L, int64_t 
           entries[mapKey] = a;
         }
       }
+    }
     }
     if (in.eof || in.pos != sn) { op.err = "state section truncated or with trailing bytes"; return FW_ERR_INVALID_ARG; }
   }
@@ -972,7 +1115,6 @@ int fwo_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layou
                           int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
   if (!e || !layout || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
   if (kg < e->op.cfg.kg_start || kg > e->op.cfg.kg_end) return FW_ERR_INVALID_ARG;
-  if (e->op.cfg.assigner == FW_SESSION) { e->op.err = "session windows: no checkpoint layout"; return FW_ERR_UNSUPPORTED; }
   JavaOut st, tm;
   snapshotKeyGroup(e->op, kg, *layout, st, tm);
   *state_len = (int64_t)st.b.size();
