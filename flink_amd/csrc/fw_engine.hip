@@ -3302,6 +3302,24 @@ struct SessDev {
   int64_t* f1;      // first-arrival f1 (keep_first_f1) / the extremal record's f1 (maxBy / minBy), or null
   unsigned long long* live;   // [D + 1] slots in flight
   unsigned long long* trig;   // [D + 1] slots whose trigger timer (at maxTimestamp) is pending
+  // checkpoint bookkeeping (fw_snapshot_kg_flink; arrival ordinals, restored entries below zero in blob order):
+  // per slot the state window's start (its end: start + gap — a state window is the window a session began as),
+  // when that state window's "window-contents" entry was created, when the window was last put into
+  // MergingWindowSet.windows, when its cleanup timer and its trigger timer were registered; per key when its
+  // MergingWindowSet was first fetched (-1: not since the operator opened) with the first fired timer's time as
+  // the tie-break of a watermark's fetches, and whether any of its records was accepted into a window
+  int64_t *sws, *swc, *put, *cre, *tre;
+  int64_t *ktouch, *ktts;
+  int32_t* kacc;
+  // a "window-contents" namespace (key group, state window) is shared by every key whose session began at that
+  // instant; it lives while any of their entries does.  nscnt counts live entries per hashed (key group, state
+  // window); an entry removed while its counter stays positive (possibly shared) is logged — key, state-window
+  // start, creation and removal ordinals — so a snapshot can tell when the namespace's current instance began
+  int32_t* nscnt;
+  uint64_t nsmask;
+  int64_t* nslog;
+  unsigned long long* nslog_n;
+  int64_t nslog_cap;
   // list state (FW_AGG_LIST): per slot the window's elements as a linked list through an element pool of pcap
   // entries, handed out from a ring of free entry indices (freeq; pool[0] head, pool[1] end of the free ones,
   // pool[2] entries freed during the current launch, listed in fpend)
@@ -3318,6 +3336,26 @@ struct SessDev {
   int64_t* hot_list;                 // run heads (sorted positions)
   unsigned long long* hot_count;
 };
+
+// "window-contents" namespace bookkeeping (SessDev::nscnt / nslog): an entry created, an entry removed at ordinal r
+__device__ __forceinline__ uint64_t sess_ns_slot(const SessDev& d, int32_t kg, int64_t sws) {
+  return fmix64(((uint64_t)(uint32_t)kg << 48) ^ fmix64((uint64_t)sws)) & d.nsmask;
+}
+__device__ __forceinline__ void sess_ns_add(const SessDev& d, int32_t kg, int64_t sws) {
+  atomicAdd(&d.nscnt[sess_ns_slot(d, kg, sws)], 1);
+}
+__device__ __forceinline__ void sess_ns_remove(const SessDev& d, int32_t kg, int64_t key, int64_t x, int64_t r) {
+  const int64_t sws = d.sws[x];
+  if (atomicSub(&d.nscnt[sess_ns_slot(d, kg, sws)], 1) <= 1) return;   // the namespace's last entry: it ends here
+  const unsigned long long pos = atomicAdd(d.nslog_n, 1ull);
+  if ((int64_t)pos >= d.nslog_cap) return;   // (overflow: the snapshot falls back to the oldest live entry)
+  int64_t* l = d.nslog + 4 * pos;
+  l[0] = key;
+  l[1] = sws;
+  l[2] = d.swc[x];
+  l[3] = r;
+}
+
 
 }  // namespace
 
@@ -3375,6 +3413,19 @@ struct fw_engine {
   // fw_restore_kg_flink: each restored timer's position in the timer sections (restoreTimersForKeyGroup adds
   // them to the set in that order, so later snapshots list them in it within a hash bucket)
   std::map<std::array<int64_t, 4>, int64_t> restored_timer_rank;
+  // session windows' checkpoints: the state tables a restore brought, per key group whether its
+  // "merging-window-set" map exists (a snapshot wrote an entry or a restore read it present), the restored
+  // merging-window-set entries (key -> rank in blob order), and the device state read back for snapshots
+  bool sess_wc_table = false, sess_mws_table = false;
+  std::vector<uint8_t> mws_created;
+  std::map<int64_t, int64_t> sess_mws_rank;
+  struct SessHost {
+    int64_t epoch = -1, wm = 0;
+    std::vector<int64_t> keys, st, en, sws, swc, put, cre, tre, sum, mn, mx, cnt, f1, ktouch, ktts, nslog;
+    bool nslog_over = false;
+    std::vector<int32_t> kacc;
+    std::vector<unsigned long long> live, trig;
+  } sess_host;
   int64_t records_in = 0;
   int64_t pushes = 0;                 // non-empty pushes (ev_consumed ring position)
   int grid = 0;
@@ -5286,10 +5337,441 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// session windows in the reference's key-group layout: WindowOperator keeps two keyed states for a merging
+// assigner (WindowOperator.java:445-460, 724-736) — "window-contents" (the reducing state, namespace = each
+// in-flight window's STATE window) and "merging-window-set" (ListState<Tuple2<W, W>> in VoidNamespace: per
+// key its in-flight windows and their state windows, MergingWindowSet.persist, MergingWindowSet.java:91-95).
+// stateTables iterates "window-contents" (HashMap bucket 12 of 16) before "merging-window-set" (bucket 15): ids
+// 0 and 1.  Engine side: k_sess_walk / k_sess_walk_hot / k_sess_wm keep per slot the state window and the
+// arrival ordinals that place each entry in its HashMap's insertion order (SessDev).
+// ------------------------------------------------------------------------------------------------
+namespace fw {
+// restored sessions: one row per in-flight window (key, slot, start, end, state-window start, its entry's rank,
+// trigger pending, sum, min / max codes, count, f1); key ids by the directory's insert
+constexpr int SESS_ROW = 12;
+__global__ __launch_bounds__(BLOCK) void k_sess_restore(Spec s, SessDev d, const int64_t* rows, int64_t n, int64_t put0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t* r = rows + i * SESS_ROW;
+  const int64_t kid = dir_find_or_insert(s, r[0]);
+  if (kid < 0) { cap_error(s, 20); return; }
+  const int q = (int)r[1];
+  const int64_t x = kid * d.sw + q;
+  d.start[x] = r[2];
+  d.end[x] = r[3];
+  d.sws[x] = r[4];
+  d.swc[x] = r[5];
+  d.put[x] = put0 + q;             // MergingWindowSet(assigner, state): puts in list order
+  d.cre[x] = d.tre[x] = put0;      // (restored timers are ordered by their blob rank)
+  if (d.sum) d.sum[x] = r[7];
+  if (d.mn) d.mn[x] = r[8];
+  if (d.mx) d.mx[x] = r[9];
+  if (d.cnt) d.cnt[x] = r[10];
+  if (d.f1) d.f1[x] = r[11];
+  sess_ns_add(d, record_key_group(s, long_hash_code(r[0])), r[4]);
+  atomicOr(&d.live[kid * d.nw + (q >> 6)], 1ull << (q & 63));
+  if (r[6]) atomicOr(&d.trig[kid * d.nw + (q >> 6)], 1ull << (q & 63));
+}
+}  // namespace fw
+
+static int session_download(fw_engine* e) {
+  fw_engine::SessHost& h = e->sess_host;
+  if (h.epoch == e->state_epoch && h.wm == e->cur_wm) return FW_OK;
+  const fw::Spec& s = e->s;
+  const SessDev& d = e->sess;
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (int rc = check_device_error(e)) return rc;
+  const size_t cells = (size_t)d.sw * (size_t)s.stride, rows = (size_t)s.stride;
+  auto get = [&](std::vector<int64_t>& v, const int64_t* p, size_t n) -> hipError_t {
+    v.assign(p ? n : 0, 0);
+    return p ? hipMemcpy(v.data(), p, 8 * n, hipMemcpyDeviceToHost) : hipSuccess;
+  };
+  HIPCHK(e, get(h.keys, s.dir_keys, (size_t)s.D));
+  HIPCHK(e, get(h.st, d.start, cells));
+  HIPCHK(e, get(h.en, d.end, cells));
+  HIPCHK(e, get(h.sws, d.sws, cells));
+  HIPCHK(e, get(h.swc, d.swc, cells));
+  HIPCHK(e, get(h.put, d.put, cells));
+  HIPCHK(e, get(h.cre, d.cre, cells));
+  HIPCHK(e, get(h.tre, d.tre, cells));
+  HIPCHK(e, get(h.sum, d.sum, cells));
+  HIPCHK(e, get(h.mn, d.mn, cells));
+  HIPCHK(e, get(h.mx, d.mx, cells));
+  HIPCHK(e, get(h.cnt, d.cnt, cells));
+  HIPCHK(e, get(h.f1, d.f1, cells));
+  HIPCHK(e, get(h.ktouch, d.ktouch, rows));
+  HIPCHK(e, get(h.ktts, d.ktts, rows));
+  h.kacc.assign(rows, 0);
+  HIPCHK(e, hipMemcpy(h.kacc.data(), d.kacc, 4 * rows, hipMemcpyDeviceToHost));
+  unsigned long long nl = 0;
+  HIPCHK(e, hipMemcpy(&nl, d.nslog_n, 8, hipMemcpyDeviceToHost));
+  h.nslog_over = (int64_t)nl > d.nslog_cap;
+  HIPCHK(e, get(h.nslog, d.nslog, 4 * (size_t)std::min<int64_t>((int64_t)nl, d.nslog_cap)));
+  h.live.assign(rows * (size_t)d.nw, 0);
+  h.trig.assign(rows * (size_t)d.nw, 0);
+  HIPCHK(e, hipMemcpy(h.live.data(), d.live, 8 * h.live.size(), hipMemcpyDeviceToHost));
+  HIPCHK(e, hipMemcpy(h.trig.data(), d.trig, 8 * h.trig.size(), hipMemcpyDeviceToHost));
+  h.epoch = e->state_epoch;
+  h.wm = e->cur_wm;
+  return FW_OK;
+}
+
+static int session_reject_config(fw_engine* e) {
+  const fw_config& c = e->cfg;
+  if (e->list)
+    return reject(e, FW_ERR_UNSUPPORTED, "session windows with list state: the elements sit in an element pool, not in "
+                                         "per-window lists (no checkpoint layout here)");
+  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0)
+    return reject(e, FW_ERR_UNSUPPORTED, "session windows under PurgingTrigger with allowed lateness: a purged "
+                                         "session's cleanup timer outlives it, which the engine does not hold");
+  if (e->mws_created.empty()) e->mws_created.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
+  if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
+  return FW_OK;
+}
+
+static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, void* state,
+                                     int64_t state_cap, int64_t* state_len, void* timers, int64_t timers_cap,
+                                     int64_t* timers_len) {
+  if (int rc = session_reject_config(e)) return rc;
+  HIPCHK(e, hipSetDevice(e->dev));
+  if (int rc = session_download(e)) return rc;
+  const fw_engine::SessHost& h = e->sess_host;
+  const fw::Spec& s = e->s;
+  const SessDev& d = e->sess;
+  const fw_config& c = e->cfg;
+  const size_t kgi = (size_t)(kg - s.kg_start);
+  struct Pane { int64_t kid, key, start, end, sws, swc, put, cre, tre; bool trig; KgPane acc; };
+  std::vector<Pane> panes;
+  std::vector<int64_t> kids;   // the key group's keys
+  int64_t n_touched = 0;
+  bool any_acc = false, kg_acc = false;
+  for (int64_t k = 0; k < s.stride; ++k) {
+    const int64_t key = k == s.D ? fw::EMPTY_KEY : h.keys[(size_t)k];
+    if (k < s.D && key == fw::EMPTY_KEY) continue;
+    if (h.ktouch[(size_t)k] >= 0) ++n_touched;
+    any_acc = any_acc || h.kacc[(size_t)k];
+    if (host_key_group(s, key) != kg) continue;
+    kids.push_back(k);
+    kg_acc = kg_acc || h.kacc[(size_t)k];
+    for (int q = 0; q < d.sw; ++q) {
+      const size_t w = (size_t)k * (size_t)d.nw + (size_t)(q >> 6);
+      if (!((h.live[w] >> (q & 63)) & 1ull)) continue;
+      const size_t x = (size_t)k * (size_t)d.sw + (size_t)q;
+      Pane p{k, key, h.st[x], h.en[x], h.sws[x], h.swc[x], h.put[x], h.cre[x], h.tre[x], ((h.trig[w] >> (q & 63)) & 1ull) != 0, {}};
+      p.acc = KgPane{p.sws, fw::jadd(p.sws, d.gap), key, h.sum.empty() ? 0 : h.sum[x], h.mn.empty() ? INT64_MAX : h.mn[x],
+                     h.mx.empty() ? INT64_MIN : h.mx[x], h.cnt.empty() ? 0 : h.cnt[x], 0, h.f1.empty() ? 0 : h.f1[x], false};
+      panes.push_back(p);
+    }
+  }
+  const bool wc_table = e->sess_wc_table || any_acc;
+  const bool mws_table = e->sess_mws_table || n_touched > 0;
+  fwkg::BeOut st, tm;
+  if (wc_table || mws_table) st.i32(kg);
+  int id = 0;
+  if (wc_table) {   // "window-contents": namespaces = state windows, created by their first record
+    const bool present = kg_acc || e->kg_touched[kgi];
+    st.i16(id++);
+    st.u8(present ? 1 : 0);
+    if (present) {
+      std::map<int64_t, std::vector<size_t>> ns;
+      for (size_t i = 0; i < panes.size(); ++i) ns[panes[i].sws].push_back(i);
+      std::vector<std::pair<int64_t, std::vector<size_t>>> nsv(ns.begin(), ns.end());
+      // when each namespace's current instance was put into the namespace map: its entries' lifetimes — the live
+      // ones and the logged entries of other keys removed while it stayed shared — chained without a gap
+      std::map<int64_t, std::vector<std::pair<int64_t, int64_t>>> life;
+      for (size_t j = 0; j + 4 <= h.nslog.size(); j += 4)
+        if (ns.count(h.nslog[j + 1]) && host_key_group(s, h.nslog[j]) == kg) life[h.nslog[j + 1]].push_back({h.nslog[j + 2], h.nslog[j + 3]});
+      std::vector<int64_t> ns_first(nsv.size(), INT64_MAX);
+      for (size_t w = 0; w < nsv.size(); ++w) {
+        auto& iv = life[nsv[w].first];
+        for (size_t i : nsv[w].second) iv.push_back({panes[i].swc, INT64_MAX});
+        std::sort(iv.begin(), iv.end());
+        int64_t from = iv[0].first, reach = iv[0].second;
+        for (const auto& x : iv) {
+          if (x.first >= reach) from = x.first;   // a gap: the namespace was removed and put again
+          reach = x.first >= reach ? x.second : std::max(reach, x.second);
+        }
+        ns_first[w] = from;
+      }
+      std::vector<size_t> wo(nsv.size());
+      for (size_t w = 0; w < wo.size(); ++w) wo[w] = w;
+      fwkg::hashmap_order(
+          wo, [&](size_t w) { return fwkg::window_hash(nsv[w].first, fw::jadd(nsv[w].first, d.gap)); },
+          [&](size_t a, size_t b) { return ns_first[a] != ns_first[b] ? ns_first[a] < ns_first[b] : nsv[a].first < nsv[b].first; });
+      st.i32((int32_t)nsv.size());
+      for (size_t w : wo) {
+        st.i64(nsv[w].first);
+        st.i64(fw::jadd(nsv[w].first, d.gap));
+        std::vector<size_t>& ent = nsv[w].second;
+        fwkg::hashmap_order(
+            ent, [&](size_t i) { return fw::long_hash_code(panes[i].key); },
+            [&](size_t a, size_t b) { return panes[a].swc != panes[b].swc ? panes[a].swc < panes[b].swc : panes[a].key < panes[b].key; });
+        st.i32((int32_t)ent.size());
+        for (size_t i : ent) {
+          st.i64(panes[i].key);
+          for (int f = 0; f < layout->n_fields; ++f) put_field(e, st, layout->field[f], panes[i].acc);
+        }
+      }
+    }
+  }
+  if (mws_table) {   // "merging-window-set", as WindowOperator.snapshotState rewrites it
+    // entries: the restored ones of keys not touched since (inserted at the restore, in blob order), then every
+    // other key with sessions in flight, re-added in mergingWindowsByKey's order (HashMap<K, MergingWindowSet>
+    // over every key fetched since the operator opened: bucket, then first fetch)
+    struct Ent { int64_t kid, key, rank; bool touched; std::vector<size_t> slots; };
+    std::vector<Ent> ents;
+    std::map<int64_t, size_t> at;
+    for (size_t i = 0; i < panes.size(); ++i) {
+      auto it = at.find(panes[i].kid);
+      if (it == at.end()) {
+        const int64_t k = panes[i].kid;
+        auto r = e->sess_mws_rank.find(panes[i].key);
+        const bool touched = h.ktouch[(size_t)k] >= 0 || r == e->sess_mws_rank.end();
+        it = at.emplace(k, ents.size()).first;
+        ents.push_back({k, panes[i].key, touched ? INT64_MAX : r->second, touched, {}});
+      }
+      ents[it->second].slots.push_back(i);
+    }
+    if (!ents.empty()) e->mws_created[kgi] = 1;
+    const bool present = e->mws_created[kgi] != 0;
+    st.i16(id++);
+    st.u8(present ? 1 : 0);
+    if (present) {
+      st.i32(ents.empty() ? 0 : 1);
+      if (!ents.empty()) {
+        st.u8(0);   // VoidNamespaceSerializer: one byte
+        const uint32_t gmask = fwkg::capacity_for((size_t)n_touched) - 1;
+        std::vector<size_t> eo(ents.size());
+        for (size_t i = 0; i < eo.size(); ++i) eo[i] = i;
+        fwkg::hashmap_order(
+            eo, [&](size_t i) { return fw::long_hash_code(ents[i].key); },
+            [&](size_t a, size_t b) {
+              const Ent &x = ents[a], &y = ents[b];
+              if (x.touched != y.touched) return !x.touched;
+              if (!x.touched) return x.rank < y.rank;
+              const uint32_t gx = (uint32_t)fwkg::spread(fw::long_hash_code(x.key)) & gmask;
+              const uint32_t gy = (uint32_t)fwkg::spread(fw::long_hash_code(y.key)) & gmask;
+              if (gx != gy) return gx < gy;
+              const int64_t tx = h.ktouch[(size_t)x.kid], ty = h.ktouch[(size_t)y.kid];
+              if (tx != ty) return tx < ty;
+              const int64_t sx = h.ktts[(size_t)x.kid], sy = h.ktts[(size_t)y.kid];
+              return sx != sy ? sx < sy : x.key < y.key;
+            });
+        st.i32((int32_t)ents.size());
+        for (size_t i : eo) {
+          std::vector<size_t>& sl = ents[i].slots;   // MergingWindowSet.windows (HashMap<W, W>): bucket, then put order
+          fwkg::hashmap_order(
+              sl, [&](size_t j) { return fwkg::window_hash(panes[j].start, panes[j].end); },
+              [&](size_t a, size_t b) { return panes[a].put < panes[b].put; });
+          st.i64(ents[i].key);
+          st.i32((int32_t)sl.size());
+          for (size_t j : sl) {
+            st.i64(panes[j].start);
+            st.i64(panes[j].end);
+            st.i64(panes[j].sws);
+            st.i64(fw::jadd(panes[j].sws, d.gap));
+          }
+        }
+      }
+    }
+  }
+  // timers: per in-flight window its trigger timer while pending (registered by onElement / onMerge) and its
+  // cleanup timer (registerCleanupTimer right after; one timer when the lateness is 0); restored ones keep their
+  // blob order ahead of every later one
+  struct Tm { int64_t key, start, end, ts, seq; int kind; int64_t rank; };
+  std::vector<Tm> tv;
+  for (const Pane& p : panes) {
+    const int64_t max_ts = fw::jsub(p.end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+    if (p.trig) tv.push_back({p.key, p.start, p.end, max_ts, p.tre, 0, INT64_MAX});
+    if (ct != max_ts) tv.push_back({p.key, p.start, p.end, ct, p.cre, 1, INT64_MAX});
+  }
+  if (!e->restored_timer_rank.empty())
+    for (Tm& t : tv) {
+      auto it = e->restored_timer_rank.find({t.key, t.start, t.end, t.ts});
+      if (it != e->restored_timer_rank.end()) t.rank = it->second;
+    }
+  std::vector<size_t> to(tv.size());
+  for (size_t i = 0; i < to.size(); ++i) to[i] = i;
+  fwkg::hashmap_order(
+      to, [&](size_t i) { return fwkg::timer_hash(tv[i].ts, tv[i].key, tv[i].start, tv[i].end); },
+      [&](size_t a, size_t b) {
+        const Tm &x = tv[a], &y = tv[b];
+        if (x.rank != y.rank) return x.rank < y.rank;
+        if (x.seq != y.seq) return x.seq < y.seq;
+        return x.kind < y.kind;
+      });
+  tm.i32((int32_t)tv.size());
+  for (size_t i : to) {
+    tm.i64(tv[i].key);
+    tm.i64(tv[i].start);
+    tm.i64(tv[i].end);
+    tm.i64(tv[i].ts);
+  }
+  tm.i32(0);
+  *state_len = (int64_t)st.b.size();
+  *timers_len = (int64_t)tm.b.size();
+  if (!state && !timers) return FW_OK;
+  if (!state || !timers || state_cap < *state_len || timers_cap < *timers_len)
+    return reject(e, FW_ERR_CAPACITY, "snapshot buffer too small");
+  if (!st.b.empty()) memcpy(state, st.b.data(), st.b.size());
+  memcpy(timers, tm.b.data(), tm.b.size());
+  return FW_OK;
+}
+
+static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
+                                    const void* state, int64_t state_len, const void* timers, int64_t timers_len) {
+  if (int rc = session_reject_config(e)) return rc;
+  const fw::Spec& s = e->s;
+  const SessDev& d = e->sess;
+  const fw_config& c = e->cfg;
+  const bool f64 = s.vt == FW_VALUE_F64;
+  const size_t kgi = (size_t)(kg - s.kg_start);
+  std::map<std::pair<int64_t, int64_t>, std::pair<KgPane, int64_t>> wc;   // (state-window start, key) -> (state, rank)
+  std::vector<std::pair<int64_t, std::vector<std::array<int64_t, 4>>>> mws;
+  bool wc_seen = false, mws_seen = false, wc_present = false, mws_present = false;
+  if (state_len > 0) {
+    fwkg::BeIn in(state, state_len);
+    if (in.i32() != kg) return reject(e, FW_ERR_INVALID_ARG, "state section of another key group");
+    for (int table = 0; in.ok && in.pos < in.n; ++table) {
+      if (in.i16() != table || table > 1) return reject(e, FW_ERR_UNSUPPORTED, "keyed state other than window-contents and merging-window-set");
+      const bool present = in.u8() != 0;
+      if (table == 0) {
+        wc_seen = true;
+        wc_present = present;
+        const int32_t nns = present ? in.i32() : 0;
+        if (nns < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
+        for (int32_t w = 0; w < nns && in.ok; ++w) {
+          const int64_t start = in.i64(), end = in.i64();
+          if (in.ok && end != fw::jadd(start, d.gap))
+            return reject(e, FW_ERR_INVALID_ARG, "namespace is not a state window [ts, ts + gap) of this assigner");
+          const int32_t ne = in.i32();
+          if (ne < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
+          for (int32_t j = 0; j < ne && in.ok; ++j) {
+            KgPane p{start, end, in.i64(), 0, INT64_MAX, INT64_MIN, 0, 0, 0, false};
+            for (int f = 0; f < layout->n_fields; ++f) {
+              const int64_t x = in.i64();
+              double dv;
+              memcpy(&dv, &x, 8);
+              switch (layout->field[f]) {
+                case FW_SF_KEY:
+                  if (in.ok && x != p.key) return reject(e, FW_ERR_UNSUPPORTED, "state key field differs from the key");
+                  break;
+                case FW_SF_F1: p.f1 = x; break;
+                case FW_SF_SUM: p.sum = x; break;
+                case FW_SF_MIN: p.mn = f64 ? (s.cmpto ? fw::f64_cmp_code(dv) : fw::f64_min_code(dv)) : x; break;
+                case FW_SF_MAX: p.mx = f64 ? (s.cmpto ? fw::f64_cmp_code(dv) : fw::f64_max_code(dv)) : x; break;
+                case FW_SF_COUNT: p.cnt = x; break;
+                case FW_SF_VALUE: p.mn = p.mx = f64 ? fw::f64_cmp_code(dv) : x; break;
+              }
+            }
+            if (!in.ok) break;
+            if (host_key_group(s, p.key) != kg) return reject(e, FW_ERR_KEY_GROUP, "state entry key outside its key group");
+            if (!wc.emplace(std::make_pair(start, p.key), std::make_pair(p, e->restore_ord++)).second)
+              return reject(e, FW_ERR_INVALID_ARG, "duplicate (window, key) entry");
+          }
+        }
+      } else {
+        mws_seen = true;
+        mws_present = present;
+        const int32_t nns = present ? in.i32() : 0;
+        if (nns < 0 || nns > 1) return reject(e, FW_ERR_INVALID_ARG, "corrupt merging-window-set section");
+        if (nns == 1 && in.u8() != 0) return reject(e, FW_ERR_INVALID_ARG, "merging-window-set namespace is not VoidNamespace");
+        const int32_t ne = nns ? in.i32() : 0;
+        if (ne < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt merging-window-set section");
+        for (int32_t j = 0; j < ne && in.ok; ++j) {
+          const int64_t key = in.i64();
+          const int32_t m = in.i32();
+          if (m < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt merging-window-set entry");
+          if (m > d.sw) return reject(e, FW_ERR_CAPACITY, "more in-flight sessions for a key than max_open_slices");
+          std::vector<std::array<int64_t, 4>> l;
+          for (int32_t q = 0; q < m && in.ok; ++q) l.push_back({in.i64(), in.i64(), in.i64(), in.i64()});
+          if (!in.ok) break;
+          if (host_key_group(s, key) != kg) return reject(e, FW_ERR_KEY_GROUP, "merging-window-set key outside its key group");
+          mws.push_back({key, std::move(l)});
+        }
+      }
+    }
+    if (!in.done()) return reject(e, FW_ERR_INVALID_ARG, "state section truncated or with trailing bytes");
+  }
+  std::vector<std::array<int64_t, 4>> got;
+  {
+    fwkg::BeIn in(timers, timers_len);
+    const int32_t nt = in.i32();
+    if (nt < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt timer section");
+    for (int32_t i = 0; i < nt && in.ok; ++i) {
+      const int64_t key = in.i64(), start = in.i64(), end = in.i64(), ts = in.i64();
+      got.push_back({key, start, end, ts});
+    }
+    const int32_t np = in.i32();
+    if (!in.done()) return reject(e, FW_ERR_INVALID_ARG, "timer section truncated or with trailing bytes");
+    if (np != 0) return reject(e, FW_ERR_UNSUPPORTED, "processing-time timers");
+  }
+  // the in-flight windows: each with its state window's contents; timers exactly the ones they imply
+  std::set<std::array<int64_t, 4>> tset(got.begin(), got.end()), want;
+  std::vector<int64_t> rows;
+  std::set<std::pair<int64_t, int64_t>> used, keys_seen;
+  for (const auto& kv : mws) {
+    if (!keys_seen.insert({kv.first, 0}).second) return reject(e, FW_ERR_INVALID_ARG, "duplicate merging-window-set key");
+    for (size_t q = 0; q < kv.second.size(); ++q) {
+      const auto& w = kv.second[q];   // window start, end, state window start, end
+      if (w[3] != fw::jadd(w[2], d.gap) || w[0] > w[2] || w[1] < w[3])
+        return reject(e, FW_ERR_INVALID_ARG, "a state window is not a session's first window inside the window");
+      auto it = wc.find({w[2], kv.first});
+      if (it == wc.end()) return reject(e, FW_ERR_INVALID_ARG, "in-flight session without window-contents state");
+      used.insert({w[2], kv.first});
+      const int64_t max_ts = fw::jsub(w[1], 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+      const std::array<int64_t, 4> trig_t{kv.first, w[0], w[1], max_ts};
+      const bool trig = tset.count(trig_t) != 0;
+      if (trig) want.insert(trig_t);
+      if (ct != max_ts) want.insert({kv.first, w[0], w[1], ct});
+      const KgPane& p = it->second.first;
+      const int64_t row[fw::SESS_ROW] = {kv.first, (int64_t)q, w[0], w[1], w[2], it->second.second,
+                                         trig ? 1 : 0, p.sum, p.mn, p.mx, p.cnt, p.f1};
+      rows.insert(rows.end(), row, row + fw::SESS_ROW);
+    }
+  }
+  if (used.size() != wc.size()) return reject(e, FW_ERR_INVALID_ARG, "window-contents state of no in-flight session");
+  if (want != tset) return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the sessions imply");
+  HIPCHK(e, hipSetDevice(e->dev));
+  for (const auto& kv : mws) e->sess_mws_rank[kv.first] = (int64_t)e->sess_mws_rank.size();
+  for (const auto& t : got) e->restored_timer_rank[t] = (int64_t)e->restored_timer_rank.size();
+  if (wc_seen) e->sess_wc_table = true;
+  if (mws_seen) e->sess_mws_table = true;
+  if (wc_present) e->kg_touched[kgi] = 1;
+  if (mws_present) e->mws_created[kgi] = 1;
+  e->restored = true;
+  e->cur_wm = watermark;
+  e->state_epoch++;
+  const int64_t n = (int64_t)(rows.size() / fw::SESS_ROW);
+  if (n == 0) return FW_OK;
+  int64_t* dr = nullptr;
+  HIPCHK(e, hipMalloc(&dr, 8 * rows.size()));
+  hipError_t r = hipMemcpyAsync(dr, rows.data(), 8 * rows.size(), hipMemcpyHostToDevice, e->stream);
+  if (r == hipSuccess) {
+    hipLaunchKernelGGL(fw::k_sess_restore, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, e->stream, e->s,
+                       e->sess, dr, n, -((int64_t)1 << 61));
+    r = hipGetLastError();
+  }
+  const hipError_t r2 = hipStreamSynchronize(e->stream);
+  (void)hipFree(dr);
+  HIPCHK(e, r);
+  HIPCHK(e, r2);
+  return check_device_error(e);
+}
+
 int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, void* state, int64_t state_cap,
                          int64_t* state_len, void* timers, int64_t timers_cap, int64_t* timers_len) {
   if (!e || !state_len || !timers_len) return FW_ERR_INVALID_ARG;
-  if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->session) {
+    if (e->sticky) return e->sticky;
+    if (kg < e->s.kg_start || kg > e->s.kg_end)
+      return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
+    if (e->used_key_hash) return reject(e, FW_ERR_UNSUPPORTED, "snapshot needs Long keys (a push carried Java key hashes)");
+    if (int rc = check_state_layout(e, layout)) return rc;
+    return session_snapshot_kg_flink(e, kg, layout, state, state_cap, state_len, timers, timers_cap, timers_len);
+  }
   if (e->list && e->cfg.assigner != FW_TUMBLING)
     return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows: a record is in several windows' lists, which "
                                          "the engine's slices hold once");
@@ -5458,7 +5940,15 @@ static int restore_list_elements(fw_engine* e, const std::vector<KgPane>& panes,
 int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
                         const void* state, int64_t state_len, const void* timers, int64_t timers_len) {
   if (!e || (!state && state_len) || !timers || state_len < 0) return FW_ERR_INVALID_ARG;
-  if (e->session) return reject(e, FW_ERR_UNSUPPORTED, "session windows: the merging-window set is keyed list state of its own (no checkpoint)");
+  if (e->session) {
+    if (e->sticky) return e->sticky;
+    if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
+    if (kg < e->s.kg_start || kg > e->s.kg_end)
+      return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
+    if (e->restored && watermark != e->cur_wm) return reject(e, FW_ERR_INVALID_ARG, "key groups restored at different watermarks");
+    if (int rc = check_state_layout(e, layout)) return rc;
+    return session_restore_kg_flink(e, kg, layout, watermark, state, state_len, timers, timers_len);
+  }
   if (e->list && e->cfg.assigner != FW_TUMBLING)
     return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows: a record is in several windows' lists, which "
                                          "the engine's slices hold once");

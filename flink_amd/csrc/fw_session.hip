@@ -200,6 +200,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
     return;
   }
   const int64_t key = kid_key(s, kid);
+  const int32_t kkg = record_key_group(s, long_hash_code(key));
   const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
   const int64_t wm = b.wm;
   const int64_t base = kid * d.sw;
@@ -225,9 +226,12 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   const unsigned long long imask = (1ull << idx_bits) - 1;
   int64_t ni = (int64_t)(k0 & imask);
   int64_t nts = b.ts[ni], nv = b.val[ni], nf1 = b.f1 ? b.f1[ni] : nts;
+  if (d.ktouch[kid] < 0) { d.ktouch[kid] = b.ord_base + ni; d.ktts[kid] = INT64_MAX; }   // getMergingWindowSet
+  bool accepted = false;
   bool more = true;
   for (int64_t j = j0; more; ++j) {
     const int64_t ts = nts, v = nv, f1 = nf1;
+    const int64_t ord = b.ord_base + ni;   // this record's arrival ordinal
     more = false;
     if (j + 1 < n) {
       const unsigned long long kn = sorted[j + 1];
@@ -303,6 +307,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
           }
           todo.clr(q);
           const int64_t x = base + q;
+          sess_ns_remove(d, kkg, key, x, ord);   // the source's state window entry cleared
           if (d.list) {   // the source's elements appended (mergePartitionedStates, list branch :315-333)
             if (d.len[x] > 0) {
               if (ll == 0) lh = d.head[x];
@@ -332,6 +337,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
         r = t;
         d.start[base + r] = cs;
         d.end[base + r] = ce;
+        d.cre[base + r] = d.tre[base + r] = ord;   // onMerge's trigger timer, then the cleanup timer
       }
     }
     const int64_t max_ts = jsub(ce, 1);
@@ -347,9 +353,14 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       trig.clr(r);
       d.start[base + r] = cs;
       d.end[base + r] = ce;
+      d.sws[base + r] = cs;
+      d.swc[base + r] = d.cre[base + r] = d.tre[base + r] = ord;
+      sess_ns_add(d, kkg, cs);
       if (d.list) d.len[base + r] = 0;
     }
     const int64_t x = base + r;
+    d.put[x] = ord;   // MergingWindowSet.addWindow re-puts the window the record lands in
+    accepted = true;
     LateAcc cur;
     if (d.list) {
       // HeapListState.add: the element appended in a free pool entry
@@ -379,13 +390,15 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
         sess_emit(s, pos, key, cs, max_ts, cur);
       }
       ++fires;
-      if (purging) retire(r);   // FIRE_AND_PURGE: cleanup(actualWindow)
+      if (purging) { sess_ns_remove(d, kkg, key, x, ord); retire(r); }   // FIRE_AND_PURGE: cleanup(actualWindow)
     } else {
+      if (!trig.test(r)) d.tre[x] = ord;   // (re-armed: a window restored below its fire)
       trig.set(r);
     }
   }
   live.store(d.live + kid * NW);
   trig.store(d.trig + kid * NW);
+  if (accepted) d.kacc[kid] = 1;
   if (late) atomicAdd(&s.stats[ST_LATE], late);
   if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
 }
@@ -455,10 +468,13 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
   const int64_t j0 = d.hot_list[blockIdx.x];
   const int64_t kid = (int64_t)(sorted[j0] >> idx_bits);
   const int64_t key = kid_key(s, kid);
+  const int32_t kkg = record_key_group(s, long_hash_code(key));
   const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
   const int64_t wm = b.wm;
   const int64_t base = kid * d.sw;
   const unsigned long long imask = (1ull << idx_bits) - 1;
+  if (lane == 0 && d.ktouch[kid] < 0) { d.ktouch[kid] = b.ord_base + (int64_t)(sorted[j0] & imask); d.ktts[kid] = INT64_MAX; }
+  bool accepted = false;
   SLane<NW> L;
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
@@ -491,11 +507,12 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
     // 64 records of the run, one per lane
     const int64_t j = jc + lane;
     bool mine = false;
-    int64_t rts = 0, rv = 0, rf1 = 0;
+    int64_t rts = 0, rv = 0, rf1 = 0, ri = 0;
     if (j < n) {
       const unsigned long long kj = sorted[j];
       if ((kj >> idx_bits) == (unsigned long long)kid) {
         const int64_t i = (int64_t)(kj & imask);
+        ri = i;
         mine = true;
         rts = b.ts[i];
         rv = b.val[i];
@@ -507,6 +524,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
     if (cnt_here < 64) done = true;
     for (int t = 0; t < cnt_here; ++t) {
       const int64_t ts = uni64(__shfl(rts, t)), v = uni64(__shfl(rv, t)), f1 = uni64(__shfl(rf1, t));
+      const int64_t ord = b.ord_base + uni64(__shfl(ri, t));
       LateAcc a;
       a.vt = s.vt;
       a.sum = v;
@@ -572,6 +590,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
               if (q < 0 || bc < bq || (bc == bq && sc < sq)) { q = c; bq = bc; sq = sc; }
             }
             todo.clr(q);
+            if (lane == 0) sess_ns_remove(d, kkg, key, base + q, ord);
             const LateAcc sv = gacc(q);
             res = hv ? sess_combine(s, res, sv) : sv;
             hv = true;
@@ -590,6 +609,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
           slane_set<NW>(L.st, r, cs);
           slane_set<NW>(L.en, r, ce);
           if (r == cr) { c_st = cs; c_en = ce; }
+          if (lane == 0) d.cre[base + r] = d.tre[base + r] = ord;
         }
       }
       const int64_t max_ts = jsub(ce, 1);
@@ -605,7 +625,10 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
         trig.clr(r);
         slane_set<NW>(L.st, r, cs);
         slane_set<NW>(L.en, r, ce);
+        if (lane == 0) { d.sws[base + r] = cs; d.swc[base + r] = d.cre[base + r] = d.tre[base + r] = ord; sess_ns_add(d, kkg, cs); }
       }
+      if (lane == 0) d.put[base + r] = ord;
+      accepted = true;
       const LateAcc cur = fresh ? a : sess_combine(s, gacc(r), a);
       slane_put<NW>(L, r, cur);
       cr = __builtin_amdgcn_readfirstlane(r);   // slot r now holds [cs, ce) and cur in every lane's copy
@@ -615,8 +638,9 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
       if (max_ts <= wm) {   // EventTimeTrigger.onElement: FIRE
         if (lane == 0) sess_emit(s, atomicAdd(s.o.count, 1ull), key, cs, max_ts, cur);
         ++fires;
-        if (purging) { live.clr(r); trig.clr(r); }
+        if (purging) { if (lane == 0) sess_ns_remove(d, kkg, key, base + r, ord); live.clr(r); trig.clr(r); }
       } else {
+        if (lane == 0 && !trig.test(r)) d.tre[base + r] = ord;
         trig.set(r);
       }
     }
@@ -637,6 +661,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
   if (lane == 0) {
     live.store(d.live + kid * NW);
     trig.store(d.trig + kid * NW);
+    if (accepted) d.kacc[kid] = 1;
     if (late) atomicAdd(&s.stats[ST_LATE], late);
     if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
   }
@@ -645,7 +670,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
 // a watermark: every in-flight window's timers up to wm_new.  One thread per key; lane by lane the it-th window of
 // each key, so the wave's appends stay aggregated (list state: one append per window, its element count)
 template <int NW>
-__global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm_new) {
+__global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm_new, int64_t touch_ord) {
   typedef SBits<NW> B;
   const bool purging = s.trigger == FW_TRIGGER_PURGING_EVENT_TIME;
   const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
@@ -655,6 +680,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
     const B live0 = live, trig0 = trig;
     // the slots' timers decided from their ends, 8 slots per memory round trip
     B fire_m = B::none(), ret_m = B::none();
+    int64_t tmin = INT64_MAX;   // the key's first timer to fire (its set is fetched then)
     if (live.any()) {
       const int64_t* en = d.end + kid * d.sw;
       for (int g = 0; g < 8 * NW; ++g) {
@@ -680,10 +706,17 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
           }
           if (fire) fire_m.set(q);
           if (retire) ret_m.set(q);
+          if (fire || retire) tmin = min(tmin, fire ? max_ts : ct);
         }
       }
       live = live.andnot(ret_m);
       trig = trig.andnot(ret_m);
+      if (tmin != INT64_MAX && d.ktouch[kid] < 0) { d.ktouch[kid] = touch_ord; d.ktts[kid] = tmin; }
+      if (ret_m.any()) {   // the retired windows' state entries cleared
+        const int64_t key = kid_key(s, kid);
+        const int32_t kkg = record_key_group(s, long_hash_code(key));
+        for (B m = ret_m; m.any();) sess_ns_remove(d, kkg, key, kid * d.sw + m.pop(), touch_ord);
+      }
     }
     // the fires (list state: and the retired windows' elements freed), the wave's appends aggregated
     B todo = d.list ? (fire_m | ret_m) : fire_m;
@@ -785,6 +818,23 @@ int session_create(fw_engine* e) {
   }
   d.live = e->alloc<unsigned long long>((size_t)s.stride * d.nw);
   d.trig = e->alloc<unsigned long long>((size_t)s.stride * d.nw);
+  d.sws = e->alloc<int64_t>(cells);
+  d.swc = e->alloc<int64_t>(cells);
+  d.put = e->alloc<int64_t>(cells);
+  d.cre = e->alloc<int64_t>(cells);
+  d.tre = e->alloc<int64_t>(cells);
+  d.ktouch = e->alloc<int64_t>((size_t)s.stride);
+  d.ktts = e->alloc<int64_t>((size_t)s.stride);
+  d.kacc = e->alloc<int32_t>((size_t)s.stride);
+  {
+    uint64_t m = 1024;
+    while (m < 2 * (uint64_t)cells) m <<= 1;
+    d.nsmask = m - 1;
+    d.nscnt = e->alloc<int32_t>((size_t)m);
+    d.nslog_cap = std::max<int64_t>(1 << 16, 2 * e->cfg.max_batch);
+    d.nslog = e->alloc<int64_t>(4 * (size_t)d.nslog_cap);
+    d.nslog_n = e->alloc<unsigned long long>(1);
+  }
   e->s.o.win_start = e->alloc<int64_t>((size_t)e->cfg.out_capacity);
   const size_t nb = (size_t)e->cfg.max_batch;
   e->sess_key = e->alloc<unsigned long long>(nb);
@@ -803,6 +853,10 @@ int session_create(fw_engine* e) {
     HIPCHK(e, hipMemsetAsync(d.len, 0, 8 * cells, e->stream));
   }
   HIPCHK(e, hipMemsetAsync(d.trig, 0, 8 * (size_t)s.stride * d.nw, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.ktouch, 0xff, 8 * (size_t)s.stride, e->stream));   // -1: no key's set fetched yet
+  HIPCHK(e, hipMemsetAsync(d.kacc, 0, 4 * (size_t)s.stride, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.nscnt, 0, 4 * (size_t)(d.nsmask + 1), e->stream));
+  HIPCHK(e, hipMemsetAsync(d.nslog_n, 0, 8, e->stream));
   return FW_OK;
 }
 
@@ -835,9 +889,9 @@ int session_watermark(fw_engine* e, int64_t wm) {
   if (wm > e->cur_wm) {
     e->phase_begin(FW_PHASE_FIRE);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid));
-    if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_wm<1>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
-    else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_wm<2>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
-    else hipLaunchKernelGGL(k_sess_wm<4>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm);
+    if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_wm<1>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
+    else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_wm<2>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
+    else hipLaunchKernelGGL(k_sess_wm<4>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
     e->phase_end(e->s.stride);
     session_pool_recycle(e);   // the entries of the windows purged
     e->cur_wm = wm;

@@ -67,8 +67,8 @@ extern "C" {
                                     produces (state window = the first one's; the others reduced / their lists
                                     appended in that order), so f1, ties and double sums match the reference.
                                     At most 256 in-flight sessions per key (max_open_slices, default 32:
-                                    FW_ERR_CAPACITY beyond).  No checkpoint (the merging-window set is keyed
-                                    list state of its own). */
+                                    FW_ERR_CAPACITY beyond).  Reference-layout checkpoints with the
+                                    merging-window set (fw_snapshot_kg_flink, reducing state). */
 
 /* ---- trigger (SJ/api/windowing/triggers) ---- */
 #define FW_TRIGGER_EVENT_TIME          0   /* EventTimeTrigger.create()                    */
@@ -268,7 +268,15 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * folded with the pane (the layout names the one aggregate).  List state (FW_AGG_LIST, tumbling windows only):
  * the state is ListSerializer's `int size | element * size`, each element the window's input tuple with the
  * fields the layout names — FW_SF_VALUE once, FW_SF_KEY and FW_SF_F1 at most once each — in arrival order.
- * Session windows: FW_ERR_UNSUPPORTED (their "merging-window-set" state is not written).
+ * Session windows (reducing state): two tables, ids in stateTables' HashMap order (WindowOperator.java:445-460,
+ * 724-736): short 0 "window-contents" as above, its namespaces the in-flight windows' STATE windows (a session's
+ * first window [ts, ts + gap): MergingWindowSet keeps the first merged window's state window), then short 1
+ * "merging-window-set" | byte present | [int 0 or 1 | byte 0 (VoidNamespace) | int n | (long key | int m |
+ * (long start | long end | long stateStart | long stateEnd) * m) * n] (ListState<Tuple2<W, W>>,
+ * MergingWindowSet.persist :91-95) as WindowOperator.snapshotState rewrites it: restored entries of keys untouched
+ * since, then every other key with sessions in flight in mergingWindowsByKey's order.  Timers: each in-flight
+ * window's pending trigger timer and its cleanup timer.  Not for session list state or PurgingTrigger with
+ * allowed lateness > 0 (FW_ERR_UNSUPPORTED).
  * Namespaces, entries and timers come in java.util.HashMap iteration order for
  * tables sized by their current size (when a JVM table iterates differently).
  * A buffer argument NULL (or too small: FW_ERR_CAPACITY) stores the required lengths only.
