@@ -5634,7 +5634,7 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
   if (state_len > 0) {
     fwkg::BeIn in(state, state_len);
     if (in.i32() != kg) return reject(e, FW_ERR_INVALID_ARG, "state section of another key group");
-    for (int table = 0; in.ok && in.pos < in.n; ++table) {
+    for (int table = 0; in.ok && (table == 0 || in.pos < in.n); ++table) {   // (at least one table)
       if (in.i16() != table || table > 1) return reject(e, FW_ERR_UNSUPPORTED, "keyed state other than window-contents and merging-window-set");
       const bool present = in.u8() != 0;
       if (table == 0) {

@@ -935,7 +935,8 @@ int restoreKeyGroup(Operator& op, int32_t kg, const fw_state_layout& L, int64_t 
     const bool session = op.cfg.assigner == FW_SESSION;
     const int32_t written = in.readInt();
     if (written != kg) { op.err = "bad key-group section"; return FW_ERR_INVALID_ARG; }
-    for (int table = 0; !in.eof && in.pos < sn; ++table) {
+    int tables = 0;
+    for (int table = 0; !in.eof && (table == 0 || in.pos < sn); ++table, ++tables) {
     const int stateId = in.readShort();
     const int present = in.readByte();
     if (stateId != table || table > (session ? 1 : 0)) { op.err = "bad key-group section"; return FW_ERR_INVALID_ARG; }
@@ -1004,7 +1005,7 @@ int restoreKeyGroup(Operator& op, int32_t kg, const fw_state_layout& L, int64_t 
       }
     }
     }
-    if (in.eof || in.pos != sn) { op.err = "state section truncated or with trailing bytes"; return FW_ERR_INVALID_ARG; }
+    if (in.eof || in.pos != sn || tables == 0) { op.err = "state section truncated or with trailing bytes"; return FW_ERR_INVALID_ARG; }
   }
   JavaIn in{tb, tn};
   const int32_t n = in.readInt();

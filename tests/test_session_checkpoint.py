@@ -151,6 +151,15 @@ def test_session_checkpoint(case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", [CASES[1], CASES[3]], ids=["f64-late400", "maxBy-late250"])
+def test_session_checkpoint_hot_walk(case, monkeypatch):
+    """The same with FW_SESS_HOT=4: keys with >= 4 records in a batch are walked by k_sess_walk_hot (one wave per
+    key), which keeps the same checkpoint bookkeeping (state windows, put / timer ordinals, namespace log)."""
+    monkeypatch.setenv("FW_SESS_HOT", "4")
+    test_session_checkpoint(case)
+
+
+@pytest.mark.gpu
 def test_session_restore_at_long_min():
     """As the oracle: a restore at Long.MIN_VALUE re-arms fired-but-kept sessions on their next record."""
     from flink_amd.windowing import WindowEngine
