@@ -467,6 +467,11 @@ struct BatchIn {
   unsigned long long* late_count;
   int64_t late_capacity;
   int32_t idx_bits;
+  // direct form, maxBy / minBy: every accepted record, (pane id << idx_bits) | idx, folded per pane in arrival
+  // order after the launch (the late path's sort, segmented scan and commit, without fires)
+  unsigned long long* by_key;
+  unsigned long long* by_count;
+  int64_t by_capacity;
   // sliding windows: one fire element per (record, window in its lateness period past maxTimestamp)
   unsigned long long* fire_key;   // (window pane id << idx_bits) | idx, window pane = floor_mod(n, P) * stride + kid
   unsigned long long* fire_count;
@@ -595,7 +600,16 @@ __global__ __launch_bounds__(BLOCK) void k_ingest_direct(Spec s, BatchIn b) {
       live = false;
     }
     int64_t idx = 0;
-    if (live) {
+    constexpr bool BY = (AGG & (FW_AGG_MAXBY | FW_AGG_MINBY)) != 0;
+    if (BY && live) {
+      // maxBy / minBy: the extremal record, a tie to the earlier (or later) arrival — an order atomics do not
+      // give; the record is listed and folded in arrival order per pane after the launch
+      idx = (int64_t)p * s.stride + kid;
+      const unsigned long long pos = atomicAdd(b.by_count, 1ull);
+      if ((int64_t)pos < b.by_capacity) b.by_key[pos] = ((unsigned long long)idx << b.idx_bits) | (unsigned long long)i;
+      else cap_error(s, 23);
+      b.new_list[i] = -1;
+    } else if (live) {
       idx = (int64_t)p * s.stride + kid;
       if (FIRST) {
         (void)pane_update<VT, AGG, false, true>(s, idx, v, 0);   // the reduce columns
@@ -2168,7 +2182,7 @@ __global__ void k_late_emit(Spec s, const unsigned long long* sorted_key, int64_
 // write the pane state after the batch's per-element fires (segment tails)
 __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int64_t nl, int32_t idx_bits,
                               const unsigned long long* seg, const LateAcc* scanned, const int64_t* f1col,
-                              int64_t ord_base, const int64_t* headpos) {
+                              int64_t ord_base, const int64_t* headpos, bool fired = true) {
   int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nl) return;
   unsigned long long pane = seg[j];
@@ -2176,7 +2190,7 @@ __global__ void k_late_commit(Spec s, const unsigned long long* sorted_key, int6
   if (!tail) return;
   int64_t idx = (int64_t)pane;
   int32_t p = (int32_t)(pane / (unsigned long long)s.stride);
-  if (s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) {
+  if (fired && s.trigger == FW_TRIGGER_PURGING_EVENT_TIME && s.assigner == FW_TUMBLING) {
     // FIRE_AND_PURGE after the last element: pane cleared (AbstractHeapState.clear).  (Sliding: the slice
     // also feeds windows that have not fired; a purged window's later per-element fires emit the record
     // alone, k_fire_emit).  The cleanup timer the segment's first record registered stays (s.gfirst)
@@ -3435,6 +3449,8 @@ struct fw_engine {
   int32_t* stg_hash[NBUF] = {};
   // late path
   unsigned long long *late_key = nullptr, *late_key_sorted = nullptr, *late_count = nullptr, *seg = nullptr;
+  bool by_direct = false;                      // maxBy / minBy on the direct form (by_key folded after each launch)
+  unsigned long long *by_key = nullptr, *by_count = nullptr;
   unsigned long long* out_base = nullptr;   // first output slot reserved for a per-element emit kernel
   unsigned long long *fire_key = nullptr, *fire_count = nullptr;   // sliding: per-element fire elements
   int64_t fire_cap = 0;
@@ -3879,8 +3895,6 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
   if ((c.agg_flags & FW_AGGF_FOLD) && (c.keep_first_f1 || !(c.agg_mask == FW_AGG_SUM || c.agg_mask == FW_AGG_MIN ||
                                                               c.agg_mask == FW_AGG_MAX || c.agg_mask == FW_AGG_COUNT)))
     return unsupported("fold: one aggregate (sum, count, min or max) from the initial value, no first-arrival f1");
-  if (by && c.ingest_mode == 1 && !e->session)
-    return unsupported("maxBy / minBy run on the partitioned ingest form (ingest_mode 0 or 2)");
   if (c.key_capacity <= 0 || c.max_batch <= 0 || c.out_capacity <= 0) return bad("capacities must be > 0");
   if (c.ingest_mode < 0 || c.ingest_mode > 3) return bad("bad ingest mode");
   HIPCHK(e, hipSetDevice(c.device));
@@ -4062,8 +4076,7 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
     if (c.ingest_mode == 2 && !fits)
       return unsupported("partitioned ingest needs <= 4096 directory slots per bucket (key_capacity <= 256 Ki)");
     e->routed = !e->session && (c.ingest_mode == 2 || (c.ingest_mode == 0 && fits && (c.max_batch >= (1 << 16) || by)));
-    if (by && !e->routed && !e->session)
-      return unsupported("maxBy / minBy need the partitioned ingest form (key_capacity <= 256 Ki)");
+    e->by_direct = by && !e->routed && !e->session;
     if (e->routed) {
       e->max_tiles = max_tiles;
       const size_t cap = (size_t)max_tiles * RT_TILE;
@@ -4125,8 +4138,14 @@ int fw_create(const fw_config* cfg_in, fw_engine** out) {
 
   for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
 
-  // late path (allowed lateness > 0)
-  if (c.allowed_lateness > 0) {
+  if (e->by_direct) {
+    e->by_key = e->alloc<unsigned long long>((size_t)c.max_batch);
+    e->by_count = e->alloc<unsigned long long>(1);
+    for (void* p : e->allocs) if (!p) { delete e; return FW_ERR_DEVICE; }
+    if (hipMemset(e->by_count, 0, 8) != hipSuccess) { delete e; return FW_ERR_DEVICE; }
+  }
+  // late path (allowed lateness > 0; its sort and segmented scan also fold the direct form's maxBy / minBy)
+  if (c.allowed_lateness > 0 || e->by_direct) {
     e->idx_bits = bits_for((uint64_t)c.max_batch);
     int pane_bits = bits_for((uint64_t)P * (uint64_t)s.stride);
     if (e->idx_bits + pane_bits > 64) { delete e; return FW_ERR_UNSUPPORTED; }
@@ -4258,6 +4277,33 @@ static int device_error(fw_engine* e, int32_t derr) {
 
 static int64_t host_window_start(const fw_config& c, int64_t n);   // (below, with the checkpoint code)
 
+// sort (pane << idx_bits | batch index) keys, then the per-pane inclusive scan of the records' accumulators in
+// arrival order (k_late_prepare, k_segscan_*); emit_n > 0 reserves that many output rows for per-element fires
+static int late_sorted_scan(fw_engine* e, unsigned long long* keys, unsigned long long n, int64_t emit_n,
+                            const int64_t* dv, const int64_t* df1) {
+  const int key_bits = std::min(64, e->idx_bits + bits_for((uint64_t)e->s.P * (uint64_t)e->s.stride));
+  size_t tb = e->temp_bytes;
+  HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, keys, e->late_key_sorted, (size_t)n, 0, key_bits, e->stream));
+  const int blocks = (int)((n + BLOCK - 1) / BLOCK);
+  hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)n,
+                     e->idx_bits, dv, e->seg, e->late_acc, e->headpos, df1, e->ordinal, emit_n, e->out_base);
+  const int32_t ntl = (int32_t)((n + LS_TILE - 1) / LS_TILE);
+  hipLaunchKernelGGL(k_segscan_tile, dim3(ntl), dim3(LS_T), 0, e->stream, e->seg, e->late_acc, (int64_t)n,
+                     e->late_scan, e->headpos_scan, e->seg_tiles, e->seg_first);
+  const SegPart* grp = nullptr;
+  if (ntl > LS_CT) {   // two levels (one workgroup's serial chunks took ~90 us at 4 K tiles)
+    const int32_t ng = (ntl + LS_CT - 1) / LS_CT;
+    hipLaunchKernelGGL(k_segscan_carry_grp, dim3(ng), dim3(LS_CT), 0, e->stream, e->seg_tiles, ntl, e->seg_groups);
+    hipLaunchKernelGGL(k_segscan_carry, dim3(1), dim3(LS_CT), 0, e->stream, e->seg_groups, ng);
+    grp = e->seg_groups;
+  } else {
+    hipLaunchKernelGGL(k_segscan_carry, dim3(1), dim3(LS_CT), 0, e->stream, e->seg_tiles, ntl);
+  }
+  hipLaunchKernelGGL(k_segscan_apply, dim3(ntl), dim3(LS_T), 0, e->stream, e->seg_tiles, grp, e->seg_first, (int64_t)n,
+                     e->late_scan, e->headpos_scan);
+  return FW_OK;
+}
+
 int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, const int64_t* f1, const int64_t* ts,
                   const void* value, int64_t n, int32_t mem) {
   if (!e) return FW_ERR_INVALID_ARG;
@@ -4320,6 +4366,9 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   b.late_count = e->late_count;
   b.late_capacity = e->late_key ? e->cfg.max_batch : 0;
   b.idx_bits = e->idx_bits;
+  b.by_key = e->by_key;
+  b.by_count = e->by_count;
+  b.by_capacity = e->by_key ? e->cfg.max_batch : 0;
   b.fire_key = e->fire_key;
   b.fire_count = e->fire_count;
   b.fire_capacity = e->fire_cap;
@@ -4339,6 +4388,21 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
   } else {
     e->phase_begin(FW_PHASE_INGEST);
     FW_DISPATCH(launch_ingest_t, e, b);
+    if (e->by_direct) {
+      // maxBy / minBy: the listed records folded per pane in arrival order into the panes (the late path's
+      // commit, no fires); the list length read back sizes the sort
+      unsigned long long nb = 0;
+      HIPCHK(e, hipMemcpyAsync(&nb, e->by_count, 8, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      nb = std::min<unsigned long long>(nb, (unsigned long long)e->cfg.max_batch);
+      if (nb > 0) {
+        if (int rc = late_sorted_scan(e, e->by_key, nb, 0, dv, df1)) return rc;
+        hipLaunchKernelGGL(k_late_commit, dim3((unsigned)((nb + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, e->stream, e->s,
+                           e->late_key_sorted, (int64_t)nb, e->idx_bits, e->seg, e->late_scan, df1, e->ordinal,
+                           e->headpos_scan, false);
+      }
+      HIPCHK(e, hipMemsetAsync(e->by_count, 0, 8, e->stream));
+    }
     e->phase_end(n);
   }
   // sliding: this batch's extra-window records into the window panes.  A record gets an extra window only
@@ -4382,26 +4446,7 @@ int fw_push_batch(fw_engine* e, const int64_t* key, const int32_t* key_hash, con
     // keys are (pane << idx_bits) | batch index, pane < P * stride: only their low bits are sorted
     const int key_bits = std::min(64, e->idx_bits + bits_for((uint64_t)e->s.P * (uint64_t)e->s.stride));
     auto sorted_scan = [&](unsigned long long* keys, unsigned long long n, int64_t emit_n) -> int {
-      size_t tb = e->temp_bytes;
-      HIPCHK(e, rocprim::radix_sort_keys(e->temp, tb, keys, e->late_key_sorted, (size_t)n, 0, key_bits, e->stream));
-      const int blocks = (int)((n + BLOCK - 1) / BLOCK);
-      hipLaunchKernelGGL(k_late_prepare, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->late_key_sorted, (int64_t)n,
-                         e->idx_bits, dv, e->seg, e->late_acc, e->headpos, df1, e->ordinal, emit_n, e->out_base);
-      const int32_t ntl = (int32_t)((n + LS_TILE - 1) / LS_TILE);
-      hipLaunchKernelGGL(k_segscan_tile, dim3(ntl), dim3(LS_T), 0, e->stream, e->seg, e->late_acc, (int64_t)n,
-                         e->late_scan, e->headpos_scan, e->seg_tiles, e->seg_first);
-      const SegPart* grp = nullptr;
-      if (ntl > LS_CT) {   // two levels (one workgroup's serial chunks took ~90 us at 4 K tiles)
-        const int32_t ng = (ntl + LS_CT - 1) / LS_CT;
-        hipLaunchKernelGGL(k_segscan_carry_grp, dim3(ng), dim3(LS_CT), 0, e->stream, e->seg_tiles, ntl, e->seg_groups);
-        hipLaunchKernelGGL(k_segscan_carry, dim3(1), dim3(LS_CT), 0, e->stream, e->seg_groups, ng);
-        grp = e->seg_groups;
-      } else {
-        hipLaunchKernelGGL(k_segscan_carry, dim3(1), dim3(LS_CT), 0, e->stream, e->seg_tiles, ntl);
-      }
-      hipLaunchKernelGGL(k_segscan_apply, dim3(ntl), dim3(LS_T), 0, e->stream, e->seg_tiles, grp, e->seg_first, (int64_t)n,
-                         e->late_scan, e->headpos_scan);
-      return FW_OK;
+      return late_sorted_scan(e, keys, n, emit_n, dv, df1);
     };
     if (nf > 0) {   // sliding: the fires first, against the slices before this batch's late records
       if (int rc = sorted_scan(e->fire_key, nf, (int64_t)nf)) return rc;

@@ -125,11 +125,8 @@ def test_parity_with_ties(name, vt, window, mode):
     from flink_amd.windowing import WindowEngine
     from oracle.oracle import OracleEngine
     red, col = _agg(name, vt)
-    if mode == 1 and red.by:
-        from flink_amd import _abi
-        with pytest.raises(_abi.FwError):
-            WindowEngine(_cfg(red, ingest_mode=1))   # maxBy/minBy run on the partitioned form only
-        return
+    # (mode 1, the direct form: maxBy / minBy records are listed and folded per pane in arrival order after each
+    # launch — the late path's sort, segmented scan and commit)
     if window == "sliding":
         cfg = _cfg(red, SlidingEventTimeWindows.of(3000, 1000), ingest_mode=mode)
     elif window == "late":

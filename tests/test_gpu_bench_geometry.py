@@ -31,7 +31,7 @@ def _stream(j, batch, n_keys, rate, vt="i64", zipf=None, ooo=0):
     return k, t, v
 
 
-def _run(cfg, batches, batch, n_keys, rate, lag, zipf=None, ooo=0, fields=("sum_i64",)):
+def _run(cfg, batches, batch, n_keys, rate, lag, zipf=None, ooo=0, fields=("sum_i64",), levels=None):
     from flink_amd.windowing import WindowEngine
     from oracle.oracle import OracleEngine
     eg, eo = WindowEngine(cfg), OracleEngine(cfg)
@@ -39,6 +39,8 @@ def _run(cfg, batches, batch, n_keys, rate, lag, zipf=None, ooo=0, fields=("sum_
     max_ts = -(1 << 63)
     for j in range(batches):
         k, t, v = _stream(j, batch, n_keys, rate, zipf=zipf, ooo=ooo)
+        if levels:   # few distinct values: ties
+            v = v % levels
         max_ts = max(max_ts, int(t.max().item()))
         wm = max_ts - lag
         eg.push(k, t, v)
@@ -240,6 +242,21 @@ def test_c2_ten_million_keys():
     sg, so = _run(cfg, 4, batch, 10_000_000, 1 << 22, 1)
     assert sg["ingest_form"] == 1   # direct: a 10 M-key directory bucket does not fit LDS
     assert sg["panes_fired"] == so["panes_fired"] > 0
+
+
+@pytest.mark.parametrize("field,first", [("maxBy", True), ("minBy", False)])
+def test_max_by_above_256k_keys(field, first):
+    """maxBy / minBy with a key directory too large for the partitioned form (1 Mi keys of capacity, 600 K keys
+    live): the direct ingest form folds the extremal records per pane in arrival order (ties by first / last
+    arrival, ComparableAggregator.java:74-81).  Values drawn from 16 levels, so ties are everywhere; bit-exact
+    (key, window, f1 = the record's timestamp, value) against the oracle."""
+    from flink_amd.windowing import Aggregations, TumblingEventTimeWindows, make_config
+    red = getattr(Aggregations, field)("i64", first=first)
+    cfg = make_config(TumblingEventTimeWindows.of(1000), red, max_parallelism=128, key_capacity=1 << 20,
+                      max_batch=1 << 20, out_capacity=1 << 22, max_open_slices=3)
+    sg, _ = _run(cfg, 4, 1 << 20, 600_000, 1 << 20, 1, fields=(("max_i64",) if field == "maxBy" else ("min_i64",)),
+                 levels=16)
+    assert sg["ingest_form"] == 1
 
 
 def test_c5_one_rank_shard():
