@@ -3427,6 +3427,9 @@ struct fw_engine {
   // fw_restore_kg_flink: each restored timer's position in the timer sections (restoreTimersForKeyGroup adds
   // them to the set in that order, so later snapshots list them in it within a hash bucket)
   std::map<std::array<int64_t, 4>, int64_t> restored_timer_rank;
+  // sliding-window list state restored in the reference layout: each (window start, key) entry's place in its
+  // namespace's insertion order (blob order; the elements' ordinals follow the merged arrival order instead)
+  std::map<std::pair<int64_t, int64_t>, int64_t> list_entry_rank;
   // session windows' checkpoints: the state tables a restore brought, per key group whether its
   // "merging-window-set" map exists (a snapshot wrote an entry or a restore read it present), the restored
   // merging-window-set entries (key -> rank in blob order), and the device state read back for snapshots
@@ -5378,6 +5381,10 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
   }
   for (auto& kv : win) {   // (sliding: a window restored disarmed and not re-armed for the key)
     kv.second.unarmed = e->snap_unarmed.count({kv.first.first, kv.first.second}) != 0;
+    if (!e->list_entry_rank.empty()) {   // a restored list entry keeps its place in the namespace's insertion order
+      auto it = e->list_entry_rank.find({kv.second.start, kv.second.key});
+      if (it != e->list_entry_rank.end()) kv.second.first = it->second - e->ordinal;
+    }
     out.push_back(kv.second);
   }
 }
@@ -5817,9 +5824,6 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
     if (int rc = check_state_layout(e, layout)) return rc;
     return session_snapshot_kg_flink(e, kg, layout, state, state_cap, state_len, timers, timers_cap, timers_len);
   }
-  if (e->list && e->cfg.assigner != FW_TUMBLING)
-    return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows: a record is in several windows' lists, which "
-                                         "the engine's slices hold once");
   if (e->sticky) return e->sticky;
   if (kg < e->s.kg_start || kg > e->s.kg_end)
     return reject(e, FW_ERR_INVALID_ARG, "Key Group " + std::to_string(kg) + " does not belong to the local range.");
@@ -5874,7 +5878,17 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
         for (size_t i : ent) {
           st.i64(panes[i].key);
           if (e->list) {   // ListSerializer.serialize: int size, then every element in insertion order
-            const auto& el = e->snap_list.at({panes[i].m, panes[i].key});
+            // (sliding: the window's list holds its slices' elements of the key, merged in arrival order)
+            std::vector<std::array<int64_t, 3>> merged;
+            if (c.assigner == FW_SLIDING) {
+              const int64_t n = fw::floor_div(fw::jsub(panes[i].start, c.offset), c.slide);
+              for (int64_t mm = n * e->s.R; mm < n * e->s.R + e->s.K; ++mm) {
+                auto it = e->snap_list.find({mm, panes[i].key});
+                if (it != e->snap_list.end()) merged.insert(merged.end(), it->second.begin(), it->second.end());
+              }
+              std::sort(merged.begin(), merged.end());
+            }
+            const auto& el = c.assigner == FW_SLIDING ? merged : e->snap_list.at({panes[i].m, panes[i].key});
             st.i32((int32_t)el.size());
             for (const auto& x : el)
               for (int f = 0; f < layout->n_fields; ++f) {
@@ -5982,6 +5996,102 @@ static int restore_list_elements(fw_engine* e, const std::vector<KgPane>& panes,
   return FW_OK;
 }
 
+// Sliding-window list state (slide dividing the size: a slice per slide, window n = slices n .. n + K - 1): the
+// reference holds each window's list; the engine holds each record once, in its slice.  Per key, the windows are
+// peeled newest first: window n's list, less the elements of slices n + 1 .. n + K - 1 (known from the newer
+// windows, matched in order as a subsequence), is slice n; its elements join the key's arrival order right after
+// the element they follow in the list.  Every window's list is then rebuilt from the slices and checked; the
+// elements get ordinals in that arrival order, ahead of every later record
+static int restore_sliding_lists(fw_engine* e, int64_t wm, const std::vector<KgPane>& panes, const std::vector<int64_t>& win,
+                                 const std::vector<std::vector<std::array<int64_t, 2>>>& lists) {
+  const fw::Spec& s = e->s;
+  const int64_t K = s.K;
+  std::map<int64_t, std::map<int64_t, size_t>> by_key;   // key -> window -> entry
+  for (size_t i = 0; i < panes.size(); ++i) {
+    by_key[panes[i].key][win[i]] = i;
+    e->list_entry_rank[{panes[i].start, panes[i].key}] = e->restore_ord++;
+  }
+  struct El { int64_t v, f1, m; };
+  std::map<std::pair<int64_t, int64_t>, std::vector<std::array<int64_t, 3>>> slices;   // (slice, key) -> (ord, v, f1)
+  for (const auto& kw : by_key) {
+    const int64_t key = kw.first;
+    const auto& wins = kw.second;
+    std::vector<El> order;
+    for (int64_t n = wins.rbegin()->first; n >= wins.begin()->first; --n) {
+      std::vector<size_t> T;   // the key's known elements of window n's newer slices, in arrival order
+      for (size_t q = 0; q < order.size(); ++q)
+        if (order[q].m > n && order[q].m < n + K) T.push_back(q);
+      auto it = wins.find(n);
+      if (it == wins.end()) {
+        if (!T.empty()) return reject(e, FW_ERR_INVALID_ARG, "a window of the key is missing between its windows");
+        continue;
+      }
+      std::vector<std::pair<size_t, El>> ins;   // (insert after this order index, or SIZE_MAX: at the front)
+      size_t t = 0, pred = SIZE_MAX;
+      for (const auto& x : lists[it->second]) {
+        if (t < T.size() && order[T[t]].v == x[0] && order[T[t]].f1 == x[1]) { pred = T[t++]; continue; }
+        ins.push_back({pred, El{x[0], x[1], n}});
+      }
+      if (t != T.size()) return reject(e, FW_ERR_INVALID_ARG, "the windows' lists of a key do not share their slices");
+      std::vector<El> next;
+      next.reserve(order.size() + ins.size());
+      size_t k = 0;
+      while (k < ins.size() && ins[k].first == SIZE_MAX) next.push_back(ins[k++].second);
+      for (size_t q = 0; q < order.size(); ++q) {
+        next.push_back(order[q]);
+        while (k < ins.size() && ins[k].first == q) next.push_back(ins[k++].second);
+      }
+      order.swap(next);
+    }
+    for (const auto& w : wins) {   // every window's list rebuilt from the slices
+      const auto& want = lists[w.second];
+      size_t j = 0;
+      for (const El& x : order) {
+        if (x.m < w.first || x.m >= w.first + K) continue;
+        if (j >= want.size() || want[j][0] != x.v || want[j][1] != x.f1)
+          return reject(e, FW_ERR_UNSUPPORTED, "sliding-window lists with equal elements in an order no slice split gives");
+        ++j;
+      }
+      if (j != want.size()) return reject(e, FW_ERR_UNSUPPORTED, "sliding-window lists with equal elements in an order no slice split gives");
+    }
+    for (const El& x : order) slices[{x.m, key}].push_back({e->restore_ord++, x.v, x.f1});
+  }
+  // the slices and keys into the directory and the slice table, then their elements into the slices' buffers
+  std::vector<int64_t> ent;
+  for (const auto& kv : slices) {
+    const int64_t w[FW_SNAP_ENTRY_WORDS] = {kv.first.first, kv.first.second, 0, INT64_MAX, INT64_MIN, 0, kv.second[0][0], 0};
+    ent.insert(ent.end(), w, w + FW_SNAP_ENTRY_WORDS);
+  }
+  int rc = restore_entries(e, wm, ent.data(), (int64_t)slices.size(), 0);
+  if (rc) return rc;
+  std::vector<int64_t> keys((size_t)s.D);
+  HIPCHK(e, hipMemcpy(keys.data(), s.dir_keys, 8 * (size_t)s.D, hipMemcpyDeviceToHost));
+  std::map<int64_t, int64_t> kid_of;
+  for (int64_t k = 0; k < s.D; ++k) if (keys[(size_t)k] != fw::EMPTY_KEY) kid_of[keys[(size_t)k]] = k;
+  std::vector<unsigned long long> lc((size_t)s.P);
+  HIPCHK(e, hipMemcpy(lc.data(), e->lst.cnt, 8 * (size_t)s.P, hipMemcpyDeviceToHost));
+  std::map<int32_t, std::vector<int64_t>> rows;   // slot -> elements (kid, ordinal, value, f1)
+  for (const auto& kv : slices) {
+    const int64_t key = kv.first.second;
+    const int64_t kid = key == fw::EMPTY_KEY ? s.D : (kid_of.count(key) ? kid_of[key] : -1);
+    if (kid < 0) return reject(e, FW_ERR_CAPACITY, "restored key not in the key directory");
+    auto& r = rows[(int32_t)fw::floor_mod(kv.first.first, s.P)];
+    for (const auto& x : kv.second) r.insert(r.end(), {kid, x[0], x[1], x[2]});
+  }
+  for (auto& kv : rows) {
+    const int32_t p = kv.first;
+    const int64_t n = (int64_t)(kv.second.size() / LST_WORDS);
+    if ((int64_t)lc[(size_t)p] + n > e->lst.cap)
+      return reject(e, FW_ERR_CAPACITY, "restored list state exceeds list_capacity for its slice");
+    HIPCHK(e, hipMemcpy(e->lst.buf + ((size_t)p * (size_t)e->lst.cap + lc[(size_t)p]) * LST_WORDS, kv.second.data(),
+                        8 * kv.second.size(), hipMemcpyHostToDevice));
+    lc[(size_t)p] += (unsigned long long)n;
+  }
+  HIPCHK(e, hipMemcpy(e->lst.cnt, lc.data(), 8 * (size_t)s.P, hipMemcpyHostToDevice));
+  e->state_epoch++;
+  return FW_OK;
+}
+
 int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout, int64_t watermark,
                         const void* state, int64_t state_len, const void* timers, int64_t timers_len) {
   if (!e || (!state && state_len) || !timers || state_len < 0) return FW_ERR_INVALID_ARG;
@@ -5994,9 +6104,9 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
     if (int rc = check_state_layout(e, layout)) return rc;
     return session_restore_kg_flink(e, kg, layout, watermark, state, state_len, timers, timers_len);
   }
-  if (e->list && e->cfg.assigner != FW_TUMBLING)
-    return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows: a record is in several windows' lists, which "
-                                         "the engine's slices hold once");
+  if (e->list && e->cfg.assigner == FW_SLIDING && e->s.R != 1)
+    return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows whose slide does not divide the size: a "
+                                         "record's slice is not recoverable from the windows' lists");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
   if (kg < e->s.kg_start || kg > e->s.kg_end)
@@ -6140,6 +6250,15 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
     }
   } else if (got != want) {
     return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
+  }
+  if (e->list && sliding) {
+    if (!dis_now.empty())
+      return reject(e, FW_ERR_UNSUPPORTED, "sliding-window list state restored below a window that fired before the "
+                                           "checkpoint");
+    for (const auto& t : got_in_order) e->restored_timer_rank[t] = (int64_t)e->restored_timer_rank.size();
+    if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(s.kg_end - s.kg_start + 1), 0);
+    if (present) e->kg_touched[(size_t)(kg - s.kg_start)] = 1;
+    return restore_sliding_lists(e, watermark, panes, slice_of, lists);
   }
   if (!dis_now.empty() && !e->s.disarm) {   // per-slot flags and per-pane re-arm marks, first needed here
     e->s.disarm = e->alloc<uint8_t>((size_t)s.P);

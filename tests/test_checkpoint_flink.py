@@ -671,15 +671,17 @@ def test_fold_checkpoint(mode, kind, initial, vt, assigner):
                                               for x, y in zip(rg, ro)), w
 
 
-def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "value"), restore_wm=None, pre=None):
-    """Tumbling list state (WindowedStream.apply: HeapListState "window-contents" of the input tuples): drive 2/3
-    of a Zipf stream, snapshot every key group in the reference layout; or restore such sections at their
-    watermark and drive the rest to a final MAX_WATERMARK."""
-    from flink_amd.windowing import ListStateDescriptor, TumblingEventTimeWindows, make_config
+def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "value"), restore_wm=None, pre=None,
+              sliding=False):
+    """List state (WindowedStream.apply: HeapListState "window-contents" of the input tuples), tumbling 1 s windows
+    or (sliding) 3 s windows every 1 s: drive 2/3 of a Zipf stream, snapshot every key group in the reference
+    layout; or restore such sections at their watermark and drive the rest to a final MAX_WATERMARK."""
+    from flink_amd.windowing import ListStateDescriptor, SlidingEventTimeWindows, TumblingEventTimeWindows, make_config
     from harness import drive, gen_stream
     keys, ts, vals = gen_stream(24_000, 1200, rate=1 << 13, zipf=1.1, ooo=300, value_type=vt)
     f1 = np.arange(len(keys), dtype=np.int64) * 7 + 3
-    cfg = make_config(TumblingEventTimeWindows.of(1000), ListStateDescriptor(vt), None, lateness, max_parallelism=128,
+    asg = SlidingEventTimeWindows.of(3000, 1000) if sliding else TumblingEventTimeWindows.of(1000)
+    cfg = make_config(asg, ListStateDescriptor(vt), None, lateness, max_parallelism=128,
                       key_capacity=1 << 12, max_batch=1 << 12, out_capacity=1 << 20, ingest_mode=mode)
     n = len(keys) * 2 // 3
     wm = int(ts[:n].max()) - 100
@@ -736,14 +738,49 @@ def test_list_checkpoint(mode, vt, lateness):
     assert eg == eo and sum(len(r) for _, r in eo) > 1000
 
 
+@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 800)])
+def test_oracle_sliding_list_checkpoint_round_trip(vt, lateness):
+    """Sliding windows' list state: every window's list of its elements (a record sits in each of its windows'
+    lists) restores and snapshots back byte for byte in the oracle."""
+    from oracle.oracle import OracleEngine
+    snaps = _list_run(OracleEngine, vt, lateness, 0, sliding=True)
+    assert sum(len(s) for s, _ in snaps.values()) > 128 * 8
+    back, _ = _list_run(OracleEngine, vt, lateness, 0, restore=snaps, sliding=True)
+    assert _diff(back, snaps) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 800)])
+def test_sliding_list_checkpoint(mode, vt, lateness):
+    """Sliding-window list state in the reference layout (round 6): the engine writes each window's list — its
+    slices' elements of the key merged in arrival order — byte-identical to the oracle's; it restores the oracle's
+    sections by peeling the windows newest first (a window's list less the elements of its newer slices, matched in
+    order, is its oldest slice), writes them back unchanged, and continues exactly as the oracle restored from the
+    same bytes."""
+    from flink_amd.windowing import WindowEngine
+    from harness import epochs_of
+    from oracle.oracle import OracleEngine
+    g = _list_run(WindowEngine, vt, lateness, mode, sliding=True)
+    o = _list_run(OracleEngine, vt, lateness, 0, sliding=True)
+    assert _diff(g, o) is None, _diff(g, o)
+    back, out_g = _list_run(WindowEngine, vt, lateness, mode, restore=o, sliding=True)
+    _, out_o = _list_run(OracleEngine, vt, lateness, 0, restore=o, sliding=True)
+    assert _diff(back, o) is None, _diff(back, o)
+    field = f"sum_{vt}"
+    eg, eo = _canon(epochs_of(out_g, [field], True)), _canon(epochs_of(out_o, [field], True))
+    assert eg == eo and sum(len(r) for _, r in eo) > 1000
+
+
 @pytest.mark.gpu
 def test_list_checkpoint_rejections():
-    """Sliding-window list state takes no reference-layout checkpoint."""
+    """Sliding-window list state whose slide does not divide the size (windows overlap by partial slides) takes no
+    reference-layout restore."""
     from flink_amd import _abi
     from flink_amd.windowing import ListStateDescriptor, SlidingEventTimeWindows, WindowEngine, make_config
-    e = WindowEngine(make_config(SlidingEventTimeWindows.of(2000, 1000), ListStateDescriptor()))
+    e = WindowEngine(make_config(SlidingEventTimeWindows.of(3000, 2000), ListStateDescriptor()))
     with pytest.raises(_abi.FwError) as ei:
-        e.snapshot_kg_flink(0, ("key", "f1", "value"))
+        e.restore_kg_flink(0, ("key", "f1", "value"), b"", struct.pack(">ii", 0, 0))
     assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
     e.close()
 
