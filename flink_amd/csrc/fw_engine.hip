@@ -3430,6 +3430,12 @@ struct fw_engine {
   // sliding-window list state restored in the reference layout: each (window start, key) entry's place in its
   // namespace's insertion order (blob order; the elements' ordinals follow the merged arrival order instead)
   std::map<std::pair<int64_t, int64_t>, int64_t> list_entry_rank;
+  // sliding windows under PurgingTrigger with allowed lateness: a fired window's state is purged (its slices stay
+  // for the windows sharing them) while each key whose first element preceded the fire keeps its cleanup timer.
+  // adv_log: (watermark, arrival ordinal) of each advance (and of the restore), to tell when a window fired;
+  // sl_ghost: restored cleanup timers without state, (window start, key)
+  std::vector<std::pair<int64_t, int64_t>> adv_log;
+  std::set<std::pair<int64_t, int64_t>> sl_ghost;
   // session windows' checkpoints: the state tables a restore brought, per key group whether its
   // "merging-window-set" map exists (a snapshot wrote an entry or a restore read it present), the restored
   // merging-window-set entries (key -> rank in blob order), and the device state read back for snapshots
@@ -4582,6 +4588,9 @@ int fw_advance_watermark(fw_engine* e, int64_t wm) {
   e->state_epoch++;
   if (e->session) return session_watermark(e, wm);
   if (e->list) return list_watermark(e, wm);
+  if (wm > e->cur_wm && e->cfg.trigger == FW_TRIGGER_PURGING_EVENT_TIME && e->cfg.allowed_lateness > 0 &&
+      e->cfg.assigner == FW_SLIDING)
+    e->adv_log.push_back({wm, e->ordinal});
   if (e->s.gtag && wm > e->cur_wm) {
     int rc = ghost_advance(e, e->cur_wm, wm);
     if (rc) return rc;
@@ -5831,14 +5840,34 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
   int rc = check_state_layout(e, layout);
   if (rc) return rc;
   const fw_config& c = e->cfg;
-  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0 && c.assigner != FW_TUMBLING)
-    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows under PurgingTrigger with allowed lateness: purged windows "
-                                         "keep timers the engine does not hold");
+  const bool sl_purge = c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0 && c.assigner == FW_SLIDING;
+  if (sl_purge && !e->s.first)
+    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows under PurgingTrigger with allowed lateness need first-arrival "
+                                         "tracking (keep_first_f1) to tell which keys' cleanup timers outlive a purge");
   HIPCHK(e, hipSetDevice(e->dev));
   rc = build_snapshot(e);
   if (rc) return rc;
   std::vector<KgPane> panes;
   kg_panes(e, kg, panes);
+  struct Ghost { int64_t key, start, end, first; };
+  std::vector<Ghost> sl_ghosts;
+  if (sl_purge) {   // fired windows: no state (FIRE_AND_PURGE); cleanup timers of the keys that had an element before
+    std::vector<KgPane> kept;
+    std::set<std::pair<int64_t, int64_t>> seen;
+    for (const KgPane& p : panes) {
+      const int64_t max_ts = fw::jsub(p.end, 1);
+      if (max_ts > e->cur_wm) { kept.push_back(p); continue; }
+      int64_t fire_ord = 0;   // the arrival ordinal at the advance that fired the window (or the restore)
+      for (const auto& a : e->adv_log) if (a.first >= max_ts) { fire_ord = a.second; break; }
+      if (p.first + e->ordinal < fire_ord && seen.insert({p.start, p.key}).second) sl_ghosts.push_back({p.key, p.start, p.end, p.first});
+    }
+    for (const auto& g : e->sl_ghost) {   // restored ones
+      const int64_t end = fw::jadd(g.first, c.size);
+      if (fw::cleanup_time(fw::jsub(end, 1), c.allowed_lateness) <= e->cur_wm || host_key_group(e->s, g.second) != kg) continue;
+      if (seen.insert({g.first, g.second}).second) sl_ghosts.push_back({g.second, g.first, end, INT64_MIN});
+    }
+    panes.swap(kept);
+  }
   const bool first = e->s.first;
   bool any_state = e->snap_any_key;
   for (uint8_t t : e->kg_touched) any_state = any_state || t;
@@ -5917,6 +5946,8 @@ int fw_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout
     if (max_ts > e->cur_wm && !p.unarmed) tv.push_back({p.key, p.start, p.end, max_ts, p.first, 0, INT64_MAX});
     if (ct != max_ts || max_ts <= e->cur_wm) tv.push_back({p.key, p.start, p.end, ct, p.first, 1, INT64_MAX});
   }
+  for (const Ghost& g : sl_ghosts)
+    tv.push_back({g.key, g.start, g.end, fw::cleanup_time(fw::jsub(g.end, 1), c.allowed_lateness), g.first, 1, INT64_MAX});
   // purged windows' cleanup timers (no state; a key whose window holds state again has the timer above)
   if (!e->snap_gkg.empty()) {
     std::set<std::pair<int64_t, int64_t>> has;
@@ -6118,6 +6149,11 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
   const bool sliding = c.assigner == FW_SLIDING;
   if (e->restored && watermark != e->cur_wm)
     return reject(e, FW_ERR_INVALID_ARG, "key groups restored at different watermarks");
+  const bool sl_purge = sliding && c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0;
+  if (sl_purge && !s.first)
+    return reject(e, FW_ERR_UNSUPPORTED, "sliding windows under PurgingTrigger with allowed lateness need first-arrival "
+                                         "tracking (keep_first_f1)");
+  if (sl_purge && e->adv_log.empty()) e->adv_log.push_back({watermark, 0});   // windows fired before: at the restore
   const bool f64 = s.vt == FW_VALUE_F64;
   std::vector<KgPane> panes;
   std::vector<int64_t> slice_of;
@@ -6247,6 +6283,24 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
         return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
       const int64_t w[FW_SNAP_ENTRY_WORDS] = {m, key, 0, 0, 0, 0, 0, 0};
       ghosts.insert(ghosts.end(), w, w + FW_SNAP_ENTRY_WORDS);
+    }
+  } else if (sl_purge && got != want) {
+    // sliding + PurgingTrigger + lateness: cleanup timers without state of fired, purged windows (each key
+    // whose first element preceded the fire)
+    if (!std::includes(got.begin(), got.end(), want.begin(), want.end()))
+      return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
+    std::vector<std::array<int64_t, 4>> extra;
+    std::set_difference(got.begin(), got.end(), want.begin(), want.end(), std::back_inserter(extra));
+    std::set<std::pair<int64_t, int64_t>> has;
+    for (const KgPane& p : panes) has.insert({p.start, p.key});
+    for (const auto& t : extra) {
+      const int64_t key = t[0], start = t[1], end = t[2], ts = t[3];
+      const int64_t n = fw::floor_div(fw::jsub(start, c.offset), c.slide);
+      const int64_t max_ts = fw::jsub(end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+      if (host_window_start(c, n) != start || end != fw::jadd(start, c.size) || ts != ct || ct == max_ts ||
+          has.count({start, key}) || host_key_group(s, key) != kg)
+        return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");
+      e->sl_ghost.insert({start, key});
     }
   } else if (got != want) {
     return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the panes imply at the restore watermark");

@@ -282,9 +282,12 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * A buffer argument NULL (or too small: FW_ERR_CAPACITY) stores the required lengths only.
  * *state_len == 0: no keyed state at all yet (no record accepted, nothing restored), for which
  * HeapKeyedStateBackend.snapshot writes no stream (:169-171).
- * Restore: before the first push.  Tumbling windows restore into their slices; sliding windows (without
- * allowed lateness) into each window's own pane (later records go to slices; a window fires its slices
- * and its pane).  Not with PurgingTrigger and allowed lateness > 0 (its purged panes keep cleanup timers).
+ * Restore: before the first push.  Tumbling windows restore into their slices; sliding windows into each
+ * window's own pane (later records go to slices; a window fires its slices and its pane); sliding list state
+ * into the slices, peeled from the windows' lists.  PurgingTrigger with allowed lateness > 0: a purged window's
+ * keys keep their cleanup timers without state (tumbling: ghost ordinals per slice slot; sliding: restored as
+ * such, and derived at snapshot for windows fired since — keys whose first element preceded the fire, which needs
+ * keep_first_f1).
  * `watermark` is the engine's watermark after restore: the reference restarts its timer service at
  * Long.MIN_VALUE (currentWatermark is not checkpointed) — pass INT64_MIN for exactly that.  The engine's
  * timers are implicit (a pane's trigger timer is pending iff its window's maxTimestamp > watermark, its

@@ -398,14 +398,14 @@ def test_restore_rejections():
     e.close()
 
 
-def _purging_lateness_run(factory_g, mode, restore_at):
+def _purging_lateness_run(factory_g, mode, restore_at, sliding=False):
     """PurgingTrigger + allowed lateness 400 (tumbling 1 s): a window's fire purges its state but each key keeps its
     cleanup timer until maxTimestamp + 400 (WindowOperator.java:365-371 clears the contents only; the timer is
     deleted at cleanup, :420-428), and a per-element fire within the lateness registers one for a key that had
     none.  Snapshot at a watermark with purged windows inside their lateness; restore (at that watermark, or at
     Long.MIN_VALUE as the reference restarts its timers) and continue."""
-    from flink_amd.windowing import (EventTimeTrigger, PurgingTrigger, ReduceFunction, TumblingEventTimeWindows,
-                                     make_config)
+    from flink_amd.windowing import (EventTimeTrigger, PurgingTrigger, ReduceFunction, SlidingEventTimeWindows,
+                                     TumblingEventTimeWindows, make_config)
     from harness import drive, gen_stream
     from oracle.oracle import OracleEngine
     keys, ts, vals = gen_stream(48_000, 2000, rate=1 << 13, zipf=1.1, ooo=300)   # ~6 s of event time
@@ -413,8 +413,11 @@ def _purging_lateness_run(factory_g, mode, restore_at):
     kw = dict(max_parallelism=128, key_capacity=1 << 13, max_batch=1 << 13, out_capacity=1 << 20)
     if mode:
         kw["ingest_mode"] = mode
-    cfg = make_config(TumblingEventTimeWindows.of(1000), ReduceFunction(("sum", "max"), "i64", True),
-                      PurgingTrigger.of(EventTimeTrigger.create()), 400, **kw)
+    # (sliding 2 s / 1 s: window [1 s, 3 s) fired and purged at the checkpoint, within its lateness; its slices
+    # also feed the unfired [2 s, 4 s))
+    asg = SlidingEventTimeWindows.of(2000, 1000) if sliding else TumblingEventTimeWindows.of(1000)
+    cfg = make_config(asg, ReduceFunction(("sum", "max"), "i64", True), PurgingTrigger.of(EventTimeTrigger.create()),
+                      400, **kw)
     layout = ("f1", "key", "max", "sum")
     n = int(3.25 * (1 << 13)) + 17   # checkpoint watermark ~3.13 s: window [2 s, 3 s) fired, within its lateness
     wm_cut = int(ts[:n].max()) - 120
@@ -461,19 +464,23 @@ def _purging_lateness_run(factory_g, mode, restore_at):
     return blobs, outs
 
 
+@pytest.mark.parametrize("sliding", [False, True])
 @pytest.mark.parametrize("restore_at", ["checkpoint", "long_min"])
-def test_oracle_purging_lateness_round_trip(restore_at):
-    _purging_lateness_run(None, 0, restore_at)
+def test_oracle_purging_lateness_round_trip(restore_at, sliding):
+    _purging_lateness_run(None, 0, restore_at, sliding)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("restore_at", ["checkpoint", "long_min"])
-def test_purging_lateness_checkpoint(mode, restore_at):
+@pytest.mark.parametrize("sliding", [False, True])
+def test_purging_lateness_checkpoint(mode, restore_at, sliding):
     """The engine's sections byte-identical with the oracle's (purged windows' cleanup timers included), its
-    restore writes them back, and the restored engine continues as the restored oracle."""
+    restore writes them back, and the restored engine continues as the restored oracle.  Sliding (round 6): a fired
+    window's state is purged though its slices stay for the windows that share them; its keys whose first element
+    preceded the fire keep a cleanup timer without state."""
     from flink_amd.windowing import WindowEngine
-    blobs, outs = _purging_lateness_run(WindowEngine, mode, restore_at)
+    blobs, outs = _purging_lateness_run(WindowEngine, mode, restore_at, sliding)
     assert _diff(blobs["g"], blobs["o"]) is None, _diff(blobs["g"], blobs["o"])
     assert outs["g"] == outs["o"]
 
