@@ -3334,6 +3334,11 @@ struct SessDev {
   int64_t* nslog;
   unsigned long long* nslog_n;
   int64_t nslog_cap;
+  // PurgingTrigger with allowed lateness: a purged session's cleanup timer outlives it (WindowOperator.cleanup
+  // clears the state and the trigger timer only); logged as (key, start, end, registration ordinal)
+  int64_t* olog;
+  unsigned long long* olog_n;
+  int64_t olog_cap;
   // list state (FW_AGG_LIST): per slot the window's elements as a linked list through an element pool of pcap
   // entries, handed out from a ring of free entry indices (freeq; pool[0] head, pool[1] end of the free ones,
   // pool[2] entries freed during the current launch, listed in fpend)
@@ -3368,6 +3373,15 @@ __device__ __forceinline__ void sess_ns_remove(const SessDev& d, int32_t kg, int
   l[1] = sws;
   l[2] = d.swc[x];
   l[3] = r;
+}
+__device__ __forceinline__ void sess_orphan(const SessDev& d, int64_t key, int64_t start, int64_t end, int64_t seq) {
+  const unsigned long long pos = atomicAdd(d.olog_n, 1ull);
+  if ((int64_t)pos >= d.olog_cap) return;   // (overflow: the snapshot reports FW_ERR_CAPACITY)
+  int64_t* l = d.olog + 4 * pos;
+  l[0] = key;
+  l[1] = start;
+  l[2] = end;
+  l[3] = seq;
 }
 
 
@@ -3442,6 +3456,13 @@ struct fw_engine {
   bool sess_wc_table = false, sess_mws_table = false;
   std::vector<uint8_t> mws_created;
   std::map<int64_t, int64_t> sess_mws_rank;
+  // PurgingTrigger with allowed lateness: purged sessions' cleanup timers — drained from the device log
+  // (key, start, end, registration ordinal) and restored ones (key, start, end); the (watermark, ordinal) of each
+  // advance; keys whose set a restored timer fetched when it fired (key -> (ordinal, timer time))
+  std::vector<std::array<int64_t, 4>> sess_orphans;
+  std::set<std::array<int64_t, 3>> sess_rorphans;
+  std::vector<std::pair<int64_t, int64_t>> sess_adv;
+  std::map<int64_t, std::pair<int64_t, int64_t>> sess_touch_adj;
   struct SessHost {
     int64_t epoch = -1, wm = 0;
     std::vector<int64_t> keys, st, en, sws, swc, put, cre, tre, sum, mn, mx, cnt, f1, ktouch, ktts, nslog;
@@ -5484,9 +5505,6 @@ static int session_reject_config(fw_engine* e) {
   if (e->list)
     return reject(e, FW_ERR_UNSUPPORTED, "session windows with list state: the elements sit in an element pool, not in "
                                          "per-window lists (no checkpoint layout here)");
-  if (c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0)
-    return reject(e, FW_ERR_UNSUPPORTED, "session windows under PurgingTrigger with allowed lateness: a purged "
-                                         "session's cleanup timer outlives it, which the engine does not hold");
   if (e->mws_created.empty()) e->mws_created.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
   if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
   return FW_OK;
@@ -5503,15 +5521,48 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
   const SessDev& d = e->sess;
   const fw_config& c = e->cfg;
   const size_t kgi = (size_t)(kg - s.kg_start);
+  const bool orphans = c.trigger == FW_TRIGGER_PURGING_EVENT_TIME && c.allowed_lateness > 0;
+  if (orphans) {   // purged sessions' cleanup timers logged since the last snapshot
+    unsigned long long no = 0;
+    HIPCHK(e, hipMemcpy(&no, d.olog_n, 8, hipMemcpyDeviceToHost));
+    if ((int64_t)no > d.olog_cap)
+      return reject(e, FW_ERR_CAPACITY, "more purged sessions since the last snapshot than the orphan timer log holds");
+    std::vector<int64_t> ol(4 * (size_t)no);
+    if (no) HIPCHK(e, hipMemcpy(ol.data(), d.olog, 8 * ol.size(), hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemset(d.olog_n, 0, 8));
+    for (size_t j = 0; j < (size_t)no; ++j) e->sess_orphans.push_back({ol[4 * j], ol[4 * j + 1], ol[4 * j + 2], ol[4 * j + 3]});
+    auto ct_of = [&](int64_t end) { return fw::cleanup_time(fw::jsub(end, 1), c.allowed_lateness); };
+    std::vector<std::array<int64_t, 4>> keep;
+    for (const auto& o : e->sess_orphans) if (ct_of(o[2]) > e->cur_wm) keep.push_back(o);
+    e->sess_orphans.swap(keep);
+    // a restored timer that fired fetched its key's set (onEventTime -> getMergingWindowSet)
+    for (auto it = e->sess_rorphans.begin(); it != e->sess_rorphans.end();) {
+      const int64_t ct = ct_of((*it)[2]);
+      if (ct > e->cur_wm) { ++it; continue; }
+      int64_t ord = 0;
+      for (const auto& a : e->sess_adv) if (a.first >= ct) { ord = a.second; break; }
+      auto adj = e->sess_touch_adj.find((*it)[0]);
+      if (adj == e->sess_touch_adj.end() || std::make_pair(ord, ct) < adj->second) e->sess_touch_adj[(*it)[0]] = {ord, ct};
+      it = e->sess_rorphans.erase(it);
+    }
+  }
   struct Pane { int64_t kid, key, start, end, sws, swc, put, cre, tre; bool trig; KgPane acc; };
   std::vector<Pane> panes;
   std::vector<int64_t> kids;   // the key group's keys
   int64_t n_touched = 0;
   bool any_acc = false, kg_acc = false;
+  // when a key's set was first fetched: the device's record or watermark, or a restored timer's firing (host)
+  auto touch_of = [&](int64_t kid, int64_t key) -> std::pair<int64_t, int64_t> {
+    std::pair<int64_t, int64_t> t{h.ktouch[(size_t)kid], h.ktts[(size_t)kid]};
+    auto adj = e->sess_touch_adj.find(key);
+    if (adj != e->sess_touch_adj.end() && (t.first < 0 || adj->second < t)) t = adj->second;
+    return t;
+  };
+  std::set<int64_t> dir_keys_touched;
   for (int64_t k = 0; k < s.stride; ++k) {
     const int64_t key = k == s.D ? fw::EMPTY_KEY : h.keys[(size_t)k];
     if (k < s.D && key == fw::EMPTY_KEY) continue;
-    if (h.ktouch[(size_t)k] >= 0) ++n_touched;
+    if (touch_of(k, key).first >= 0) { ++n_touched; dir_keys_touched.insert(key); }
     any_acc = any_acc || h.kacc[(size_t)k];
     if (host_key_group(s, key) != kg) continue;
     kids.push_back(k);
@@ -5526,6 +5577,7 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
       panes.push_back(p);
     }
   }
+  for (const auto& a : e->sess_touch_adj) if (!dir_keys_touched.count(a.first)) ++n_touched;   // (keys not in the directory)
   const bool wc_table = e->sess_wc_table || any_acc;
   const bool mws_table = e->sess_mws_table || n_touched > 0;
   fwkg::BeOut st, tm;
@@ -5589,7 +5641,7 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
       if (it == at.end()) {
         const int64_t k = panes[i].kid;
         auto r = e->sess_mws_rank.find(panes[i].key);
-        const bool touched = h.ktouch[(size_t)k] >= 0 || r == e->sess_mws_rank.end();
+        const bool touched = touch_of(k, panes[i].key).first >= 0 || r == e->sess_mws_rank.end();
         it = at.emplace(k, ents.size()).first;
         ents.push_back({k, panes[i].key, touched ? INT64_MAX : r->second, touched, {}});
       }
@@ -5615,10 +5667,8 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
               const uint32_t gx = (uint32_t)fwkg::spread(fw::long_hash_code(x.key)) & gmask;
               const uint32_t gy = (uint32_t)fwkg::spread(fw::long_hash_code(y.key)) & gmask;
               if (gx != gy) return gx < gy;
-              const int64_t tx = h.ktouch[(size_t)x.kid], ty = h.ktouch[(size_t)y.kid];
-              if (tx != ty) return tx < ty;
-              const int64_t sx = h.ktts[(size_t)x.kid], sy = h.ktts[(size_t)y.kid];
-              return sx != sy ? sx < sy : x.key < y.key;
+              const auto tx = touch_of(x.kid, x.key), ty = touch_of(y.kid, y.key);
+              return tx != ty ? tx < ty : x.key < y.key;
             });
         st.i32((int32_t)ents.size());
         for (size_t i : eo) {
@@ -5647,6 +5697,19 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
     const int64_t max_ts = fw::jsub(p.end, 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
     if (p.trig) tv.push_back({p.key, p.start, p.end, max_ts, p.tre, 0, INT64_MAX});
     if (ct != max_ts) tv.push_back({p.key, p.start, p.end, ct, p.cre, 1, INT64_MAX});
+  }
+  if (orphans) {   // purged sessions' cleanup timers (the same timer as a later in-flight window's keeps its place)
+    std::map<std::array<int64_t, 3>, size_t> at;
+    for (size_t i = 0; i < tv.size(); ++i) if (tv[i].kind == 1) at[{tv[i].key, tv[i].start, tv[i].end}] = i;
+    auto add = [&](int64_t key, int64_t start, int64_t end, int64_t seq) {
+      if (host_key_group(s, key) != kg) return;
+      auto it = at.find({key, start, end});
+      if (it != at.end()) { tv[it->second].seq = std::min(tv[it->second].seq, seq); return; }
+      at[{key, start, end}] = tv.size();
+      tv.push_back({key, start, end, fw::cleanup_time(fw::jsub(end, 1), c.allowed_lateness), seq, 1, INT64_MAX});
+    };
+    for (const auto& o : e->sess_rorphans) add(o[0], o[1], o[2], INT64_MIN);
+    for (const auto& o : e->sess_orphans) add(o[0], o[1], o[2], o[3]);
   }
   if (!e->restored_timer_rank.empty())
     for (Tm& t : tv) {
@@ -5794,9 +5857,21 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
     }
   }
   if (used.size() != wc.size()) return reject(e, FW_ERR_INVALID_ARG, "window-contents state of no in-flight session");
-  if (want != tset) return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the sessions imply");
+  if (!std::includes(tset.begin(), tset.end(), want.begin(), want.end()))
+    return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the sessions imply");
+  std::vector<std::array<int64_t, 3>> rorph;   // PurgingTrigger + lateness: cleanup timers of purged sessions
+  for (const auto& t : tset) {
+    if (want.count(t)) continue;
+    const int64_t max_ts = fw::jsub(t[2], 1), ct = fw::cleanup_time(max_ts, c.allowed_lateness);
+    if (c.trigger != FW_TRIGGER_PURGING_EVENT_TIME || ct == max_ts || t[3] != ct || t[2] <= t[1] ||
+        host_key_group(s, t[0]) != kg)
+      return reject(e, FW_ERR_UNSUPPORTED, "timers differ from the ones the sessions imply");
+    rorph.push_back({t[0], t[1], t[2]});
+  }
   HIPCHK(e, hipSetDevice(e->dev));
   for (const auto& kv : mws) e->sess_mws_rank[kv.first] = (int64_t)e->sess_mws_rank.size();
+  e->sess_rorphans.insert(rorph.begin(), rorph.end());
+  if (e->sess_adv.empty()) e->sess_adv.push_back({watermark, 0});
   for (const auto& t : got) e->restored_timer_rank[t] = (int64_t)e->restored_timer_rank.size();
   if (wc_seen) e->sess_wc_table = true;
   if (mws_seen) e->sess_mws_table = true;

@@ -271,12 +271,12 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       mask = mask | grew;
     }
     int r = -1;          // slot of the resulting window
-    bool fresh = false;
+    bool fresh = false, contained = false;
     if (!mask.any()) {
       fresh = true;
     } else {
       r = mask.first();
-      const bool contained = mask.count() == 1 && st[r] == cs && en[r] == ce;   // new window inside an existing one
+      contained = mask.count() == 1 && st[r] == cs && en[r] == ce;   // new window inside an existing one
       if (!contained) {
         // merge: the group's HashSet holds the merged in-flight windows and the new one (distinct from all of
         // them here); iterated by (bucket, insertion = start order), the first window's state is the target,
@@ -390,7 +390,11 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
         sess_emit(s, pos, key, cs, max_ts, cur);
       }
       ++fires;
-      if (purging) { sess_ns_remove(d, kkg, key, x, ord); retire(r); }   // FIRE_AND_PURGE: cleanup(actualWindow)
+      if (purging) {   // FIRE_AND_PURGE: cleanup(actualWindow); an unchanged window's cleanup timer stays
+        if (contained && s.lateness > 0) sess_orphan(d, key, cs, ce, d.cre[x]);
+        sess_ns_remove(d, kkg, key, x, ord);
+        retire(r);
+      }
     } else {
       if (!trig.test(r)) d.tre[x] = ord;   // (re-armed: a window restored below its fire)
       trig.set(r);
@@ -558,12 +562,12 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
         }
       }
       int r = -1;
-      bool fresh = false;
+      bool fresh = false, contained = false;
       if (!mask.any()) {
         fresh = true;
       } else {
         r = mask.first();
-        const bool contained = mask.count() == 1 && gst(r) == cs && gen(r) == ce;
+        contained = mask.count() == 1 && gst(r) == cs && gen(r) == ce;
         if (!contained) {   // merge, in the JDK HashSet order (see k_sess_walk)
           const uint32_t cap = sess_set_cap(mask.count() + 1);
           int tq = -1;
@@ -638,7 +642,14 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
       if (max_ts <= wm) {   // EventTimeTrigger.onElement: FIRE
         if (lane == 0) sess_emit(s, atomicAdd(s.o.count, 1ull), key, cs, max_ts, cur);
         ++fires;
-        if (purging) { if (lane == 0) sess_ns_remove(d, kkg, key, base + r, ord); live.clr(r); trig.clr(r); }
+        if (purging) {
+          if (lane == 0) {
+            if (contained && s.lateness > 0) sess_orphan(d, key, cs, ce, d.cre[base + r]);
+            sess_ns_remove(d, kkg, key, base + r, ord);
+          }
+          live.clr(r);
+          trig.clr(r);
+        }
       } else {
         if (lane == 0 && !trig.test(r)) d.tre[base + r] = ord;
         trig.set(r);
@@ -699,6 +710,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
             fire = true;
             trig.clr(q);
             if (purging || ct == max_ts) retire = true;       // FIRE_AND_PURGE, or isCleanupTime
+            if (purging && ct != max_ts && ct > wm_new)       // the purged window's cleanup timer stays
+              sess_orphan(d, kid_key(s, kid), d.start[kid * d.sw + q], e8[k], d.cre[kid * d.sw + q]);
           }
           if (!retire && ct <= wm_new) {                    // onEventTime(cleanupTime): cleanup
             if (!fire && ct == max_ts) fire = true;         // (one timer at maxTimestamp == cleanupTime)
@@ -834,6 +847,9 @@ int session_create(fw_engine* e) {
     d.nslog_cap = std::max<int64_t>(1 << 16, 2 * e->cfg.max_batch);
     d.nslog = e->alloc<int64_t>(4 * (size_t)d.nslog_cap);
     d.nslog_n = e->alloc<unsigned long long>(1);
+    d.olog_cap = std::max<int64_t>(1 << 16, 2 * e->cfg.max_batch);
+    d.olog = e->alloc<int64_t>(4 * (size_t)d.olog_cap);
+    d.olog_n = e->alloc<unsigned long long>(1);
   }
   e->s.o.win_start = e->alloc<int64_t>((size_t)e->cfg.out_capacity);
   const size_t nb = (size_t)e->cfg.max_batch;
@@ -857,6 +873,7 @@ int session_create(fw_engine* e) {
   HIPCHK(e, hipMemsetAsync(d.kacc, 0, 4 * (size_t)s.stride, e->stream));
   HIPCHK(e, hipMemsetAsync(d.nscnt, 0, 4 * (size_t)(d.nsmask + 1), e->stream));
   HIPCHK(e, hipMemsetAsync(d.nslog_n, 0, 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.olog_n, 0, 8, e->stream));
   return FW_OK;
 }
 
@@ -887,6 +904,7 @@ int session_push(fw_engine* e, const BatchIn& b) {
 
 int session_watermark(fw_engine* e, int64_t wm) {
   if (wm > e->cur_wm) {
+    e->sess_adv.push_back({wm, e->ordinal});   // (checkpoints: when a restored orphan timer fired)
     e->phase_begin(FW_PHASE_FIRE);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((e->s.stride + BLOCK - 1) / BLOCK, e->grid));
     if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_wm<1>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);

@@ -31,6 +31,7 @@ CASES = [
     ("f64", ("sum", "min", "max", "count"), 400, False),
     ("i64", ("sum", "count"), 0, True),
     ("i64", ("maxBy",), 250, False),
+    ("i64", ("sum", "count"), 300, True),   # a purged session's cleanup timer outlives it
 ]
 
 
@@ -116,12 +117,12 @@ def test_oracle_session_checkpoint_round_trip(case):
     assert ea == eb and sum(len(r) for _, r in ea) > 1000
 
 
-def test_oracle_session_restore_at_long_min():
+@pytest.mark.parametrize("case", [CASES[1], CASES[4]], ids=["f64-late400", "purging-late300"])
+def test_oracle_session_restore_at_long_min(case):
     """Restored at Long.MIN_VALUE (the reference's timer service restarts there): sessions whose trigger fired before
     the checkpoint (kept for their allowed lateness, cleanup timer only) re-arm on their next record and fire again;
     the sections are written back unchanged."""
     from oracle.oracle import OracleEngine
-    case = CASES[1]
     snaps, _ = _run(OracleEngine, case)
     back, out = _run(OracleEngine, case, restore=snaps[-1], restore_wm=LONG_MIN)
     assert _diff(back[0], snaps[-1]) is None
@@ -160,11 +161,12 @@ def test_session_checkpoint_hot_walk(case, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_session_restore_at_long_min():
-    """As the oracle: a restore at Long.MIN_VALUE re-arms fired-but-kept sessions on their next record."""
+@pytest.mark.parametrize("case", [CASES[1], CASES[4]], ids=["f64-late400", "purging-late300"])
+def test_session_restore_at_long_min(case):
+    """As the oracle: a restore at Long.MIN_VALUE re-arms fired-but-kept sessions on their next record (PurgingTrigger:
+    purged sessions' restored cleanup timers fire with nothing to clean, fetching their keys' sets)."""
     from flink_amd.windowing import WindowEngine
     from oracle.oracle import OracleEngine
-    case = CASES[1]
     o, _ = _run(OracleEngine, case)
     back, out_g = _run(WindowEngine, case, restore=o[-1], restore_wm=LONG_MIN)
     _, out_o = _run(OracleEngine, case, restore=o[-1], restore_wm=LONG_MIN)
@@ -174,13 +176,11 @@ def test_session_restore_at_long_min():
 
 @pytest.mark.gpu
 def test_session_checkpoint_rejections():
-    """Configurations whose session state the engine does not hold in the reference's form fail loudly: list state
-    (an element pool, not per-window lists in arrival order) and PurgingTrigger with allowed lateness (a purged
-    session's cleanup timer outlives it)."""
+    """Session list state (an element pool, not per-window lists in arrival order) takes no reference-layout
+    checkpoint: it fails loudly."""
     from flink_amd import _abi
     from flink_amd.windowing import WindowEngine
-    for cfg, layout in ((_config("i64", (), 0, False, list_state=True), ("key", "f1", "value")),
-                        (_config("i64", ("sum",), 300, True), ("key", "f1", "sum"))):
+    for cfg, layout in ((_config("i64", (), 0, False, list_state=True), ("key", "f1", "value")),):
         e = WindowEngine(cfg)
         with pytest.raises(_abi.FwError) as ei:
             e.snapshot_kg_flink(0, layout)
