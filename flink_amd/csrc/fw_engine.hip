@@ -3463,9 +3463,11 @@ struct fw_engine {
   std::set<std::array<int64_t, 3>> sess_rorphans;
   std::vector<std::pair<int64_t, int64_t>> sess_adv;
   std::map<int64_t, std::pair<int64_t, int64_t>> sess_touch_adj;
+  int64_t sess_pool_used = 0;   // session list state: pool entries a restore laid elements in
   struct SessHost {
     int64_t epoch = -1, wm = 0;
     std::vector<int64_t> keys, st, en, sws, swc, put, cre, tre, sum, mn, mx, cnt, f1, ktouch, ktts, nslog;
+    std::vector<int64_t> lhead, llen, pv, pf1, pnext;   // list state: per slot its element chain; the pool
     bool nslog_over = false;
     std::vector<int32_t> kacc;
     std::vector<unsigned long long> live, trig;
@@ -5432,7 +5434,7 @@ static void kg_panes(const fw_engine* e, int32_t kg, std::vector<KgPane>& out) {
 namespace fw {
 // restored sessions: one row per in-flight window (key, slot, start, end, state-window start, its entry's rank,
 // trigger pending, sum, min / max codes, count, f1); key ids by the directory's insert
-constexpr int SESS_ROW = 12;
+constexpr int SESS_ROW = 15;
 __global__ __launch_bounds__(BLOCK) void k_sess_restore(Spec s, SessDev d, const int64_t* rows, int64_t n, int64_t put0) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -5452,6 +5454,11 @@ __global__ __launch_bounds__(BLOCK) void k_sess_restore(Spec s, SessDev d, const
   if (d.mx) d.mx[x] = r[9];
   if (d.cnt) d.cnt[x] = r[10];
   if (d.f1) d.f1[x] = r[11];
+  if (d.list) {   // list state: the window's elements, chained in pool entries the host laid out
+    d.head[x] = r[12];
+    d.tail[x] = r[13];
+    d.len[x] = r[14];
+  }
   sess_ns_add(d, record_key_group(s, long_hash_code(r[0])), r[4]);
   atomicOr(&d.live[kid * d.nw + (q >> 6)], 1ull << (q & 63));
   if (r[6]) atomicOr(&d.trig[kid * d.nw + (q >> 6)], 1ull << (q & 63));
@@ -5484,6 +5491,11 @@ static int session_download(fw_engine* e) {
   HIPCHK(e, get(h.cnt, d.cnt, cells));
   HIPCHK(e, get(h.f1, d.f1, cells));
   HIPCHK(e, get(h.ktouch, d.ktouch, rows));
+  HIPCHK(e, get(h.lhead, d.list ? d.head : nullptr, cells));
+  HIPCHK(e, get(h.llen, d.list ? d.len : nullptr, cells));
+  HIPCHK(e, get(h.pv, d.list ? d.pv : nullptr, (size_t)d.pcap));
+  HIPCHK(e, get(h.pf1, d.list ? d.pf1 : nullptr, (size_t)d.pcap));
+  HIPCHK(e, get(h.pnext, d.list ? d.pnext : nullptr, (size_t)d.pcap));
   HIPCHK(e, get(h.ktts, d.ktts, rows));
   h.kacc.assign(rows, 0);
   HIPCHK(e, hipMemcpy(h.kacc.data(), d.kacc, 4 * rows, hipMemcpyDeviceToHost));
@@ -5502,9 +5514,6 @@ static int session_download(fw_engine* e) {
 
 static int session_reject_config(fw_engine* e) {
   const fw_config& c = e->cfg;
-  if (e->list)
-    return reject(e, FW_ERR_UNSUPPORTED, "session windows with list state: the elements sit in an element pool, not in "
-                                         "per-window lists (no checkpoint layout here)");
   if (e->mws_created.empty()) e->mws_created.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
   if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
   return FW_OK;
@@ -5546,7 +5555,7 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
       it = e->sess_rorphans.erase(it);
     }
   }
-  struct Pane { int64_t kid, key, start, end, sws, swc, put, cre, tre; bool trig; KgPane acc; };
+  struct Pane { int64_t kid, key, start, end, sws, swc, put, cre, tre; bool trig; KgPane acc; int64_t lhead, llen; };
   std::vector<Pane> panes;
   std::vector<int64_t> kids;   // the key group's keys
   int64_t n_touched = 0;
@@ -5571,7 +5580,8 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
       const size_t w = (size_t)k * (size_t)d.nw + (size_t)(q >> 6);
       if (!((h.live[w] >> (q & 63)) & 1ull)) continue;
       const size_t x = (size_t)k * (size_t)d.sw + (size_t)q;
-      Pane p{k, key, h.st[x], h.en[x], h.sws[x], h.swc[x], h.put[x], h.cre[x], h.tre[x], ((h.trig[w] >> (q & 63)) & 1ull) != 0, {}};
+      Pane p{k, key, h.st[x], h.en[x], h.sws[x], h.swc[x], h.put[x], h.cre[x], h.tre[x], ((h.trig[w] >> (q & 63)) & 1ull) != 0, {},
+             h.lhead.empty() ? -1 : h.lhead[x], h.llen.empty() ? 0 : h.llen[x]};
       p.acc = KgPane{p.sws, fw::jadd(p.sws, d.gap), key, h.sum.empty() ? 0 : h.sum[x], h.mn.empty() ? INT64_MAX : h.mn[x],
                      h.mx.empty() ? INT64_MIN : h.mx[x], h.cnt.empty() ? 0 : h.cnt[x], 0, h.f1.empty() ? 0 : h.f1[x], false};
       panes.push_back(p);
@@ -5624,6 +5634,19 @@ static int session_snapshot_kg_flink(fw_engine* e, int32_t kg, const fw_state_la
         st.i32((int32_t)ent.size());
         for (size_t i : ent) {
           st.i64(panes[i].key);
+          if (d.list) {   // ListSerializer: int size, then the window's elements in list order
+            st.i32((int32_t)panes[i].llen);
+            int64_t el = panes[i].lhead;
+            for (int64_t j = 0; j < panes[i].llen && el >= 0 && el < d.pcap; ++j, el = h.pnext[(size_t)el])
+              for (int f = 0; f < layout->n_fields; ++f) {
+                const int fld = layout->field[f];
+                if (fld == FW_SF_KEY) st.i64(panes[i].key);
+                else if (fld == FW_SF_F1) st.i64(h.pf1[(size_t)el]);
+                else if (s.vt == FW_VALUE_F64) { double dv; memcpy(&dv, &h.pv[(size_t)el], 8); st.f64(dv); }
+                else st.i64(h.pv[(size_t)el]);
+              }
+            continue;
+          }
           for (int f = 0; f < layout->n_fields; ++f) put_field(e, st, layout->field[f], panes[i].acc);
         }
       }
@@ -5752,7 +5775,8 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
   const fw_config& c = e->cfg;
   const bool f64 = s.vt == FW_VALUE_F64;
   const size_t kgi = (size_t)(kg - s.kg_start);
-  std::map<std::pair<int64_t, int64_t>, std::pair<KgPane, int64_t>> wc;   // (state-window start, key) -> (state, rank)
+  struct WcEnt { KgPane p; int64_t rank; std::vector<std::array<int64_t, 2>> el; };   // (list state: value, f1)
+  std::map<std::pair<int64_t, int64_t>, WcEnt> wc;   // (state-window start, key) -> its state
   std::vector<std::pair<int64_t, std::vector<std::array<int64_t, 4>>>> mws;
   bool wc_seen = false, mws_seen = false, wc_present = false, mws_present = false;
   if (state_len > 0) {
@@ -5774,7 +5798,23 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
           if (ne < 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt state section");
           for (int32_t j = 0; j < ne && in.ok; ++j) {
             KgPane p{start, end, in.i64(), 0, INT64_MAX, INT64_MIN, 0, 0, 0, false};
-            for (int f = 0; f < layout->n_fields; ++f) {
+            std::vector<std::array<int64_t, 2>> el;
+            if (e->list) {   // ListSerializer: int size, then the elements (the layout's fields of the input tuple)
+              const int32_t nel = in.i32();
+              if (nel <= 0) return reject(e, FW_ERR_INVALID_ARG, "corrupt or empty list state entry");
+              for (int32_t q = 0; q < nel && in.ok; ++q) {
+                std::array<int64_t, 2> x{0, 0};
+                for (int f = 0; f < layout->n_fields; ++f) {
+                  const int64_t v = in.i64();
+                  if (layout->field[f] == FW_SF_KEY && in.ok && v != p.key)
+                    return reject(e, FW_ERR_UNSUPPORTED, "element key field differs from the key");
+                  if (layout->field[f] == FW_SF_F1) x[1] = v;
+                  if (layout->field[f] == FW_SF_VALUE) x[0] = v;
+                }
+                el.push_back(x);
+              }
+            }
+            for (int f = 0; f < layout->n_fields && !e->list; ++f) {
               const int64_t x = in.i64();
               double dv;
               memcpy(&dv, &x, 8);
@@ -5792,7 +5832,7 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
             }
             if (!in.ok) break;
             if (host_key_group(s, p.key) != kg) return reject(e, FW_ERR_KEY_GROUP, "state entry key outside its key group");
-            if (!wc.emplace(std::make_pair(start, p.key), std::make_pair(p, e->restore_ord++)).second)
+            if (!wc.emplace(std::make_pair(start, p.key), WcEnt{p, e->restore_ord++, std::move(el)}).second)
               return reject(e, FW_ERR_INVALID_ARG, "duplicate (window, key) entry");
           }
         }
@@ -5835,6 +5875,7 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
   // the in-flight windows: each with its state window's contents; timers exactly the ones they imply
   std::set<std::array<int64_t, 4>> tset(got.begin(), got.end()), want;
   std::vector<int64_t> rows;
+  std::vector<std::array<int64_t, 4>> pool;   // list state: (entry, value, f1, next)
   std::set<std::pair<int64_t, int64_t>> used, keys_seen;
   for (const auto& kv : mws) {
     if (!keys_seen.insert({kv.first, 0}).second) return reject(e, FW_ERR_INVALID_ARG, "duplicate merging-window-set key");
@@ -5850,9 +5891,22 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
       const bool trig = tset.count(trig_t) != 0;
       if (trig) want.insert(trig_t);
       if (ct != max_ts) want.insert({kv.first, w[0], w[1], ct});
-      const KgPane& p = it->second.first;
-      const int64_t row[fw::SESS_ROW] = {kv.first, (int64_t)q, w[0], w[1], w[2], it->second.second,
-                                         trig ? 1 : 0, p.sum, p.mn, p.mx, p.cnt, p.f1};
+      const KgPane& p = it->second.p;
+      int64_t lh = -1, lt = -1, ln = 0;
+      if (e->list) {   // the elements into pool entries, chained in list order
+        const auto& el = it->second.el;
+        if (e->sess_pool_used + (int64_t)el.size() > d.pcap)
+          return reject(e, FW_ERR_CAPACITY, "restored session elements exceed list_capacity");
+        lh = e->sess_pool_used;
+        for (size_t j = 0; j < el.size(); ++j) {
+          const int64_t at = e->sess_pool_used++;
+          pool.push_back({at, el[j][0], el[j][1], j + 1 < el.size() ? at + 1 : -1});
+        }
+        lt = e->sess_pool_used - 1;
+        ln = (int64_t)el.size();
+      }
+      const int64_t row[fw::SESS_ROW] = {kv.first, (int64_t)q, w[0], w[1], w[2], it->second.rank,
+                                         trig ? 1 : 0, p.sum, p.mn, p.mx, p.cnt, p.f1, lh, lt, ln};
       rows.insert(rows.end(), row, row + fw::SESS_ROW);
     }
   }
@@ -5880,6 +5934,16 @@ static int session_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_lay
   e->restored = true;
   e->cur_wm = watermark;
   e->state_epoch++;
+  if (!pool.empty()) {   // the entries the restored elements took (the pool's free ring hands out the rest)
+    std::vector<int64_t> pv(pool.size()), pf(pool.size()), pn(pool.size());
+    const int64_t first = pool[0][0];
+    for (size_t j = 0; j < pool.size(); ++j) { pv[j] = pool[j][1]; pf[j] = pool[j][2]; pn[j] = pool[j][3]; }
+    HIPCHK(e, hipMemcpy(d.pv + first, pv.data(), 8 * pv.size(), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(d.pf1 + first, pf.data(), 8 * pf.size(), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(d.pnext + first, pn.data(), 8 * pn.size(), hipMemcpyHostToDevice));
+    const unsigned long long taken = (unsigned long long)e->sess_pool_used;
+    HIPCHK(e, hipMemcpy(d.pool, &taken, 8, hipMemcpyHostToDevice));
+  }
   const int64_t n = (int64_t)(rows.size() / fw::SESS_ROW);
   if (n == 0) return FW_OK;
   int64_t* dr = nullptr;

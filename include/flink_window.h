@@ -276,7 +276,7 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * MergingWindowSet.persist :91-95) as WindowOperator.snapshotState rewrites it: restored entries of keys untouched
  * since, then every other key with sessions in flight in mergingWindowsByKey's order.  Timers: each in-flight
  * window's pending trigger timer and its cleanup timer (PurgingTrigger with allowed lateness: also purged
- * sessions' cleanup timers until their time).  Not for session list state (FW_ERR_UNSUPPORTED).
+ * sessions' cleanup timers until their time); list state: each window's elements in list order.
  * Namespaces, entries and timers come in java.util.HashMap iteration order for
  * tables sized by their current size (when a JVM table iterates differently).
  * A buffer argument NULL (or too small: FW_ERR_CAPACITY) stores the required lengths only.

@@ -32,11 +32,12 @@ CASES = [
     ("i64", ("sum", "count"), 0, True),
     ("i64", ("maxBy",), 250, False),
     ("i64", ("sum", "count"), 300, True),   # a purged session's cleanup timer outlives it
+    ("f64", ("list",), 200, False),          # WindowedStream.apply: each session's elements (HeapListState)
 ]
 
 
 def _layout(fields):
-    return ("key", "f1") + (("value",) if fields in (("maxBy",), ("minBy",)) else tuple(fields))
+    return ("key", "f1") + (("value",) if fields in (("maxBy",), ("minBy",), ("list",)) else tuple(fields))
 
 
 def _stream(vt):
@@ -47,6 +48,7 @@ def _stream(vt):
 
 
 def _config(vt, fields, lateness, purging, list_state=False):
+    list_state = list_state or fields == ("list",)
     from flink_amd.windowing import (EventTimeSessionWindows, EventTimeTrigger, ListStateDescriptor, PurgingTrigger,
                                      ReduceFunction, make_config)
     trig = PurgingTrigger.of(EventTimeTrigger.create()) if purging else EventTimeTrigger.create()
@@ -99,7 +101,12 @@ def _diff(got, want):
 def _epochs(out, case):
     from harness import epochs_of
     vt, fields, _, _ = case
-    cols = ["max_" + vt] if fields == ("maxBy",) else [f"{f}_{vt}" if f != "count" else "count" for f in fields]
+    if fields == ("list",):
+        cols = ["sum_" + vt]   # (list state: one row per element, its value in the sum column)
+    elif fields == ("maxBy",):
+        cols = ["max_" + vt]
+    else:
+        cols = [f"{f}_{vt}" if f != "count" else "count" for f in fields]
     return epochs_of(out, cols, True)   # (double sums compared exactly: the same values reduced in the same order)
 
 
@@ -176,13 +183,14 @@ def test_session_restore_at_long_min(case):
 
 @pytest.mark.gpu
 def test_session_checkpoint_rejections():
-    """Session list state (an element pool, not per-window lists in arrival order) takes no reference-layout
-    checkpoint: it fails loudly."""
+    """A restored window-contents namespace that is not a session's first window [ts, ts + gap) fails loudly."""
+    import struct
     from flink_amd import _abi
     from flink_amd.windowing import WindowEngine
-    for cfg, layout in ((_config("i64", (), 0, False, list_state=True), ("key", "f1", "value")),):
-        e = WindowEngine(cfg)
-        with pytest.raises(_abi.FwError) as ei:
-            e.snapshot_kg_flink(0, layout)
-        assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
-        e.close()
+    e = WindowEngine(_config("i64", ("sum",), 0, False))
+    kg = 5
+    st = struct.pack(">ihbi", kg, 0, 1, 1) + struct.pack(">qqi", 100, 100 + 151, 0)
+    with pytest.raises(_abi.FwError) as ei:
+        e.restore_kg_flink(kg, ("key", "f1", "sum"), st, struct.pack(">ii", 0, 0))
+    assert ei.value.code == _abi.FW_ERR_INVALID_ARG
+    e.close()
