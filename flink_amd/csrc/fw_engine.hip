@@ -3339,6 +3339,9 @@ struct SessDev {
   int64_t* olog;
   unsigned long long* olog_n;
   int64_t olog_cap;
+  int64_t* rlist;   // slots a watermark retired (k_sess_wm -> k_sess_ns_retire)
+  unsigned long long* rlist_n;
+  int64_t rlist_cap;
   // list state (FW_AGG_LIST): per slot the window's elements as a linked list through an element pool of pcap
   // entries, handed out from a ring of free entry indices (freeq; pool[0] head, pool[1] end of the free ones,
   // pool[2] entries freed during the current launch, listed in fpend)

@@ -725,11 +725,22 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
       live = live.andnot(ret_m);
       trig = trig.andnot(ret_m);
       if (tmin != INT64_MAX && d.ktouch[kid] < 0) { d.ktouch[kid] = touch_ord; d.ktts[kid] = tmin; }
-      if (ret_m.any()) {   // the retired windows' state entries cleared
-        const int64_t key = kid_key(s, kid);
-        const int32_t kkg = record_key_group(s, long_hash_code(key));
-        for (B m = ret_m; m.any();) sess_ns_remove(d, kkg, key, kid * d.sw + m.pop(), touch_ord);
+    }
+    {   // the retired windows' state entries cleared: listed (one reservation per wave) for k_sess_ns_retire, whose
+        // thread per entry keeps the namespace counts off this kernel's per-key chain
+      const int c = ret_m.count();
+      int incl = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if ((int)(threadIdx.x & 63) >= o) incl += y;
       }
+      const int total = __shfl(incl, 63);
+      unsigned long long base = 0;
+      if ((threadIdx.x & 63) == 63 && total) base = atomicAdd(d.rlist_n, (unsigned long long)total);
+      base = __shfl(base, 63);
+      unsigned long long pos = base + (unsigned long long)(incl - c);
+      for (B m = ret_m; m.any(); ++pos)
+        if ((int64_t)pos < d.rlist_cap) d.rlist[pos] = kid * d.sw + m.pop(); else m.pop();
     }
     // the fires (list state: and the retired windows' elements freed), the wave's appends aggregated
     B todo = d.list ? (fire_m | ret_m) : fire_m;
@@ -758,6 +769,16 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
     }
     if (live != live0) live.store(d.live + kid * NW);
     if (trig != trig0) trig.store(d.trig + kid * NW);
+  }
+}
+
+// the state entries k_sess_wm retired: namespace counts (and the shared-namespace log), a thread per entry
+__global__ __launch_bounds__(BLOCK) void k_sess_ns_retire(Spec s, SessDev d, int64_t touch_ord) {
+  const int64_t n = min((int64_t)*d.rlist_n, d.rlist_cap);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = d.rlist[i], kid = x / d.sw;
+    const int64_t key = kid_key(s, kid);
+    sess_ns_remove(d, record_key_group(s, long_hash_code(key)), key, x, touch_ord);
   }
 }
 
@@ -850,6 +871,9 @@ int session_create(fw_engine* e) {
     d.olog_cap = std::max<int64_t>(1 << 16, 2 * e->cfg.max_batch);
     d.olog = e->alloc<int64_t>(4 * (size_t)d.olog_cap);
     d.olog_n = e->alloc<unsigned long long>(1);
+    d.rlist_cap = (int64_t)cells;   // (a watermark retires at most every slot)
+    d.rlist = e->alloc<int64_t>(cells);
+    d.rlist_n = e->alloc<unsigned long long>(1);
   }
   e->s.o.win_start = e->alloc<int64_t>((size_t)e->cfg.out_capacity);
   const size_t nb = (size_t)e->cfg.max_batch;
@@ -874,6 +898,7 @@ int session_create(fw_engine* e) {
   HIPCHK(e, hipMemsetAsync(d.nscnt, 0, 4 * (size_t)(d.nsmask + 1), e->stream));
   HIPCHK(e, hipMemsetAsync(d.nslog_n, 0, 8, e->stream));
   HIPCHK(e, hipMemsetAsync(d.olog_n, 0, 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.rlist_n, 0, 8, e->stream));
   return FW_OK;
 }
 
@@ -910,6 +935,8 @@ int session_watermark(fw_engine* e, int64_t wm) {
     if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_wm<1>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
     else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_wm<2>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
     else hipLaunchKernelGGL(k_sess_wm<4>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
+    hipLaunchKernelGGL(k_sess_ns_retire, dim3(e->grid), dim3(BLOCK), 0, e->stream, e->s, e->sess, e->ordinal);
+    HIPCHK(e, hipMemsetAsync(e->sess.rlist_n, 0, 8, e->stream));
     e->phase_end(e->s.stride);
     session_pool_recycle(e);   // the entries of the windows purged
     e->cur_wm = wm;
