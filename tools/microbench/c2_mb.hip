@@ -8,6 +8,10 @@
 //   V4  V3 with a plain load + store instead of the atomic (racy: throughput only)
 //   V5  rows {key, sum, first, f1} 32 B: the directory key and the pane in one line
 //   V6  SoA, plain load + store instead of the atomic (racy)
+//   V7  round 6: records first partitioned by directory range (NRANGE ranges of D / NRANGE
+//       slots: per-tile LDS histograms, a column scan, a scatter of (slot, value) pairs), then V1 over the ranges
+//       with range r's records on XCD r % 8 (the blocks of one XCD take its ranges in turn), so a range's directory
+//       and pane lines are reused while they sit in that XCD's L2 — prints the partition and the update apart
 // Build: hipcc --offload-arch=gfx950 -O3 c2_mb.hip -o c2_mb
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -84,6 +88,66 @@ __global__ __launch_bounds__(256) void k_pane(Cols c, int n, i64* dir, u64* sum,
   if (acc == 0x123456789) sink[0] = acc;
 }
 
+// ---- V7: partition by directory range, then the SoA update over each range's records ----
+constexpr int NRANGE = 1024, PT = 4096, PBLK = NB / PT;   // ranges; records per partition tile; tiles
+__device__ __forceinline__ int range_of(u64 slot) { return (int)(slot / (D / NRANGE)); }
+__global__ __launch_bounds__(1024) void k_phist(Cols c, unsigned* hist) {   // hist[range][tile]
+  __shared__ unsigned h[NRANGE];
+  for (int i = threadIdx.x; i < NRANGE; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < PT; i += blockDim.x)
+    atomicAdd(&h[range_of(fmix64((u64)c.key[(size_t)blockIdx.x * PT + i]) & (D - 1))], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < NRANGE; i += blockDim.x) hist[(size_t)i * PBLK + blockIdx.x] = h[i];
+}
+// exclusive scan of hist in (range, tile) order, one block; also each range's start
+__global__ __launch_bounds__(1024) void k_pscan(unsigned* hist, unsigned* rstart) {
+  __shared__ unsigned tot[NRANGE];
+  for (int r = threadIdx.x; r < NRANGE; r += blockDim.x) {
+    unsigned s = 0;
+    for (int b = 0; b < PBLK; ++b) { const unsigned x = hist[(size_t)r * PBLK + b]; hist[(size_t)r * PBLK + b] = s; s += x; }
+    tot[r] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned s = 0;
+    for (int r = 0; r < NRANGE; ++r) { rstart[r] = s; s += tot[r]; }
+    rstart[NRANGE] = s;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < NRANGE; r += blockDim.x)
+    for (int b = 0; b < PBLK; ++b) hist[(size_t)r * PBLK + b] += rstart[r];
+}
+__global__ __launch_bounds__(1024) void k_pscatter(Cols c, const unsigned* hist, u64* out_slot, i64* out_val) {
+  __shared__ unsigned cur[NRANGE];
+  for (int i = threadIdx.x; i < NRANGE; i += blockDim.x) cur[i] = hist[(size_t)i * PBLK + blockIdx.x];
+  __syncthreads();
+  for (int i = threadIdx.x; i < PT; i += blockDim.x) {
+    const size_t g = (size_t)blockIdx.x * PT + i;
+    const u64 slot = fmix64((u64)c.key[g]) & (D - 1);
+    const unsigned pos = atomicAdd(&cur[range_of(slot)], 1u);
+    out_slot[pos] = slot;
+    out_val[pos] = c.val[g];
+  }
+}
+// blocks: XCD x = b % 8 takes the ranges r = x (mod 8) in turn, PER blocks per range
+constexpr int PER = 4;
+__global__ __launch_bounds__(256) void k_prange(const u64* slots, const i64* vals, const unsigned* rstart, i64* dir,
+                                                u64* sum, i64* first, i64 ord_base, i64* sink) {
+  const int x = blockIdx.x & 7, idx = blockIdx.x >> 3;
+  const int r = (idx / PER) * 8 + x, part = idx % PER;
+  if (r >= NRANGE) return;
+  const unsigned lo = rstart[r], hi = rstart[r + 1];
+  i64 acc = 0;
+  for (unsigned i = lo + part * blockDim.x + threadIdx.x; i < hi; i += PER * blockDim.x) {
+    const u64 slot = slots[i];
+    acc ^= dir[slot];
+    atomicAdd(&sum[slot], (u64)vals[i]);
+    if (ord_base + (i64)i < first[slot]) acc ^= 1;
+  }
+  if (acc == 0x123456789) sink[0] = acc;
+}
+
 struct Timer {
   hipEvent_t a, b;
   Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -128,6 +192,30 @@ int main() {
       const double us = t.stop() * 1e3 / IT;
       printf("%-44s grid=%5d %8.1f us/batch %6.2f G rec/s\n", names[mode], grid, us, NB / us / 1e3);
     }
+  }
+  {   // V7
+    unsigned *hist, *rstart; u64* pslot; i64* pval;
+    CK(hipMalloc(&hist, (size_t)NRANGE * PBLK * 4)); CK(hipMalloc(&rstart, (NRANGE + 1) * 4));
+    CK(hipMalloc(&pslot, (size_t)NB * 8)); CK(hipMalloc(&pval, (size_t)NB * 8));
+    const int ublocks = NRANGE / 8 * PER * 8;
+    auto part = [&](int r) {
+      k_phist<<<PBLK, 1024>>>(batch(r), hist);
+      k_pscan<<<1, 1024>>>(hist, rstart);
+      k_pscatter<<<PBLK, 1024>>>(batch(r), hist, pslot, pval);
+    };
+    auto upd = [&](int r) { k_prange<<<ublocks, 256>>>(pslot, pval, rstart, dir, sum, first, (i64)r * NB, sink); };
+    for (int w = 0; w < 4; ++w) { part(w); upd(w); }
+    t.start();
+    for (int r = 0; r < IT; ++r) part(r);
+    const double us_p = t.stop() * 1e3 / IT;
+    t.start();
+    for (int r = 0; r < IT; ++r) upd(r);
+    const double us_u = t.stop() * 1e3 / IT;
+    t.start();
+    for (int r = 0; r < IT; ++r) { part(r); upd(r); }
+    const double us = t.stop() * 1e3 / IT;
+    printf("%-44s partition %6.1f us + update %6.1f us = %6.1f us/batch %6.2f G rec/s\n",
+           "V7 range-partitioned, XCD-local update", us_p, us_u, us, NB / us / 1e3);
   }
   CK(hipDeviceSynchronize());
   return 0;
