@@ -3339,6 +3339,7 @@ struct SessDev {
   int64_t* olog;
   unsigned long long* olog_n;
   int64_t olog_cap;
+  int32_t ckpt;     // checkpoint bookkeeping on (FW_SESS_CKPT=0: off; fw_snapshot_kg_flink / restore then fail)
   int64_t* rlist;   // slots a watermark retired (k_sess_wm -> k_sess_ns_retire)
   unsigned long long* rlist_n;
   int64_t rlist_cap;
@@ -5517,6 +5518,9 @@ static int session_download(fw_engine* e) {
 
 static int session_reject_config(fw_engine* e) {
   const fw_config& c = e->cfg;
+  (void)c;
+  if (!e->sess.ckpt)
+    return reject(e, FW_ERR_UNSUPPORTED, "session checkpoint bookkeeping is off (FW_SESS_CKPT=0)");
   if (e->mws_created.empty()) e->mws_created.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
   if (e->kg_touched.empty()) e->kg_touched.assign((size_t)(e->s.kg_end - e->s.kg_start + 1), 0);
   return FW_OK;

@@ -226,7 +226,8 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
   const unsigned long long imask = (1ull << idx_bits) - 1;
   int64_t ni = (int64_t)(k0 & imask);
   int64_t nts = b.ts[ni], nv = b.val[ni], nf1 = b.f1 ? b.f1[ni] : nts;
-  if (d.ktouch[kid] < 0) { d.ktouch[kid] = b.ord_base + ni; d.ktts[kid] = INT64_MAX; }   // getMergingWindowSet
+  const bool ck = d.ckpt != 0;   // checkpoint bookkeeping (FW_SESS_CKPT=0: off)
+  if (ck && d.ktouch[kid] < 0) { d.ktouch[kid] = b.ord_base + ni; d.ktts[kid] = INT64_MAX; }   // getMergingWindowSet
   bool accepted = false;
   bool more = true;
   for (int64_t j = j0; more; ++j) {
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
           }
           todo.clr(q);
           const int64_t x = base + q;
-          sess_ns_remove(d, kkg, key, x, ord);   // the source's state window entry cleared
+          if (ck) sess_ns_remove(d, kkg, key, x, ord);   // the source's state window entry cleared
           if (d.list) {   // the source's elements appended (mergePartitionedStates, list branch :315-333)
             if (d.len[x] > 0) {
               if (ll == 0) lh = d.head[x];
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
         r = t;
         d.start[base + r] = cs;
         d.end[base + r] = ce;
-        d.cre[base + r] = d.tre[base + r] = ord;   // onMerge's trigger timer, then the cleanup timer
+        if (ck) d.cre[base + r] = d.tre[base + r] = ord;   // onMerge's trigger timer, then the cleanup timer
       }
     }
     const int64_t max_ts = jsub(ce, 1);
@@ -353,13 +354,15 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       trig.clr(r);
       d.start[base + r] = cs;
       d.end[base + r] = ce;
-      d.sws[base + r] = cs;
-      d.swc[base + r] = d.cre[base + r] = d.tre[base + r] = ord;
-      sess_ns_add(d, kkg, cs);
+      if (ck) {
+        d.sws[base + r] = cs;
+        d.swc[base + r] = d.cre[base + r] = d.tre[base + r] = ord;
+        sess_ns_add(d, kkg, cs);
+      }
       if (d.list) d.len[base + r] = 0;
     }
     const int64_t x = base + r;
-    d.put[x] = ord;   // MergingWindowSet.addWindow re-puts the window the record lands in
+    if (ck) d.put[x] = ord;   // MergingWindowSet.addWindow re-puts the window the record lands in
     accepted = true;
     LateAcc cur;
     if (d.list) {
@@ -391,18 +394,18 @@ __global__ __launch_bounds__(BLOCK) void k_sess_walk(Spec s, SessDev d, BatchIn 
       }
       ++fires;
       if (purging) {   // FIRE_AND_PURGE: cleanup(actualWindow); an unchanged window's cleanup timer stays
-        if (contained && s.lateness > 0) sess_orphan(d, key, cs, ce, d.cre[x]);
-        sess_ns_remove(d, kkg, key, x, ord);
+        if (ck && contained && s.lateness > 0) sess_orphan(d, key, cs, ce, d.cre[x]);
+        if (ck) sess_ns_remove(d, kkg, key, x, ord);
         retire(r);
       }
     } else {
-      if (!trig.test(r)) d.tre[x] = ord;   // (re-armed: a window restored below its fire)
+      if (ck && !trig.test(r)) d.tre[x] = ord;   // (re-armed: a window restored below its fire)
       trig.set(r);
     }
   }
   live.store(d.live + kid * NW);
   trig.store(d.trig + kid * NW);
-  if (accepted) d.kacc[kid] = 1;
+  if (ck && accepted) d.kacc[kid] = 1;
   if (late) atomicAdd(&s.stats[ST_LATE], late);
   if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
 }
@@ -477,7 +480,8 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
   const int64_t wm = b.wm;
   const int64_t base = kid * d.sw;
   const unsigned long long imask = (1ull << idx_bits) - 1;
-  if (lane == 0 && d.ktouch[kid] < 0) { d.ktouch[kid] = b.ord_base + (int64_t)(sorted[j0] & imask); d.ktts[kid] = INT64_MAX; }
+  const bool ck = d.ckpt != 0;
+  if (ck && lane == 0 && d.ktouch[kid] < 0) { d.ktouch[kid] = b.ord_base + (int64_t)(sorted[j0] & imask); d.ktts[kid] = INT64_MAX; }
   bool accepted = false;
   SLane<NW> L;
 #pragma unroll
@@ -594,7 +598,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
               if (q < 0 || bc < bq || (bc == bq && sc < sq)) { q = c; bq = bc; sq = sc; }
             }
             todo.clr(q);
-            if (lane == 0) sess_ns_remove(d, kkg, key, base + q, ord);
+            if (ck && lane == 0) sess_ns_remove(d, kkg, key, base + q, ord);
             const LateAcc sv = gacc(q);
             res = hv ? sess_combine(s, res, sv) : sv;
             hv = true;
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
           slane_set<NW>(L.st, r, cs);
           slane_set<NW>(L.en, r, ce);
           if (r == cr) { c_st = cs; c_en = ce; }
-          if (lane == 0) d.cre[base + r] = d.tre[base + r] = ord;
+          if (ck && lane == 0) d.cre[base + r] = d.tre[base + r] = ord;
         }
       }
       const int64_t max_ts = jsub(ce, 1);
@@ -629,9 +633,9 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
         trig.clr(r);
         slane_set<NW>(L.st, r, cs);
         slane_set<NW>(L.en, r, ce);
-        if (lane == 0) { d.sws[base + r] = cs; d.swc[base + r] = d.cre[base + r] = d.tre[base + r] = ord; sess_ns_add(d, kkg, cs); }
+        if (ck && lane == 0) { d.sws[base + r] = cs; d.swc[base + r] = d.cre[base + r] = d.tre[base + r] = ord; sess_ns_add(d, kkg, cs); }
       }
-      if (lane == 0) d.put[base + r] = ord;
+      if (ck && lane == 0) d.put[base + r] = ord;
       accepted = true;
       const LateAcc cur = fresh ? a : sess_combine(s, gacc(r), a);
       slane_put<NW>(L, r, cur);
@@ -643,7 +647,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
         if (lane == 0) sess_emit(s, atomicAdd(s.o.count, 1ull), key, cs, max_ts, cur);
         ++fires;
         if (purging) {
-          if (lane == 0) {
+          if (ck && lane == 0) {
             if (contained && s.lateness > 0) sess_orphan(d, key, cs, ce, d.cre[base + r]);
             sess_ns_remove(d, kkg, key, base + r, ord);
           }
@@ -651,7 +655,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
           trig.clr(r);
         }
       } else {
-        if (lane == 0 && !trig.test(r)) d.tre[base + r] = ord;
+        if (ck && lane == 0 && !trig.test(r)) d.tre[base + r] = ord;
         trig.set(r);
       }
     }
@@ -672,7 +676,7 @@ __global__ __launch_bounds__(64) void k_sess_walk_hot(Spec s, SessDev d, BatchIn
   if (lane == 0) {
     live.store(d.live + kid * NW);
     trig.store(d.trig + kid * NW);
-    if (accepted) d.kacc[kid] = 1;
+    if (ck && accepted) d.kacc[kid] = 1;
     if (late) atomicAdd(&s.stats[ST_LATE], late);
     if (fires) { atomicAdd(&s.stats[ST_FIRED], fires); atomicAdd(&s.stats[ST_LATE_FIRES], fires); }
   }
@@ -710,7 +714,7 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
             fire = true;
             trig.clr(q);
             if (purging || ct == max_ts) retire = true;       // FIRE_AND_PURGE, or isCleanupTime
-            if (purging && ct != max_ts && ct > wm_new)       // the purged window's cleanup timer stays
+            if (d.ckpt && purging && ct != max_ts && ct > wm_new)   // the purged window's cleanup timer stays
               sess_orphan(d, kid_key(s, kid), d.start[kid * d.sw + q], e8[k], d.cre[kid * d.sw + q]);
           }
           if (!retire && ct <= wm_new) {                    // onEventTime(cleanupTime): cleanup
@@ -724,9 +728,9 @@ __global__ __launch_bounds__(BLOCK) void k_sess_wm(Spec s, SessDev d, int64_t wm
       }
       live = live.andnot(ret_m);
       trig = trig.andnot(ret_m);
-      if (tmin != INT64_MAX && d.ktouch[kid] < 0) { d.ktouch[kid] = touch_ord; d.ktts[kid] = tmin; }
+      if (d.ckpt && tmin != INT64_MAX && d.ktouch[kid] < 0) { d.ktouch[kid] = touch_ord; d.ktts[kid] = tmin; }
     }
-    {   // the retired windows' state entries cleared: listed (one reservation per wave) for k_sess_ns_retire, whose
+    if (d.ckpt) {   // the retired windows' state entries cleared: listed (one reservation per wave) for k_sess_ns_retire, whose
         // thread per entry keeps the namespace counts off this kernel's per-key chain
       const int c = ret_m.count();
       int incl = c;
@@ -860,6 +864,10 @@ int session_create(fw_engine* e) {
   d.ktouch = e->alloc<int64_t>((size_t)s.stride);
   d.ktts = e->alloc<int64_t>((size_t)s.stride);
   d.kacc = e->alloc<int32_t>((size_t)s.stride);
+  {   // FW_SESS_CKPT=0: no checkpoint bookkeeping (the reference-layout snapshot then fails; ~13-16 % faster)
+    const char* cv = getenv("FW_SESS_CKPT");
+    d.ckpt = (cv && atoi(cv) == 0) ? 0 : 1;
+  }
   {
     uint64_t m = 1024;
     while (m < 2 * (uint64_t)cells) m <<= 1;
@@ -935,8 +943,10 @@ int session_watermark(fw_engine* e, int64_t wm) {
     if (e->sess.nw == 1) hipLaunchKernelGGL(k_sess_wm<1>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
     else if (e->sess.nw == 2) hipLaunchKernelGGL(k_sess_wm<2>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
     else hipLaunchKernelGGL(k_sess_wm<4>, dim3(blocks), dim3(BLOCK), 0, e->stream, e->s, e->sess, wm, e->ordinal);
-    hipLaunchKernelGGL(k_sess_ns_retire, dim3(e->grid), dim3(BLOCK), 0, e->stream, e->s, e->sess, e->ordinal);
-    HIPCHK(e, hipMemsetAsync(e->sess.rlist_n, 0, 8, e->stream));
+    if (e->sess.ckpt) {
+      hipLaunchKernelGGL(k_sess_ns_retire, dim3(e->grid), dim3(BLOCK), 0, e->stream, e->s, e->sess, e->ordinal);
+      HIPCHK(e, hipMemsetAsync(e->sess.rlist_n, 0, 8, e->stream));
+    }
     e->phase_end(e->s.stride);
     session_pool_recycle(e);   // the entries of the windows purged
     e->cur_wm = wm;

@@ -194,3 +194,27 @@ def test_session_checkpoint_rejections():
         e.restore_kg_flink(kg, ("key", "f1", "sum"), st, struct.pack(">ii", 0, 0))
     assert ei.value.code == _abi.FW_ERR_INVALID_ARG
     e.close()
+
+
+@pytest.mark.gpu
+def test_session_checkpoint_bookkeeping_off(monkeypatch):
+    """FW_SESS_CKPT=0 drops the checkpoint bookkeeping (13-16 % of session throughput): results are
+    unchanged, and a reference-layout snapshot fails loudly instead of writing wrong bytes."""
+    from flink_amd import _abi
+    from flink_amd.windowing import WindowEngine
+    from harness import drive
+    from oracle.oracle import OracleEngine
+    monkeypatch.setenv("FW_SESS_CKPT", "0")
+    case = CASES[1]
+    vt, fields, lateness, purging = case
+    keys, ts, vals, f1 = _stream(vt)
+    outs = {}
+    for name, factory in (("g", WindowEngine), ("o", OracleEngine)):
+        e = factory(_config(vt, fields, lateness, purging))
+        outs[name] = _epochs(drive(e, keys, ts, vals, 2048, 100, LONG_MAX, f1=f1), case)
+        if name == "g":
+            with pytest.raises(_abi.FwError) as ei:
+                e.snapshot_kg_flink(0, _layout(fields))
+            assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+        e.close()
+    assert outs["g"] == outs["o"] and sum(len(r) for _, r in outs["o"]) > 1000
