@@ -6190,11 +6190,78 @@ static int restore_sliding_lists(fw_engine* e, int64_t wm, const std::vector<KgP
   }
   struct El { int64_t v, f1, m; };
   std::map<std::pair<int64_t, int64_t>, std::vector<std::array<int64_t, 3>>> slices;   // (slice, key) -> (ord, v, f1)
+  const int64_t R = s.R;
+  // the oldest window still in its lifetime at wm (every newer one exists once a record of its slices arrived)
+  int64_t n_alive = INT64_MIN / 4;
+  if (wm != INT64_MIN) {
+    const __int128 x = (__int128)wm - e->cfg.allowed_lateness - e->cfg.offset - e->cfg.size + 1;
+    const __int128 sl = e->cfg.slide;
+    __int128 q = x / sl;
+    if (x % sl != 0 && x < 0) --q;
+    n_alive = (int64_t)std::max<__int128>(q + 1, (__int128)(INT64_MIN / 4));
+  }
   for (const auto& kw : by_key) {
     const int64_t key = kw.first;
     const auto& wins = kw.second;
     std::vector<El> order;
-    for (int64_t n = wins.rbegin()->first; n >= wins.begin()->first; --n) {
+    if (R != 1) {
+      // a slide that does not divide the size: each element (distinct within a window) is identified across the
+      // windows' lists; its live windows [lo, hi] pick a slice m with floor(m / R) = hi whose oldest live window is
+      // lo; the arrival order is any order every list agrees with (a topological order of their successions)
+      std::map<std::pair<int64_t, int64_t>, int64_t> id;
+      std::vector<El> el;
+      std::vector<std::pair<int64_t, int64_t>> span;   // (lo, hi) of windows holding the element
+      std::vector<int64_t> nwin;
+      std::vector<std::vector<int64_t>> seqs;
+      for (const auto& w : wins) {
+        std::set<int64_t> seen;
+        std::vector<int64_t> seq;
+        for (const auto& x : lists[w.second]) {
+          auto it = id.find({x[0], x[1]});
+          int64_t k;
+          if (it == id.end()) {
+            k = (int64_t)el.size();
+            id[{x[0], x[1]}] = k;
+            el.push_back({x[0], x[1], 0});
+            span.push_back({w.first, w.first});
+            nwin.push_back(0);
+          } else {
+            k = it->second;
+          }
+          if (!seen.insert(k).second)
+            return reject(e, FW_ERR_UNSUPPORTED, "sliding-window lists with equal elements (slide not dividing the size)");
+          span[(size_t)k].first = std::min(span[(size_t)k].first, w.first);
+          span[(size_t)k].second = std::max(span[(size_t)k].second, w.first);
+          nwin[(size_t)k]++;
+          seq.push_back(k);
+        }
+        seqs.push_back(std::move(seq));
+      }
+      for (size_t k = 0; k < el.size(); ++k) {
+        const int64_t lo = span[k].first, hi = span[k].second;
+        if (nwin[k] != hi - lo + 1) return reject(e, FW_ERR_INVALID_ARG, "an element missing from a window between its windows");
+        bool found = false;
+        for (int64_t m = hi * R; m < hi * R + R && !found; ++m) {
+          const int64_t first_w = fw::floor_div(m - K + 1 + R - 1, R);
+          if (std::max(first_w, n_alive) == lo) { el[k].m = m; found = true; }
+        }
+        if (!found) return reject(e, FW_ERR_INVALID_ARG, "an element's windows are not those of any slice");
+      }
+      std::vector<std::vector<int64_t>> succ(el.size());
+      std::vector<int64_t> indeg(el.size(), 0);
+      for (const auto& seq : seqs)
+        for (size_t j = 1; j < seq.size(); ++j) { succ[(size_t)seq[j - 1]].push_back(seq[j]); indeg[(size_t)seq[j]]++; }
+      std::set<int64_t> ready;
+      for (size_t k = 0; k < el.size(); ++k) if (!indeg[k]) ready.insert((int64_t)k);
+      while (!ready.empty()) {
+        const int64_t k = *ready.begin();
+        ready.erase(ready.begin());
+        order.push_back(el[(size_t)k]);
+        for (int64_t nx : succ[(size_t)k]) if (--indeg[(size_t)nx] == 0) ready.insert(nx);
+      }
+      if (order.size() != el.size()) return reject(e, FW_ERR_INVALID_ARG, "the windows' lists disagree on the arrival order");
+    }
+    for (int64_t n = wins.rbegin()->first; R == 1 && n >= wins.begin()->first; --n) {
       std::vector<size_t> T;   // the key's known elements of window n's newer slices, in arrival order
       for (size_t q = 0; q < order.size(); ++q)
         if (order[q].m > n && order[q].m < n + K) T.push_back(q);
@@ -6224,7 +6291,7 @@ static int restore_sliding_lists(fw_engine* e, int64_t wm, const std::vector<KgP
       const auto& want = lists[w.second];
       size_t j = 0;
       for (const El& x : order) {
-        if (x.m < w.first || x.m >= w.first + K) continue;
+        if (x.m < w.first * R || x.m >= w.first * R + K) continue;
         if (j >= want.size() || want[j][0] != x.v || want[j][1] != x.f1)
           return reject(e, FW_ERR_UNSUPPORTED, "sliding-window lists with equal elements in an order no slice split gives");
         ++j;
@@ -6281,9 +6348,6 @@ int fw_restore_kg_flink(fw_engine* e, int32_t kg, const fw_state_layout* layout,
     if (int rc = check_state_layout(e, layout)) return rc;
     return session_restore_kg_flink(e, kg, layout, watermark, state, state_len, timers, timers_len);
   }
-  if (e->list && e->cfg.assigner == FW_SLIDING && e->s.R != 1)
-    return reject(e, FW_ERR_UNSUPPORTED, "list state of sliding windows whose slide does not divide the size: a "
-                                         "record's slice is not recoverable from the windows' lists");
   if (e->sticky) return e->sticky;
   if (e->pushes > 0 || e->records_in > 0) return reject(e, FW_ERR_INVALID_ARG, "restore after the first push");
   if (kg < e->s.kg_start || kg > e->s.kg_end)

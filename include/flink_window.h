@@ -265,7 +265,7 @@ int         fw_restore_kg(fw_engine* e, int32_t kg, const void* buf, int64_t len
  * 8-byte LongSerializer / DoubleSerializer field (TupleSerializer.serialize :120-129).  The layout must
  * name every aggregate the config computes (FW_SF_VALUE for maxBy/minBy), FW_SF_F1 iff keep_first_f1,
  * FW_SF_KEY at most once.  Fold (FW_AGGF_FOLD): the state is HeapFoldingState's accumulator, the initial value
- * folded with the pane (the layout names the one aggregate).  List state (FW_AGG_LIST; sliding windows: the slide dividing the size):
+ * folded with the pane (the layout names the one aggregate).  List state (FW_AGG_LIST):
  * the state is ListSerializer's `int size | element * size`, each element the window's input tuple with the
  * fields the layout names — FW_SF_VALUE once, FW_SF_KEY and FW_SF_F1 at most once each — in arrival order.
  * Session windows (reducing state): two tables, ids in stateTables' HashMap order (WindowOperator.java:445-460,

@@ -679,7 +679,7 @@ def test_fold_checkpoint(mode, kind, initial, vt, assigner):
 
 
 def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "value"), restore_wm=None, pre=None,
-              sliding=False):
+              sliding=False, slide=1000):
     """List state (WindowedStream.apply: HeapListState "window-contents" of the input tuples), tumbling 1 s windows
     or (sliding) 3 s windows every 1 s: drive 2/3 of a Zipf stream, snapshot every key group in the reference
     layout; or restore such sections at their watermark and drive the rest to a final MAX_WATERMARK."""
@@ -687,7 +687,7 @@ def _list_run(factory, vt, lateness, mode, restore=None, layout=("key", "f1", "v
     from harness import drive, gen_stream
     keys, ts, vals = gen_stream(24_000, 1200, rate=1 << 13, zipf=1.1, ooo=300, value_type=vt)
     f1 = np.arange(len(keys), dtype=np.int64) * 7 + 3
-    asg = SlidingEventTimeWindows.of(3000, 1000) if sliding else TumblingEventTimeWindows.of(1000)
+    asg = SlidingEventTimeWindows.of(3000, slide) if sliding else TumblingEventTimeWindows.of(1000)
     cfg = make_config(asg, ListStateDescriptor(vt), None, lateness, max_parallelism=128,
                       key_capacity=1 << 12, max_batch=1 << 12, out_capacity=1 << 20, ingest_mode=mode)
     n = len(keys) * 2 // 3
@@ -745,34 +745,36 @@ def test_list_checkpoint(mode, vt, lateness):
     assert eg == eo and sum(len(r) for _, r in eo) > 1000
 
 
-@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 800)])
-def test_oracle_sliding_list_checkpoint_round_trip(vt, lateness):
+@pytest.mark.parametrize("vt,lateness,slide", [("i64", 0, 1000), ("f64", 800, 1000), ("i64", 500, 2000)])
+def test_oracle_sliding_list_checkpoint_round_trip(vt, lateness, slide):
     """Sliding windows' list state: every window's list of its elements (a record sits in each of its windows'
     lists) restores and snapshots back byte for byte in the oracle."""
     from oracle.oracle import OracleEngine
-    snaps = _list_run(OracleEngine, vt, lateness, 0, sliding=True)
+    snaps = _list_run(OracleEngine, vt, lateness, 0, sliding=True, slide=slide)
     assert sum(len(s) for s, _ in snaps.values()) > 128 * 8
-    back, _ = _list_run(OracleEngine, vt, lateness, 0, restore=snaps, sliding=True)
+    back, _ = _list_run(OracleEngine, vt, lateness, 0, restore=snaps, sliding=True, slide=slide)
     assert _diff(back, snaps) is None
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("vt,lateness", [("i64", 0), ("f64", 800)])
-def test_sliding_list_checkpoint(mode, vt, lateness):
+@pytest.mark.parametrize("vt,lateness,slide", [("i64", 0, 1000), ("f64", 800, 1000), ("i64", 500, 2000)])
+def test_sliding_list_checkpoint(mode, vt, lateness, slide):
     """Sliding-window list state in the reference layout (round 6): the engine writes each window's list — its
     slices' elements of the key merged in arrival order — byte-identical to the oracle's; it restores the oracle's
     sections by peeling the windows newest first (a window's list less the elements of its newer slices, matched in
     order, is its oldest slice), writes them back unchanged, and continues exactly as the oracle restored from the
-    same bytes."""
+    same bytes.  A slide that does not divide the size (3 s every 2 s: slices of 1 s, a window starting every second
+    slice): each element is identified across its windows' lists, its live windows pick its slice, and the arrival
+    order is one every list agrees with."""
     from flink_amd.windowing import WindowEngine
     from harness import epochs_of
     from oracle.oracle import OracleEngine
-    g = _list_run(WindowEngine, vt, lateness, mode, sliding=True)
-    o = _list_run(OracleEngine, vt, lateness, 0, sliding=True)
+    g = _list_run(WindowEngine, vt, lateness, mode, sliding=True, slide=slide)
+    o = _list_run(OracleEngine, vt, lateness, 0, sliding=True, slide=slide)
     assert _diff(g, o) is None, _diff(g, o)
-    back, out_g = _list_run(WindowEngine, vt, lateness, mode, restore=o, sliding=True)
-    _, out_o = _list_run(OracleEngine, vt, lateness, 0, restore=o, sliding=True)
+    back, out_g = _list_run(WindowEngine, vt, lateness, mode, restore=o, sliding=True, slide=slide)
+    _, out_o = _list_run(OracleEngine, vt, lateness, 0, restore=o, sliding=True, slide=slide)
     assert _diff(back, o) is None, _diff(back, o)
     field = f"sum_{vt}"
     eg, eo = _canon(epochs_of(out_g, [field], True)), _canon(epochs_of(out_o, [field], True))
@@ -781,14 +783,26 @@ def test_sliding_list_checkpoint(mode, vt, lateness):
 
 @pytest.mark.gpu
 def test_list_checkpoint_rejections():
-    """Sliding-window list state whose slide does not divide the size (windows overlap by partial slides) takes no
-    reference-layout restore."""
+    """Sliding-window list state (slide not dividing the size) whose windows' lists share no consistent slices — an
+    element missing from a window between two that hold it — is refused."""
     from flink_amd import _abi
+    from flink_amd.keygroups import assign_to_key_group
     from flink_amd.windowing import ListStateDescriptor, SlidingEventTimeWindows, WindowEngine, make_config
-    e = WindowEngine(make_config(SlidingEventTimeWindows.of(3000, 2000), ListStateDescriptor()))
+    e = WindowEngine(make_config(SlidingEventTimeWindows.of(3000, 1000 * 2), ListStateDescriptor(),
+                                 max_parallelism=128))
+    key = 7
+    kg = assign_to_key_group(key, 128)
+    el = struct.pack(">qqq", key, 11, 5)   # (key, f1, value)
+    other = struct.pack(">qqq", key, 12, 6)
+    body = struct.pack(">i", 3)
+    for start, elems in ((0, [el]), (2000, [other]), (4000, [el])):   # el in windows 0 and 2, not in window 1
+        body += struct.pack(">qqi", start, start + 3000, 1) + struct.pack(">q", key) + struct.pack(">i", len(elems))
+        body += b"".join(elems)
+    st = struct.pack(">ihb", kg, 0, 1) + body
+    tm = b"".join(struct.pack(">qqqq", key, s0, s0 + 3000, s0 + 2999) for s0 in (0, 2000, 4000))
     with pytest.raises(_abi.FwError) as ei:
-        e.restore_kg_flink(0, ("key", "f1", "value"), b"", struct.pack(">ii", 0, 0))
-    assert ei.value.code == _abi.FW_ERR_UNSUPPORTED
+        e.restore_kg_flink(kg, ("key", "f1", "value"), st, struct.pack(">i", 3) + tm + struct.pack(">i", 0), -1)
+    assert ei.value.code in (_abi.FW_ERR_INVALID_ARG, _abi.FW_ERR_UNSUPPORTED)
     e.close()
 
 
